@@ -1,0 +1,168 @@
+/*
+ * webpgpu.h -- C ABI of libwebpgpu.so, the MI355X (gfx950) implementation of
+ * the deepteams/webp internal/dsp hot path.
+ *
+ * This header is the drop-in boundary.  Every entry point is extern "C",
+ * takes plain pointers / sizes, and replaces one reference interface (cited
+ * as path:line relative to the reference root).  Conventions:
+ *
+ *  - All buffer pointers are DEVICE pointers (hipMalloc / torch CUDA tensor
+ *    storage) unless the name ends in _host.  `stream` is a hipStream_t
+ *    (NULL = default stream).  Calls are asynchronous on `stream`.
+ *  - Return value: WG_OK (0) or a negative WG_E* status.  A HIP runtime
+ *    failure is reported, never papered over: there is no CPU fallback in
+ *    this library.  wg_last_error() returns a message for the calling thread.
+ *  - "Batched" entry points run the reference's per-block function over n
+ *    independent instances.  Instance i's buffer starts at base + i*stride.
+ *  - Frame entry points take `n_images` same-sized images laid out back to
+ *    back with the given per-image byte pitch (image_pitch).
+ *
+ * The Go-side binding a maintainer adds (cgo) is shown in INTEGRATION.md.
+ */
+#ifndef WEBPGPU_H
+#define WEBPGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WG_OK 0
+#define WG_EINVAL (-1)   /* bad argument (shape, mode, NULL) */
+#define WG_EHIP (-2)     /* HIP runtime / launch failure */
+#define WG_ENODEV (-3)   /* no gfx950 device */
+#define WG_ENOMEM (-4)
+
+#define WG_BPS 32 /* internal/dsp/dsp.go:5 */
+/* reference work-buffer layout, internal/lossy/constants.go:70-75 */
+#define WG_YUV_SIZE (WG_BPS * 17 + WG_BPS * 9)
+#define WG_YOFF (WG_BPS * 1 + 8)
+#define WG_UOFF (WG_YOFF + WG_BPS * 16 + WG_BPS)
+#define WG_VOFF (WG_UOFF + 16)
+
+const char* wg_last_error(void);
+int wg_version(void);
+/* Checks that the current device is gfx950 and the kernels are loadable. */
+int wg_device_check(void);
+
+/* ===================================================================== *
+ * 1. Block-level layer: the internal/dsp function variables, batched.
+ *    Each replaces the Go function variable / table named in the comment
+ *    (internal/dsp/dsp.go:10-37, ssim.go:251-254).
+ * ===================================================================== */
+
+/* PredLuma4[mode](buf, off) -- predict_lossy.go:185-451, dsp.go:36.
+ * For i < n: PredLuma4[modes[i]](bufs + i*buf_stride, offs ? offs[i] : off). */
+int wg_pred_luma4(const uint8_t* modes, uint8_t* bufs, int64_t buf_stride, const int32_t* offs, int32_t off,
+                  int32_t n, void* stream);
+/* PredLuma16[mode] -- predict_lossy.go:27-102, dsp.go:34 */
+int wg_pred_luma16(const uint8_t* modes, uint8_t* bufs, int64_t buf_stride, const int32_t* offs, int32_t off,
+                   int32_t n, void* stream);
+/* PredChroma8[mode] -- predict_lossy.go:106-181, dsp.go:35 */
+int wg_pred_chroma8(const uint8_t* modes, uint8_t* bufs, int64_t buf_stride, const int32_t* offs, int32_t off,
+                    int32_t n, void* stream);
+
+/* Decoder transforms, dsp.go:18-24.  coeffs: int16[n][coeff_pitch]; dst
+ * blocks at dst + i*dst_stride, BPS row stride.
+ * kind: 0 Transform(doTwo=0) 1 Transform(doTwo=1) 2 TransformAC3 3 TransformDC
+ *       4 TransformUV 5 TransformDCUV  (transforms.go:139-216) */
+int wg_transform(int32_t kind, const int16_t* coeffs, int64_t coeff_pitch, uint8_t* dst, int64_t dst_stride,
+                 int32_t n, void* stream);
+/* TransformWHT (transforms.go:223): in int16[n][16] -> out int16[n][256] */
+int wg_transform_wht(const int16_t* in, int16_t* out, int32_t n, void* stream);
+/* FTransformWHT (transforms.go:500): in int16[n][16] (flat) -> out int16[n][16] */
+int wg_ftransform_wht(const int16_t* in, int16_t* out, int32_t n, void* stream);
+/* ITransform(ref, in, dst, doTwo) (transforms.go:256): ref/dst blocks at
+ * +i*blk_stride (BPS rows), in int16[n][32]. */
+int wg_itransform(const uint8_t* ref, const int16_t* in, uint8_t* dst, int64_t blk_stride, int32_t do_two,
+                  int32_t n, void* stream);
+/* FTransform / FTransform2 (transforms.go:371,487): out int16[n][16 or 32] */
+int wg_ftransform(const uint8_t* src, const uint8_t* ref, int64_t blk_stride, int16_t* out, int32_t two,
+                  int32_t n, void* stream);
+
+/* MetricFunc SSE4x4/SSE16x16/TDisto4x4/TDisto16x16 (ssim.go:188-335).
+ * kind: 0 SSE4x4 1 SSE16x16 2 TDisto4x4 3 TDisto16x16.  out int32[n]. */
+int wg_metric(int32_t kind, const uint8_t* pix, const uint8_t* ref, int64_t blk_stride, int32_t* out,
+              int32_t n, void* stream);
+/* SSIMGet / SSIMGetClipped (ssim.go:116,132). xywh: int32[n][4] (xo,yo,W,H)
+ * or NULL for the unclipped 7x7 window at the buffer origin.  out double[n]. */
+int wg_ssim_get(const uint8_t* s1, const uint8_t* s2, int64_t buf_stride, int32_t row_stride,
+                const int32_t* xywh, double* out, int32_t n, void* stream);
+
+/* Loop filters (filter.go:93-242), applied in place to each instance buffer
+ * p + i*buf_stride at `base` with row `stride`.
+ * kind: 0 SimpleVFilter16 1 SimpleHFilter16 2 SimpleVFilter16i 3 SimpleHFilter16i
+ *       4 VFilter16 5 HFilter16 6 VFilter16i 7 HFilter16i
+ *       8 VFilter8 9 HFilter8 10 VFilter8i 11 HFilter8i (u = p, v = p + uv_delta)
+ * thresh/ithresh/hev are per instance (int32[n]); ithresh/hev unused by kinds 0-3. */
+int wg_filter(int32_t kind, uint8_t* p, int64_t buf_stride, int32_t base, int32_t stride, int32_t uv_delta,
+              const int32_t* thresh, const int32_t* ithresh, const int32_t* hev, int32_t n, void* stream);
+
+/* ===================================================================== *
+ * 2. Frame layer: the reference's row/frame seams.
+ * ===================================================================== */
+
+/* Parsed macroblock (mirrors MBData internal/lossy/decode.go:115-126 and
+ * FInfo :107-112).  32 bytes.  Coefficients travel separately as
+ * int16[n_mb][384] (Coeffs, already dequantised, I16 DC already WHT'd). */
+typedef struct wg_mb_info {
+  uint32_t non_zero_y;  /* 2-bit nz code per luma block, block 0 in bits 31..30 */
+  uint32_t non_zero_uv; /* U codes in bits 0..7, V in bits 8..15 */
+  uint8_t imodes[16];   /* I16: imodes[0]; I4: 16 sub-block modes, raster order */
+  uint8_t is_i4x4;
+  uint8_t uv_mode;
+  uint8_t skip;
+  uint8_t segment;
+  uint8_t f_limit;      /* FInfo.FLimit; 0 disables filtering of this MB */
+  uint8_t f_ilevel;
+  uint8_t f_inner;
+  uint8_t hev_thresh;
+} wg_mb_info;
+
+/* Decoder reconstruct + loop filter for whole frames: replaces the
+ * reconstructRow / filterRowAt calls of parseFrame
+ * (internal/lossy/decode.go:532-560, decode_frame.go:83-342).
+ * Output planes: Y stride 16*mbw (16*mbh rows), U/V stride 8*mbw, like the
+ * decoder caches (decode.go:441-530).  filter_type: 0 none, 1 simple, 2 normal.
+ * `work` is scratch of wg_decode_work_bytes(mbw, mbh, n_images) bytes. */
+size_t wg_decode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images);
+int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int32_t filter_type, int32_t mbw, int32_t mbh,
+                     int32_t n_images, uint8_t* y, uint8_t* u, uint8_t* v, void* work, void* stream);
+
+/* RGBA -> YUV420 import: replaces VP8Encoder.importImage
+ * (internal/lossy/encode.go:671-943, non-dithered path).  rgba: w x h, row
+ * pitch `stride`, image pitch rgba_pitch.  Outputs padded planes (Y stride
+ * 16*mbw, U/V stride 8*mbw) with per-image pitches y_pitch / uv_pitch. */
+int wg_import_rgba(const uint8_t* rgba, int32_t w, int32_t h, int32_t stride, int64_t rgba_pitch,
+                   int32_t has_alpha, uint8_t* y, uint8_t* u, uint8_t* v, int64_t y_pitch, int64_t uv_pitch,
+                   int32_t n_images, void* stream);
+
+/* Encoder analysis: replaces computeAlphas (internal/lossy/encode_analysis.go:245-307).
+ * Outputs per MB: alphas (mixed), lum/uv parts (may be NULL); uv_sum[img] is
+ * the sum of uv alphas (the reference's return value = uv_sum / nMB). */
+int wg_analysis_alphas(const uint8_t* y, const uint8_t* u, const uint8_t* v, int32_t w, int32_t h,
+                       int64_t y_pitch, int64_t uv_pitch, int32_t n_images, int32_t* alphas, int32_t* lum,
+                       int32_t* uva, int32_t* uv_sum, void* stream);
+
+/* Fancy upsampling YUV420 -> NRGBA: replaces buildNRGBA (webp.go:379-450)
+ * -> dsp.UpsampleLinePairNRGBA (upsample_direct_amd64.go:10).  alpha may be
+ * NULL (A = 255) else w x h plane with pitch a_pitch per image.
+ * out: h rows of 4*w bytes, out_pitch per image. */
+int wg_upsample_nrgba(const uint8_t* y, int32_t y_stride, int64_t y_pitch, const uint8_t* u, const uint8_t* v,
+                      int32_t uv_stride, int64_t uv_pitch, const uint8_t* alpha, int64_t a_pitch, int32_t w,
+                      int32_t h, uint8_t* out, int64_t out_pitch, int32_t n_images, void* stream);
+
+/* Plane SSIM (libwebp AccumulateSSIM built from SSIMGet/SSIMGetClipped,
+ * ssim.go:116-160): out[img] = sum over pixels of the clipped-window SSIM.
+ * `work` needs wg_plane_ssim_work_bytes(w, h, n_images) bytes. */
+size_t wg_plane_ssim_work_bytes(int32_t w, int32_t h, int32_t n_images);
+int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uint8_t* b, int32_t b_stride,
+                  int64_t b_pitch, int32_t w, int32_t h, int32_t n_images, double* out, void* work,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WEBPGPU_H */

@@ -1,0 +1,187 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes view of the C restatement in oracle/.
+
+The oracle restates deepteams/webp's Go internal/dsp hot path (and the lossy
+decoder/encoder loops that drive it) in plain C.  Only tests/, the graft
+smoke() check and bench.py's ``cpu_baseline`` leg may import this module, as
+the checker / CPU baseline.  The product (webp_amd) never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "liboracle.so")
+
+MB_INFO_DTYPE = np.dtype([
+    ("non_zero_y", "<u4"), ("non_zero_uv", "<u4"), ("imodes", "u1", (16,)),
+    ("is_i4x4", "u1"), ("uv_mode", "u1"), ("skip", "u1"), ("segment", "u1"),
+    ("f_limit", "u1"), ("f_ilevel", "u1"), ("f_inner", "u1"), ("hev_thresh", "u1"),
+])
+assert MB_INFO_DTYPE.itemsize == 32
+
+BPS = 32
+YUV_SIZE = BPS * 17 + BPS * 9
+YOFF = BPS + 8
+UOFF = YOFF + BPS * 16 + BPS
+VOFF = UOFF + 16
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def _load():
+    if not os.path.exists(_SO):
+        build()
+    return ctypes.CDLL(_SO)
+
+
+lib = _load()
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_i16p = ctypes.POINTER(ctypes.c_int16)
+_u16p = ctypes.POINTER(ctypes.c_uint16)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i = ctypes.c_int
+
+_SIGS = {
+    "or_transform": (None, [_i16p, _u8p, _i]),
+    "or_transform_dc": (None, [_i16p, _u8p]),
+    "or_transform_ac3": (None, [_i16p, _u8p]),
+    "or_transform_uv": (None, [_i16p, _u8p]),
+    "or_transform_dcuv": (None, [_i16p, _u8p]),
+    "or_transform_wht": (None, [_i16p, _i16p]),
+    "or_itransform": (None, [_u8p, _i16p, _u8p, _i]),
+    "or_ftransform": (None, [_u8p, _u8p, _i16p]),
+    "or_ftransform2": (None, [_u8p, _u8p, _i16p]),
+    "or_ftransform_wht": (None, [_i16p, _i16p]),
+    "or_pred_luma16": (None, [_i, _u8p, _i]),
+    "or_pred_chroma8": (None, [_i, _u8p, _i]),
+    "or_pred_luma4": (None, [_i, _u8p, _i]),
+    "or_simple_vfilter16": (None, [_u8p, _i, _i, _i]),
+    "or_simple_hfilter16": (None, [_u8p, _i, _i, _i]),
+    "or_simple_vfilter16i": (None, [_u8p, _i, _i, _i]),
+    "or_simple_hfilter16i": (None, [_u8p, _i, _i, _i]),
+    "or_vfilter16": (None, [_u8p, _i, _i, _i, _i, _i]),
+    "or_hfilter16": (None, [_u8p, _i, _i, _i, _i, _i]),
+    "or_vfilter16i": (None, [_u8p, _i, _i, _i, _i, _i]),
+    "or_hfilter16i": (None, [_u8p, _i, _i, _i, _i, _i]),
+    "or_vfilter8": (None, [_u8p, _u8p, _i, _i, _i, _i, _i, _i]),
+    "or_hfilter8": (None, [_u8p, _u8p, _i, _i, _i, _i, _i, _i]),
+    "or_vfilter8i": (None, [_u8p, _u8p, _i, _i, _i, _i, _i, _i]),
+    "or_hfilter8i": (None, [_u8p, _u8p, _i, _i, _i, _i, _i, _i]),
+    "or_yuv_to_rgb": (None, [_i, _i, _i, _u8p]),
+    "or_rgb_to_y": (_i, [_i, _i, _i]),
+    "or_rgb_to_u": (_i, [_i, _i, _i, _i]),
+    "or_rgb_to_v": (_i, [_i, _i, _i, _i]),
+    "or_gamma_to_linear": (ctypes.c_uint32, [_i]),
+    "or_linear_to_gamma": (_i, [ctypes.c_uint32, _i]),
+    "or_accumulate_rgba": (None, [_u8p, _u8p, _u8p, _u8p, _i, _u16p, _i]),
+    "or_convert_rgba32_to_uv": (None, [_u16p, _u8p, _u8p, _i]),
+    "or_upsample_line_pair_nrgba": (None, [_u8p] * 10 + [_i]),
+    "or_upsample_line_pair_rgb": (None, [_u8p] * 8 + [_i]),
+    "or_build_nrgba": (None, [_i, _i, _u8p, _i, _u8p, _u8p, _i, _u8p, _u8p]),
+    "or_sse4x4": (_i, [_u8p, _u8p]),
+    "or_sse16x16": (_i, [_u8p, _u8p]),
+    "or_tdisto4x4": (_i, [_u8p, _u8p]),
+    "or_tdisto16x16": (_i, [_u8p, _u8p]),
+    "or_ssim_get": (ctypes.c_double, [_u8p, _i, _u8p, _i]),
+    "or_ssim_get_clipped": (ctypes.c_double, [_u8p, _i, _u8p, _i, _i, _i, _i, _i]),
+    "or_plane_ssim": (ctypes.c_double, [_u8p, _i, _u8p, _i, _i, _i]),
+    "or_sse_plane": (ctypes.c_uint64, [_u8p, _i, _u8p, _i, _i, _i]),
+    "or_import_rgba": (None, [_u8p, _i, _i, _i, _i, _u8p, _u8p, _u8p]),
+    "or_compute_alphas": (_i, [_u8p, _u8p, _u8p, _i, _i, _i32p, _i32p, _i32p]),
+    "or_decode_reconstruct": (None, [ctypes.c_void_p, _i16p, _i, _i, _u8p, _u8p, _u8p]),
+    "or_decode_filter": (None, [ctypes.c_void_p, _i, _i, _i, _u8p, _u8p, _u8p]),
+    "or_decode_frame": (None, [ctypes.c_void_p, _i16p, _i, _i, _i, _u8p, _u8p, _u8p]),
+}
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+def ptr(a, ctype=ctypes.c_uint8, offset=0):
+    """Pointer to a[...] + offset elements (a must be C-contiguous)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return ctypes.cast(a.ctypes.data + offset * a.itemsize, ctypes.POINTER(ctype))
+
+
+def u8(a, offset=0):
+    return ptr(a, ctypes.c_uint8, offset)
+
+
+def i16(a, offset=0):
+    return ptr(a, ctypes.c_int16, offset)
+
+
+# ---- frame-level helpers (numpy in / numpy out) ----
+
+def plane_dims(w, h):
+    mbw, mbh = (w + 15) >> 4, (h + 15) >> 4
+    return mbw, mbh
+
+
+def import_rgba(rgba, has_alpha=True):
+    """importImage: rgba (h, w, 4) uint8 -> padded Y, U, V planes."""
+    h, w, _ = rgba.shape
+    rgba = np.ascontiguousarray(rgba)
+    mbw, mbh = plane_dims(w, h)
+    Y = np.zeros((mbh * 16, mbw * 16), np.uint8)
+    U = np.zeros((mbh * 8, mbw * 8), np.uint8)
+    V = np.zeros((mbh * 8, mbw * 8), np.uint8)
+    lib.or_import_rgba(u8(rgba), w, h, w * 4, int(has_alpha), u8(Y), u8(U), u8(V))
+    return Y, U, V
+
+
+def compute_alphas(Y, U, V, w, h):
+    mbw, mbh = plane_dims(w, h)
+    alphas = np.zeros(mbw * mbh, np.int32)
+    lum = np.zeros_like(alphas)
+    uva = np.zeros_like(alphas)
+    uvavg = lib.or_compute_alphas(u8(Y), u8(U), u8(V), w, h, ptr(alphas, ctypes.c_int32),
+                                  ptr(lum, ctypes.c_int32), ptr(uva, ctypes.c_int32))
+    return alphas, lum, uva, uvavg
+
+
+def decode_frame(mb, coeffs, filter_type, mbw, mbh, recon=True, filt=True):
+    """Reconstruct (+ loop filter) a frame of parsed macroblocks."""
+    mb = np.ascontiguousarray(mb, dtype=MB_INFO_DTYPE)
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.int16)
+    Y = np.zeros((mbh * 16, mbw * 16), np.uint8)
+    U = np.zeros((mbh * 8, mbw * 8), np.uint8)
+    V = np.zeros((mbh * 8, mbw * 8), np.uint8)
+    if recon and filt:
+        lib.or_decode_frame(mb.ctypes.data, i16(coeffs), filter_type, mbw, mbh, u8(Y), u8(U), u8(V))
+    elif recon:
+        lib.or_decode_reconstruct(mb.ctypes.data, i16(coeffs), mbw, mbh, u8(Y), u8(U), u8(V))
+    return Y, U, V
+
+
+def filter_frame(mb, filter_type, mbw, mbh, Y, U, V):
+    mb = np.ascontiguousarray(mb, dtype=MB_INFO_DTYPE)
+    Y, U, V = Y.copy(), U.copy(), V.copy()
+    lib.or_decode_filter(mb.ctypes.data, filter_type, mbw, mbh, u8(Y), u8(U), u8(V))
+    return Y, U, V
+
+
+def build_nrgba(Y, U, V, w, h, alpha=None):
+    out = np.zeros((h, w, 4), np.uint8)
+    Y = np.ascontiguousarray(Y)
+    U = np.ascontiguousarray(U)
+    V = np.ascontiguousarray(V)
+    a = None if alpha is None else np.ascontiguousarray(alpha)
+    lib.or_build_nrgba(w, h, u8(Y), Y.shape[1], u8(U), u8(V), U.shape[1], u8(a) if a is not None else None,
+                       u8(out))
+    return out
+
+
+def plane_ssim(a, b):
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    h, w = a.shape
+    return lib.or_plane_ssim(u8(a), a.shape[1], u8(b), b.shape[1], w, h)

@@ -1,0 +1,151 @@
+/*
+ * oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the deepteams/webp internal/dsp hot path (and the
+ * lossy/webp callers that drive it), written from the Go source so that the
+ * HIP kernels in webp_amd/ can be checked bit-for-bit.  Every function cites
+ * the reference file:line it follows (paths relative to the reference root).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker / CPU baseline -- never as the
+ * product path.  The product library (webp_amd/libwebpgpu.so) does not link
+ * it and has no CPU fallback.
+ *
+ * Integer widths: Go `int` is 64-bit, so arithmetic that Go does in `int`
+ * and that can exceed 2^31 (IDCT second pass) is done in int64_t here.
+ */
+#ifndef WEBP_ORACLE_H
+#define WEBP_ORACLE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OR_BPS 32 /* internal/dsp/dsp.go:5 */
+/* internal/lossy/constants.go:70-75 */
+#define OR_YUV_SIZE (OR_BPS * 17 + OR_BPS * 9)
+#define OR_YOFF (OR_BPS * 1 + 8)
+#define OR_UOFF (OR_YOFF + OR_BPS * 16 + OR_BPS)
+#define OR_VOFF (OR_UOFF + 16)
+
+/* ---- clip helpers (internal/dsp/cliptables.go) ---- */
+int or_clip8b(int64_t v);
+
+/* ---- transforms (internal/dsp/transforms.go) ---- */
+void or_transform(const int16_t* in, uint8_t* dst, int do_two);   /* transformTwo :139 */
+void or_transform_dc(const int16_t* in, uint8_t* dst);            /* :148 */
+void or_transform_ac3(const int16_t* in, uint8_t* dst);           /* :170 */
+void or_transform_uv(const int16_t* in, uint8_t* dst);            /* :197 */
+void or_transform_dcuv(const int16_t* in, uint8_t* dst);          /* :203 */
+void or_transform_wht(const int16_t* in, int16_t* out);           /* :223 */
+void or_itransform(const uint8_t* ref, const int16_t* in, uint8_t* dst, int do_two); /* :256 */
+void or_ftransform(const uint8_t* src, const uint8_t* ref, int16_t* out);            /* :371 */
+void or_ftransform2(const uint8_t* src, const uint8_t* ref, int16_t* out);           /* :487 */
+void or_ftransform_wht(const int16_t* in, int16_t* out);          /* :500 */
+
+/* ---- intra predictors (internal/dsp/predict_lossy.go); buf+off is the block origin ---- */
+void or_pred_luma16(int mode, uint8_t* buf, int off);   /* :27-102 */
+void or_pred_chroma8(int mode, uint8_t* buf, int off);  /* :106-181 */
+void or_pred_luma4(int mode, uint8_t* buf, int off);    /* :185-451 */
+
+/* ---- loop filters (internal/dsp/filter.go) ---- */
+void or_simple_vfilter16(uint8_t* p, int base, int stride, int thresh);  /* :93 */
+void or_simple_hfilter16(uint8_t* p, int base, int stride, int thresh);  /* :109 */
+void or_simple_vfilter16i(uint8_t* p, int base, int stride, int thresh); /* :126 */
+void or_simple_hfilter16i(uint8_t* p, int base, int stride, int thresh); /* :134 */
+void or_vfilter16(uint8_t* p, int base, int stride, int thresh, int ithresh, int hev_t);  /* :194 */
+void or_hfilter16(uint8_t* p, int base, int stride, int thresh, int ithresh, int hev_t);  /* :199 */
+void or_vfilter16i(uint8_t* p, int base, int stride, int thresh, int ithresh, int hev_t); /* :217 */
+void or_hfilter16i(uint8_t* p, int base, int stride, int thresh, int ithresh, int hev_t); /* :224 */
+void or_vfilter8(uint8_t* u, uint8_t* v, int ubase, int vbase, int stride, int thresh, int ithresh, int hev_t);  /* :205 */
+void or_hfilter8(uint8_t* u, uint8_t* v, int ubase, int vbase, int stride, int thresh, int ithresh, int hev_t);  /* :211 */
+void or_vfilter8i(uint8_t* u, uint8_t* v, int ubase, int vbase, int stride, int thresh, int ithresh, int hev_t); /* :232 */
+void or_hfilter8i(uint8_t* u, uint8_t* v, int ubase, int vbase, int stride, int thresh, int ithresh, int hev_t); /* :238 */
+
+/* ---- YUV <-> RGB (internal/dsp/yuv.go) ---- */
+void or_yuv_to_rgb(int y, int u, int v, uint8_t* rgb);          /* YUVToRGB :105 */
+int or_rgb_to_y(int r, int g, int b);                            /* :151 */
+int or_rgb_to_u(int r, int g, int b, int rounding);              /* :164 */
+int or_rgb_to_v(int r, int g, int b, int rounding);              /* :169 */
+uint32_t or_gamma_to_linear(int v);                              /* :226 */
+int or_linear_to_gamma(uint32_t base, int shift);               /* :236 */
+void or_accumulate_rgba(const uint8_t* r, const uint8_t* g, const uint8_t* b, const uint8_t* a,
+                        int stride, uint16_t* dst, int width);   /* :486 */
+void or_convert_rgba32_to_uv(const uint16_t* rgb, uint8_t* u, uint8_t* v, int width); /* :553 */
+
+/* ---- VP8Random (internal/dsp/random.go) ---- */
+typedef struct { int index1, index2; uint32_t tab[55]; int amp; } or_random;
+void or_random_init(or_random* rg, float dithering);            /* :39 */
+int or_random_bits2(or_random* rg, int num_bits, int amp);      /* :54 */
+
+/* ---- upsampling (internal/dsp/upsample.go, webp.go) ---- */
+void or_upsample_line_pair_nrgba(const uint8_t* top_y, const uint8_t* bot_y,
+                                 const uint8_t* top_u, const uint8_t* top_v,
+                                 const uint8_t* bot_u, const uint8_t* bot_v,
+                                 uint8_t* top_dst, uint8_t* bot_dst,
+                                 const uint8_t* alpha_top, const uint8_t* alpha_bot, int width); /* :130 */
+void or_upsample_line_pair_rgb(const uint8_t* top_y, const uint8_t* bot_y,
+                               const uint8_t* top_u, const uint8_t* top_v,
+                               const uint8_t* bot_u, const uint8_t* bot_v,
+                               uint8_t* top_dst, uint8_t* bot_dst, int width); /* :45 */
+/* buildNRGBA (webp.go:379-450): alpha may be NULL (then A=255); out stride = 4*w */
+void or_build_nrgba(int w, int h, const uint8_t* y, int y_stride, const uint8_t* u, const uint8_t* v,
+                    int uv_stride, const uint8_t* alpha, uint8_t* out);
+
+/* ---- distortion / SSIM (internal/dsp/ssim.go) ---- */
+int or_sse4x4(const uint8_t* a, const uint8_t* b);               /* :188 */
+int or_sse16x16(const uint8_t* a, const uint8_t* b);             /* :220 */
+int or_tdisto4x4(const uint8_t* a, const uint8_t* b);            /* :315 */
+int or_tdisto16x16(const uint8_t* a, const uint8_t* b);          /* :327 */
+double or_ssim_get(const uint8_t* s1, int st1, const uint8_t* s2, int st2);   /* :116 */
+double or_ssim_get_clipped(const uint8_t* s1, int st1, const uint8_t* s2, int st2,
+                           int xo, int yo, int w, int h);         /* :132 */
+/* plane SSIM sum = libwebp AccumulateSSIM: sum over all pixels of SSIMGetClipped */
+double or_plane_ssim(const uint8_t* a, int sa, const uint8_t* b, int sb, int w, int h);
+uint64_t or_sse_plane(const uint8_t* a, int sa, const uint8_t* b, int sb, int w, int h); /* SSE :172 */
+
+/* ---- lossy encoder DSP drivers ---- */
+/* importImage (internal/lossy/encode.go:671-943), non-dithered direct path:
+ * rgba (stride bytes) w x h -> Y (stride 16*mbW, 16*mbH rows), U/V (stride 8*mbW, 8*mbH rows).
+ * has_alpha=0 forces A=255 for chroma averaging (encode.go:862-866). */
+void or_import_rgba(const uint8_t* rgba, int w, int h, int stride, int has_alpha,
+                    uint8_t* y, uint8_t* u, uint8_t* v);
+/* computeAlphas (encode_analysis.go:245-307): alphas[mbW*mbH] mixed alpha, returns uv alpha avg.
+ * lum_alpha/uv_alpha (optional, may be NULL) receive the per-MB parts. */
+int or_compute_alphas(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h,
+                      int32_t* alphas, int32_t* lum_alpha, int32_t* uv_alpha);
+
+/* ---- lossy decoder reconstruct + loop filter (internal/lossy/decode_frame.go) ---- */
+/* Parsed macroblock, the GPU wire format (mirrors MBData decode.go:115-126 and FInfo :107-112). */
+typedef struct {
+  uint32_t non_zero_y;   /* 2 bits/block, block 0 in bits 31..30 */
+  uint32_t non_zero_uv;  /* U in bits 0..7, V in bits 8..15 */
+  uint8_t imodes[16];    /* I16: imodes[0]; I4: 16 sub-block modes (raster) */
+  uint8_t is_i4x4;
+  uint8_t uv_mode;
+  uint8_t skip;
+  uint8_t segment;
+  uint8_t f_limit;       /* FInfo.FLimit (0 = no filtering) */
+  uint8_t f_ilevel;      /* FInfo.FILevel */
+  uint8_t f_inner;       /* FInfo.FInner */
+  uint8_t hev_thresh;    /* FInfo.HevThresh */
+} or_mb_info;            /* 32 bytes */
+
+/* reconstructRow over all rows (decode_frame.go:83-218): coeffs int16[nMB][384].
+ * Planes have stride 16*mbW (Y) and 8*mbW (U/V), like the decoder caches (decode.go:441-530). */
+void or_decode_reconstruct(const or_mb_info* mb, const int16_t* coeffs, int mbw, int mbh,
+                           uint8_t* y, uint8_t* u, uint8_t* v);
+/* filterRowAt/doFilter over all rows, raster MB order (decode_frame.go:283-342). */
+void or_decode_filter(const or_mb_info* mb, int filter_type, int mbw, int mbh,
+                      uint8_t* y, uint8_t* u, uint8_t* v);
+/* parseFrame order (decode.go:532-560): reconstruct row then filter row. */
+void or_decode_frame(const or_mb_info* mb, const int16_t* coeffs, int filter_type, int mbw, int mbh,
+                     uint8_t* y, uint8_t* u, uint8_t* v);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,141 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes bridge to the third-party libwebp that
+ships with Pillow in this image (libwebp 1.6.0 / libsharpyuv 0.4.2).
+
+Used as a *secondary* external oracle to pin the C restatement in oracle/
+(SURVEY.md 8(c)): VP8 decoding is normative, so WebPDecodeYUV pins
+reconstruct + loop filter; WebPDecodeRGBA pins fancy upsampling + YUV->RGB;
+WebPPictureImportRGBA pins the RGBA->YUV420 import; WebPPlaneDistortion pins
+plane SSIM.  Nothing here is part of the product.  Every entry point returns
+None-able results so tests can skip when Pillow's libwebp is absent.
+"""
+import ctypes
+import glob
+import os
+
+import numpy as np
+
+_LIBS = glob.glob("/usr/local/lib/python3.10/dist-packages/pillow.libs/libwebp-*.so*")
+_SHARP = glob.glob("/usr/local/lib/python3.10/dist-packages/pillow.libs/libsharpyuv-*.so*")
+
+lib = None
+if _LIBS:
+    try:
+        if _SHARP:
+            ctypes.CDLL(_SHARP[0], mode=ctypes.RTLD_GLOBAL)
+        lib = ctypes.CDLL(_LIBS[0])
+    except OSError:
+        lib = None
+
+available = lib is not None
+
+if available:
+    _u8p = ctypes.POINTER(ctypes.c_uint8)
+    _ip = ctypes.POINTER(ctypes.c_int)
+    lib.WebPEncodeRGBA.restype = ctypes.c_size_t
+    lib.WebPEncodeRGBA.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                   ctypes.POINTER(_u8p)]
+    lib.WebPEncodeLosslessRGBA.restype = ctypes.c_size_t
+    lib.WebPEncodeLosslessRGBA.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(_u8p)]
+    lib.WebPDecodeYUV.restype = _u8p
+    lib.WebPDecodeYUV.argtypes = [ctypes.c_void_p, ctypes.c_size_t, _ip, _ip, ctypes.POINTER(_u8p),
+                                  ctypes.POINTER(_u8p), _ip, _ip]
+    lib.WebPDecodeRGBA.restype = _u8p
+    lib.WebPDecodeRGBA.argtypes = [ctypes.c_void_p, ctypes.c_size_t, _ip, _ip]
+    lib.WebPFree.argtypes = [ctypes.c_void_p]
+    lib.WebPPlaneDistortion.restype = ctypes.c_int
+    lib.WebPPlaneDistortion.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    lib.WebPPictureInitInternal.restype = ctypes.c_int
+    lib.WebPPictureInitInternal.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.WebPPictureImportRGBA.restype = ctypes.c_int
+    lib.WebPPictureImportRGBA.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    lib.WebPPictureFree.argtypes = [ctypes.c_void_p]
+    lib.WebPPictureSharpARGBToYUVA.restype = ctypes.c_int
+    lib.WebPPictureSharpARGBToYUVA.argtypes = [ctypes.c_void_p]
+
+
+def encode_lossy(rgba, quality=75.0):
+    """libwebp WebPEncodeRGBA -> bytes."""
+    h, w, _ = rgba.shape
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = lib.WebPEncodeRGBA(rgba.ctypes.data, w, h, w * 4, float(quality), ctypes.byref(out))
+    data = ctypes.string_at(out, n)
+    lib.WebPFree(out)
+    return data
+
+
+def decode_yuv(data):
+    """WebPDecodeYUV -> (Y, U, V) cropped planes (h x w, (h+1)/2 x (w+1)/2)."""
+    w, h = ctypes.c_int(), ctypes.c_int()
+    u = ctypes.POINTER(ctypes.c_uint8)()
+    v = ctypes.POINTER(ctypes.c_uint8)()
+    ys, uvs = ctypes.c_int(), ctypes.c_int()
+    y = lib.WebPDecodeYUV(data, len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(u), ctypes.byref(v),
+                          ctypes.byref(ys), ctypes.byref(uvs))
+    W, H = w.value, h.value
+    cw, ch = (W + 1) // 2, (H + 1) // 2
+    Y = np.ctypeslib.as_array(y, shape=(H * ys.value,)).reshape(H, ys.value)[:, :W].copy()
+    U = np.ctypeslib.as_array(u, shape=((ch - 1) * uvs.value + cw,))
+    V = np.ctypeslib.as_array(v, shape=((ch - 1) * uvs.value + cw,))
+    Uo = np.stack([U[r * uvs.value: r * uvs.value + cw] for r in range(ch)])
+    Vo = np.stack([V[r * uvs.value: r * uvs.value + cw] for r in range(ch)])
+    lib.WebPFree(y)
+    return Y, Uo, Vo
+
+
+def decode_rgba(data):
+    w, h = ctypes.c_int(), ctypes.c_int()
+    p = lib.WebPDecodeRGBA(data, len(data), ctypes.byref(w), ctypes.byref(h))
+    out = np.ctypeslib.as_array(p, shape=(h.value, w.value, 4)).copy()
+    lib.WebPFree(p)
+    return out
+
+
+def plane_ssim(a, b):
+    """WebPPlaneDistortion(type=1): float32 sum of per-pixel SSIM (x_step=1)."""
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    h, w = a.shape
+    dist, res = ctypes.c_float(), ctypes.c_float()
+    ok = lib.WebPPlaneDistortion(a.ctypes.data, w, b.ctypes.data, w, w, h, 1, 1, ctypes.byref(dist),
+                                 ctypes.byref(res))
+    assert ok
+    return float(dist.value)
+
+
+# WebPPicture field offsets (libwebp encode.h, LP64)
+_PIC_SIZE = 512
+_OFF_USE_ARGB, _OFF_W, _OFF_H, _OFF_Y, _OFF_U, _OFF_V, _OFF_YS, _OFF_UVS = 0, 8, 12, 16, 24, 32, 40, 44
+
+
+def _pic_planes(buf, w, h):
+    def rd(off, t):
+        return t.from_buffer(buf, off).value
+    y = rd(_OFF_Y, ctypes.c_void_p)
+    u = rd(_OFF_U, ctypes.c_void_p)
+    v = rd(_OFF_V, ctypes.c_void_p)
+    ys = rd(_OFF_YS, ctypes.c_int)
+    uvs = rd(_OFF_UVS, ctypes.c_int)
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    Y = np.ctypeslib.as_array(ctypes.cast(y, ctypes.POINTER(ctypes.c_uint8)), shape=(h, ys))[:, :w].copy()
+    U = np.ctypeslib.as_array(ctypes.cast(u, ctypes.POINTER(ctypes.c_uint8)), shape=(ch, uvs))[:, :cw].copy()
+    V = np.ctypeslib.as_array(ctypes.cast(v, ctypes.POINTER(ctypes.c_uint8)), shape=(ch, uvs))[:, :cw].copy()
+    return Y, U, V
+
+
+def import_rgba(rgba):
+    """WebPPictureImportRGBA with use_argb=0 -> (Y, U, V) cropped planes."""
+    h, w, _ = rgba.shape
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    buf = (ctypes.c_uint8 * _PIC_SIZE)()
+    assert lib.WebPPictureInitInternal(buf, 0x0200 + 0x10)
+    ctypes.c_int.from_buffer(buf, _OFF_USE_ARGB).value = 0
+    ctypes.c_int.from_buffer(buf, _OFF_W).value = w
+    ctypes.c_int.from_buffer(buf, _OFF_H).value = h
+    assert lib.WebPPictureImportRGBA(buf, rgba.ctypes.data, w * 4)
+    planes = _pic_planes(buf, w, h)
+    lib.WebPPictureFree(buf)
+    return planes

@@ -1,0 +1,65 @@
+"""CPU: the C-ABI library loads and exports every symbol include/webpgpu.h
+declares (no compute calls without a GPU), the Python mirror binds them, and
+argument validation rejects bad shapes without touching the device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "webpgpu.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(wg_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert len(syms) >= 20, syms
+
+
+def test_library_exports_every_declared_symbol():
+    from webp_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header():
+    from webp_amd import _lib
+    assert sorted(_lib.SIGNATURES) == declared_symbols()
+
+
+def test_invalid_arguments_are_rejected_without_gpu():
+    from webp_amd import _lib
+    lib = _lib.lib
+    assert lib.wg_decode_frames(None, None, 2, 1, 1, 1, None, None, None, None, None) == -1
+    assert b"invalid argument" in lib.wg_last_error()
+    assert lib.wg_import_rgba(None, 0, 0, 0, 0, 0, None, None, None, 0, 0, 1, None) == -1
+    assert lib.wg_transform(9, None, 0, None, 0, 1, None) == -1
+    assert lib.wg_filter(12, None, 0, 0, 0, 0, None, None, None, 1, None) == -1
+
+
+def test_work_size_helpers():
+    from webp_amd import _lib
+    assert _lib.lib.wg_decode_work_bytes(120, 68, 2) == 2 * (120 * 32 + 68 * 64)
+    assert _lib.lib.wg_decode_work_bytes(0, 68, 2) == 0
+    assert _lib.lib.wg_plane_ssim_work_bytes(33, 17, 1) == 8 * 3 * 2
+
+
+def test_library_is_gfx950_only():
+    """The shipped code object targets gfx950 and nothing else."""
+    from webp_amd import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+    for other in (b"gfx942", b"gfx90a", b"gfx1100"):
+        assert other not in blob
+
+
+@pytest.mark.parametrize("mod", ["webp_amd.dsp", "webp_amd.frames"])
+def test_modules_import(mod):
+    __import__(mod)

@@ -1,0 +1,158 @@
+"""CPU: pin the C restatement (oracle/) before trusting it as the checker.
+
+1. Known-answer tests the reference's own Go tests hold
+   (internal/dsp/upsample_test.go, random_test.go).
+2. Golden fixtures produced by libwebp 1.6.0 (tests/golden/make_golden.py):
+   RGBA->YUV import, fancy upsampling of normatively decoded planes, plane SSIM.
+3. Where the reference checkout is present (build container only), verbatim
+   reference tables are re-read and compared.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import REFERENCE
+
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "libwebp_fixtures.npz"))
+
+
+def yuv_to_rgb(y, u, v):
+    out = (ctypes.c_uint8 * 3)()
+    O.lib.or_yuv_to_rgb(y, u, v, out)
+    return tuple(out)
+
+
+def upsample_rgb(ty, by, tu, tv, bu, bv, width):
+    arr = lambda x: None if x is None else np.asarray(x, np.uint8)  # noqa: E731
+    ty, by, tu, tv, bu, bv = map(arr, (ty, by, tu, tv, bu, bv))
+    td = np.zeros(width * 3, np.uint8)
+    bd = np.zeros(width * 3, np.uint8) if by is not None else None
+    O.lib.or_upsample_line_pair_rgb(O.u8(ty), O.u8(by) if by is not None else None, O.u8(tu), O.u8(tv), O.u8(bu),
+                                    O.u8(bv), O.u8(td), O.u8(bd) if bd is not None else None, width)
+    return td, bd
+
+
+# ---------------- upsample_test.go KATs ----------------
+
+def test_diamond_kernel_values():
+    """upsample_test.go:40-139: tl,t,l,cur = 80,160,120,240 -> 113/158 top, 138/193 bottom."""
+    y = [128] * 4
+    td, bd = upsample_rgb(y, y, [80, 160], [80, 160], [120, 240], [120, 240], 4)
+    assert tuple(td[3:6]) == yuv_to_rgb(128, 113, 113)
+    assert tuple(td[6:9]) == yuv_to_rgb(128, 158, 158)
+    assert tuple(bd[3:6]) == yuv_to_rgb(128, 138, 138)
+    assert tuple(bd[6:9]) == yuv_to_rgb(128, 193, 193)
+
+
+def test_single_pixel_width():
+    """upsample_test.go:141-160."""
+    td, _ = upsample_rgb([128], None, [128], [128], [128], [128], 1)
+    assert tuple(td[:3]) == yuv_to_rgb(128, 128, 128)
+
+
+def test_even_width_last_pixel():
+    """upsample_test.go:228-266: last pixel of width 6 uses chroma 200."""
+    y = [128] * 6
+    c = [100, 150, 200]
+    td, bd = upsample_rgb(y, y, c, c, c, c, 6)
+    assert tuple(td[15:18]) == yuv_to_rgb(128, 200, 200)
+
+
+def test_nrgba_matches_rgb_and_alpha():
+    """upsample_test.go:162-226."""
+    ty, by = np.array([100, 120, 140, 160], np.uint8), np.array([110, 130, 150, 170], np.uint8)
+    tu, tv = np.array([80, 160], np.uint8), np.array([90, 170], np.uint8)
+    bu, bv = np.array([120, 200], np.uint8), np.array([130, 210], np.uint8)
+    trgb, brgb = upsample_rgb(ty, by, tu, tv, bu, bv, 4)
+    at, ab = np.array([200, 201, 202, 203], np.uint8), np.array([210, 211, 212, 213], np.uint8)
+    for alpha in (False, True):
+        tn, bn = np.zeros(16, np.uint8), np.zeros(16, np.uint8)
+        O.lib.or_upsample_line_pair_nrgba(O.u8(ty), O.u8(by), O.u8(tu), O.u8(tv), O.u8(bu), O.u8(bv), O.u8(tn),
+                                          O.u8(bn), O.u8(at) if alpha else None, O.u8(ab) if alpha else None, 4)
+        assert (tn.reshape(4, 4)[:, :3] == trgb.reshape(4, 3)).all()
+        assert (bn.reshape(4, 4)[:, :3] == brgb.reshape(4, 3)).all()
+        assert (tn.reshape(4, 4)[:, 3] == (at if alpha else 255)).all()
+        assert (bn.reshape(4, 4)[:, 3] == (ab if alpha else 255)).all()
+
+
+# ---------------- random_test.go KATs ----------------
+
+class _Rand(ctypes.Structure):
+    _fields_ = [("index1", ctypes.c_int), ("index2", ctypes.c_int), ("tab", ctypes.c_uint32 * 55),
+                ("amp", ctypes.c_int)]
+
+
+@pytest.mark.parametrize("dith,amp", [(0.0, 0), (-1.0, 0), (0.5, 128), (1.0, 256), (2.0, 256)])
+def test_random_init(dith, amp):
+    rg = _Rand()
+    O.lib.or_random_init.argtypes = [ctypes.POINTER(_Rand), ctypes.c_float]
+    O.lib.or_random_init(ctypes.byref(rg), dith)
+    assert rg.index1 == 0 and rg.index2 == 31 and rg.amp == amp
+    assert rg.tab[0] == 0x0de15230 and rg.tab[54] == 0x27e5ed3c
+
+
+def test_random_bits_centered():
+    """random_test.go:52-...: full amplitude stays within [0, 2^16) around 2^15."""
+    rg = _Rand()
+    O.lib.or_random_init.argtypes = [ctypes.POINTER(_Rand), ctypes.c_float]
+    O.lib.or_random_bits2.argtypes = [ctypes.POINTER(_Rand), ctypes.c_int, ctypes.c_int]
+    O.lib.or_random_init(ctypes.byref(rg), 1.0)
+    vals = [O.lib.or_random_bits2(ctypes.byref(rg), 16, 256) for _ in range(2000)]
+    assert min(vals) >= 0 and max(vals) < (1 << 16)
+    assert abs(np.mean(vals) - (1 << 15)) < 2000
+
+
+# ---------------- libwebp golden fixtures ----------------
+
+@pytest.mark.parametrize("name", ["imp_a", "imp_b", "imp_c"])
+def test_import_vs_libwebp(name):
+    rgba = GOLD[name + "_rgba"]
+    h, w, _ = rgba.shape
+    Y, U, V = O.import_rgba(rgba, has_alpha=True)
+    ey, eu, ev = GOLD[name + "_y"], GOLD[name + "_u"], GOLD[name + "_v"]
+    assert (Y[:h, :w] == ey).all()
+    assert (U[:eu.shape[0], :eu.shape[1]] == eu).all()
+    assert (V[:ev.shape[0], :ev.shape[1]] == ev).all()
+
+
+@pytest.mark.parametrize("name", ["dec_a", "dec_b"])
+def test_upsample_vs_libwebp(name):
+    Y, U, V, rgba = (GOLD[name + k] for k in ("_y", "_u", "_v", "_rgba"))
+    h, w = Y.shape
+    out = O.build_nrgba(Y, U, V, w, h)
+    assert (out == rgba).all()
+
+
+def test_plane_ssim_vs_libwebp():
+    for a, b, v in (("ssim_a", "ssim_b", "ssim_value"), ("ssim_c", "ssim_d", "ssim_value2")):
+        got = O.plane_ssim(GOLD[a], GOLD[b])
+        want = float(GOLD[v][0])
+        assert abs(got - want) <= 1e-6 * abs(want) + 1e-4  # libwebp reports float32
+
+
+def test_ssim_identity():
+    """testc/ssim identity (ssim_test.go:178): SSIM of a plane with itself is 1 per pixel."""
+    p = GOLD["ssim_a"]
+    assert abs(O.plane_ssim(p, p) - p.size) < 1e-6 * p.size
+
+
+# ---------------- reference tables (build container only) ----------------
+
+@pytest.mark.skipif(not os.path.isdir(REFERENCE), reason="reference checkout not present")
+def test_inv_alpha_table_is_floor_division():
+    """yuv.go:343-447 kInvAlpha[a] == floor(2^19 / a): the oracle and the GPU compute it."""
+    src = open(os.path.join(REFERENCE, "internal/dsp/yuv.go")).read()
+    body = re.search(r"var kInvAlpha = \[4\*0xff \+ 1\]uint32\{(.*?)\n\}", src, re.S).group(1)
+    vals = [int(x) for x in re.findall(r"\d+", re.sub(r"//.*", "", body))]
+    assert len(vals) == 1021 and vals[0] == 0
+    assert all(vals[a] == (1 << 19) // a for a in range(1, 1021))
+
+
+def test_gamma_tables_monotone_and_bounded():
+    lin = [O.lib.or_gamma_to_linear(i) for i in range(256)]
+    assert lin[0] == 0 and lin[255] == 4095 and all(b >= a for a, b in zip(lin, lin[1:]))
+    assert O.lib.or_linear_to_gamma(4095 * 4, 0) == 4 * 255  # sum-of-4 scale (yuv.go:229-249)

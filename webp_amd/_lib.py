@@ -1,0 +1,74 @@
+"""ctypes binding of webp_amd/libwebpgpu.so (the C ABI in include/webpgpu.h).
+
+The library is built in-tree for gfx950 (``make -C webp_amd``).  There is no
+fallback: if the shared object is missing or a call fails, an exception is
+raised.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libwebpgpu.so")
+
+
+class WebpGpuError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise WebpGpuError(
+            f"{LIB_PATH} not found: build it with `make -C webp_amd` (hipcc --offload-arch=gfx950); "
+            "webp_amd has no CPU fallback")
+    return ctypes.CDLL(LIB_PATH)
+
+
+lib = _load()
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+
+# name -> argtypes (all return int status unless listed in _RES)
+SIGNATURES = {
+    "wg_last_error": [],
+    "wg_version": [],
+    "wg_device_check": [],
+    "wg_pred_luma4": [_vp, _vp, _i64, _vp, _i32, _i32, _vp],
+    "wg_pred_luma16": [_vp, _vp, _i64, _vp, _i32, _i32, _vp],
+    "wg_pred_chroma8": [_vp, _vp, _i64, _vp, _i32, _i32, _vp],
+    "wg_transform": [_i32, _vp, _i64, _vp, _i64, _i32, _vp],
+    "wg_transform_wht": [_vp, _vp, _i32, _vp],
+    "wg_ftransform_wht": [_vp, _vp, _i32, _vp],
+    "wg_itransform": [_vp, _vp, _vp, _i64, _i32, _i32, _vp],
+    "wg_ftransform": [_vp, _vp, _i64, _vp, _i32, _i32, _vp],
+    "wg_metric": [_i32, _vp, _vp, _i64, _vp, _i32, _vp],
+    "wg_ssim_get": [_vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp],
+    "wg_filter": [_i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp],
+    "wg_decode_work_bytes": [_i32, _i32, _i32],
+    "wg_decode_frames": [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
+    "wg_import_rgba": [_vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
+    "wg_analysis_alphas": [_vp, _vp, _vp, _i32, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp],
+    "wg_upsample_nrgba": [_vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp],
+    "wg_plane_ssim_work_bytes": [_i32, _i32, _i32],
+    "wg_plane_ssim": [_vp, _i32, _i64, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp],
+}
+_RES = {"wg_last_error": ctypes.c_char_p, "wg_decode_work_bytes": ctypes.c_size_t,
+        "wg_plane_ssim_work_bytes": ctypes.c_size_t}
+
+for _name, _args in SIGNATURES.items():
+    _f = getattr(lib, _name)
+    _f.argtypes = _args
+    _f.restype = _RES.get(_name, ctypes.c_int)
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib.wg_last_error().decode(errors="replace")
+        raise WebpGpuError(f"{what or 'webpgpu call'} failed (status {rc}): {msg}")
+    return rc
+
+
+def call(name, *args):
+    """Invoke a status-returning entry point and raise on failure."""
+    return check(getattr(lib, name)(*args), name)

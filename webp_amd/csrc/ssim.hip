@@ -1,0 +1,116 @@
+// ssim.hip -- whole-plane SSIM on gfx950.  The reference's SSIM primitives
+// are SSIMGet / SSIMGetClipped (internal/dsp/ssim.go:116-160); the plane sum
+// is libwebp's AccumulateSSIM as fixed in SURVEY.md 8(a) A22: a 7x7 hat
+// window per pixel, clipped at the borders (an interior window equals
+// SSIMGet since N = 256 there).
+//
+// A 16x16 tile of pixels per 256-thread workgroup; the 22x22 source tiles
+// (3-pixel halo) of both planes are staged in LDS.  Window statistics are
+// exact integers (any summation order), the per-pixel SSIM is the same
+// float64 expression as the reference; the plane sum is a per-tile partial
+// plus a second deterministic pass.
+#include "wg_common.h"
+#include "wg_dsp.h"
+
+namespace {
+using namespace wg;
+
+constexpr int TILE = 16, HALO = 3, TS = TILE + 2 * HALO;  // 22
+
+struct SsimArgs {
+  const uint8_t *a, *b;
+  int64_t a_pitch, b_pitch;
+  int a_stride, b_stride, w, h, tiles_x, tiles_y;
+  double* partial;
+};
+
+__global__ __launch_bounds__(256) void k_plane_ssim(const SsimArgs p) {
+  __shared__ uint8_t ta[TS * TS], tb[TS * TS];
+  __shared__ double red[4];
+  const int tiles = p.tiles_x * p.tiles_y;
+  const int img = blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
+  const int tx0 = (tile % p.tiles_x) * TILE, ty0 = (tile / p.tiles_x) * TILE;
+  const uint8_t* A = p.a + img * p.a_pitch;
+  const uint8_t* B = p.b + img * p.b_pitch;
+  for (int i = threadIdx.x; i < TS * TS; i += blockDim.x) {
+    const int yy = ty0 - HALO + i / TS, xx = tx0 - HALO + i % TS;
+    const bool in = xx >= 0 && xx < p.w && yy >= 0 && yy < p.h;
+    ta[i] = in ? A[(int64_t)yy * p.a_stride + xx] : 0;
+    tb[i] = in ? B[(int64_t)yy * p.b_stride + xx] : 0;
+  }
+  __syncthreads();
+  const int lx = threadIdx.x % TILE, ly = threadIdx.x / TILE;
+  const int xo = tx0 + lx, yo = ty0 + ly;
+  double v = 0.0;
+  if (xo < p.w && yo < p.h) {
+    const uint32_t kw[7] = {1, 2, 3, 4, 3, 2, 1};
+    SsimStats s = {0, 0, 0, 0, 0, 0};
+    for (int dy = 0; dy < 7; dy++) {
+      const int yy = yo - 3 + dy;
+      if (yy < 0 || yy >= p.h) continue;
+      for (int dx = 0; dx < 7; dx++) {
+        const int xx = xo - 3 + dx;
+        if (xx < 0 || xx >= p.w) continue;
+        const uint32_t wt = kw[dx] * kw[dy];
+        const int li = (ly + dy) * TS + lx + dx;
+        const uint32_t x = ta[li], y = tb[li];
+        s.w += wt;
+        s.xm += wt * x;
+        s.ym += wt * y;
+        s.xxm += wt * x * x;
+        s.xym += wt * x * y;
+        s.yym += wt * y * y;
+      }
+    }
+    v = ssim_calc(s, s.w);  // SSIMFromStatsClipped; s.w == 256 for interior windows
+  }
+  // block reduction (fixed order -> deterministic)
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) p.partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void k_sum_partials(const double* partial, int per_img, double* out) {
+  __shared__ double red[4];
+  const int img = blockIdx.x;
+  double v = 0.0;
+  for (int i = threadIdx.x; i < per_img; i += blockDim.x) v += partial[(int64_t)img * per_img + i];
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) out[img] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+}  // namespace
+
+extern "C" size_t wg_plane_ssim_work_bytes(int32_t w, int32_t h, int32_t n_images) {
+  if (w <= 0 || h <= 0 || n_images <= 0) return 0;
+  return sizeof(double) * (size_t)n_images * ((w + TILE - 1) / TILE) * ((h + TILE - 1) / TILE);
+}
+
+extern "C" int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uint8_t* b, int32_t b_stride,
+                             int64_t b_pitch, int32_t w, int32_t h, int32_t n_images, double* out, void* work,
+                             void* stream) {
+  WG_REQUIRE(a && b && out && work && w > 0 && h > 0 && n_images > 0 && a_stride >= w && b_stride >= w);
+  SsimArgs p;
+  p.a = a;
+  p.b = b;
+  p.a_pitch = a_pitch;
+  p.b_pitch = b_pitch;
+  p.a_stride = a_stride;
+  p.b_stride = b_stride;
+  p.w = w;
+  p.h = h;
+  p.tiles_x = (w + TILE - 1) / TILE;
+  p.tiles_y = (h + TILE - 1) / TILE;
+  p.partial = static_cast<double*>(work);
+  hipStream_t s = wg::as_stream(stream);
+  const int per = p.tiles_x * p.tiles_y;
+  hipLaunchKernelGGL(k_plane_ssim, dim3((unsigned)(per * n_images)), dim3(256), 0, s, p);
+  int rc = wg::check_launch("k_plane_ssim");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)n_images), dim3(256), 0, s, p.partial, per, out);
+  return wg::check_launch("k_sum_partials");
+}

@@ -1,0 +1,220 @@
+"""Host mirror of deepteams/webp ``internal/dsp`` (dsp.go:10-37, ssim.go:251-254)
+over the batched GPU entry points of libwebpgpu.so.
+
+Every function keeps the reference's name and argument meaning, with one
+batch dimension in front: ``bufs`` is a (n, L) uint8 CUDA tensor of n
+independent caller-owned buffers (the reference's ``[]byte``), ``off`` is
+the block origin inside each buffer, and results are written in place
+exactly where the Go function writes them.  Computation always runs on the
+GPU; there is no CPU path.
+"""
+import torch
+
+from ._lib import call
+
+BPS = 32  # internal/dsp/dsp.go:5
+YUV_SIZE = BPS * 17 + BPS * 9  # internal/lossy/constants.go:70-75
+YOFF = BPS + 8
+UOFF = YOFF + BPS * 16 + BPS
+VOFF = UOFF + 16
+
+# transform kinds (webpgpu.h wg_transform)
+_T_ONE, _T_TWO, _T_AC3, _T_DC, _T_UV, _T_DCUV = range(6)
+# metric kinds
+_M_SSE4, _M_SSE16, _M_TD4, _M_TD16 = range(4)
+# filter kinds (webpgpu.h wg_filter)
+FILTER_KINDS = {
+    "SimpleVFilter16": 0, "SimpleHFilter16": 1, "SimpleVFilter16i": 2, "SimpleHFilter16i": 3,
+    "VFilter16": 4, "HFilter16": 5, "VFilter16i": 6, "HFilter16i": 7,
+    "VFilter8": 8, "HFilter8": 9, "VFilter8i": 10, "HFilter8i": 11,
+}
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(t, dtype=None):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise TypeError("webp_amd.dsp expects CUDA (HIP) tensors")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError("tensor must be contiguous")
+    return t
+
+
+def _modes(modes, n, device):
+    if isinstance(modes, int):
+        modes = torch.full((n,), modes, dtype=torch.uint8, device=device)
+    return _dev(modes.to(torch.uint8) if modes.dtype != torch.uint8 else modes)
+
+
+def _offs(off, n, device):
+    if isinstance(off, int):
+        return None, off
+    return _dev(off.to(torch.int32).to(device).contiguous()), 0
+
+
+# ---- intra predictors (predict_lossy.go, dsp.go:33-37) ----
+
+def _pred(name, modes, bufs, off):
+    _dev(bufs, torch.uint8)
+    n = bufs.shape[0]
+    m = _modes(modes, n, bufs.device)
+    offs, o = _offs(off, n, bufs.device)
+    call(name, m.data_ptr(), bufs.data_ptr(), bufs.stride(0), offs.data_ptr() if offs is not None else None, o, n,
+         _stream())
+
+
+def PredLuma4(modes, bufs, off):
+    """PredLuma4[mode](buf, off) for each buffer (predict_lossy.go:185-451)."""
+    _pred("wg_pred_luma4", modes, bufs, off)
+
+
+def PredLuma16(modes, bufs, off):
+    """PredLuma16[mode](buf, off) (predict_lossy.go:27-102)."""
+    _pred("wg_pred_luma16", modes, bufs, off)
+
+
+def PredChroma8(modes, bufs, off):
+    """PredChroma8[mode](buf, off) (predict_lossy.go:106-181)."""
+    _pred("wg_pred_chroma8", modes, bufs, off)
+
+
+# ---- transforms (transforms.go, dsp.go:10-24) ----
+
+def _transform(kind, coeffs, dst, off):
+    _dev(coeffs, torch.int16)
+    _dev(dst, torch.uint8)
+    n = dst.shape[0]
+    call("wg_transform", kind, coeffs.data_ptr(), coeffs.stride(0), dst.data_ptr() + off, dst.stride(0), n,
+         _stream())
+
+
+def Transform(coeffs, dst, do_two, off=0):
+    """Transform(coeffs, dst[off:], doTwo) -- transformTwo (transforms.go:139)."""
+    _transform(_T_TWO if do_two else _T_ONE, coeffs, dst, off)
+
+
+def TransformAC3(coeffs, dst, off=0):
+    _transform(_T_AC3, coeffs, dst, off)
+
+
+def TransformDC(coeffs, dst, off=0):
+    _transform(_T_DC, coeffs, dst, off)
+
+
+def TransformUV(coeffs, dst, off=0):
+    _transform(_T_UV, coeffs, dst, off)
+
+
+def TransformDCUV(coeffs, dst, off=0):
+    _transform(_T_DCUV, coeffs, dst, off)
+
+
+def TransformWHT(inp, out):
+    """TransformWHT(in[16], out[256]) (transforms.go:223): DCs land at out[16*k]."""
+    _dev(inp, torch.int16)
+    _dev(out, torch.int16)
+    call("wg_transform_wht", inp.data_ptr(), out.data_ptr(), inp.shape[0], _stream())
+
+
+def FTransformWHT(inp, out):
+    """FTransformWHT on a flat 4x4 DC array (transforms.go:500)."""
+    _dev(inp, torch.int16)
+    _dev(out, torch.int16)
+    call("wg_ftransform_wht", inp.data_ptr(), out.data_ptr(), inp.shape[0], _stream())
+
+
+def ITransform(ref, inp, dst, do_two, ref_off=0, dst_off=0):
+    """ITransform(ref, in, dst, doTwo) (transforms.go:256).  ref and dst are the
+    same (n, L) buffer tensor at offsets ref_off / dst_off."""
+    _dev(ref, torch.uint8)
+    _dev(inp, torch.int16)
+    _dev(dst, torch.uint8)
+    assert ref.stride(0) == dst.stride(0) and inp.shape[1] == 32
+    call("wg_itransform", ref.data_ptr() + ref_off, inp.data_ptr(), dst.data_ptr() + dst_off, ref.stride(0),
+         int(do_two), ref.shape[0], _stream())
+
+
+def FTransform(src, ref, out, src_off=0, ref_off=0, two=False):
+    """FTransform(src, ref, out) (transforms.go:371); two=True is FTransform2."""
+    _dev(src, torch.uint8)
+    _dev(ref, torch.uint8)
+    _dev(out, torch.int16)
+    assert src.stride(0) == ref.stride(0)
+    call("wg_ftransform", src.data_ptr() + src_off, ref.data_ptr() + ref_off, src.stride(0), out.data_ptr(),
+         int(two), src.shape[0], _stream())
+
+
+def FTransform2(src, ref, out, src_off=0, ref_off=0):
+    FTransform(src, ref, out, src_off, ref_off, two=True)
+
+
+# ---- distortion (ssim.go) ----
+
+def _metric(kind, pix, ref, pix_off, ref_off):
+    _dev(pix, torch.uint8)
+    _dev(ref, torch.uint8)
+    assert pix.stride(0) == ref.stride(0)
+    out = torch.empty(pix.shape[0], dtype=torch.int32, device=pix.device)
+    call("wg_metric", kind, pix.data_ptr() + pix_off, ref.data_ptr() + ref_off, pix.stride(0), out.data_ptr(),
+         pix.shape[0], _stream())
+    return out
+
+
+def SSE4x4(pix, ref, pix_off=0, ref_off=0):
+    return _metric(_M_SSE4, pix, ref, pix_off, ref_off)
+
+
+def SSE16x16(pix, ref, pix_off=0, ref_off=0):
+    return _metric(_M_SSE16, pix, ref, pix_off, ref_off)
+
+
+def TDisto4x4(a, b, a_off=0, b_off=0):
+    return _metric(_M_TD4, a, b, a_off, b_off)
+
+
+def TDisto16x16(a, b, a_off=0, b_off=0):
+    return _metric(_M_TD16, a, b, a_off, b_off)
+
+
+def SSIMGet(src1, src2, stride):
+    """SSIMGet(src1, stride, src2, stride) (ssim.go:116) per buffer pair."""
+    _dev(src1, torch.uint8)
+    _dev(src2, torch.uint8)
+    out = torch.empty(src1.shape[0], dtype=torch.float64, device=src1.device)
+    call("wg_ssim_get", src1.data_ptr(), src2.data_ptr(), src1.stride(0), stride, None, out.data_ptr(),
+         src1.shape[0], _stream())
+    return out
+
+
+def SSIMGetClipped(src1, src2, stride, xywh):
+    """SSIMGetClipped(src1, stride, src2, stride, xo, yo, W, H) (ssim.go:132); xywh (n, 4) int32."""
+    _dev(src1, torch.uint8)
+    _dev(src2, torch.uint8)
+    xywh = _dev(xywh.to(torch.int32).contiguous())
+    out = torch.empty(src1.shape[0], dtype=torch.float64, device=src1.device)
+    call("wg_ssim_get", src1.data_ptr(), src2.data_ptr(), src1.stride(0), stride, xywh.data_ptr(), out.data_ptr(),
+         src1.shape[0], _stream())
+    return out
+
+
+# ---- loop filters (filter.go:93-242) ----
+
+def filter_edge(name, p, base, stride, thresh, ithresh=None, hev=None, uv_delta=0):
+    """Apply dsp.<name>(p, base, stride, thresh[, ithresh, hevT]) to every buffer.
+    For the 8-pixel chroma filters the V plane is p + uv_delta."""
+    _dev(p, torch.uint8)
+    n = p.shape[0]
+
+    def vec(x):
+        if x is None:
+            return None
+        if isinstance(x, int):
+            x = torch.full((n,), x, dtype=torch.int32, device=p.device)
+        return _dev(x.to(torch.int32).contiguous())
+    t, it, h = vec(thresh), vec(ithresh), vec(hev)
+    call("wg_filter", FILTER_KINDS[name], p.data_ptr(), p.stride(0), base, stride, uv_delta, t.data_ptr(),
+         it.data_ptr() if it is not None else None, h.data_ptr() if h is not None else None, n, _stream())

@@ -1,0 +1,115 @@
+"""Frame-level entry points: the reference's row/frame seams.
+
+  decode_frames     internal/lossy/decode.go:532-560 (reconstructRow + filterRowAt)
+  import_rgba       internal/lossy/encode.go:671-943 (importImage)
+  analysis_alphas   internal/lossy/encode_analysis.go:245-307 (computeAlphas)
+  build_nrgba       webp.go:379-450 (buildNRGBA -> UpsampleLinePairNRGBA)
+  plane_ssim        AccumulateSSIM over ssim.go:116-160
+
+All take / return CUDA tensors; a leading batch dimension means "n images of
+the same size".  Everything runs in libwebpgpu.so on the GPU.
+"""
+import numpy as np
+import torch
+
+from ._lib import call, lib
+
+MB_INFO_DTYPE = np.dtype([
+    ("non_zero_y", "<u4"), ("non_zero_uv", "<u4"), ("imodes", "u1", (16,)),
+    ("is_i4x4", "u1"), ("uv_mode", "u1"), ("skip", "u1"), ("segment", "u1"),
+    ("f_limit", "u1"), ("f_ilevel", "u1"), ("f_inner", "u1"), ("hev_thresh", "u1"),
+])  # wg_mb_info, include/webpgpu.h
+assert MB_INFO_DTYPE.itemsize == 32
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def mb_dims(w, h):
+    return (w + 15) >> 4, (h + 15) >> 4
+
+
+def mb_info_tensor(mb, device="cuda"):
+    """numpy structured array (.., MB_INFO_DTYPE) -> (n, 32) uint8 device tensor."""
+    arr = np.ascontiguousarray(mb, dtype=MB_INFO_DTYPE).reshape(-1)
+    return torch.from_numpy(arr.view(np.uint8).reshape(-1, 32).copy()).to(device)
+
+
+def decode_frames(mb_info, coeffs, filter_type, mbw, mbh, n_images=1, out=None, work=None):
+    """Reconstruct + loop-filter n frames of parsed macroblocks.
+
+    mb_info: (n*mbh*mbw, 32) uint8, coeffs: (n*mbh*mbw, 384) int16 (CUDA).
+    Returns (Y, U, V) of shapes (n, 16*mbh, 16*mbw) and (n, 8*mbh, 8*mbw)."""
+    dev = coeffs.device
+    assert mb_info.is_cuda and coeffs.is_cuda and coeffs.dtype == torch.int16
+    assert mb_info.numel() == 32 * n_images * mbw * mbh and coeffs.numel() == 384 * n_images * mbw * mbh
+    if out is None:
+        Y = torch.empty((n_images, 16 * mbh, 16 * mbw), dtype=torch.uint8, device=dev)
+        U = torch.empty((n_images, 8 * mbh, 8 * mbw), dtype=torch.uint8, device=dev)
+        V = torch.empty_like(U)
+    else:
+        Y, U, V = out
+    if work is None:
+        work = torch.empty(lib.wg_decode_work_bytes(mbw, mbh, n_images), dtype=torch.uint8, device=dev)
+    call("wg_decode_frames", mb_info.data_ptr(), coeffs.data_ptr(), filter_type, mbw, mbh, n_images, Y.data_ptr(),
+         U.data_ptr(), V.data_ptr(), work.data_ptr(), _stream())
+    return Y, U, V
+
+
+def import_rgba(rgba, has_alpha=True, out=None):
+    """importImage: (n, h, w, 4) uint8 RGBA -> padded (Y, U, V) planes."""
+    assert rgba.is_cuda and rgba.dtype == torch.uint8 and rgba.dim() == 4 and rgba.is_contiguous()
+    n, h, w, _ = rgba.shape
+    mbw, mbh = mb_dims(w, h)
+    if out is None:
+        Y = torch.empty((n, 16 * mbh, 16 * mbw), dtype=torch.uint8, device=rgba.device)
+        U = torch.empty((n, 8 * mbh, 8 * mbw), dtype=torch.uint8, device=rgba.device)
+        V = torch.empty_like(U)
+    else:
+        Y, U, V = out
+    call("wg_import_rgba", rgba.data_ptr(), w, h, 4 * w, 4 * w * h, int(bool(has_alpha)), Y.data_ptr(), U.data_ptr(),
+         V.data_ptr(), Y[0].numel(), U[0].numel(), n, _stream())
+    return Y, U, V
+
+
+def analysis_alphas(Y, U, V, w, h, parts=False, out=None):
+    """computeAlphas: per-MB mixed alpha (n, mbh*mbw) int32 and the UV alpha average per image."""
+    n = Y.shape[0]
+    mbw, mbh = mb_dims(w, h)
+    dev = Y.device
+    if out is None:
+        alphas = torch.empty((n, mbw * mbh), dtype=torch.int32, device=dev)
+        uv_sum = torch.empty((n,), dtype=torch.int32, device=dev)
+        lum = torch.empty_like(alphas) if parts else None
+        uva = torch.empty_like(alphas) if parts else None
+    else:
+        alphas, uv_sum, lum, uva = out
+    call("wg_analysis_alphas", Y.data_ptr(), U.data_ptr(), V.data_ptr(), w, h, Y[0].numel(), U[0].numel(), n,
+         alphas.data_ptr(), lum.data_ptr() if lum is not None else None,
+         uva.data_ptr() if uva is not None else None, uv_sum.data_ptr(), _stream())
+    if parts:
+        return alphas, uv_sum, lum, uva
+    return alphas, uv_sum
+
+
+def build_nrgba(Y, U, V, w, h, alpha=None, out=None):
+    """buildNRGBA (webp.go:379): (n, H, Ws) planes -> (n, h, w, 4) NRGBA."""
+    n = Y.shape[0]
+    if out is None:
+        out = torch.empty((n, h, w, 4), dtype=torch.uint8, device=Y.device)
+    a_ptr, a_pitch = (None, 0) if alpha is None else (alpha.data_ptr(), alpha[0].numel())
+    call("wg_upsample_nrgba", Y.data_ptr(), Y.shape[-1], Y[0].numel(), U.data_ptr(), V.data_ptr(), U.shape[-1],
+         U[0].numel(), a_ptr, a_pitch, w, h, out.data_ptr(), out[0].numel(), n, _stream())
+    return out
+
+
+def plane_ssim(a, b, work=None):
+    """Sum of per-pixel clipped-window SSIM for each image pair; (n,) float64."""
+    n, h, w = a.shape
+    if work is None:
+        work = torch.empty(lib.wg_plane_ssim_work_bytes(w, h, n), dtype=torch.uint8, device=a.device)
+    out = torch.empty((n,), dtype=torch.float64, device=a.device)
+    call("wg_plane_ssim", a.data_ptr(), a.shape[-1], a[0].numel(), b.data_ptr(), b.shape[-1], b[0].numel(), w, h, n,
+         out.data_ptr(), work.data_ptr(), _stream())
+    return out
