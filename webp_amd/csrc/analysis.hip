@@ -83,9 +83,10 @@ __global__ __launch_bounds__(TPB) void k_analysis(const AnArgs a, int64_t total)
       tl = top_row[x0 - 1];
     }
     for (int by = 0; by < 4; by++) {
-      int left4[4];
+      int left4[4] = {128, 128, 128, 128};  // only read when mbx > 0 (TM mode)
+      if (mode == 1)
 #pragma unroll
-      for (int r = 0; r < 4; r++) left4[r] = Y[(int64_t)min(y0 + 4 * by + r, a.h - 1) * ys + x0 - 1];
+        for (int r = 0; r < 4; r++) left4[r] = Y[(int64_t)min(y0 + 4 * by + r, a.h - 1) * ys + x0 - 1];
       for (int bx = 0; bx < 4; bx++) {
         uint32_t top4 = 0;
         if (mode == 1) {

@@ -41,12 +41,12 @@ constexpr int FC_STRIDE = 16, FC_X0 = 8;
 constexpr int TOP_BYTES = 32;   // per MB column: Y16 U8 V8
 constexpr int LEFT_BYTES = 64;  // per MB row: Ycol16 Ucol8 Vcol8 tlY tlU tlV
 
-__device__ __forceinline__ int check_mode(int mbx, int mby, int mode) {  // decode_frame.go:6-19
-  if (mode == 0) {
-    if (mbx == 0) return mby == 0 ? 6 : 5;
-    if (mby == 0) return 4;
-  }
-  return mode;
+// checkMode (decode_frame.go:6-19).  Written as one select chain: the
+// early-return form was miscompiled by hipcc (ROCm 7.2, -O3) -- the NoTop
+// constant overwrote the register holding `mode` on the mbx>0 && mby>0 path.
+__device__ __forceinline__ int check_mode(int mbx, int mby, int mode) {
+  const int edge = (mbx == 0) ? ((mby == 0) ? 6 : 5) : ((mby == 0) ? 4 : 0);
+  return mode == 0 ? edge : mode;
 }
 
 struct DecArgs {

@@ -55,11 +55,41 @@ __device__ __forceinline__ int clip_uv(int uv) {  // VP8ClipUV :138 with roundin
   return (uv & ~0xff) == 0 ? uv : (uv < 0 ? 0 : 255);
 }
 
+// One 2x2 quad: gamma-correct (alpha-weighted when 0 < sum(A) < 1020) average
+// of R, G, B, then RGBToU / RGBToV on the sum-of-4 values.  Returns u | v << 8.
+__device__ __forceinline__ uint32_t quad_uv(const uint32_t* tl, const uint32_t* tg, uint32_t p0, uint32_t p1,
+                                         uint32_t p2, uint32_t p3, int has_alpha) {
+  const uint32_t a0 = has_alpha ? p0 >> 24 : 255u, a1 = has_alpha ? p1 >> 24 : 255u;
+  const uint32_t a2 = has_alpha ? p2 >> 24 : 255u, a3 = has_alpha ? p3 >> 24 : 255u;
+  const uint32_t ta = a0 + a1 + a2 + a3;
+  const bool plain = (ta == 4 * 255) || (ta == 0);
+  const uint32_t inv = plain ? 0u : (1u << 19) / ta;  // kInvAlpha[ta], yuv.go:343-447
+  int c3[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    const int sh = 8 * c;
+    const uint32_t l0 = tl[(p0 >> sh) & 0xff], l1 = tl[(p1 >> sh) & 0xff];
+    const uint32_t l2 = tl[(p2 >> sh) & 0xff], l3 = tl[(p3 >> sh) & 0xff];
+    const uint32_t sum = plain ? l0 + l1 + l2 + l3 : ((a0 * l0 + a1 * l1 + a2 * l2 + a3 * l3) * inv) >> 17;
+    c3[c] = lin_to_gamma(tg, sum, 0);
+  }
+  int u = clip_uv(-9719 * c3[0] - 19081 * c3[1] + 28800 * c3[2]);
+  int v = clip_uv(28800 * c3[0] - 24116 * c3[1] - 4684 * c3[2]);
+  // Keep the two clamps separate: hipcc (ROCm 7.2) otherwise fuses
+  // "sat_u8(x>>18) | sat_u8(y>>18)<<8" into v_ashr_pk_u8_i32 and then assumes
+  // the upper 16 bits of that result are zero, which the hardware does not
+  // guarantee -- V picked up stray bits.  (Found by the parity tests.)
+  asm volatile("" : "+v"(u));
+  asm volatile("" : "+v"(v));
+  return (uint32_t)u | ((uint32_t)v << 8);
+}
+
 struct ImportArgs {
   const uint8_t* rgba;
   uint8_t *y, *u, *v;
   int64_t rgba_pitch, y_pitch, uv_pitch;
   int w, h, stride, has_alpha, padw, padh, groups;  // groups = padw / 8
+  int aligned;  // rows start 16-byte aligned -> 2 x 16 B loads per row
   GammaTabs tabs;
 };
 
@@ -80,11 +110,12 @@ __global__ __launch_bounds__(256) void k_import(const ImportArgs a, int64_t tota
 
   // gather 2 rows x 8 pixels (clamped to the real image)
   uint32_t px[2][8];
+  const bool fast = a.aligned && x0 + 8 <= a.w;  // same path for both rows
 #pragma unroll
   for (int r = 0; r < 2; r++) {
     const int sy = min(2 * yp + r, a.h - 1);
     const uint8_t* row = src + (int64_t)sy * a.stride;
-    if (x0 + 8 <= a.w && ((reinterpret_cast<uintptr_t>(row + 4 * x0) & 15) == 0)) {
+    if (fast) {
       const uint4 q0 = *reinterpret_cast<const uint4*>(row + 4 * x0);
       const uint4 q1 = *reinterpret_cast<const uint4*>(row + 4 * x0 + 16);
       px[r][0] = q0.x; px[r][1] = q0.y; px[r][2] = q0.z; px[r][3] = q0.w;
@@ -108,34 +139,12 @@ __global__ __launch_bounds__(256) void k_import(const ImportArgs a, int64_t tota
     *reinterpret_cast<uint2*>(a.y + img * a.y_pitch + (int64_t)(2 * yp + r) * a.padw + x0) = make_uint2(lo, hi);
   }
   // U/V: AccumulateRGBA (yuv.go:486-517) + ConvertRGBA32ToUV (:553-562)
-  uint32_t uo = 0, vo = 0;
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint32_t p[4] = {px[0][2 * q], px[0][2 * q + 1], px[1][2 * q], px[1][2 * q + 1]};
-    uint32_t al[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) al[k] = a.has_alpha ? (p[k] >> 24) : 255u;
-    const uint32_t ta = al[0] + al[1] + al[2] + al[3];
-    int c3[3];
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-      const int sh = 8 * c;
-      if (ta == 4 * 255 || ta == 0) {
-        const uint32_t s = tl[(p[0] >> sh) & 0xff] + tl[(p[1] >> sh) & 0xff] + tl[(p[2] >> sh) & 0xff] +
-                           tl[(p[3] >> sh) & 0xff];
-        c3[c] = lin_to_gamma(tg, s, 0);
-      } else {  // LinearToGammaWeighted :466 with kInvAlpha[a] = floor(2^19 / a)
-        uint32_t s = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) s += al[k] * tl[(p[k] >> sh) & 0xff];
-        c3[c] = lin_to_gamma(tg, (s * ((1u << 19) / ta)) >> 17, 0);
-      }
-    }
-    const int uu = clip_uv(-9719 * c3[0] - 19081 * c3[1] + 28800 * c3[2]);
-    const int vv = clip_uv(28800 * c3[0] - 24116 * c3[1] - 4684 * c3[2]);
-    uo |= (uint32_t)uu << (8 * q);
-    vo |= (uint32_t)vv << (8 * q);
-  }
+  const uint32_t uv0 = quad_uv(tl, tg, px[0][0], px[0][1], px[1][0], px[1][1], a.has_alpha);
+  const uint32_t uv1 = quad_uv(tl, tg, px[0][2], px[0][3], px[1][2], px[1][3], a.has_alpha);
+  const uint32_t uv2 = quad_uv(tl, tg, px[0][4], px[0][5], px[1][4], px[1][5], a.has_alpha);
+  const uint32_t uv3 = quad_uv(tl, tg, px[0][6], px[0][7], px[1][6], px[1][7], a.has_alpha);
+  const uint32_t uo = (uv0 & 0xff) | ((uv1 & 0xff) << 8) | ((uv2 & 0xff) << 16) | ((uv3 & 0xff) << 24);
+  const uint32_t vo = (uv0 >> 8) | ((uv1 >> 8) << 8) | ((uv2 >> 8) << 16) | ((uv3 >> 8) << 24);
   const int64_t co = img * a.uv_pitch + (int64_t)yp * (a.padw / 2) + x0 / 2;
   *reinterpret_cast<uint32_t*>(a.u + co) = uo;
   *reinterpret_cast<uint32_t*>(a.v + co) = vo;
@@ -169,6 +178,7 @@ extern "C" int wg_import_rgba(const uint8_t* rgba, int32_t w, int32_t h, int32_t
   a.padh = 16 * mbh;
   a.groups = a.padw / 8;
   a.tabs = host_tabs();
+  a.aligned = ((reinterpret_cast<uintptr_t>(rgba) | (uintptr_t)stride | (uintptr_t)rgba_pitch) & 15) == 0;
   const int64_t total = (int64_t)n_images * (a.padh / 2) * a.groups;
   hipLaunchKernelGGL(k_import, dim3(wg::blocks_for(total, 256)), dim3(256), 0, wg::as_stream(stream), a, total);
   return wg::check_launch("k_import");
