@@ -131,6 +131,11 @@ size_t wg_decode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images);
 int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int32_t filter_type, int32_t mbw, int32_t mbh,
                      int32_t n_images, uint8_t* y, uint8_t* u, uint8_t* v, void* work, void* stream);
 
+/* After wg_decode_frames on the same stream: WG_OK, or WG_EHIP if a row
+ * dependency wait timed out inside the kernel (output invalid).  Synchronises
+ * the stream. */
+int wg_decode_status(const void* work, int32_t mbw, int32_t n_images, void* stream);
+
 /* RGBA -> YUV420 import: replaces VP8Encoder.importImage
  * (internal/lossy/encode.go:671-943, non-dithered path).  rgba: w x h, row
  * pitch `stride`, image pitch rgba_pitch.  Outputs padded planes (Y stride

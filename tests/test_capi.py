@@ -46,7 +46,7 @@ def test_invalid_arguments_are_rejected_without_gpu():
 
 def test_work_size_helpers():
     from webp_amd import _lib
-    assert _lib.lib.wg_decode_work_bytes(120, 68, 2) == 2 * (120 * 32 + 68 * 64)
+    assert _lib.lib.wg_decode_work_bytes(120, 68, 2) == 2 * 120 * 32 + 4 * (2 * 68 + 4)
     assert _lib.lib.wg_decode_work_bytes(0, 68, 2) == 0
     assert _lib.lib.wg_plane_ssim_work_bytes(33, 17, 1) == 8 * 3 * 2
 

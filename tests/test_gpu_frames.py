@@ -33,7 +33,7 @@ def host(t):
 
 def run_decode(mbw, mbh, n_img, filter_type, seed, **kw):
     mb, co = synth.random_macroblocks(n_img * mbw * mbh, seed=seed, **kw)
-    Y, U, V = frames.decode_frames(frames.mb_info_tensor(mb), dev(co), filter_type, mbw, mbh, n_img)
+    Y, U, V = frames.decode_frames(frames.mb_info_tensor(mb), dev(co), filter_type, mbw, mbh, n_img, check=True)
     Y, U, V = host(Y), host(U), host(V)
     per = mbw * mbh
     for i in range(n_img):

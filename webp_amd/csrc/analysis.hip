@@ -48,8 +48,9 @@ __global__ __launch_bounds__(TPB) void k_analysis(const AnArgs a, int64_t total)
   __shared__ uint32_t bins_all[32 * TPB];
   uint32_t* bins = bins_all + threadIdx.x;
   for (int k = 0; k < 32; k++) bins[k * TPB] = 0;
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= total) return;
+  const int64_t tid_raw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = tid_raw < total;  // no early exit: the uv_sum reduction below is wave-wide
+  const int64_t tid = valid ? tid_raw : total - 1;
   const int mbs = a.mbw * a.mbh;
   const int img = (int)(tid / mbs);
   const int idx = (int)(tid % mbs);
@@ -161,10 +162,24 @@ __global__ __launch_bounds__(TPB) void k_analysis(const AnArgs a, int64_t total)
   int mixed = 255 - ((3 * lum + uva + 2) >> 2);
   mixed = min(max(mixed, 0), 255);
   const int64_t o = (int64_t)img * mbs + idx;
-  a.alphas[o] = mixed;
-  if (a.lum) a.lum[o] = lum;
-  if (a.uva) a.uva[o] = uva;
-  if (a.uv_sum) atomicAdd(&a.uv_sum[img], uva);
+  if (valid) {
+    a.alphas[o] = mixed;
+    if (a.lum) a.lum[o] = lum;
+    if (a.uva) a.uva[o] = uva;
+  }
+  if (a.uv_sum) {
+    // one atomic per (wave, image) instead of one per macroblock: the per-MB
+    // form serialised ~8k atomics on each image's counter.
+    const int img0 = __shfl(img, 0, 64);
+    const bool uniform = __all(img == img0);
+    if (uniform) {
+      int s = valid ? uva : 0;
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+      if ((threadIdx.x & 63) == 0) atomicAdd(&a.uv_sum[img], s);
+    } else if (valid) {
+      atomicAdd(&a.uv_sum[img], uva);
+    }
+  }
 }
 
 }  // namespace

@@ -2,22 +2,26 @@
 // gfx950 (replaces reconstructRow / filterRowAt of parseFrame,
 // internal/lossy/decode.go:532-560 and decode_frame.go:83-342).
 //
-// Schedule.  Macroblock (x, y) needs the *unfiltered* reconstruction of
-// (x-1, y), (x-1..x+1, y-1) for intra prediction, and its loop filter needs
-// (x-1, y), (x, y-1), (x+1, y-1) already filtered (their edge filters write
-// 3 pixels into it).  Both dependencies are satisfied by the anti-diagonal
-// order t = x + 2y, so one launch per t processes every MB on that diagonal
-// of every image in the batch: reconstruct, then filter, in the same wave.
-// Unfiltered context travels through two small side buffers (the GPU form of
-// the decoder's yuvT / left-sample rotation, decode_frame.go:118-126,190):
-//   top[img][mbx]  : bottom row of the MB above   (Y16 U8 V8)
-//   left[img][mby] : right column of the MB to the left + its top-left pixels
+// Schedule: one persistent launch per batch.  Each 64-lane workgroup
+// dequeues a macroblock ROW (ordered counter, row-major over y then image)
+// and walks it left to right, exactly like the reference's serial row loop,
+// keeping the left context (the decoder's yuvB rotation,
+// decode_frame.go:118-126) in LDS.  Row y may process MB x once row y-1 has
+// completed MB x+1: that covers intra prediction (top / top-right from the
+// unfiltered MB above) and the loop filter (the MB above and above-right
+// already filtered, since their edge filters write 3 pixels into row y-1's
+// bottom rows).  Because rows are dequeued in order, a row only ever waits
+// on rows owned by already-running workgroups: no deadlock for any grid
+// size, and every wait is bounded (a timeout sets an error flag).
 //
-// One 64-lane wave per macroblock.  Luma lanes: block b = lane/4 (raster),
-// row r = lane%4, 4 pixels per lane.  Chroma: lanes 0-15 U, 16-31 V.  The MB
-// and its prediction border live in LDS with the reference's BPS=32 stride;
-// the filter works on a 20x20 (Y) / 12x12 (U, V) LDS tile that includes the
-// 4 pixels on the far side of the left and top edges.
+// Cross-workgroup hand-off (MI355X_MICROARCH.md, "Valid forms", sc1 row):
+// every byte another workgroup reads -- the unfiltered top context and all
+// frame pixels -- is stored with sc1 (write-through) stores and loaded with
+// sc1 loads; the producer drains its stores (s_waitcnt vmcnt(0)) before the
+// progress flag store; the consumer polls the flag with sc1 loads.
+//
+// Lane mapping per macroblock: luma block b = lane/4 (raster), row lane%4,
+// 4 pixels per lane; chroma lanes 0-15 U, 16-31 V.
 #include "wg_common.h"
 #include "wg_dsp.h"
 
@@ -25,29 +29,41 @@ namespace {
 
 using namespace wg;
 
-// LDS work-buffer layout (stride WG_BPS).  Origins are 16-byte aligned so
-// whole rows move with one 16-byte access.  The Y top-right pixels at
-// columns 16..19 land in columns 0..3 of the next row, which nothing else
-// uses (the left border is column 15, the V block's left border column 31).
+// LDS work-buffer layout (stride WG_BPS).  Origins are 16-byte aligned.  The Y
+// top-right pixels at columns 16..19 land in columns 0..3 of the next row,
+// which nothing else uses (the left border is column 15, the V block's left
+// border column 31 of the previous row).
 constexpr int LY = 1 * WG_BPS + 16;   // Y origin: row 1, col 16
 constexpr int LU = 19 * WG_BPS + 16;  // U origin: row 19, col 16
-constexpr int LV = 19 * WG_BPS + 0;   // V origin: row 19, col 0 (left border = col 31 of the row above)
+constexpr int LV = 19 * WG_BPS + 0;   // V origin: row 19, col 0
 constexpr int WB_SIZE = 27 * WG_BPS;
 
-// Filter tiles: Y 20 rows x 32 (cols -4..15 at bytes 12..31), UV 12 rows x 16 (cols -4..7 at 4..15)
-constexpr int FY_STRIDE = 32, FY_X0 = 16;
+// Filter tiles: rows -4..15 (Y) / -4..7 (U,V) of the MB, columns -4..15 / -4..7.
+constexpr int FY_STRIDE = 32, FY_X0 = 16;  // Y col c at byte FY_X0 + c
 constexpr int FC_STRIDE = 16, FC_X0 = 8;
 
-constexpr int TOP_BYTES = 32;   // per MB column: Y16 U8 V8
-constexpr int LEFT_BYTES = 64;  // per MB row: Ycol16 Ucol8 Vcol8 tlY tlU tlV
+constexpr int TOP_BYTES = 32;  // per MB column: unfiltered Y16 U8 V8 of the MB above
 
-// checkMode (decode_frame.go:6-19).  Written as one select chain: the
-// early-return form was miscompiled by hipcc (ROCm 7.2, -O3) -- the NoTop
-// constant overwrote the register holding `mode` on the mbx>0 && mby>0 path.
 __device__ __forceinline__ int check_mode(int mbx, int mby, int mode) {
+  // checkMode (decode_frame.go:6-19) as one select chain: the early-return
+  // form was miscompiled by hipcc (ROCm 7.2, -O3; the NoTop constant
+  // overwrote `mode` on the mbx>0 && mby>0 path).
   const int edge = (mbx == 0) ? ((mby == 0) ? 6 : 5) : ((mby == 0) ? 4 : 0);
   return mode == 0 ? edge : mode;
 }
+
+// sc1 (agent-coherent, L1-bypassing, write-through) accesses for hand-off data.
+__device__ __forceinline__ uint64_t ld_sc1_64(const uint8_t* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_64(uint8_t* p, uint64_t v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_32(uint8_t* p, uint32_t v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lds64(const uint8_t* p) { return *reinterpret_cast<const uint64_t*>(p); }
+__device__ __forceinline__ uint32_t lds32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 
 struct DecArgs {
   const wg_mb_info* mb;
@@ -55,260 +71,342 @@ struct DecArgs {
   uint8_t* Y;
   uint8_t* U;
   uint8_t* V;
-  uint8_t* top;
-  uint8_t* left;
-  int filter_type, mbw, mbh;
+  uint8_t* top;   // [n_img][mbw][TOP_BYTES]
+  int* progress;  // [n_img][mbh]: macroblocks completed (reconstructed + filtered + stored)
+  int* ctl;       // [0] row dequeue counter, [1] error flag (wait timeout)
+  int filter_type, mbw, mbh, n_img;
 };
 
-__global__ __launch_bounds__(64) void k_decode_diag(DecArgs a, int t, int x_lo, int count) {
+#ifdef WG_STAMPS
+// Diagnostic build only: cycles spent per phase, summed over all macroblocks.
+__device__ unsigned long long g_phase[16];
+#define STAMP_DECL unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0
+#define STAMP(k)                                                                   \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long ts_;                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");  \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    if ((k) > 0) st_acc[(k)-1] += ts_ - st_prev;                                   \
+    st_prev = ts_;                                                                 \
+  } while (0)
+#define STAMP_FLUSH()                                                          \
+  do {                                                                         \
+    if (lane == 0)                                                             \
+      for (int k_ = 0; k_ < 10; k_++) atomicAdd(&g_phase[k_], st_acc[k_]);     \
+  } while (0)
+#else
+#define STAMP_DECL int st_unused_ = 0
+#define STAMP(k) (void)st_unused_
+#define STAMP_FLUSH() (void)st_unused_
+#endif
+
+constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of the 100 MHz s_memrealtime clock per wait
+
+__global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t wb[WB_SIZE];
+  __shared__ __attribute__((aligned(16))) int16_t cof[384];
   __shared__ __attribute__((aligned(16))) uint8_t fy[20 * FY_STRIDE];
   __shared__ __attribute__((aligned(16))) uint8_t fu[12 * FC_STRIDE];
   __shared__ __attribute__((aligned(16))) uint8_t fv[12 * FC_STRIDE];
+  __shared__ int sh_word;
 
   const int lane = threadIdx.x;
-  const int img = blockIdx.x / count;
-  const int mbx = x_lo + 2 * (blockIdx.x % count);
-  const int mby = (t - mbx) >> 1;
   const int mbw = a.mbw, mbh = a.mbh;
-  const int64_t mbi = (int64_t)img * mbw * mbh + (int64_t)mby * mbw + mbx;
-  const wg_mb_info info = a.mb[mbi];
-  const int16_t* co = a.coeffs + mbi * 384;
-  uint8_t* top = a.top + (int64_t)img * mbw * TOP_BYTES;
-  uint8_t* left = a.left + ((int64_t)img * mbh + mby) * LEFT_BYTES;
+  const int total_rows = a.n_img * mbh;
   const int ys = 16 * mbw, uvs = 8 * mbw;
-  uint8_t* Yp = a.Y + (int64_t)img * ys * 16 * mbh;
-  uint8_t* Up = a.U + (int64_t)img * uvs * 8 * mbh;
-  uint8_t* Vp = a.V + (int64_t)img * uvs * 8 * mbh;
+  const bool luma_only = a.filter_type == 1;
+  STAMP_DECL;
 
-  // ---- 1. prediction context (decode_frame.go:93-160) ----
-  {
-    const uint8_t* tc = top + mbx * TOP_BYTES;
-    int v;
-    if (lane < 16) {  // Y top row
-      v = mby > 0 ? tc[lane] : 127;
-      wb[LY - WG_BPS + lane] = v;
-    } else if (lane < 20) {  // Y top-right (cols 16..19)
-      if (mby == 0) v = 127;
-      else if (mbx < mbw - 1) v = tc[TOP_BYTES + lane - 16];
-      else v = tc[15];
-      wb[LY - WG_BPS + lane] = v;
-    } else if (lane < 23) {  // top-left of Y, U, V
-      const int pl = lane - 20;
-      v = mby == 0 ? 127 : (mbx == 0 ? 129 : left[48 + pl]);
-      const int o = pl == 0 ? LY : (pl == 1 ? LU : LV);
-      wb[o - WG_BPS - 1] = v;
-    } else if (lane >= 24 && lane < 40) {  // U / V top row
-      const int pl = (lane - 24) >> 3, i = (lane - 24) & 7;
-      v = mby > 0 ? tc[16 + 8 * pl + i] : 127;
-      wb[(pl ? LV : LU) - WG_BPS + i] = v;
-    } else if (lane >= 40 && lane < 56) {  // Y left column
-      const int j = lane - 40;
-      wb[LY - 1 + j * WG_BPS] = mbx > 0 ? left[j] : 129;
-    } else if (lane >= 56) {  // U left column
-      const int j = lane - 56;
-      wb[LU - 1 + j * WG_BPS] = mbx > 0 ? left[16 + j] : 129;
-    }
-    if (lane < 8) wb[LV - 1 + lane * WG_BPS] = mbx > 0 ? left[24 + lane] : 129;
-  }
-  __syncthreads();
-  if (info.is_i4x4 && lane < 12) {  // replicate top-right down to rows 3, 7, 11 (:155-160)
-    const int r = 4 * (lane / 4 + 1) - 1, i = lane & 3;
-    wb[LY + r * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
-  }
-  __syncthreads();
+  for (;;) {
+    if (lane == 0) sh_word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int row = __builtin_amdgcn_readfirstlane(sh_word);
+    __syncthreads();
+    if (row >= total_rows) break;
+    const int mby = row / a.n_img, img = row % a.n_img;
+    uint8_t* top = a.top + (int64_t)img * mbw * TOP_BYTES;
+    int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
+    int* prog_mine = a.progress + (int64_t)img * mbh + mby;
+    uint8_t* Yp = a.Y + (int64_t)img * ys * 16 * mbh;
+    uint8_t* Up = a.U + (int64_t)img * uvs * 8 * mbh;
+    uint8_t* Vp = a.V + (int64_t)img * uvs * 8 * mbh;
 
-  // ---- 2. luma prediction + residual ----
-  {
-    const int blk = lane >> 2, r = lane & 3, bx = blk & 3, by = blk >> 2;
-    const int off = LY + (4 * by + r) * WG_BPS + 4 * bx;
-    const int code = (info.non_zero_y >> (30 - 2 * blk)) & 3;
-    const int16_t* bco = co + blk * 16;
-    if (!info.is_i4x4) {
-      const int mode = check_mode(mbx, mby, info.imodes[0]);
-      const int dc = predsq_dc(mode, wb + LY, 16);
-      const uint32_t pred = predsq_row4(mode, wb + LY, 4 * bx, 4 * by + r, dc);
-      int res[4];
-      dec_residual_row(bco, code, r, res);
-      *reinterpret_cast<uint32_t*>(wb + off) =
-          pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
-                clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
-    } else {
-      const int my_step = bx + 2 * by;  // in-MB dependency wavefront
-      int res[4];
-      dec_residual_row(bco, code, r, res);
-      const int mode = info.imodes[blk];
-      for (int s = 0; s < 10; s++) {
-        if (s == my_step) {
-          int X, T[8], L[4];
-          pred4_ctx(wb, LY + 4 * by * WG_BPS + 4 * bx, X, T, L);
-          const uint32_t pred = pred4_row(mode, r, X, T, L);
+    // row start: left border 129, top-left 129 (127 on the first row) -- decode_frame.go:93-110
+    if (lane < 16) wb[LY - 1 + lane * WG_BPS] = 129;
+    else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = 129;
+    else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = 129;
+    else if (lane < 35) wb[(lane == 32 ? LY : lane == 33 ? LU : LV) - WG_BPS - 1] = mby > 0 ? 129 : 127;
+    int seen = 0;  // progress of the row above observed so far
+
+    for (int mbx = 0; mbx < mbw; mbx++) {
+      const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
+      STAMP(0);
+      // ---- dependency on the row above ----
+      if (mby > 0) {
+        const int need = min(mbx + 2, mbw);
+        if (seen < need) {
+          int v = 0;
+          if (lane == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t it = 0;; it++) {
+              v = __hip_atomic_load(prog_above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (v >= need) break;
+              // never hang the GPU: after SPIN_TICKS (or once any row has timed out)
+              // flag the error and carry on with whatever is in memory
+              if ((it & 63) == 63 &&
+                  (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+                   __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+                __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v = mbw;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(2);
+            }
+          }
+          seen = __shfl(v, 0, 64);
+        }
+      }
+      STAMP(1);
+      // ---- loads: macroblock info (scalar), coefficients -> LDS, top context, filter rows above ----
+      const wg_mb_info* ip = a.mb + mbi;
+      const uint32_t nz_y = ip->non_zero_y, nz_uv = ip->non_zero_uv;
+      const uint32_t im0 = reinterpret_cast<const uint32_t*>(ip->imodes)[0];
+      const int is_i4 = ip->is_i4x4, uv_mode = ip->uv_mode;
+      const int f_limit = ip->f_limit, ilevel = ip->f_ilevel, f_inner = ip->f_inner, hev_t = ip->hev_thresh;
+      if (lane < 48)
+        reinterpret_cast<int4*>(cof)[lane] = reinterpret_cast<const int4*>(a.coeffs + mbi * 384)[lane];
+      // rotate the filter tile: the left MB's final columns 12..15 become columns -4..-1
+      if (mbx > 0) {
+        if (lane < 16) {
+          uint8_t* r = fy + (lane + 4) * FY_STRIDE + FY_X0;
+          *reinterpret_cast<uint32_t*>(r - 4) = lds32(r + 12);
+        } else if (lane < 32) {
+          const int j = (lane - 16) & 7;
+          uint8_t* r = ((lane < 24) ? fu : fv) + (j + 4) * FC_STRIDE + FC_X0;
+          *reinterpret_cast<uint32_t*>(r - 4) = lds32(r + 4);
+        }
+      }
+      if (mby > 0) {
+        const uint8_t* tc = top + mbx * TOP_BYTES;
+        if (lane >= 48 && lane < 52) {  // unfiltered top context Y16 U8 V8
+          const uint64_t w = ld_sc1_64(tc + 8 * (lane - 48));
+          const int k = lane - 48;
+          uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
+          *reinterpret_cast<uint64_t*>(dst) = w;
+        } else if (lane >= 52 && lane < 60) {  // filtered frame rows 16y-4..16y-1 (Y)
+          const int k = lane - 52, rr = k >> 1, half = k & 1;
+          const uint64_t w = ld_sc1_64(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half);
+          *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = w;
+        } else if (lane >= 60) {  // U rows 8y-4..8y-1
+          const int rr = lane - 60;
+          *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) =
+              ld_sc1_64(Up + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
+        } else if (lane >= 44) {  // V rows (lanes 44..47)
+          const int rr = lane - 44;
+          *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) =
+              ld_sc1_64(Vp + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
+        }
+        if (is_i4 && lane == 0) {  // top-right: next MB's top context, or replicate top[15] at the right edge
+          uint32_t tr;
+          if (mbx < mbw - 1) tr = (uint32_t)ld_sc1_64(tc + TOP_BYTES);
+          else tr = 0x01010101u * (uint32_t)(ld_sc1_64(tc + 8) >> 56);
+          *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
+        }
+      } else {  // first row: everything above is 127 (decode_frame.go:104-108)
+        if (lane < 21) wb[LY - WG_BPS + lane - 1] = 127;
+        else if (lane < 30) wb[LU - WG_BPS + lane - 22] = 127;
+        else if (lane < 39) wb[LV - WG_BPS + lane - 31] = 127;
+      }
+      __syncthreads();
+      if (is_i4 && lane < 12) {  // replicate top-right down to rows 3, 7, 11 (:155-160)
+        const int r = 4 * (lane / 4 + 1) - 1, i = lane & 3;
+        wb[LY + r * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
+      }
+      __syncthreads();
+
+      STAMP(2);
+      // ---- luma prediction + residual ----
+      {
+        const int blk = lane >> 2, r = lane & 3, bx = blk & 3, by = blk >> 2;
+        const int off = LY + (4 * by + r) * WG_BPS + 4 * bx;
+        const int code = (nz_y >> (30 - 2 * blk)) & 3;
+        int res[4];
+        dec_residual_row(cof + blk * 16, code, r, res);
+        if (!is_i4) {
+          const int mode = check_mode(mbx, mby, im0 & 0xff);
+          const int dc = predsq_dc(mode, wb + LY, 16);
+          const uint32_t pred = predsq_row4(mode, wb + LY, 4 * bx, 4 * by + r, dc);
           *reinterpret_cast<uint32_t*>(wb + off) =
               pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
                     clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+        } else {
+          const int my_step = bx + 2 * by;  // in-MB dependency wavefront
+          const int mode = reinterpret_cast<const uint8_t*>(ip->imodes)[blk];
+          for (int s = 0; s < 10; s++) {
+            if (s == my_step) {
+              int X, T[8], L[4];
+              pred4_ctx(wb, LY + 4 * by * WG_BPS + 4 * bx, X, T, L);
+              const uint32_t pred = pred4_row(mode, r, X, T, L);
+              *reinterpret_cast<uint32_t*>(wb + off) =
+                  pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
+                        clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+            }
+            __syncthreads();
+          }
+        }
+      }
+      STAMP(3);
+      // ---- chroma prediction + residual (doUVTransform :47-68) ----
+      if (lane < 32) {
+        const int pl = lane >> 4, cblk = (lane >> 2) & 3, r = lane & 3;
+        const int cbx = cblk & 1, cby = cblk >> 1;
+        const int base = pl ? LV : LU;
+        const int mode = check_mode(mbx, mby, uv_mode);
+        const int dc = predsq_dc(mode, wb + base, 8);
+        const uint32_t pred = predsq_row4(mode, wb + base, 4 * cbx, 4 * cby + r, dc);
+        const uint32_t bits = nz_uv >> (8 * pl);
+        const int16_t* bco = cof + (16 + 4 * pl + cblk) * 16;
+        int res[4] = {0, 0, 0, 0};
+        if (bits & 0xff) {
+          if (bits & 0xaa) dec_residual_row(bco, 3, r, res);
+          else if (bco[0] != 0) dec_residual_row(bco, 1, r, res);
+        }
+        *reinterpret_cast<uint32_t*>(wb + base + (4 * cby + r) * WG_BPS + 4 * cbx) =
+            pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
+                  clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+      }
+      __syncthreads();
+
+      STAMP(4);
+      // ---- unfiltered top context for the row below (:190-194) + MB into the filter tiles ----
+      if (mby < mbh - 1 && lane >= 32 && lane < 36) {
+        const int k = lane - 32;
+        const uint8_t* src =
+            k < 2 ? wb + LY + 15 * WG_BPS + 8 * k : (k == 2 ? wb + LU + 7 * WG_BPS : wb + LV + 7 * WG_BPS);
+        st_sc1_64(top + mbx * TOP_BYTES + 8 * k, lds64(src));
+      }
+      if (lane < 16) {
+        *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) =
+            *reinterpret_cast<const uint4*>(wb + LY + lane * WG_BPS);
+      } else if (lane < 32) {
+        const int pl = lane >= 24, j = (lane - 16) & 7;
+        *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0) =
+            lds64(wb + (pl ? LV : LU) + j * WG_BPS);
+      }
+      __syncthreads();
+
+      STAMP(5);
+      // ---- loop filter (doFilter :293-342): H edges (left MB edge, inner x=4,8,12), then V edges ----
+      const bool do_filter = a.filter_type > 0 && f_limit > 0;
+      const bool inner = f_inner != 0;
+      if (do_filter) {
+        if (lane < 16) {
+          uint8_t* rowp = fy + (lane + 4) * FY_STRIDE + FY_X0;
+          if (luma_only) {
+            if (mbx > 0) f_simple(rowp, 0, 1, f_limit + 4);
+            if (inner)
+              for (int e = 4; e < 16; e += 4) f_simple(rowp, e, 1, f_limit);
+          } else {
+            if (mbx > 0) f_complex(rowp, 0, 1, f_limit + 4, ilevel, hev_t, false);
+            if (inner)
+              for (int e = 4; e < 16; e += 4) f_complex(rowp, e, 1, f_limit, ilevel, hev_t, true);
+          }
+        } else if (!luma_only && lane < 32) {
+          const int pl = lane >= 24, j = (lane - 16) & 7;
+          uint8_t* rowp = (pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0;
+          if (mbx > 0) f_complex(rowp, 0, 1, f_limit + 4, ilevel, hev_t, false);
+          if (inner) f_complex(rowp, 4, 1, f_limit, ilevel, hev_t, true);
+        }
+        __syncthreads();
+        if (lane < 16) {
+          uint8_t* col = fy + 4 * FY_STRIDE + FY_X0 + lane;
+          if (luma_only) {
+            if (mby > 0) f_simple(col, 0, FY_STRIDE, f_limit + 4);
+            if (inner)
+              for (int e = 4; e < 16; e += 4) f_simple(col, e * FY_STRIDE, FY_STRIDE, f_limit);
+          } else {
+            if (mby > 0) f_complex(col, 0, FY_STRIDE, f_limit + 4, ilevel, hev_t, false);
+            if (inner)
+              for (int e = 4; e < 16; e += 4)
+                f_complex(col, e * FY_STRIDE, FY_STRIDE, f_limit, ilevel, hev_t, true);
+          }
+        } else if (!luma_only && lane < 32) {
+          const int pl = lane >= 24, i = (lane - 16) & 7;
+          uint8_t* col = (pl ? fv : fu) + 4 * FC_STRIDE + FC_X0 + i;
+          if (mby > 0) f_complex(col, 0, FC_STRIDE, f_limit + 4, ilevel, hev_t, false);
+          if (inner) f_complex(col, 4 * FC_STRIDE, FC_STRIDE, f_limit, ilevel, hev_t, true);
         }
         __syncthreads();
       }
-    }
-  }
-  // ---- 3. chroma prediction + residual (doUVTransform :47-68) ----
-  if (lane < 32) {
-    const int pl = lane >> 4, cblk = (lane >> 2) & 3, r = lane & 3;
-    const int cbx = cblk & 1, cby = cblk >> 1;
-    const int base = pl ? LV : LU;
-    const int mode = check_mode(mbx, mby, info.uv_mode);
-    const int dc = predsq_dc(mode, wb + base, 8);
-    const uint32_t pred = predsq_row4(mode, wb + base, 4 * cbx, 4 * cby + r, dc);
-    const uint32_t bits = info.non_zero_uv >> (8 * pl);
-    const int16_t* bco = co + (16 + 4 * pl + cblk) * 16;
-    int res[4] = {0, 0, 0, 0};
-    if (bits & 0xff) {
-      if (bits & 0xaa) dec_residual_row(bco, 3, r, res);
-      else if (bco[0] != 0) dec_residual_row(bco, 1, r, res);
-    }
-    *reinterpret_cast<uint32_t*>(wb + base + (4 * cby + r) * WG_BPS + 4 * cbx) =
-        pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
-              clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
-  }
-  __syncthreads();
 
-  // ---- 4. unfiltered context for the neighbours (:190-194 and the rotation :118-126) ----
-  if (mby < mbh - 1) {
-    uint8_t* tc = top + mbx * TOP_BYTES;
-    if (lane == 32) *reinterpret_cast<uint4*>(tc) = *reinterpret_cast<const uint4*>(wb + LY + 15 * WG_BPS);
-    if (lane == 33) *reinterpret_cast<uint2*>(tc + 16) = *reinterpret_cast<const uint2*>(wb + LU + 7 * WG_BPS);
-    if (lane == 34) *reinterpret_cast<uint2*>(tc + 24) = *reinterpret_cast<const uint2*>(wb + LV + 7 * WG_BPS);
-  }
-  if (mbx < mbw - 1) {
-    if (lane >= 40 && lane < 56) left[lane - 40] = wb[LY + (lane - 40) * WG_BPS + 15];
-    if (lane >= 56) left[16 + lane - 56] = wb[LU + (lane - 56) * WG_BPS + 7];
-    if (lane < 8) left[24 + lane] = wb[LV + lane * WG_BPS + 7];
-    if (lane == 8) left[48] = wb[LY - WG_BPS + 15];
-    if (lane == 9) left[49] = wb[LU - WG_BPS + 7];
-    if (lane == 10) left[50] = wb[LV - WG_BPS + 7];
-  }
-
-  const bool do_filter = a.filter_type > 0 && info.f_limit > 0;
-  if (!do_filter) {
-    if (lane < 16)
-      *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby + lane) * ys + 16 * mbx) =
-          *reinterpret_cast<const uint4*>(wb + LY + lane * WG_BPS);
-    else if (lane < 24)
-      *reinterpret_cast<uint2*>(Up + (int64_t)(8 * mby + lane - 16) * uvs + 8 * mbx) =
-          *reinterpret_cast<const uint2*>(wb + LU + (lane - 16) * WG_BPS);
-    else if (lane < 32)
-      *reinterpret_cast<uint2*>(Vp + (int64_t)(8 * mby + lane - 24) * uvs + 8 * mbx) =
-          *reinterpret_cast<const uint2*>(wb + LV + (lane - 24) * WG_BPS);
-    return;
-  }
-
-  // ---- 5. loop filter (doFilter :293-342) on the LDS tiles ----
-  const bool luma_only = a.filter_type == 1;
-  // 5a. load tiles: MB from wb, left 4 columns and top 4 rows from the (already filtered) frame
-  if (lane < 16) {
-    *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) =
-        *reinterpret_cast<const uint4*>(wb + LY + lane * WG_BPS);
-    if (mbx > 0)
-      *reinterpret_cast<uint32_t*>(fy + (lane + 4) * FY_STRIDE + FY_X0 - 4) =
-          *reinterpret_cast<const uint32_t*>(Yp + (int64_t)(16 * mby + lane) * ys + 16 * mbx - 4);
-  } else if (lane < 20) {
-    if (mby > 0)
-      *reinterpret_cast<uint4*>(fy + (lane - 16) * FY_STRIDE + FY_X0) =
-          *reinterpret_cast<const uint4*>(Yp + (int64_t)(16 * mby - 4 + lane - 16) * ys + 16 * mbx);
-  } else if (!luma_only && lane < 44) {
-    // lanes 20..31: U rows -4..7, lanes 32..43: V rows -4..7
-    const int pl = lane >= 32, j = (pl ? lane - 32 : lane - 20) - 4;
-    uint8_t* ft = pl ? fv : fu;
-    uint8_t* P = pl ? Vp : Up;
-    const uint8_t* src = wb + (pl ? LV : LU);
-    if (j >= 0) {
-      *reinterpret_cast<uint2*>(ft + (j + 4) * FC_STRIDE + FC_X0) = *reinterpret_cast<const uint2*>(src + j * WG_BPS);
-      if (mbx > 0)
-        *reinterpret_cast<uint32_t*>(ft + (j + 4) * FC_STRIDE + FC_X0 - 4) =
-            *reinterpret_cast<const uint32_t*>(P + (int64_t)(8 * mby + j) * uvs + 8 * mbx - 4);
-    } else if (mby > 0) {
-      *reinterpret_cast<uint2*>(ft + (j + 4) * FC_STRIDE + FC_X0) =
-          *reinterpret_cast<const uint2*>(P + (int64_t)(8 * mby + j) * uvs + 8 * mbx);
+      STAMP(6);
+      // ---- stores (all sc1: the row below reads them) ----
+      if (lane < 32) {  // Y rows, 2 x 8 B
+        const int j = lane >> 1, half = lane & 1;
+        st_sc1_64(Yp + (int64_t)(16 * mby + j) * ys + 16 * mbx + 8 * half,
+                  lds64(fy + (j + 4) * FY_STRIDE + FY_X0 + 8 * half));
+      } else if (lane < 48) {  // U, V rows
+        const int pl = lane >= 40, j = (lane - 32) & 7;
+        st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx,
+                  lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0));
+      }
+      if (do_filter) {
+        if (mbx > 0) {  // the 3 columns of the left MB modified by our left-edge filter
+          if (lane >= 48) {
+            st_sc1_32(Yp + (int64_t)(16 * mby + lane - 48) * ys + 16 * mbx - 4,
+                      lds32(fy + (lane - 48 + 4) * FY_STRIDE + FY_X0 - 4));
+          } else if (!luma_only && lane < 16) {
+            const int pl = lane >= 8, j = lane & 7;
+            st_sc1_32((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx - 4,
+                      lds32((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 - 4));
+          }
+        }
+        if (mby > 0) {  // the 3 rows of the MB above modified by our top-edge filter
+          if (lane >= 16 && lane < 22) {
+            const int k = lane - 16, rr = 1 + (k >> 1), half = k & 1;
+            st_sc1_64(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half,
+                      lds64(fy + rr * FY_STRIDE + FY_X0 + 8 * half));
+          } else if (!luma_only && lane >= 22 && lane < 28) {
+            const int k = lane - 22, pl = k >= 3, rr = 1 + (k % 3);
+            st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx,
+                      lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0));
+          }
+        }
+      }
+      // ---- rotate the reconstruction context for the next MB (:118-126) ----
+      if (lane < 16) wb[LY - 1 + lane * WG_BPS] = wb[LY + 15 + lane * WG_BPS];
+      else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = wb[LU + 7 + (lane - 16) * WG_BPS];
+      else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = wb[LV + 7 + (lane - 24) * WG_BPS];
+      else if (lane == 32) wb[LY - WG_BPS - 1] = wb[LY - WG_BPS + 15];
+      else if (lane == 33) wb[LU - WG_BPS - 1] = wb[LU - WG_BPS + 7];
+      else if (lane == 34) wb[LV - WG_BPS - 1] = wb[LV - WG_BPS + 7];
+      __syncthreads();
+      STAMP(7);
+      // ---- publish: every store of this MB is complete before the flag ----
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      STAMP(8);
     }
   }
-  __syncthreads();
-
-  const int limit = info.f_limit, ilevel = info.f_ilevel, hev_t = info.hev_thresh;
-  const bool inner = info.f_inner != 0;
-  // 5b. horizontal filtering across vertical edges: left MB edge, then inner edges x = 4, 8, 12
-  if (lane < 16) {
-    uint8_t* row = fy + (lane + 4) * FY_STRIDE + FY_X0;
-    if (luma_only) {
-      if (mbx > 0) f_simple(row, 0, 1, limit + 4);
-      if (inner)
-        for (int e = 4; e < 16; e += 4) f_simple(row, e, 1, limit);
-    } else {
-      if (mbx > 0) f_complex(row, 0, 1, limit + 4, ilevel, hev_t, false);
-      if (inner)
-        for (int e = 4; e < 16; e += 4) f_complex(row, e, 1, limit, ilevel, hev_t, true);
-    }
-  } else if (!luma_only && lane < 32) {
-    const int pl = lane >= 24, j = lane - (pl ? 24 : 16);
-    uint8_t* row = (pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0;
-    if (mbx > 0) f_complex(row, 0, 1, limit + 4, ilevel, hev_t, false);
-    if (inner) f_complex(row, 4, 1, limit, ilevel, hev_t, true);
-  }
-  __syncthreads();
-  // 5c. vertical filtering across horizontal edges: top MB edge, then inner edges y = 4, 8, 12
-  if (lane < 16) {
-    uint8_t* col = fy + 4 * FY_STRIDE + FY_X0 + lane;
-    if (luma_only) {
-      if (mby > 0) f_simple(col, 0, FY_STRIDE, limit + 4);
-      if (inner)
-        for (int e = 4; e < 16; e += 4) f_simple(col, e * FY_STRIDE, FY_STRIDE, limit);
-    } else {
-      if (mby > 0) f_complex(col, 0, FY_STRIDE, limit + 4, ilevel, hev_t, false);
-      if (inner)
-        for (int e = 4; e < 16; e += 4) f_complex(col, e * FY_STRIDE, FY_STRIDE, limit, ilevel, hev_t, true);
-    }
-  } else if (!luma_only && lane < 32) {
-    const int pl = lane >= 24, i = lane - (pl ? 24 : 16);
-    uint8_t* col = (pl ? fv : fu) + 4 * FC_STRIDE + FC_X0 + i;
-    if (mby > 0) f_complex(col, 0, FC_STRIDE, limit + 4, ilevel, hev_t, false);
-    if (inner) f_complex(col, 4 * FC_STRIDE, FC_STRIDE, limit, ilevel, hev_t, true);
-  }
-  __syncthreads();
-
-  // 5d. write back: the MB, the 3 modified columns of the left MB, the 3 modified rows above
-  if (lane < 16) {
-    *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby + lane) * ys + 16 * mbx) =
-        *reinterpret_cast<const uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0);
-    if (mbx > 0)
-      *reinterpret_cast<uint32_t*>(Yp + (int64_t)(16 * mby + lane) * ys + 16 * mbx - 4) =
-          *reinterpret_cast<const uint32_t*>(fy + (lane + 4) * FY_STRIDE + FY_X0 - 4);
-  } else if (lane < 19) {
-    if (mby > 0) {
-      const int j = lane - 16 + 1;  // rows -3..-1
-      *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby - 4 + j) * ys + 16 * mbx) =
-          *reinterpret_cast<const uint4*>(fy + j * FY_STRIDE + FY_X0);
-    }
-  } else if (lane >= 20 && lane < 44) {
-    const int pl = lane >= 32, j = (pl ? lane - 32 : lane - 20) - 4;
-    const uint8_t* ft = pl ? fv : fu;
-    uint8_t* P = pl ? Vp : Up;
-    const uint8_t* src = luma_only ? wb + (pl ? LV : LU) + j * WG_BPS : ft + (j + 4) * FC_STRIDE + FC_X0;
-    if (j >= 0) {
-      *reinterpret_cast<uint2*>(P + (int64_t)(8 * mby + j) * uvs + 8 * mbx) = *reinterpret_cast<const uint2*>(src);
-      if (!luma_only && mbx > 0)
-        *reinterpret_cast<uint32_t*>(P + (int64_t)(8 * mby + j) * uvs + 8 * mbx - 4) =
-            *reinterpret_cast<const uint32_t*>(ft + (j + 4) * FC_STRIDE + FC_X0 - 4);
-    } else if (!luma_only && mby > 0 && j >= -3) {
-      *reinterpret_cast<uint2*>(P + (int64_t)(8 * mby + j) * uvs + 8 * mbx) =
-          *reinterpret_cast<const uint2*>(ft + (j + 4) * FC_STRIDE + FC_X0);
-    }
-  }
+  STAMP_FLUSH();
 }
+
+int g_num_cus = 0;
 
 }  // namespace
 
+#ifdef WG_STAMPS
+extern "C" int wg_debug_phases(unsigned long long* host, int n) {
+  hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n);
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif
+
 extern "C" size_t wg_decode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images) {
   if (mbw <= 0 || mbh <= 0 || n_images <= 0) return 0;
-  return (size_t)n_images * ((size_t)mbw * TOP_BYTES + (size_t)mbh * LEFT_BYTES);
+  return (size_t)n_images * mbw * TOP_BYTES + sizeof(int) * ((size_t)n_images * mbh + 4);
 }
 
 extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int32_t filter_type, int32_t mbw,
@@ -317,8 +415,9 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   WG_REQUIRE(mb && coeffs && y && u && v && work);
   WG_REQUIRE(mbw > 0 && mbh > 0 && n_images > 0);
   WG_REQUIRE(filter_type >= 0 && filter_type <= 2);
-  WG_REQUIRE((reinterpret_cast<uintptr_t>(y) & 15) == 0 && (reinterpret_cast<uintptr_t>(u) & 7) == 0 &&
-             (reinterpret_cast<uintptr_t>(v) & 7) == 0 && (reinterpret_cast<uintptr_t>(coeffs) & 15) == 0);
+  WG_REQUIRE(((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(v)) &
+              7) == 0 &&
+             (reinterpret_cast<uintptr_t>(coeffs) & 15) == 0 && (reinterpret_cast<uintptr_t>(work) & 15) == 0);
   DecArgs a;
   a.mb = mb;
   a.coeffs = coeffs;
@@ -326,19 +425,40 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   a.U = u;
   a.V = v;
   a.top = static_cast<uint8_t*>(work);
-  a.left = a.top + (size_t)n_images * mbw * TOP_BYTES;
+  a.ctl = reinterpret_cast<int*>(a.top + (size_t)n_images * mbw * TOP_BYTES);
+  a.progress = a.ctl + 4;
   a.filter_type = filter_type;
   a.mbw = mbw;
   a.mbh = mbh;
+  a.n_img = n_images;
   hipStream_t s = wg::as_stream(stream);
-  const int T = mbw + 2 * (mbh - 1);
-  for (int t = 0; t < T; t++) {
-    int x_lo = t - 2 * (mbh - 1);
-    if (x_lo < 0) x_lo = (t & 1);  // smallest x >= 0 with x == t (mod 2)
-    const int x_hi = t < mbw - 1 ? t : mbw - 1;
-    if (x_hi < x_lo) continue;
-    const int count = (x_hi - x_lo) / 2 + 1;
-    hipLaunchKernelGGL(k_decode_diag, dim3((unsigned)(count * n_images)), dim3(64), 0, s, a, t, x_lo, count);
+  if (g_num_cus == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      return wg::check_launch("hipDeviceGetAttribute");
+    g_num_cus = cus;
   }
-  return wg::check_launch("k_decode_diag");
+  if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
+    return wg::check_launch("hipMemsetAsync(decode ctl)");
+  const int rows = n_images * mbh;
+  const int grid = rows < 8 * g_num_cus ? rows : 8 * g_num_cus;
+  hipLaunchKernelGGL(k_decode_rows, dim3((unsigned)grid), dim3(64), 0, s, a);
+  return wg::check_launch("k_decode_rows");
+}
+
+extern "C" int wg_decode_status(const void* work, int32_t mbw, int32_t n_images, void* stream) {
+  WG_REQUIRE(work && mbw > 0 && n_images > 0);
+  const int* ctl =
+      reinterpret_cast<const int*>(static_cast<const uint8_t*>(work) + (size_t)n_images * mbw * TOP_BYTES);
+  int flag = 0;
+  hipStream_t s = wg::as_stream(stream);
+  if (hipMemcpyAsync(&flag, ctl + 1, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return wg::check_launch("wg_decode_status");
+  if (flag) {
+    wg::set_error("decode: a row dependency wait timed out (output invalid)");
+    return WG_EHIP;
+  }
+  return WG_OK;
 }

@@ -36,7 +36,7 @@ def mb_info_tensor(mb, device="cuda"):
     return torch.from_numpy(arr.view(np.uint8).reshape(-1, 32).copy()).to(device)
 
 
-def decode_frames(mb_info, coeffs, filter_type, mbw, mbh, n_images=1, out=None, work=None):
+def decode_frames(mb_info, coeffs, filter_type, mbw, mbh, n_images=1, out=None, work=None, check=False):
     """Reconstruct + loop-filter n frames of parsed macroblocks.
 
     mb_info: (n*mbh*mbw, 32) uint8, coeffs: (n*mbh*mbw, 384) int16 (CUDA).
@@ -54,6 +54,8 @@ def decode_frames(mb_info, coeffs, filter_type, mbw, mbh, n_images=1, out=None, 
         work = torch.empty(lib.wg_decode_work_bytes(mbw, mbh, n_images), dtype=torch.uint8, device=dev)
     call("wg_decode_frames", mb_info.data_ptr(), coeffs.data_ptr(), filter_type, mbw, mbh, n_images, Y.data_ptr(),
          U.data_ptr(), V.data_ptr(), work.data_ptr(), _stream())
+    if check:  # synchronises: raises if an in-kernel dependency wait timed out
+        call("wg_decode_status", work.data_ptr(), mbw, n_images, _stream())
     return Y, U, V
 
 
