@@ -3,7 +3,7 @@
 One step = one pass of the hot path over this rank's batch of synthetic
 1920x1080 frames, all inputs resident in HBM before timing starts:
   encode side  import RGBA->YUV420 (k_import)  ->  analysis alphas (k_analysis)
-  decode side  reconstruct + loop filter of parsed macroblocks (k_decode_diag)
+  decode side  reconstruct + loop filter of parsed macroblocks (k_decode_rows)
                ->  fancy upsample to NRGBA (k_upsample)
 The decode side consumes seeded synthetic macroblock data (tools/synth.py,
 SURVEY.md 8(d) C3 recipe) because the encoder's RD/quantiser stage that would
@@ -36,6 +36,21 @@ BYTES_PER_PX = {
     "decode": (384 * 2 + 32 + 384) / 256.0,  # coeffs + mb info in, YUV out (recon and filter fused)
     "upsample": 1.5 + 4.0,            # YUV in, NRGBA out
 }
+
+
+KERNELS = {"import": "k_import", "analysis": "k_analysis", "decode": "k_decode_rows", "upsample": "k_upsample"}
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
+    (tools/profile.sh -> tools/pmc_summary.py --json; FETCH_SIZE doubled per
+    MI355X_MICROARCH.md's gfx950 correction, + WRITE_SIZE), or None."""
+    try:
+        rec = json.load(open(PMC_FILE))[kernel]
+        return int(rec["hbm_bytes_per_launch"]), os.path.relpath(PMC_FILE, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def parse():
@@ -182,8 +197,9 @@ def main():
         value = px_total / elapsed / 1e6
         dominant = max(stage, key=stage.get)
         px_rank_step = args.batch * W * H
-        launches = {"import": 1, "analysis": 1, "decode": MBW + 2 * (MBH - 1), "upsample": 1}[dominant]
+        kernel = KERNELS[dominant]
         achieved = BYTES_PER_PX[dominant] * px_rank_step / (stage[dominant] / 1e3) / 1e9
+        traffic, traffic_src = pmc_traffic(kernel)
         rec = {
             "metric": "MPixels/s encode+decode DSP path (1920x1080 q75)",
             "value": round(value, 1),
@@ -201,11 +217,14 @@ def main():
                                    "import+analysis (encode DSP) + reconstruct+loopfilter+upsample (decode DSP)",
                        "frames_per_gpu": args.batch, "width": W, "height": H, "parallelism": f"frames sharded x{world}"},
             "stage_ms": {k: round(v, 3) for k, v in stage.items()},
-            "roofline": {"kernel": {"import": "k_import", "analysis": "k_analysis", "decode": "k_decode_diag",
-                                    "upsample": "k_upsample"}[dominant],
-                         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_per_px": BYTES_PER_PX[dominant], "launches_per_step": launches},
+            "roofline": {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src, "bytes_per_px": BYTES_PER_PX[dominant],
+                         "algorithmic_bytes_per_launch": int(BYTES_PER_PX[dominant] * px_rank_step),
+                         "avg_launch_ms": round(stage[dominant], 4), "launches_per_step": 1},
+            "stage_roofline": {k: {"kernel": KERNELS[k], "GB/s": round(BYTES_PER_PX[k] * px_rank_step / (v / 1e3) / 1e9, 1),
+                                   "frac": round(BYTES_PER_PX[k] * px_rank_step / (v / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+                               for k, v in stage.items()},
         }
         if not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds, mb_co)

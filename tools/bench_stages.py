@@ -38,6 +38,8 @@ def main():
     rgba = img.unsqueeze(0).repeat(B, 1, 1, 1).contiguous()
     Y, U, V = frames.import_rgba(rgba, has_alpha=False)
     px = B * W * H
+    if os.environ.get("DECODE_ONLY"):
+        return decode_cases(Y, U, V, px, dev)
     t = timeit(lambda: frames.import_rgba(rgba, has_alpha=False, out=(Y, U, V)))
     print(f"import      {t:8.3f} ms  {px / t / 1e3:9.1f} MPix/s  {5.5 * px / t / 1e6:7.1f} GB/s")
     al = torch.empty((B, MBW * MBH), dtype=torch.int32, device=dev)
@@ -47,6 +49,10 @@ def main():
     out = torch.empty((B, H, W, 4), dtype=torch.uint8, device=dev)
     t = timeit(lambda: frames.build_nrgba(Y, U, V, W, H, out=out))
     print(f"upsample    {t:8.3f} ms  {px / t / 1e3:9.1f} MPix/s  {5.5 * px / t / 1e6:7.1f} GB/s")
+    decode_cases(Y, U, V, px, dev)
+
+
+def decode_cases(Y, U, V, px, dev):
     work = torch.empty(_lib.lib.wg_decode_work_bytes(MBW, MBH, B), dtype=torch.uint8, device=dev)
     dY, dU, dV = torch.empty_like(Y), torch.empty_like(U), torch.empty_like(V)
     for ft, p_i4 in ((2, 0.5), (0, 0.5), (2, 0.0), (2, 1.0), (1, 0.5)):

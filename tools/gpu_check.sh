@@ -10,3 +10,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 cat gpurun_out/smoke.log
 timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.log 2>&1
 cat gpurun_out/bench.log
+timeout -k 10 1500 bash tools/profile.sh > gpurun_out/profile.log 2>&1 && tail -30 gpurun_out/profile.log

@@ -1,5 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel-trace stats + separate PMC passes (FETCH_SIZE, WRITE_SIZE) of the bench.
+# Results land in gpurun_out/prof; copy the summaries into profiles/ (tools/save_profiles.sh).
 set -e
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
@@ -8,4 +9,5 @@ ARGS="--steps ${STEPS:-5} --warmup 2 --no-cpu-baseline ${EXTRA:-}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1
+python3 tools/pmc_summary.py --json $OUT/pmc_traffic.json $(find $OUT/fetch $OUT/write -name "*counter_collection.csv")
 find $OUT -name "*.csv" | head -20

@@ -22,6 +22,9 @@
 //
 // Lane mapping per macroblock: luma block b = lane/4 (raster), row lane%4,
 // 4 pixels per lane; chroma lanes 0-15 U, 16-31 V.
+#include <cstddef>
+#include <cstdlib>
+
 #include "wg_common.h"
 #include "wg_dsp.h"
 
@@ -65,6 +68,10 @@ __device__ __forceinline__ void st_sc1_32(uint8_t* p, uint32_t v) {
 __device__ __forceinline__ uint64_t lds64(const uint8_t* p) { return *reinterpret_cast<const uint64_t*>(p); }
 __device__ __forceinline__ uint32_t lds32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 
+static_assert(sizeof(wg_mb_info) == 32 && offsetof(wg_mb_info, imodes) == 8 && offsetof(wg_mb_info, is_i4x4) == 24 &&
+                  offsetof(wg_mb_info, f_limit) == 28 && offsetof(wg_mb_info, hev_thresh) == 31,
+              "k_decode_rows reads wg_mb_info as 8 words");
+
 struct DecArgs {
   const wg_mb_info* mb;
   const int16_t* coeffs;
@@ -101,17 +108,80 @@ __device__ unsigned long long g_phase[16];
 #define STAMP_FLUSH() (void)st_unused_
 #endif
 
+// Loop filter of one MB on the LDS tiles (doFilter, decode_frame.go:293-342):
+// lanes 0-15 luma line 0-15, lanes 16-31 chroma line 0-7 of U / V.  A line is
+// 20 (luma) / 12 (chroma) pixels: 4 of the left / upper neighbour, then the
+// MB.  Each lane filters all edges of its line in registers (rf_line); the
+// row pass (H edges) completes before the column pass (V edges).
+template <bool COMPLEX>
+__device__ __forceinline__ void filter_mb(uint8_t* fy, uint8_t* fu, uint8_t* fv, int lane, bool chroma, bool left,
+                                          bool top, bool inner, int limit, int ilevel, int hev_t) {
+  const bool luma = lane < 16;
+  const bool active = luma || (chroma && lane < 32);
+  const int pl = lane >= 24, j = (lane - 16) & 7;
+  if (active) {
+    uint8_t* rowp = luma ? fy + (lane + 4) * FY_STRIDE + FY_X0 - 4 : (pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 - 4;
+    // chroma lanes read 8 bytes past their 12-pixel line (in-bounds LDS: the
+    // next row, or the tile that follows); they are never written back
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) w[k] = *reinterpret_cast<const uint32_t*>(rowp + 4 * k);
+    int v[20];
+#pragma unroll
+    for (int k = 0; k < 20; k++) v[k] = byte_of(w[k >> 2], k & 3);
+    rf_line<COMPLEX>(v, left, inner, luma, limit, ilevel, hev_t);
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      *reinterpret_cast<uint32_t*>(rowp + 4 * k) = pack4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    if (luma) {
+      *reinterpret_cast<uint32_t*>(rowp + 12) = pack4(v[12], v[13], v[14], v[15]);
+      *reinterpret_cast<uint32_t*>(rowp + 16) = pack4(v[16], v[17], v[18], v[19]);
+    }
+  }
+  __syncthreads();
+  if (active) {
+    uint8_t* col = luma ? fy + FY_X0 + lane : (pl ? fv : fu) + FC_X0 + j;
+    const int st = luma ? FY_STRIDE : FC_STRIDE;
+    int v[20];
+#pragma unroll
+    for (int k = 0; k < 20; k++) v[k] = col[k * st];
+    rf_line<COMPLEX>(v, top, inner, luma, limit, ilevel, hev_t);
+#pragma unroll
+    for (int k = 1; k < 12; k++) col[k * st] = (uint8_t)v[k];
+    if (luma) {
+#pragma unroll
+      for (int k = 12; k < 20; k++) col[k * st] = (uint8_t)v[k];
+    }
+  }
+  __syncthreads();
+}
+
+// threadIdx.x through an opaque move, re-read at every phase of the MB loop:
+// stops the compiler from hoisting each phase's lane-derived LDS / global
+// addresses out of the loop, where they would pin ~60 VGPRs for the whole
+// kernel and cut the resident workgroups per CU.
+__device__ __forceinline__ int opaque_lane() {
+  int l;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"((int)threadIdx.x));
+  return l;
+}
+
 constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of the 100 MHz s_memrealtime clock per wait
 
 __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t wb[WB_SIZE];
-  __shared__ __attribute__((aligned(16))) int16_t cof[384];
-  __shared__ __attribute__((aligned(16))) uint8_t fy[20 * FY_STRIDE];
-  __shared__ __attribute__((aligned(16))) uint8_t fu[12 * FC_STRIDE];
-  __shared__ __attribute__((aligned(16))) uint8_t fv[12 * FC_STRIDE];
+  // prefetch landing zone: coefficients (48 x 16 B) then the wg_mb_info (2 x 16 B)
+  __shared__ __attribute__((aligned(16))) int4 stage[50];
+  int16_t* const cof = reinterpret_cast<int16_t*>(stage);
+  // filter tiles Y | U | V, then slack that chroma lanes of filter_mb read
+  // (never write) when they run the 20-pixel luma code path
+  __shared__ __attribute__((aligned(16))) uint8_t ftiles[20 * FY_STRIDE + 2 * 12 * FC_STRIDE + 8 * FC_STRIDE];
+  uint8_t* const fy = ftiles;
+  uint8_t* const fu = ftiles + 20 * FY_STRIDE;
+  uint8_t* const fv = fu + 12 * FC_STRIDE;
   __shared__ int sh_word;
 
-  const int lane = threadIdx.x;
+  int lane = threadIdx.x;
   const int mbw = a.mbw, mbh = a.mbh;
   const int total_rows = a.n_img * mbh;
   const int ys = 16 * mbw, uvs = 8 * mbw;
@@ -138,6 +208,14 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
     else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = 129;
     else if (lane < 35) wb[(lane == 32 ? LY : lane == 33 ? LU : LV) - WG_BPS - 1] = mby > 0 ? 129 : 127;
     int seen = 0;  // progress of the row above observed so far
+    // Register prefetch of the next macroblock's coefficients + info (lanes
+    // 0-47 / 48-49): issued once the current MB's hand-off loads are consumed,
+    // so it overlaps the MB's compute (loads retire in order: issuing it
+    // earlier would make every wait on a hand-off load wait for it too).
+    const int64_t row_mb0 = ((int64_t)img * mbh + mby) * mbw;
+    int4 pf = make_int4(0, 0, 0, 0);
+    if (lane < 48) pf = reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384)[lane];
+    else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + row_mb0)[lane - 48];
 
     for (int mbx = 0; mbx < mbw; mbx++) {
       const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
@@ -168,14 +246,9 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
         }
       }
       STAMP(1);
+      lane = opaque_lane();
       // ---- loads: macroblock info (scalar), coefficients -> LDS, top context, filter rows above ----
-      const wg_mb_info* ip = a.mb + mbi;
-      const uint32_t nz_y = ip->non_zero_y, nz_uv = ip->non_zero_uv;
-      const uint32_t im0 = reinterpret_cast<const uint32_t*>(ip->imodes)[0];
-      const int is_i4 = ip->is_i4x4, uv_mode = ip->uv_mode;
-      const int f_limit = ip->f_limit, ilevel = ip->f_ilevel, f_inner = ip->f_inner, hev_t = ip->hev_thresh;
-      if (lane < 48)
-        reinterpret_cast<int4*>(cof)[lane] = reinterpret_cast<const int4*>(a.coeffs + mbi * 384)[lane];
+      if (lane < 50) stage[lane] = pf;
       // rotate the filter tile: the left MB's final columns 12..15 become columns -4..-1
       if (mbx > 0) {
         if (lane < 16) {
@@ -207,7 +280,7 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
           *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) =
               ld_sc1_64(Vp + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
         }
-        if (is_i4 && lane == 0) {  // top-right: next MB's top context, or replicate top[15] at the right edge
+        if (lane == 0) {  // top-right: next MB's top context, or replicate top[15] at the right edge
           uint32_t tr;
           if (mbx < mbw - 1) tr = (uint32_t)ld_sc1_64(tc + TOP_BYTES);
           else tr = 0x01010101u * (uint32_t)(ld_sc1_64(tc + 8) >> 56);
@@ -219,6 +292,17 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
         else if (lane < 39) wb[LV - WG_BPS + lane - 31] = 127;
       }
       __syncthreads();
+      if (mbx + 1 < mbw) {  // prefetch the next MB (see above)
+        if (lane < 48) pf = reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384)[lane];
+        else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + mbi + 1)[lane - 48];
+      }
+      const uint32_t* iw = reinterpret_cast<const uint32_t*>(stage + 48);  // wg_mb_info words
+      const uint32_t nz_y = __builtin_amdgcn_readfirstlane(iw[0]), nz_uv = __builtin_amdgcn_readfirstlane(iw[1]);
+      const uint32_t im0 = __builtin_amdgcn_readfirstlane(iw[2]);
+      const uint32_t w6 = __builtin_amdgcn_readfirstlane(iw[6]), w7 = __builtin_amdgcn_readfirstlane(iw[7]);
+      const int is_i4 = w6 & 0xff, uv_mode = (w6 >> 8) & 0xff;
+      const int f_limit = w7 & 0xff, ilevel = (w7 >> 8) & 0xff, f_inner = (w7 >> 16) & 0xff, hev_t = w7 >> 24;
+      const uint8_t* imodes = reinterpret_cast<const uint8_t*>(stage + 48) + 8;
       if (is_i4 && lane < 12) {  // replicate top-right down to rows 3, 7, 11 (:155-160)
         const int r = 4 * (lane / 4 + 1) - 1, i = lane & 3;
         wb[LY + r * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
@@ -226,6 +310,7 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
       __syncthreads();
 
       STAMP(2);
+      lane = opaque_lane();
       // ---- luma prediction + residual ----
       {
         const int blk = lane >> 2, r = lane & 3, bx = blk & 3, by = blk >> 2;
@@ -242,7 +327,7 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
                     clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
         } else {
           const int my_step = bx + 2 * by;  // in-MB dependency wavefront
-          const int mode = reinterpret_cast<const uint8_t*>(ip->imodes)[blk];
+          const int mode = imodes[blk];
           for (int s = 0; s < 10; s++) {
             if (s == my_step) {
               int X, T[8], L[4];
@@ -257,6 +342,7 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
         }
       }
       STAMP(3);
+      lane = opaque_lane();
       // ---- chroma prediction + residual (doUVTransform :47-68) ----
       if (lane < 32) {
         const int pl = lane >> 4, cblk = (lane >> 2) & 3, r = lane & 3;
@@ -279,6 +365,7 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
       __syncthreads();
 
       STAMP(4);
+      lane = opaque_lane();
       // ---- unfiltered top context for the row below (:190-194) + MB into the filter tiles ----
       if (mby < mbh - 1 && lane >= 32 && lane < 36) {
         const int k = lane - 32;
@@ -297,50 +384,17 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
       __syncthreads();
 
       STAMP(5);
+      lane = opaque_lane();
       // ---- loop filter (doFilter :293-342): H edges (left MB edge, inner x=4,8,12), then V edges ----
       const bool do_filter = a.filter_type > 0 && f_limit > 0;
       const bool inner = f_inner != 0;
       if (do_filter) {
-        if (lane < 16) {
-          uint8_t* rowp = fy + (lane + 4) * FY_STRIDE + FY_X0;
-          if (luma_only) {
-            if (mbx > 0) f_simple(rowp, 0, 1, f_limit + 4);
-            if (inner)
-              for (int e = 4; e < 16; e += 4) f_simple(rowp, e, 1, f_limit);
-          } else {
-            if (mbx > 0) f_complex(rowp, 0, 1, f_limit + 4, ilevel, hev_t, false);
-            if (inner)
-              for (int e = 4; e < 16; e += 4) f_complex(rowp, e, 1, f_limit, ilevel, hev_t, true);
-          }
-        } else if (!luma_only && lane < 32) {
-          const int pl = lane >= 24, j = (lane - 16) & 7;
-          uint8_t* rowp = (pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0;
-          if (mbx > 0) f_complex(rowp, 0, 1, f_limit + 4, ilevel, hev_t, false);
-          if (inner) f_complex(rowp, 4, 1, f_limit, ilevel, hev_t, true);
-        }
-        __syncthreads();
-        if (lane < 16) {
-          uint8_t* col = fy + 4 * FY_STRIDE + FY_X0 + lane;
-          if (luma_only) {
-            if (mby > 0) f_simple(col, 0, FY_STRIDE, f_limit + 4);
-            if (inner)
-              for (int e = 4; e < 16; e += 4) f_simple(col, e * FY_STRIDE, FY_STRIDE, f_limit);
-          } else {
-            if (mby > 0) f_complex(col, 0, FY_STRIDE, f_limit + 4, ilevel, hev_t, false);
-            if (inner)
-              for (int e = 4; e < 16; e += 4)
-                f_complex(col, e * FY_STRIDE, FY_STRIDE, f_limit, ilevel, hev_t, true);
-          }
-        } else if (!luma_only && lane < 32) {
-          const int pl = lane >= 24, i = (lane - 16) & 7;
-          uint8_t* col = (pl ? fv : fu) + 4 * FC_STRIDE + FC_X0 + i;
-          if (mby > 0) f_complex(col, 0, FC_STRIDE, f_limit + 4, ilevel, hev_t, false);
-          if (inner) f_complex(col, 4 * FC_STRIDE, FC_STRIDE, f_limit, ilevel, hev_t, true);
-        }
-        __syncthreads();
+        if (a.filter_type == 2) filter_mb<true>(fy, fu, fv, lane, true, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
+        else filter_mb<false>(fy, fu, fv, lane, false, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
       }
 
       STAMP(6);
+      lane = opaque_lane();
       // ---- stores (all sc1: the row below reads them) ----
       if (lane < 32) {  // Y rows, 2 x 8 B
         const int j = lane >> 1, half = lane & 1;
@@ -383,6 +437,7 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
       else if (lane == 34) wb[LV - WG_BPS - 1] = wb[LV - WG_BPS + 7];
       __syncthreads();
       STAMP(7);
+      lane = opaque_lane();
       // ---- publish: every store of this MB is complete before the flag ----
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -393,6 +448,7 @@ __global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
 }
 
 int g_num_cus = 0;
+int g_rows_per_cu = 0;  // resident workgroups per CU (occupancy)
 
 }  // namespace
 
@@ -417,7 +473,7 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   WG_REQUIRE(filter_type >= 0 && filter_type <= 2);
   WG_REQUIRE(((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(v)) &
               7) == 0 &&
-             (reinterpret_cast<uintptr_t>(coeffs) & 15) == 0 && (reinterpret_cast<uintptr_t>(work) & 15) == 0);
+             (reinterpret_cast<uintptr_t>(coeffs) & 15) == 0 && (reinterpret_cast<uintptr_t>(mb) & 15) == 0 && (reinterpret_cast<uintptr_t>(work) & 15) == 0);
   DecArgs a;
   a.mb = mb;
   a.coeffs = coeffs;
@@ -433,16 +489,19 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   a.n_img = n_images;
   hipStream_t s = wg::as_stream(stream);
   if (g_num_cus == 0) {
-    int dev = 0, cus = 0;
+    int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      return wg::check_launch("hipDeviceGetAttribute");
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0 ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_rows, 64, 0) != hipSuccess || per_cu <= 0)
+      return wg::check_launch("decode occupancy query");
     g_num_cus = cus;
+    g_rows_per_cu = per_cu;
+    if (const char* e = getenv("WG_DECODE_WG_PER_CU")) g_rows_per_cu = atoi(e) > 0 ? atoi(e) : per_cu;  // tuning
   }
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(decode ctl)");
   const int rows = n_images * mbh;
-  const int grid = rows < 8 * g_num_cus ? rows : 8 * g_num_cus;
+  const int grid = rows < g_rows_per_cu * g_num_cus ? rows : g_rows_per_cu * g_num_cus;
   hipLaunchKernelGGL(k_decode_rows, dim3((unsigned)grid), dim3(64), 0, s, a);
   return wg::check_launch("k_decode_rows");
 }

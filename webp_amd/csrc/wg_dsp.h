@@ -345,6 +345,77 @@ __device__ __forceinline__ void f_complex(uint8_t* p, int off, int step, int thr
 }
 
 // ------------------------------------------------------------------------
+// Register forms: one line of pixels (a row for the horizontal pass, a column
+// for the vertical one) held in v[], an edge between v[K-1] and v[K].  Same
+// arithmetic as f_simple / f_complex, written branch-free: conditions are
+// combined with `&` (never `&&`) and applied as selects, and a disabled edge
+// gets threshold -1 instead of an `if`, so the compiler keeps v[] in place
+// (an `if` around array updates made it copy the whole line per edge).
+template <int K, int N>
+__device__ __forceinline__ void rf_simple(int (&v)[N], int t2) {
+  const int p1 = v[K - 2], p0 = v[K - 1], q0 = v[K], q1 = v[K + 1];
+  const int a = 3 * (q0 - p0) + sclip1(p1 - q1);
+  const int a1 = sclip2((a + 4) >> 3), a2 = sclip2((a + 3) >> 3);
+  const bool on = 4 * abs(p0 - q0) + abs(p1 - q1) <= t2;
+  v[K - 1] = on ? clip8(p0 + a2) : p0;
+  v[K] = on ? clip8(q0 - a1) : q0;
+}
+template <int K, int N, bool INNER>
+__device__ __forceinline__ void rf_complex(int (&v)[N], int t2, int it, int hev_t) {
+  const int p3 = v[K - 4], p2 = v[K - 3], p1 = v[K - 2], p0 = v[K - 1];
+  const int q0 = v[K], q1 = v[K + 1], q2 = v[K + 2], q3 = v[K + 3];
+  const int m = max(max(max(abs(p3 - p2), abs(p2 - p1)), max(abs(p1 - p0), abs(q3 - q2))),
+                    max(abs(q2 - q1), abs(q1 - q0)));
+  const bool on = (4 * abs(p0 - q0) + abs(p1 - q1) <= t2) & (m <= it);
+  const bool hev = max(abs(p1 - p0), abs(q1 - q0)) > hev_t;
+  if (INNER) {  // doFilter2 when hev, else doFilter4
+    const int a = 3 * (q0 - p0) + (hev ? sclip1(p1 - q1) : 0);
+    const int a1 = sclip2((a + 4) >> 3), a2 = sclip2((a + 3) >> 3), a3 = (a1 + 1) >> 1;
+    const bool four = on & !hev;
+    v[K - 2] = four ? clip8(p1 + a3) : p1;
+    v[K - 1] = on ? clip8(p0 + a2) : p0;
+    v[K] = on ? clip8(q0 - a1) : q0;
+    v[K + 1] = four ? clip8(q1 - a3) : q1;
+  } else {  // doFilter2 when hev, else doFilter6
+    const int b = 3 * (q0 - p0) + sclip1(p1 - q1);
+    const int w = sclip1(b);
+    const int h1 = sclip2((b + 4) >> 3), h2 = sclip2((b + 3) >> 3);
+    const int a1 = (27 * w + 63) >> 7, a2 = (18 * w + 63) >> 7, a3 = (9 * w + 63) >> 7;
+    const bool six = on & !hev;
+    v[K - 3] = six ? clip8(p2 + a3) : p2;
+    v[K - 2] = six ? clip8(p1 + a2) : p1;
+    v[K - 1] = on ? clip8(p0 + (hev ? h2 : a1)) : p0;
+    v[K] = on ? clip8(q0 - (hev ? h1 : a1)) : q0;
+    v[K + 1] = six ? clip8(q1 - a2) : q1;
+    v[K + 2] = six ? clip8(q2 - a3) : q2;
+  }
+}
+// All edges of one 20-pixel line in the reference's order: the MB edge between
+// v[3] and v[4], then the inner edges at v[8], v[12], v[16].  Chroma lines
+// (12 pixels: MB edge + one inner edge at v[8]) run the same code with
+// `luma` false, which turns the edges at v[12] and v[16] off, so luma and
+// chroma lanes share one instruction stream.  COMPLEX: filter type 2 (the
+// simple filter, type 1, never reaches chroma).
+template <bool COMPLEX>
+__device__ __forceinline__ void rf_line(int (&v)[20], bool mb_edge, bool inner, bool luma, int limit, int ilevel,
+                                        int hev_t) {
+  const int t_mb = mb_edge ? 2 * (limit + 4) + 1 : -1;
+  const int t_in = inner ? 2 * limit + 1 : -1;
+  const int t_l = luma ? t_in : -1;
+  if (COMPLEX) {
+    rf_complex<4, 20, false>(v, t_mb, ilevel, hev_t);
+    rf_complex<8, 20, true>(v, t_in, ilevel, hev_t);
+    rf_complex<12, 20, true>(v, t_l, ilevel, hev_t);
+    rf_complex<16, 20, true>(v, t_l, ilevel, hev_t);
+  } else {
+    rf_simple<4, 20>(v, t_mb);
+    rf_simple<8, 20>(v, t_in);
+    rf_simple<12, 20>(v, t_l);
+    rf_simple<16, 20>(v, t_l);
+  }
+}
+
+// ------------------------------------------------------------------------
 // Distortion metrics (ssim.go:188-335), one block per lane.
 __device__ __forceinline__ int sse_nxn(const uint8_t* a, const uint8_t* b, int n) {
   int s = 0;
