@@ -131,6 +131,19 @@ size_t wg_decode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images);
 int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int32_t filter_type, int32_t mbw, int32_t mbh,
                      int32_t n_images, uint8_t* y, uint8_t* u, uint8_t* v, void* work, void* stream);
 
+/* VP8 bitstream parse (HOST memory in and out; no device work): the CPU
+ * half of the reference's decoder as a parse-all-rows-first pass that feeds
+ * wg_decode_frames.  Replaces the parsing in DecodeFrame / parseFrame
+ * (internal/lossy/decode.go:207-560: parseHeaders, parseIntraModeRow
+ * decode_tree.go:35, decodeMB / parseResiduals decode_mb.go:272-430,
+ * precomputeFilterStrengths decode_frame.go:220).  `data` is a RIFF/WEBP
+ * file with a "VP8 " chunk, or a raw VP8 key frame.  dims[5] receives
+ * width, height, filter_type, mbw, mbh.  With mb == NULL only the headers
+ * are parsed; otherwise mb[mbw*mbh] and coeffs[mbw*mbh][384] (dequantised,
+ * I16 DCs already inverse-WHT'd, as the decoder stores them) are filled. */
+int wg_vp8_parse(const uint8_t* data, size_t size, int32_t* dims, wg_mb_info* mb, int16_t* coeffs,
+                 int64_t max_mbs);
+
 /* After wg_decode_frames on the same stream: WG_OK, or WG_EHIP if a row
  * dependency wait timed out inside the kernel (output invalid).  Synchronises
  * the stream. */

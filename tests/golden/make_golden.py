@@ -61,7 +61,42 @@ def main():
     out["ssim_c"], out["ssim_d"] = g, q[:45, :61].copy()
     out["ssim_value2"] = np.array([L.plane_ssim(g, out["ssim_d"])], np.float64)
     np.savez_compressed(os.path.join(HERE, "libwebp_fixtures.npz"), **out)
+    make_decode_fixtures(img)
     print("wrote", os.path.join(HERE, "libwebp_fixtures.npz"), sum(v.nbytes for v in out.values()), "bytes raw")
+
+
+# Bitstreams covering the decoder's header / token / filter space: simple and
+# normal filter, sharpness, 4 token partitions, segment maps, q0..q100,
+# method 6 (I4-heavy), odd and tiny sizes.  (name, rgba, encoder config)
+def decode_cases(img):
+    return [
+        ("v_q10", img[40:104, 10:106], dict(quality=10)),
+        ("v_simple", img[200:248, 300:380], dict(quality=90, filter_type=0, filter_sharpness=3)),
+        ("v_parts", img[300:372, 400:520], dict(quality=50, partitions=3, filter_sharpness=7)),
+        ("v_q100", img[64:128, 64:128], dict(quality=100)),
+        ("v_q0", img[500:536, 600:700], dict(quality=0, filter_strength=100)),
+        ("v_seg1", img[120:195, 220:295], dict(quality=75, segments=1, filter_type=0)),
+        ("v_m6", img[10:90, 700:748], dict(quality=60, method=6, filter_strength=0)),
+        ("v_big", img[100:292, 200:456], dict(quality=75)),
+        ("v_sharp", img[260:324, 100:164], dict(quality=40, filter_sharpness=5, partitions=1)),
+        ("v_noise", synth.noise_rgba(64, 48, seed=7), dict(quality=75)),
+        ("v_grad", synth.gradient_rgba(100, 36), dict(quality=30)),
+        ("v_1x1", img[5:6, 5:6], dict(quality=75)),
+        ("v_17x1", img[7:8, 30:47], dict(quality=75)),
+        ("v_1x17", img[7:24, 30:31], dict(quality=20)),
+    ]
+
+
+def make_decode_fixtures(img):
+    out = {}
+    for name, rgba, cfg in decode_cases(img):
+        data = L.encode_lossy_cfg(np.ascontiguousarray(rgba), **cfg)
+        Y, U, V = L.decode_yuv(data)
+        out[name + "_webp"] = np.frombuffer(data, np.uint8).copy()
+        out[name + "_y"], out[name + "_u"], out[name + "_v"] = Y, U, V
+    path = os.path.join(HERE, "libwebp_decode.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
 
 
 if __name__ == "__main__":

@@ -139,3 +139,54 @@ def import_rgba(rgba):
     planes = _pic_planes(buf, w, h)
     lib.WebPPictureFree(buf)
     return planes
+
+
+# WebPConfig field offsets (libwebp encode.h; all 4-byte fields)
+_CFG_SIZE = 256
+_CFG_FIELDS = {"quality": (4, ctypes.c_float), "method": (8, ctypes.c_int), "segments": (24, ctypes.c_int),
+               "sns_strength": (28, ctypes.c_int), "filter_strength": (32, ctypes.c_int),
+               "filter_sharpness": (36, ctypes.c_int), "filter_type": (40, ctypes.c_int),
+               "autofilter": (44, ctypes.c_int), "partitions": (72, ctypes.c_int),
+               "use_sharp_yuv": (104, ctypes.c_int)}
+_OFF_WRITER, _OFF_CUSTOM = 96, 104
+
+if available:
+    lib.WebPConfigInitInternal.restype = ctypes.c_int
+    lib.WebPConfigInitInternal.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int]
+    lib.WebPValidateConfig.restype = ctypes.c_int
+    lib.WebPValidateConfig.argtypes = [ctypes.c_void_p]
+    lib.WebPEncode.restype = ctypes.c_int
+    lib.WebPEncode.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.WebPMemoryWriterInit.argtypes = [ctypes.c_void_p]
+    lib.WebPMemoryWriterClear.argtypes = [ctypes.c_void_p]
+
+
+def encode_lossy_cfg(rgba, quality=75.0, **fields):
+    """WebPEncode with an advanced WebPConfig (filter_type 0 = simple / 1 = strong,
+    filter_sharpness, filter_strength, partitions, segments, method, ...) -> bytes."""
+    h, w, _ = rgba.shape
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    cfg = (ctypes.c_uint8 * _CFG_SIZE)()
+    assert lib.WebPConfigInitInternal(cfg, 0, float(quality), 0x0210)
+    for k, v in fields.items():
+        off, t = _CFG_FIELDS[k]
+        t.from_buffer(cfg, off).value = v
+    assert lib.WebPValidateConfig(cfg), fields
+    pic = (ctypes.c_uint8 * _PIC_SIZE)()
+    assert lib.WebPPictureInitInternal(pic, 0x0210)
+    ctypes.c_int.from_buffer(pic, _OFF_USE_ARGB).value = 0
+    ctypes.c_int.from_buffer(pic, _OFF_W).value = w
+    ctypes.c_int.from_buffer(pic, _OFF_H).value = h
+    assert lib.WebPPictureImportRGBA(pic, rgba.ctypes.data, w * 4)
+    mw = (ctypes.c_uint8 * 64)()
+    lib.WebPMemoryWriterInit(mw)
+    ctypes.c_void_p.from_buffer(pic, _OFF_WRITER).value = ctypes.cast(lib.WebPMemoryWrite, ctypes.c_void_p).value
+    ctypes.c_void_p.from_buffer(pic, _OFF_CUSTOM).value = ctypes.addressof(mw)
+    ok = lib.WebPEncode(cfg, pic)
+    mem = ctypes.c_void_p.from_buffer(mw, 0).value
+    size = ctypes.c_size_t.from_buffer(mw, 8).value
+    data = ctypes.string_at(mem, size) if ok else None
+    lib.WebPMemoryWriterClear(mw)
+    lib.WebPPictureFree(pic)
+    assert ok, "WebPEncode failed"
+    return data

@@ -75,6 +75,28 @@ def test_decode_4096_square(cuda):
     run_decode(256, 256, 1, 2, seed=4096, levels=(20,))
 
 
+# ---------------- real bitstreams: host parse -> GPU reconstruct + filter ----------------
+
+DEC = np.load(os.path.join(os.path.dirname(__file__), "golden", "libwebp_decode.npz"))
+DEC_NAMES = sorted({k[:-5] for k in DEC.files if k.endswith("_webp")})
+
+
+@pytest.mark.parametrize("name", DEC_NAMES)
+def test_decode_bitstreams(cuda, name):
+    """libwebp-encoded streams (q0..q100, simple/normal filter, sharpness,
+    partitions, segments, tiny sizes): GPU == oracle under the reference's
+    rules, and GPU == libwebp WebPDecodeYUV under libwebp's skip rule
+    (test_oracle.libwebp_skip_rule)."""
+    from test_oracle import crop_eq, libwebp_skip_rule
+    dims, mb, co = frames.vp8_parse(DEC[name + "_webp"].tobytes())
+    ft, mbw, mbh = dims["filter_type"], dims["mbw"], dims["mbh"]
+    for info, want in ((mb, O.decode_frame(mb, co, ft, mbw, mbh)),
+                       (libwebp_skip_rule(mb), (DEC[name + "_y"], DEC[name + "_u"], DEC[name + "_v"]))):
+        got = frames.decode_frames(frames.mb_info_tensor(info), dev(co), ft, mbw, mbh, 1, check=True)
+        for g, w in zip(got, want):
+            assert crop_eq(host(g)[0], w), name
+
+
 # ---------------- RGBA -> YUV420 import ----------------
 
 @pytest.mark.parametrize("w,h,kind,alpha", [(1, 1, "noise", False), (17, 33, "noise", True), (96, 80, "grad", False),

@@ -4,7 +4,11 @@
    (internal/dsp/upsample_test.go, random_test.go).
 2. Golden fixtures produced by libwebp 1.6.0 (tests/golden/make_golden.py):
    RGBA->YUV import, fancy upsampling of normatively decoded planes, plane SSIM.
-3. Where the reference checkout is present (build container only), verbatim
+3. libwebp-encoded bitstreams (tests/golden/libwebp_decode.npz): parsed by the
+   product's host parser (wg_vp8_parse, no GPU), reconstructed + loop-filtered
+   by the oracle, compared with libwebp's normative WebPDecodeYUV.  This pins
+   the oracle's predictors, inverse transforms and loop filters (A2-A13).
+4. Where the reference checkout is present (build container only), verbatim
    reference tables are re-read and compared.
 """
 import ctypes
@@ -18,6 +22,42 @@ import oracle as O
 from conftest import REFERENCE
 
 GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "libwebp_fixtures.npz"))
+DEC = np.load(os.path.join(os.path.dirname(__file__), "golden", "libwebp_decode.npz"))
+DEC_NAMES = sorted({k[:-5] for k in DEC.files if k.endswith("_webp")})
+
+
+def libwebp_skip_rule(mb):
+    """The one place the reference's decoder departs from libwebp: decode_mb.go:
+    290-296 keeps FInner set for an I16 macroblock whose residuals are all
+    zero when skip was not signalled, libwebp (VP8DecodeMB) treats that MB as
+    skipped and does not filter its inner edges.  The product follows the
+    reference; comparisons with libwebp apply libwebp's rule to the parse."""
+    lw = mb.copy()
+    zero = (lw["non_zero_y"] == 0) & (lw["non_zero_uv"] == 0) & (lw["is_i4x4"] == 0)
+    lw["f_inner"] = np.where(zero, 0, lw["f_inner"])
+    return lw
+
+
+def crop_eq(got, want):
+    return (got[:want.shape[0], :want.shape[1]] == want).all()
+
+
+@pytest.mark.parametrize("name", DEC_NAMES)
+def test_decode_bitstreams_vs_libwebp(name):
+    from webp_amd import frames
+    dims, mb, co = frames.vp8_parse(DEC[name + "_webp"].tobytes())
+    y, u, v = O.decode_frame(libwebp_skip_rule(mb), co, dims["filter_type"], dims["mbw"], dims["mbh"])
+    assert crop_eq(y, DEC[name + "_y"]) and crop_eq(u, DEC[name + "_u"]) and crop_eq(v, DEC[name + "_v"])
+
+
+def test_parser_rejects_garbage():
+    from webp_amd import frames
+    from webp_amd._lib import WebpGpuError
+    data = DEC["v_q10_webp"].tobytes()
+    with pytest.raises(WebpGpuError):
+        frames.vp8_parse(data[:40])          # truncated
+    with pytest.raises(WebpGpuError):
+        frames.vp8_parse(b"RIFF\x04\x00\x00\x00WEBPVP8L")  # no VP8 chunk
 
 
 def yuv_to_rgb(y, u, v):

@@ -47,6 +47,7 @@ SIGNATURES = {
     "wg_filter": [_i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp],
     "wg_decode_work_bytes": [_i32, _i32, _i32],
     "wg_decode_frames": [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
+    "wg_vp8_parse": [_vp, ctypes.c_size_t, _vp, _vp, _vp, _i64],
     "wg_decode_status": [_vp, _i32, _i32, _vp],
     "wg_import_rgba": [_vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "wg_analysis_alphas": [_vp, _vp, _vp, _i32, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp],

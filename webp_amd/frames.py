@@ -115,3 +115,17 @@ def plane_ssim(a, b, work=None):
     call("wg_plane_ssim", a.data_ptr(), a.shape[-1], a[0].numel(), b.data_ptr(), b.shape[-1], b[0].numel(), w, h, n,
          out.data_ptr(), work.data_ptr(), _stream())
     return out
+
+
+def vp8_parse(data):
+    """Parse a lossy WebP (RIFF "VP8 " chunk or raw VP8 frame) on the host:
+    returns (dims dict, mb_info structured array, coeffs int16 (n_mb, 384))."""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8)
+    dims = np.zeros(5, dtype=np.int32)
+    call("wg_vp8_parse", buf.ctypes.data, buf.size, dims.ctypes.data, None, None, 0)
+    n = int(dims[3]) * int(dims[4])
+    mb = np.zeros(n, dtype=MB_INFO_DTYPE)
+    co = np.zeros((n, 384), dtype=np.int16)
+    call("wg_vp8_parse", buf.ctypes.data, buf.size, dims.ctypes.data, mb.ctypes.data, co.ctypes.data, n)
+    keys = ("width", "height", "filter_type", "mbw", "mbh")
+    return {k: int(v) for k, v in zip(keys, dims)}, mb, co
