@@ -180,6 +180,36 @@ int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uin
                   int64_t b_pitch, int32_t w, int32_t h, int32_t n_images, double* out, void* work,
                   void* stream);
 
+/* ===================================================================== *
+ * 3. VP8L (lossless) predictor transform.
+ *    ARGB images are uint32 [n_images][image_pitch] (width*height used),
+ *    one 0xAARRGGBB word per pixel like the reference's []uint32.
+ * ===================================================================== */
+
+/* lossless.ResidualImage (internal/lossless/encode_predictor.go:378-455):
+ * per 2^bits tile the predictor with the lowest entropy estimate among the
+ * first 4 / 8 / 14 (quality <25 / <50 / else), written as mode<<8|0xff000000
+ * to modes[n_images][tiles_y*tiles_x]; residuals[n_images][image_pitch] =
+ * ARGB -mod prediction from the original pixels.  bits in [2, 9]. */
+int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32_t height, int64_t image_pitch,
+                           int32_t bits, int32_t quality, int32_t n_images, uint32_t* modes, uint32_t* residuals,
+                           void* stream);
+/* predictorInverseTransform (internal/lossless/decode_transform.go:202-360):
+ * out = residuals +mod prediction from reconstructed pixels.  `work` needs
+ * wg_vp8l_inverse_work_bytes(height, n_images) bytes. */
+size_t wg_vp8l_inverse_work_bytes(int32_t height, int32_t n_images);
+int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, int32_t width, int32_t height,
+                              int64_t image_pitch, int32_t n_images, const uint32_t* residuals, uint32_t* out,
+                              void* work, void* stream);
+/* After wg_vp8l_inverse_predictor on the same stream: WG_OK or WG_EHIP if a
+ * band wait timed out.  Synchronises the stream. */
+int wg_vp8l_inverse_status(const void* work, void* stream);
+/* SubtractGreen (encode_predictor.go:461) when add == 0, AddGreenToBlueAndRed
+ * (dsp/lossless_dsp.go:12) when add != 0; in place over n pixels. */
+int wg_vp8l_green(uint32_t* argb, int64_t n, int32_t add, void* stream);
+/* The fastSLog2 table (encode_histogram.go:359-368) the selection uses, host copy. */
+int wg_vp8l_slog2_lut_host(double* out, int32_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -96,6 +96,14 @@ _SIGS = {
     "or_decode_reconstruct": (None, [ctypes.c_void_p, _i16p, _i, _i, _u8p, _u8p, _u8p]),
     "or_decode_filter": (None, [ctypes.c_void_p, _i, _i, _i, _u8p, _u8p, _u8p]),
     "or_decode_frame": (None, [ctypes.c_void_p, _i16p, _i, _i, _i, _u8p, _u8p, _u8p]),
+    "or_go_log2": (ctypes.c_double, [ctypes.c_double]),
+    "or_vp8l_slog2_lut": (None, [ctypes.c_void_p, _i]),
+    "or_vp8l_predict": (ctypes.c_uint32, [_i, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    "or_vp8l_estimate_entropy": (ctypes.c_double, [ctypes.c_void_p, _i, _i, _i, _i, _i, _i]),
+    "or_vp8l_residual_image": (None, [ctypes.c_void_p, _i, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
+    "or_vp8l_inverse_predictor": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
+    "or_vp8l_subtract_green": (None, [ctypes.c_void_p, ctypes.c_size_t]),
+    "or_vp8l_add_green": (None, [ctypes.c_void_p, ctypes.c_size_t]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
@@ -185,3 +193,46 @@ def plane_ssim(a, b):
     b = np.ascontiguousarray(b)
     h, w = a.shape
     return lib.or_plane_ssim(u8(a), a.shape[1], u8(b), b.shape[1], w, h)
+
+
+# ---------------- VP8L predictor transform ----------------
+
+def vp8l_subsample(size, bits):
+    return (size + (1 << bits) - 1) >> bits
+
+
+def vp8l_residual_image(argb, bits, quality):
+    """ResidualImage: argb (h, w) uint32 -> (modes (th, tw) uint32, residuals (h, w) uint32)."""
+    argb = np.ascontiguousarray(argb, np.uint32)
+    h, w = argb.shape
+    modes = np.zeros((vp8l_subsample(h, bits), vp8l_subsample(w, bits)), np.uint32)
+    res = np.zeros_like(argb)
+    lib.or_vp8l_residual_image(argb.ctypes.data, w, h, bits, quality, modes.ctypes.data, res.ctypes.data)
+    return modes, res
+
+
+def vp8l_inverse_predictor(modes, bits, residuals):
+    residuals = np.ascontiguousarray(residuals, np.uint32)
+    modes = np.ascontiguousarray(modes, np.uint32)
+    h, w = residuals.shape
+    out = np.zeros_like(residuals)
+    lib.or_vp8l_inverse_predictor(modes.ctypes.data, bits, w, h, residuals.ctypes.data, out.ctypes.data)
+    return out
+
+
+def vp8l_estimate_entropy(argb, bits, tx, ty, mode):
+    argb = np.ascontiguousarray(argb, np.uint32)
+    h, w = argb.shape
+    return lib.or_vp8l_estimate_entropy(argb.ctypes.data, w, h, tx, ty, bits, mode)
+
+
+def vp8l_slog2_lut(n=65536):
+    out = np.zeros(n, np.float64)
+    lib.or_vp8l_slog2_lut(out.ctypes.data, n)
+    return out
+
+
+def vp8l_subtract_green(argb):
+    a = np.ascontiguousarray(argb, np.uint32).copy()
+    lib.or_vp8l_subtract_green(a.ctypes.data, a.size)
+    return a

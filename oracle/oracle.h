@@ -145,6 +145,18 @@ void or_decode_filter(const or_mb_info* mb, int filter_type, int mbw, int mbh,
 void or_decode_frame(const or_mb_info* mb, const int16_t* coeffs, int filter_type, int mbw, int mbh,
                      uint8_t* y, uint8_t* u, uint8_t* v);
 
+/* ---- VP8L predictor transform (lossless.c; encode_predictor.go, decode_transform.go) ---- */
+double or_go_log2(double x);
+void or_vp8l_slog2_lut(double* out, int n);
+uint32_t or_vp8l_predict(int mode, uint32_t l, uint32_t t, uint32_t tr, uint32_t tl);
+double or_vp8l_estimate_entropy(const uint32_t* argb, int width, int height, int tx, int ty, int bits, int mode);
+void or_vp8l_residual_image(const uint32_t* argb, int width, int height, int bits, int quality, uint32_t* modes,
+                            uint32_t* residuals);
+void or_vp8l_inverse_predictor(const uint32_t* modes, int bits, int width, int height, const uint32_t* in,
+                               uint32_t* out);
+void or_vp8l_subtract_green(uint32_t* argb, size_t n);
+void or_vp8l_add_green(uint32_t* argb, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,9 +54,15 @@ SIGNATURES = {
     "wg_upsample_nrgba": [_vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp],
     "wg_plane_ssim_work_bytes": [_i32, _i32, _i32],
     "wg_plane_ssim": [_vp, _i32, _i64, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp],
+    "wg_vp8l_residual_image": [_vp, _i32, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp],
+    "wg_vp8l_inverse_work_bytes": [_i32, _i32],
+    "wg_vp8l_inverse_predictor": [_vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _vp, _vp],
+    "wg_vp8l_inverse_status": [_vp, _vp],
+    "wg_vp8l_green": [_vp, _i64, _i32, _vp],
+    "wg_vp8l_slog2_lut_host": [_vp, _i32],
 }
 _RES = {"wg_last_error": ctypes.c_char_p, "wg_decode_work_bytes": ctypes.c_size_t,
-        "wg_plane_ssim_work_bytes": ctypes.c_size_t}
+        "wg_plane_ssim_work_bytes": ctypes.c_size_t, "wg_vp8l_inverse_work_bytes": ctypes.c_size_t}
 
 for _name, _args in SIGNATURES.items():
     _f = getattr(lib, _name)

@@ -1,0 +1,450 @@
+// vp8l.hip -- VP8L predictor transform on gfx950.
+//
+//   k_vp8l_select    ResidualImage phase 1: per tile, the entropy estimate of
+//                    every candidate predictor and its argmin
+//                    (internal/lossless/encode_predictor.go:194-277, 396-440)
+//   k_vp8l_residual  ResidualImage phase 2: residual = ARGB -mod prediction
+//                    from ORIGINAL pixels (copyImageWithPrediction :298-363)
+//   k_vp8l_inverse   predictorInverseTransform (decode_transform.go:202-360)
+//   k_vp8l_green     SubtractGreen (encode_predictor.go:461) / AddGreenToBlueAndRed
+//
+// Bit-exactness of the mode choice: the entropy is a float64 sum that the
+// reference accumulates in a fixed order (count term first, then bins 0..255
+// of alpha, red, green, blue); k_vp8l_select keeps exactly that order (one lane
+// per channel walks its 256 bins) and takes fastSLog2 values from the same
+// LUT the reference builds (i * math.Log2(i), built on the host by
+// vp8l_host.cpp's restatement of Go's math.Log2).  No FMA contraction anywhere
+// in this file.
+#include "wg_common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr uint32_t ARGB_BLACK = 0xff000000u;
+
+// LDS written by this wave is visible to all its lanes, and the compiler may
+// not move LDS accesses across this point.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+constexpr int SLOG2_LUT = 65536;
+
+__device__ __forceinline__ uint32_t sub_pixels(uint32_t a, uint32_t b) {
+  const uint32_t ag = 0x00ff00ffu + (a & 0xff00ff00u) - (b & 0xff00ff00u);
+  const uint32_t rb = 0xff00ff00u + (a & 0x00ff00ffu) - (b & 0x00ff00ffu);
+  return (ag & 0xff00ff00u) | (rb & 0x00ff00ffu);
+}
+__device__ __forceinline__ uint32_t add_pixels(uint32_t a, uint32_t b) {
+  const uint32_t ag = (a & 0xff00ff00u) + (b & 0xff00ff00u);
+  const uint32_t rb = (a & 0x00ff00ffu) + (b & 0x00ff00ffu);
+  return (ag & 0xff00ff00u) | (rb & 0x00ff00ffu);
+}
+__device__ __forceinline__ uint32_t avg2(uint32_t a, uint32_t b) { return (((a ^ b) & 0xfefefefeu) >> 1) + (a & b); }
+__device__ __forceinline__ int chan(uint32_t v, int s) { return (int)((v >> s) & 0xff); }
+__device__ __forceinline__ uint32_t select_pred(uint32_t l, uint32_t t, uint32_t tl) {
+  int pa = 0;
+#pragma unroll
+  for (int s = 0; s < 32; s += 8) pa += abs(chan(l, s) - chan(tl, s)) - abs(chan(t, s) - chan(tl, s));
+  return pa <= 0 ? t : l;
+}
+__device__ __forceinline__ uint32_t clamp_add_sub_full(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int s = 0; s < 32; s += 8) r |= (uint32_t)min(max(chan(a, s) + chan(b, s) - chan(c, s), 0), 255) << s;
+  return r;
+}
+__device__ __forceinline__ uint32_t clamp_add_sub_half(uint32_t avg, uint32_t c) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int s = 0; s < 32; s += 8) {
+    const int va = chan(avg, s), vc = chan(c, s);
+    r |= (uint32_t)min(max(va + (va - vc) / 2, 0), 255) << s;  // '/' truncates toward zero, as Go's
+  }
+  return r;
+}
+// predictPixel (encode_predictor.go:148-180); the decoder's switch
+// (decode_transform.go:257-350) computes the same predictors.
+__device__ __forceinline__ uint32_t predict(int mode, uint32_t l, uint32_t t, uint32_t tr, uint32_t tl) {
+  switch (mode) {
+    case 1: return l;
+    case 2: return t;
+    case 3: return tr;
+    case 4: return tl;
+    case 5: return avg2(avg2(l, tr), t);
+    case 6: return avg2(l, tl);
+    case 7: return avg2(l, t);
+    case 8: return avg2(tl, t);
+    case 9: return avg2(t, tr);
+    case 10: return avg2(avg2(l, tl), avg2(t, tr));
+    case 11: return select_pred(l, t, tl);
+    case 12: return clamp_add_sub_full(l, t, tl);
+    case 13: return clamp_add_sub_half(avg2(l, t), tl);
+    default: return ARGB_BLACK;
+  }
+}
+
+// Go math.Log / math.Log2 (src/math/log.go, log10.go) for counts beyond the
+// LUT (tiles of 512 px at bits = 9); same operation sequence as the host LUT.
+__device__ double go_log(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01;
+  const double L3 = 2.857142874366239149e-01, L4 = 2.222219843214978396e-01;
+  const double L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01;
+  const double L7 = 1.479819860511658591e-01;
+  int ki;
+  double f1 = frexp(x, &ki);
+  if (f1 < 0.70710678118654752440) {
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1, k = (double)ki;
+  const double s = f / (2 + f), s2 = s * s, s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2, hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+__device__ double fast_slog2(const double* __restrict__ lut, uint32_t v) {
+  if (v < (uint32_t)SLOG2_LUT) return lut[v];
+  int e;
+  const double fv = (double)v;
+  const double frac = frexp(fv, &e);
+  const double l2 = frac == 0.5 ? (double)(e - 1) : go_log(frac) * 0x1.71547652b82fep+0 + (double)e;
+  return fv * l2;
+}
+
+struct SelArgs {
+  const uint32_t* argb;
+  int64_t pitch;  // pixels per image
+  uint32_t* modes;
+  const double* lut;
+  int width, height, bits, tiles_x, tiles_y, max_mode;
+};
+
+constexpr int SEL_WAVES = 4;
+
+// One workgroup per tile; wave w evaluates modes w, w+4, ...  Histograms
+// (4 x 256 u32) per wave in LDS; the per-channel float64 sums run on lanes
+// 0-3, each walking its channel's bins in order.
+__global__ __launch_bounds__(64 * SEL_WAVES) void k_vp8l_select(SelArgs a) {
+  __shared__ uint32_t hist[SEL_WAVES][4 * 256];
+  __shared__ double chan_cost[SEL_WAVES][4];
+  __shared__ double cost[14];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile = blockIdx.x % (a.tiles_x * a.tiles_y);
+  const int img = blockIdx.x / (a.tiles_x * a.tiles_y);
+  const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+  const uint32_t* argb = a.argb + img * a.pitch;
+  const int ts = 1 << a.bits, w = a.width, h = a.height;
+  const int x0 = tx * ts, y0 = ty * ts;
+  const int x1 = min(x0 + ts, w), y1 = min(y0 + ts, h);
+  const int ystep = (y1 - y0 > 16) ? 2 : 1;
+  const int tw = x1 - x0, rows = (y1 - y0 + ystep - 1) / ystep;
+  const uint32_t count = (uint32_t)(tw * rows);
+  uint32_t* hg = hist[wave];
+
+  for (int mode = wave; mode < a.max_mode; mode += SEL_WAVES) {
+    for (int i = lane; i < 4 * 256; i += 64) hg[i] = 0;
+    wave_lds_sync();  // this wave's zeroing lands before its adds
+    for (int i = lane; i < tw * rows; i += 64) {
+      const int x = x0 + i % tw, y = y0 + (i / tw) * ystep;
+      const uint32_t* row = argb + (int64_t)y * w;
+      uint32_t l = 0, t = 0, tr = 0, tl = 0;
+      if (x > 0) l = row[x - 1];
+      if (y > 0) {
+        const uint32_t* prev = row - w;
+        t = prev[x];
+        if (x > 0) tl = prev[x - 1];
+        tr = (x < w - 1) ? prev[x + 1] : t;
+      }
+      const uint32_t res = sub_pixels(row[x], predict(mode, l, t, tr, tl));
+      atomicAdd(&hg[0 * 256 + ((res >> 24) & 0xff)], 1u);
+      atomicAdd(&hg[1 * 256 + ((res >> 16) & 0xff)], 1u);
+      atomicAdd(&hg[2 * 256 + ((res >> 8) & 0xff)], 1u);
+      atomicAdd(&hg[3 * 256 + (res & 0xff)], 1u);
+    }
+    wave_lds_sync();
+    if (lane < 4) {  // estimateEntropy's float64 sum, in the reference's order
+      const uint32_t* hc = hg + lane * 256;
+      double ce = fast_slog2(a.lut, count);
+      for (int i = 0; i < 256; i++) {
+        const uint32_t v = hc[i];
+        if (v > 0) ce -= fast_slog2(a.lut, v);
+      }
+      chan_cost[wave][lane] = ce;
+    }
+    wave_lds_sync();
+    if (lane == 0) {
+      double e = 0.0;
+      for (int c = 0; c < 4; c++) e += chan_cost[wave][c];
+      cost[mode] = count == 0 ? 0.0 : e;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int best = 0;
+    double best_cost = 1.7976931348623157e308;
+    for (int m = 0; m < a.max_mode; m++)
+      if (cost[m] < best_cost) {
+        best_cost = cost[m];
+        best = m;
+      }
+    a.modes[(int64_t)img * a.tiles_x * a.tiles_y + tile] = ((uint32_t)best << 8) | ARGB_BLACK;
+  }
+}
+
+struct ResArgs {
+  const uint32_t* argb;
+  const uint32_t* modes;
+  uint32_t* out;
+  int64_t pitch;
+  int width, height, bits, tiles_x, tiles_y;
+};
+
+// copyImageWithPrediction: one thread per pixel, predictions from original
+// pixels; at the right edge TR is the current row's first pixel
+// (upperRow[width]); row 0 / column 0 use black / left / top.
+__global__ __launch_bounds__(256) void k_vp8l_residual(ResArgs a, int64_t total) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const int64_t per = (int64_t)a.width * a.height;
+  const int img = (int)(gid / per);
+  const int64_t p = gid - img * per;
+  const int y = (int)(p / a.width), x = (int)(p - (int64_t)y * a.width);
+  const uint32_t* cur = a.argb + img * a.pitch + (int64_t)y * a.width;
+  uint32_t pred;
+  if (y == 0) {
+    pred = x == 0 ? ARGB_BLACK : cur[x - 1];
+  } else if (x == 0) {
+    pred = cur[-a.width];
+  } else {
+    const uint32_t* up = cur - a.width;
+    const int mode =
+        (int)((a.modes[(int64_t)img * a.tiles_x * a.tiles_y + (y >> a.bits) * a.tiles_x + (x >> a.bits)] >> 8) & 0xff);
+    const uint32_t tr = (x < a.width - 1) ? up[x + 1] : cur[0];
+    pred = predict(mode, cur[x - 1], up[x], tr, up[x - 1]);
+  }
+  a.out[img * a.pitch + p] = sub_pixels(cur[x], pred);
+}
+
+struct InvArgs {
+  const uint32_t* modes;
+  const uint32_t* in;
+  uint32_t* out;
+  int* ctl;       // [0] band dequeue counter, [1] error flag (wait timeout)
+  int* progress;  // [n_img][bands]: columns of the band's last row completed (multiples of 64, or width)
+  int64_t pitch;
+  int width, height, bits, tiles_x, tiles_y, bands, n_img;
+};
+
+constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
+
+// predictorInverseTransform.  Rows depend on the row above (T, TL, TR) and on
+// their own left neighbour.  A wave takes a band of 64 rows and walks it as a
+// diagonal: at step s lane k reconstructs pixel x = s - 2k of row
+// band*64 + k.  The row above comes from the previous lane's last three
+// outputs (lane shift); every value was produced at an earlier step.  Lane 0
+// reads the band above's last row, 64 columns at a time, into LDS once the
+// band above has published them (sc1 stores + progress counter, as in
+// decode.hip).  Bands are dequeued in (band, image) order from a counter, so
+// a band only ever waits on a band owned by a running wave.
+__global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
+  __shared__ uint32_t up_buf[66];  // row above, columns c0-1 .. c0+64
+  __shared__ int sh_band;
+  const int lane = threadIdx.x;
+  const int w = a.width;
+  const int total = a.bands * a.n_img;
+  for (;;) {
+    if (lane == 0) sh_band = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int idx = __builtin_amdgcn_readfirstlane(sh_band);
+    __syncthreads();
+    if (idx >= total) break;
+    const int band = idx / a.n_img, img = idx % a.n_img;
+    const int y = band * 64 + lane;
+    const bool live = y < a.height;
+    const uint32_t* in = a.in + img * a.pitch;
+    uint32_t* out = a.out + img * a.pitch;
+    const int* prog_above = a.progress + img * a.bands + band - 1;
+    int* prog_mine = a.progress + img * a.bands + band;
+    const int last_lane = min(63, a.height - 1 - band * 64);
+    const uint32_t* mrow =
+        a.modes + (int64_t)img * a.tiles_x * a.tiles_y + (int64_t)(min(y, a.height - 1) >> a.bits) * a.tiles_x;
+    uint32_t o1 = 0, o2 = 0, o3 = 0, first = 0;  // this lane's outputs at x-1, x-2, x-3
+    const int steps = w + 2 * last_lane;
+    for (int s = 0; s < steps; s++) {
+      const int x = s - 2 * lane;
+      if (band > 0 && (s & 63) == 0 && s < w) {  // next 64 columns of the band above's last row
+        const int need = min(s + 65, w);
+        int seen = 0;
+        if (lane == 0) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          for (uint32_t it = 0;; it++) {
+            seen = __hip_atomic_load(prog_above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (seen >= need) break;
+            if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+                                    __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+              __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+        const uint32_t* up = out + (int64_t)(band * 64 - 1) * w;
+        const int c = s - 1 + lane;
+        if (c >= 0 && c < w) up_buf[lane] = __hip_atomic_load(up + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane < 2 && s + 63 + lane < w)
+          up_buf[64 + lane] = __hip_atomic_load(up + s + 63 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+      // row-above values from lane-1's previous step: its x+1 (o1), x (o2), x-1 (o3)
+      uint32_t up_x1 = __shfl_up(o1, 1, 64), up_x = __shfl_up(o2, 1, 64), up_xm1 = __shfl_up(o3, 1, 64);
+      if (lane == 0 && band > 0 && x < w) {
+        const int k = x - (s & ~63) + 1;  // == x - c0 + 1
+        up_xm1 = up_buf[k - 1];
+        up_x = up_buf[k];
+        up_x1 = up_buf[k + 1];
+      }
+      if (live && x >= 0 && x < w) {
+        const uint32_t r = in[(int64_t)y * w + x];
+        uint32_t v;
+        if (y == 0) {
+          v = add_pixels(r, x == 0 ? ARGB_BLACK : o1);
+        } else if (x == 0) {
+          v = add_pixels(r, up_x);
+        } else {
+          const int mode = (int)((mrow[x >> a.bits] >> 8) & 0xf);
+          const uint32_t tr = (x < w - 1) ? up_x1 : first;
+          v = add_pixels(r, predict(mode, o1, up_x, tr, up_xm1));
+        }
+        if (x == 0) first = v;
+        o3 = o2;
+        o2 = o1;
+        o1 = v;
+        uint32_t* dst = out + (int64_t)y * w + x;
+        if (lane == last_lane) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *dst = v;
+      } else {
+        o3 = o2;
+        o2 = o1;
+        o1 = 0;
+      }
+      // publish the band's last row every 64 columns (and at its end)
+      const int xl = s - 2 * last_lane;
+      if (band + 1 < a.bands && xl >= 0 && ((xl & 63) == 63 || xl == w - 1)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == last_lane) __hip_atomic_store(prog_mine, xl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_vp8l_green(uint32_t* argb, int64_t n, int add) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = argb[i], g = (p >> 8) & 0xff;
+  const uint32_t r = (p >> 16) & 0xff, b = p & 0xff;
+  const uint32_t r2 = (add ? r + g : r - g) & 0xff, b2 = (add ? b + g : b - g) & 0xff;
+  argb[i] = (p & 0xff00ff00u) | (r2 << 16) | b2;
+}
+
+int subsample(int size, int bits) { return (size + (1 << bits) - 1) >> bits; }
+
+}  // namespace
+
+namespace wg {
+const double* vp8l_slog2_lut_device();  // vp8l_host.cpp
+}
+
+extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32_t height, int64_t image_pitch,
+                                      int32_t bits, int32_t quality, int32_t n_images, uint32_t* modes,
+                                      uint32_t* residuals, void* stream) {
+  WG_REQUIRE(argb && modes && residuals && width > 0 && height > 0 && n_images > 0);
+  WG_REQUIRE(bits >= 2 && bits <= 9 && image_pitch >= (int64_t)width * height);
+  const double* lut = wg::vp8l_slog2_lut_device();
+  if (!lut) return WG_EHIP;
+  hipStream_t s = wg::as_stream(stream);
+  SelArgs sa;
+  sa.argb = argb;
+  sa.pitch = image_pitch;
+  sa.modes = modes;
+  sa.lut = lut;
+  sa.width = width;
+  sa.height = height;
+  sa.bits = bits;
+  sa.tiles_x = subsample(width, bits);
+  sa.tiles_y = subsample(height, bits);
+  sa.max_mode = quality < 25 ? 4 : (quality < 50 ? 8 : 14);
+  const int64_t tiles = (int64_t)sa.tiles_x * sa.tiles_y * n_images;
+  WG_REQUIRE(tiles < (1ll << 31));
+  hipLaunchKernelGGL(k_vp8l_select, dim3((unsigned)tiles), dim3(64 * SEL_WAVES), 0, s, sa);
+  int rc = wg::check_launch("k_vp8l_select");
+  if (rc != WG_OK) return rc;
+  ResArgs ra;
+  ra.argb = argb;
+  ra.modes = modes;
+  ra.out = residuals;
+  ra.pitch = image_pitch;
+  ra.width = width;
+  ra.height = height;
+  ra.bits = bits;
+  ra.tiles_x = sa.tiles_x;
+  ra.tiles_y = sa.tiles_y;
+  const int64_t total = (int64_t)width * height * n_images;
+  hipLaunchKernelGGL(k_vp8l_residual, dim3(wg::blocks_for(total, 256)), dim3(256), 0, s, ra, total);
+  return wg::check_launch("k_vp8l_residual");
+}
+
+extern "C" size_t wg_vp8l_inverse_work_bytes(int32_t height, int32_t n_images) {
+  if (height <= 0 || n_images <= 0) return 0;
+  return sizeof(int) * ((size_t)n_images * ((height + 63) / 64) + 4);
+}
+
+extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, int32_t width, int32_t height,
+                                         int64_t image_pitch, int32_t n_images, const uint32_t* residuals,
+                                         uint32_t* out, void* work, void* stream) {
+  WG_REQUIRE(modes && residuals && out && work && width > 0 && height > 0 && n_images > 0);
+  WG_REQUIRE(bits >= 2 && bits <= 9 && image_pitch >= (int64_t)width * height);
+  hipStream_t s = wg::as_stream(stream);
+  InvArgs a;
+  a.modes = modes;
+  a.in = residuals;
+  a.out = out;
+  a.bands = (height + 63) / 64;
+  a.n_img = n_images;
+  a.ctl = static_cast<int*>(work);
+  a.progress = a.ctl + 4;
+  a.pitch = image_pitch;
+  a.width = width;
+  a.height = height;
+  a.bits = bits;
+  a.tiles_x = subsample(width, bits);
+  a.tiles_y = subsample(height, bits);
+  if (hipMemsetAsync(work, 0, wg_vp8l_inverse_work_bytes(height, n_images), s) != hipSuccess)
+    return wg::check_launch("hipMemsetAsync(vp8l work)");
+  const int total = a.bands * n_images;
+  const int grid = total < 2048 ? total : 2048;
+  hipLaunchKernelGGL(k_vp8l_inverse, dim3((unsigned)grid), dim3(64), 0, s, a);
+  return wg::check_launch("k_vp8l_inverse");
+}
+
+extern "C" int wg_vp8l_inverse_status(const void* work, void* stream) {
+  WG_REQUIRE(work);
+  int flag = 0;
+  hipStream_t s = wg::as_stream(stream);
+  if (hipMemcpyAsync(&flag, static_cast<const int*>(work) + 1, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return wg::check_launch("wg_vp8l_inverse_status");
+  if (flag) {
+    wg::set_error("vp8l inverse: a band dependency wait timed out (output invalid)");
+    return WG_EHIP;
+  }
+  return WG_OK;
+}
+
+extern "C" int wg_vp8l_green(uint32_t* argb, int64_t n, int32_t add, void* stream) {
+  WG_REQUIRE(argb && n >= 0);
+  if (n == 0) return WG_OK;
+  hipLaunchKernelGGL(k_vp8l_green, dim3(wg::blocks_for(n, 256)), dim3(256), 0, wg::as_stream(stream), argb, n,
+                     add ? 1 : 0);
+  return wg::check_launch("k_vp8l_green");
+}
