@@ -1,0 +1,62 @@
+"""C5 stages on one GPU (BASELINE.json configs[4]: 4096x4096 RGBA lossless
+predictor + SharpYUV + SSIM; the 8-GPU run shards images): per-stage device
+time with HIP events on the current stream and the HBM roofline fraction of
+each kernel from its algorithmic bytes.  Prints one JSON line."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from tools import synth  # noqa: E402
+from webp_amd import frames, lossless as L  # noqa: E402
+
+N = int(os.environ.get("N", "4096"))
+REPS = int(os.environ.get("REPS", "10"))
+PEAK = 8000.0
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(REPS):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts))
+
+
+def main():
+    rgba = synth.blobs_rgba(N, N, seed=5, alpha=True).astype(np.uint32)
+    argb = (rgba[..., 3] << 24) | (rgba[..., 0] << 16) | (rgba[..., 1] << 8) | rgba[..., 2]
+    t = L.to_argb_tensor(argb[None])
+    px = N * N
+    out = {}
+    ms = timed(lambda: L.SubtractGreen(t))
+    out["subtract_green"] = {"ms": ms, "GB/s": 8 * px / ms / 1e6}
+    modes, res = L.ResidualImage(t, 5, 75)
+    ms = timed(lambda: L.ResidualImage(t, 5, 75, out=(modes, res)))
+    out["residual_image"] = {"ms": ms, "MPix/s": px / ms / 1e3, "GB/s": 8 * px / ms / 1e6}
+    inv = torch.empty_like(res)
+    ms = timed(lambda: L.predictor_inverse(modes, 5, res, out=inv))
+    out["inverse_predictor"] = {"ms": ms, "MPix/s": px / ms / 1e3, "GB/s": 8 * px / ms / 1e6}
+    y = torch.from_numpy(rgba[..., 1].astype(np.uint8)).cuda().unsqueeze(0)
+    y2 = torch.clamp(y.int() + torch.randint(-8, 9, y.shape, device="cuda", dtype=torch.int32), 0, 255).to(torch.uint8)
+    ms = timed(lambda: frames.plane_ssim(y, y2))
+    out["plane_ssim"] = {"ms": ms, "MPix/s": px / ms / 1e3, "GB/s": 2 * px / ms / 1e6}
+    for v in out.values():
+        if "GB/s" in v:
+            v["frac"] = v["GB/s"] / PEAK
+        for k in list(v):
+            v[k] = round(v[k], 4)
+    print(json.dumps({"config": f"C5 {N}x{N} RGBA, bits 5, q75, 1 GPU", "stages": out}))
+
+
+if __name__ == "__main__":
+    main()
