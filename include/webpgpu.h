@@ -210,6 +210,24 @@ int wg_vp8l_green(uint32_t* argb, int64_t n, int32_t add, void* stream);
 /* The fastSLog2 table (encode_histogram.go:359-368) the selection uses, host copy. */
 int wg_vp8l_slog2_lut_host(double* out, int32_t n);
 
+/* ===================================================================== *
+ * 4. SharpYUV: sharpyuv.Convert with SharpEnabled and the
+ *    sRGB transfer (sharpyuv/sharpyuv.go:39-64, convertSharp :170-269).
+ * ===================================================================== */
+
+/* rgb: packed 8-bit RGB (3 bytes per pixel), row stride rgb_stride, image
+ * pitch rgb_pitch.  matrix_host: 12 ints (HOST memory), ConversionMatrix
+ * RGBToY[4], RGBToU[4], RGBToV[4] (sharpyuv/csp.go:62-90; WebP's matrix is
+ * what the encoder uses).  Outputs Y (stride y_stride, pitch y_pitch) and
+ * U / V ((width+1)/2 x (height+1)/2, stride uv_stride, pitch uv_pitch).
+ * `work`: wg_sharpyuv_work_bytes(width, height, n_images).  width <= 16384. */
+size_t wg_sharpyuv_work_bytes(int32_t width, int32_t height, int32_t n_images);
+int wg_sharpyuv_convert(const uint8_t* rgb, int32_t width, int32_t height, int32_t rgb_stride, int64_t rgb_pitch,
+                        const int32_t* matrix_host, int32_t n_images, uint8_t* y, int32_t y_stride, int64_t y_pitch,
+                        uint8_t* u, uint8_t* v, int32_t uv_stride, int64_t uv_pitch, void* work, void* stream);
+/* The gamma tables used (gamma.go:48-88), host copies: g2l[1026], l2g[514]. */
+int wg_sharpyuv_tables_host(uint32_t* g2l, uint32_t* l2g);
+
 #ifdef __cplusplus
 }
 #endif

@@ -104,6 +104,9 @@ _SIGS = {
     "or_vp8l_inverse_predictor": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
     "or_vp8l_subtract_green": (None, [ctypes.c_void_p, ctypes.c_size_t]),
     "or_vp8l_add_green": (None, [ctypes.c_void_p, ctypes.c_size_t]),
+    "or_sharpyuv_tables": (None, [ctypes.c_void_p, ctypes.c_void_p]),
+    "or_sharpyuv_convert": (_i, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i, ctypes.c_void_p, ctypes.c_void_p, _i,
+                                 ctypes.c_void_p]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
@@ -236,3 +239,30 @@ def vp8l_subtract_green(argb):
     a = np.ascontiguousarray(argb, np.uint32).copy()
     lib.or_vp8l_subtract_green(a.ctypes.data, a.size)
     return a
+
+
+# ---------------- SharpYUV ----------------
+
+WEBP_MATRIX = np.array([16839, 33059, 6420, 16 << 16, -9719, -19081, 28800, 128 << 16,
+                        28800, -24116, -4684, 128 << 16], np.int32)  # sharpyuv/csp.go:66-70
+
+
+def sharpyuv_convert(rgb, matrix=WEBP_MATRIX):
+    """convertSharp: rgb (h, w, 3) uint8 -> (Y (h, w), U, V ((h+1)//2, (w+1)//2), iterations)."""
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    h, w, _ = rgb.shape
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    Y = np.zeros((h, w), np.uint8)
+    U = np.zeros((ch, cw), np.uint8)
+    V = np.zeros((ch, cw), np.uint8)
+    m = np.ascontiguousarray(matrix, np.int32)
+    it = lib.or_sharpyuv_convert(rgb.ctypes.data, w, h, 3 * w, Y.ctypes.data, w, U.ctypes.data, V.ctypes.data, cw,
+                                 m.ctypes.data)
+    return Y, U, V, it
+
+
+def sharpyuv_tables():
+    g = np.zeros(1026, np.uint32)
+    l = np.zeros(514, np.uint32)  # noqa: E741
+    lib.or_sharpyuv_tables(g.ctypes.data, l.ctypes.data)
+    return g, l

@@ -157,6 +157,11 @@ void or_vp8l_inverse_predictor(const uint32_t* modes, int bits, int width, int h
 void or_vp8l_subtract_green(uint32_t* argb, size_t n);
 void or_vp8l_add_green(uint32_t* argb, size_t n);
 
+/* ---- SharpYUV (sharpyuv.c; sharpyuv/sharpyuv.go, gamma.go) ---- */
+void or_sharpyuv_tables(uint32_t* g2l_out /* 1026 */, uint32_t* l2g_out /* 514 */);
+int or_sharpyuv_convert(const uint8_t* rgb, int width, int height, int rgb_stride, uint8_t* y, int y_stride,
+                        uint8_t* u, uint8_t* v, int uv_stride, const int32_t* matrix /* 12 */);
+
 #ifdef __cplusplus
 }
 #endif

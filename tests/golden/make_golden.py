@@ -62,6 +62,7 @@ def main():
     out["ssim_value2"] = np.array([L.plane_ssim(g, out["ssim_d"])], np.float64)
     np.savez_compressed(os.path.join(HERE, "libwebp_fixtures.npz"), **out)
     make_decode_fixtures(img)
+    make_sharpyuv_fixtures(img)
     print("wrote", os.path.join(HERE, "libwebp_fixtures.npz"), sum(v.nbytes for v in out.values()), "bytes raw")
 
 
@@ -95,6 +96,25 @@ def make_decode_fixtures(img):
         out[name + "_webp"] = np.frombuffer(data, np.uint8).copy()
         out[name + "_y"], out[name + "_u"], out[name + "_v"] = Y, U, V
     path = os.path.join(HERE, "libwebp_decode.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def make_sharpyuv_fixtures(img):
+    """libsharpyuv 0.4.2 SharpYuvConvert (WebP matrix, sRGB, 8-bit) outputs:
+    the C library the reference's testc/sharpyuv compares its Go code with."""
+    webp_matrix = np.array([16839, 33059, 6420, 16 << 16, -9719, -19081, 28800, 128 << 16,
+                            28800, -24116, -4684, 128 << 16], np.int32)
+    cases = [("s_photo", img[100:196, 200:328, :3]), ("s_odd", img[300:337, 50:103, :3]),
+             ("s_noise", synth.noise_rgba(61, 45, seed=11)[..., :3]), ("s_grad", synth.gradient_rgba(128, 64)[..., :3]),
+             ("s_2x2", np.array([[[255, 0, 0], [0, 255, 0]], [[0, 0, 255], [255, 255, 0]]], np.uint8)),
+             ("s_1x1", img[10:11, 10:11, :3]), ("s_3x5", img[20:25, 40:43, :3])]
+    out = {}
+    for name, rgb in cases:
+        rgb = np.ascontiguousarray(rgb)
+        Y, U, V = L.sharpyuv_convert(rgb, webp_matrix)
+        out[name + "_rgb"], out[name + "_y"], out[name + "_u"], out[name + "_v"] = rgb, Y, U, V
+    path = os.path.join(HERE, "libsharpyuv_fixtures.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes")
 

@@ -190,3 +190,34 @@ def encode_lossy_cfg(rgba, quality=75.0, **fields):
     lib.WebPPictureFree(pic)
     assert ok, "WebPEncode failed"
     return data
+
+
+# libsharpyuv 0.4.2 (Pillow's copy): SharpYuvConvert, the C library the
+# reference's testc/sharpyuv compares its Go SharpYUV against (tolerance +-1).
+sharp = None
+if _SHARP:
+    try:
+        sharp = ctypes.CDLL(_SHARP[0])
+        sharp.SharpYuvInit.argtypes = [ctypes.c_void_p]
+        sharp.SharpYuvConvert.restype = ctypes.c_int
+        sharp.SharpYuvConvert.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_int] * 3 + \
+            [ctypes.c_int] * 3 + [ctypes.c_void_p]
+        sharp.SharpYuvInit(None)
+    except (OSError, AttributeError):
+        sharp = None
+
+
+def sharpyuv_convert(rgb, matrix):
+    """SharpYuvConvert on packed RGB (h, w, 3) -> (Y, U, V) 8-bit planes."""
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    h, w, _ = rgb.shape
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    Y = np.zeros((h, w), np.uint8)
+    U = np.zeros((ch, cw), np.uint8)
+    V = np.zeros((ch, cw), np.uint8)
+    m = np.ascontiguousarray(matrix, np.int32)
+    base = rgb.ctypes.data
+    ok = sharp.SharpYuvConvert(base, base + 1, base + 2, 3, 3 * w, 8, Y.ctypes.data, w, U.ctypes.data, cw,
+                               V.ctypes.data, cw, 8, w, h, m.ctypes.data)
+    assert ok
+    return Y, U, V

@@ -1,0 +1,84 @@
+"""SharpYUV.
+
+CPU: the C restatement (oracle/sharpyuv.c) against libsharpyuv 0.4.2 fixtures
+(tests/golden/libsharpyuv_fixtures.npz) -- the reference's own testc accepts
++-1 against that library; the restatement matches it exactly on every
+fixture, so the tests require exact equality.  The product's host gamma
+tables equal the oracle's.
+GPU (-m gpu): wg_sharpyuv_convert == oracle, bit-exact, on odd / tiny /
+batched / 1080p / 4096-wide images."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from tools import synth
+
+FIX = np.load(os.path.join(os.path.dirname(__file__), "golden", "libsharpyuv_fixtures.npz"))
+NAMES = sorted({k[:-4] for k in FIX.files if k.endswith("_rgb")})
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_vs_libsharpyuv(name):
+    y, u, v, _ = O.sharpyuv_convert(FIX[name + "_rgb"])
+    assert (y == FIX[name + "_y"]).all() and (u == FIX[name + "_u"]).all() and (v == FIX[name + "_v"]).all()
+
+
+def test_gamma_tables_product_equals_oracle():
+    from webp_amd._lib import call
+    g, l = np.zeros(1026, np.uint32), np.zeros(514, np.uint32)  # noqa: E741
+    call("wg_sharpyuv_tables_host", g.ctypes.data, l.ctypes.data)
+    og, ol = O.sharpyuv_tables()
+    assert (g == og).all() and (l == ol).all()
+    assert g[0] == 0 and g[1024] == 65536 and l[512] == 65536 and (np.diff(g.astype(np.int64)) >= 0).all()
+
+
+def rgb_cases():
+    rng = np.random.default_rng(4)
+    yield "1x1", rng.integers(0, 256, (1, 1, 3), dtype=np.uint8)
+    yield "2x1", rng.integers(0, 256, (1, 2, 3), dtype=np.uint8)
+    yield "3x5", rng.integers(0, 256, (5, 3, 3), dtype=np.uint8)
+    yield "noise", rng.integers(0, 256, (37, 53, 3), dtype=np.uint8)
+    yield "grad", np.ascontiguousarray(synth.gradient_rgba(96, 70)[..., :3])
+    yield "blobs", np.ascontiguousarray(synth.blobs_rgba(130, 66, seed=3)[..., :3])
+    yield "flat", np.full((16, 16, 3), 77, np.uint8)
+
+
+@pytest.mark.gpu
+def test_gpu_matches_oracle(cuda):
+    import torch
+    from webp_amd import frames
+    for name, rgb in rgb_cases():
+        Y, U, V = frames.sharpyuv_convert(torch.from_numpy(rgb[None].copy()).cuda())
+        ey, eu, ev, _ = O.sharpyuv_convert(rgb)
+        torch.cuda.synchronize()
+        assert (Y[0].cpu().numpy() == ey).all(), name
+        assert (U[0].cpu().numpy() == eu).all() and (V[0].cpu().numpy() == ev).all(), name
+
+
+@pytest.mark.gpu
+def test_gpu_fixtures_and_batch(cuda):
+    import torch
+    from webp_amd import frames
+    for name in NAMES:
+        Y, U, V = frames.sharpyuv_convert(torch.from_numpy(FIX[name + "_rgb"][None].copy()).cuda())
+        assert (Y[0].cpu().numpy() == FIX[name + "_y"]).all(), name
+        assert (U[0].cpu().numpy() == FIX[name + "_u"]).all() and (V[0].cpu().numpy() == FIX[name + "_v"]).all()
+    imgs = np.stack([synth.noise_rgba(45, 33, seed=s)[..., :3] for s in range(3)])
+    Y, U, V = frames.sharpyuv_convert(torch.from_numpy(imgs).cuda())
+    for i in range(3):
+        ey, eu, ev, _ = O.sharpyuv_convert(imgs[i])
+        assert (Y[i].cpu().numpy() == ey).all() and (U[i].cpu().numpy() == eu).all() and (V[i].cpu().numpy() == ev).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h", [(1920, 1080), (4096, 256), (4100, 40)])
+def test_gpu_wide(cuda, w, h):
+    """1080p, the C5 width (4096), and a width past 4096 (the 8-column path)."""
+    import torch
+    from webp_amd import frames
+    rgb = np.ascontiguousarray(synth.blobs_rgba(w, h, seed=w)[..., :3])
+    Y, U, V = frames.sharpyuv_convert(torch.from_numpy(rgb[None].copy()).cuda())
+    ey, eu, ev, _ = O.sharpyuv_convert(rgb)
+    assert (Y[0].cpu().numpy() == ey).all() and (U[0].cpu().numpy() == eu).all() and (V[0].cpu().numpy() == ev).all()

@@ -46,6 +46,11 @@ def main():
     inv = torch.empty_like(res)
     ms = timed(lambda: L.predictor_inverse(modes, 5, res, out=inv))
     out["inverse_predictor"] = {"ms": ms, "MPix/s": px / ms / 1e3, "GB/s": 8 * px / ms / 1e6}
+    rgb = torch.from_numpy(np.ascontiguousarray(rgba[..., :3].astype(np.uint8))).cuda().unsqueeze(0)
+    Ys, Us, Vs = frames.sharpyuv_convert(rgb)
+    work = torch.empty(frames.lib.wg_sharpyuv_work_bytes(N, N, 1), dtype=torch.uint8, device="cuda")
+    ms = timed(lambda: frames.sharpyuv_convert(rgb, out=(Ys, Us, Vs), work=work))
+    out["sharpyuv"] = {"ms": ms, "MPix/s": px / ms / 1e3, "GB/s": 4.5 * px / ms / 1e6}
     y = torch.from_numpy(rgba[..., 1].astype(np.uint8)).cuda().unsqueeze(0)
     y2 = torch.clamp(y.int() + torch.randint(-8, 9, y.shape, device="cuda", dtype=torch.int32), 0, 255).to(torch.uint8)
     ms = timed(lambda: frames.plane_ssim(y, y2))

@@ -129,3 +129,27 @@ def vp8_parse(data):
     call("wg_vp8_parse", buf.ctypes.data, buf.size, dims.ctypes.data, mb.ctypes.data, co.ctypes.data, n)
     keys = ("width", "height", "filter_type", "mbw", "mbh")
     return {k: int(v) for k, v in zip(keys, dims)}, mb, co
+
+
+WEBP_MATRIX = np.array([16839, 33059, 6420, 16 << 16, -9719, -19081, 28800, 128 << 16,
+                        28800, -24116, -4684, 128 << 16], np.int32)  # sharpyuv/csp.go:66-70
+
+
+def sharpyuv_convert(rgb, matrix=WEBP_MATRIX, out=None, work=None):
+    """sharpyuv.Convert (SharpEnabled, sRGB): (n, h, w, 3) uint8 RGB -> Y (n, h, w),
+    U, V (n, (h+1)//2, (w+1)//2)."""
+    assert rgb.is_cuda and rgb.dtype == torch.uint8 and rgb.dim() == 4 and rgb.is_contiguous()
+    n, h, w, _ = rgb.shape
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    if out is None:
+        Y = torch.empty((n, h, w), dtype=torch.uint8, device=rgb.device)
+        U = torch.empty((n, ch, cw), dtype=torch.uint8, device=rgb.device)
+        V = torch.empty_like(U)
+    else:
+        Y, U, V = out
+    if work is None:
+        work = torch.empty(lib.wg_sharpyuv_work_bytes(w, h, n), dtype=torch.uint8, device=rgb.device)
+    m = np.ascontiguousarray(matrix, np.int32)
+    call("wg_sharpyuv_convert", rgb.data_ptr(), w, h, 3 * w, 3 * w * h, m.ctypes.data, n, Y.data_ptr(), w, h * w,
+         U.data_ptr(), V.data_ptr(), cw, cw * ch, work.data_ptr(), _stream())
+    return Y, U, V
