@@ -105,6 +105,9 @@ _SIGS = {
     "or_vp8l_subtract_green": (None, [ctypes.c_void_p, ctypes.c_size_t]),
     "or_vp8l_add_green": (None, [ctypes.c_void_p, ctypes.c_size_t]),
     "or_sharpyuv_tables": (None, [ctypes.c_void_p, ctypes.c_void_p]),
+    "or_setup_segment": (None, [_i] * 8 + [ctypes.c_void_p]),
+    "or_fixed_costs_i4": (None, [ctypes.c_void_p]),
+    "or_encode_frame_rd": (None, [ctypes.c_void_p] * 3 + [_i] * 4 + [ctypes.c_void_p] * 3 + [_i, _i, ctypes.c_void_p]),
     "or_sharpyuv_convert": (_i, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i, ctypes.c_void_p, ctypes.c_void_p, _i,
                                  ctypes.c_void_p]),
 }
@@ -266,3 +269,46 @@ def sharpyuv_tables():
     l = np.zeros(514, np.uint32)  # noqa: E741
     lib.or_sharpyuv_tables(g.ctypes.data, l.ctypes.data)
     return g, l
+
+
+# ---------------- encoder MB RD loop (Phase A) ----------------
+
+SQUANT_DTYPE = np.dtype([("quant", "<i4"), ("iquant", "<i4"), ("bias", "<i4"), ("zthresh", "<i4"),
+                         ("dc_quant", "<i4"), ("dc_iquant", "<i4"), ("dc_bias", "<i4"), ("dc_zthresh", "<i4"),
+                         ("sharpen", "<i2", (16,))])
+SEGMENT_DTYPE = np.dtype([("y1", SQUANT_DTYPE), ("y2", SQUANT_DTYPE), ("uv", SQUANT_DTYPE),
+                          ("lambda_i4", "<i4"), ("lambda_i16", "<i4"), ("lambda_uv", "<i4"), ("lambda_mode", "<i4"),
+                          ("tlambda_i4", "<i4"), ("tlambda_i16", "<i4"), ("tlambda_uv", "<i4"), ("tlambda_sd", "<i4")])
+MB_ENC_DTYPE = np.dtype([("coeffs", "<i2", (400,)), ("modes", "u1", (16,)), ("nz_y", "u1", (16,)),
+                         ("nz_uv", "u1", (8,)), ("non_zero_y", "<u4"), ("non_zero_uv", "<u4"),
+                         ("mb_type", "u1"), ("i16_mode", "u1"), ("uv_mode", "u1"), ("nz_dc", "u1"),
+                         ("skip", "u1"), ("segment", "u1"), ("pad", "u1", (2,)), ("score", "<u8")])
+assert SQUANT_DTYPE.itemsize == 64 and SEGMENT_DTYPE.itemsize == 224 and MB_ENC_DTYPE.itemsize == 864
+
+
+def setup_segment(q, dq=(0, 0, 0, 0, 0), method=4, sns_strength=50):
+    seg = np.zeros(1, SEGMENT_DTYPE)
+    lib.or_setup_segment(q, *dq, method, sns_strength, seg.ctypes.data)
+    return seg[0]
+
+
+def default_proba():
+    """CoeffsProba0 (internal/lossy/proba.go:45), the tables Phase A uses after ResetProba."""
+    import re
+    txt = open(os.path.join(_HERE, "vp8_tables.h")).read()
+    body = txt[txt.index("vp8_coeffs_proba0["):]
+    body = body[body.index("{") + 1:body.index("};")]
+    return np.array([int(x) for x in re.findall(r"\d+", body)], np.uint8)
+
+
+def encode_frame_rd(Y, U, V, width, height, segments, segs, proba, method=4, quality=75):
+    """Phase A over one frame: returns (mb_enc array (mbh*mbw,), reconstructed Y, U, V)."""
+    Y, U, V = (np.ascontiguousarray(p, np.uint8).copy() for p in (Y, U, V))
+    mbw, mbh = Y.shape[1] // 16, Y.shape[0] // 16
+    out = np.zeros(mbw * mbh, MB_ENC_DTYPE)
+    seg_ids = np.ascontiguousarray(segments, np.uint8)
+    segs = np.ascontiguousarray(segs, SEGMENT_DTYPE)
+    proba = np.ascontiguousarray(proba, np.uint8)
+    lib.or_encode_frame_rd(Y.ctypes.data, U.ctypes.data, V.ctypes.data, width, height, mbw, mbh, seg_ids.ctypes.data,
+                           segs.ctypes.data, proba.ctypes.data, method, quality, out.ctypes.data)
+    return out, Y, U, V

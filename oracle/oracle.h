@@ -157,6 +157,35 @@ void or_vp8l_inverse_predictor(const uint32_t* modes, int bits, int width, int h
 void or_vp8l_subtract_green(uint32_t* argb, size_t n);
 void or_vp8l_add_green(uint32_t* argb, size_t n);
 
+/* ---- Encoder MB RD loop (lossy_rd.c; encode_parallel.go Phase A) ---- */
+typedef struct {          /* SegmentQuant (encode.go:311-323) */
+  int32_t quant, iquant, bias, zthresh;
+  int32_t dc_quant, dc_iquant, dc_bias, dc_zthresh;
+  int16_t sharpen[16];
+} or_squant;              /* 64 bytes */
+typedef struct {          /* SegmentInfo fields Phase A reads (encode.go:278-309) */
+  or_squant y1, y2, uv;
+  int32_t lambda_i4, lambda_i16, lambda_uv, lambda_mode;
+  int32_t tlambda_i4, tlambda_i16, tlambda_uv, tlambda_sd;
+} or_segment;             /* 224 bytes */
+typedef struct {          /* MBEncInfo (encode.go:241-276), Phase A outputs */
+  int16_t coeffs[400];    /* 16 Y, 4 U, 4 V blocks (raster), then the WHT DC block */
+  uint8_t modes[16];
+  uint8_t nz_y[16];
+  uint8_t nz_uv[8];
+  uint32_t non_zero_y;    /* bit b: Y block b has a non-zero level; bit 24: DC block */
+  uint32_t non_zero_uv;   /* bit ch*4+b */
+  uint8_t mb_type, i16_mode, uv_mode, nz_dc;
+  uint8_t skip, segment, pad0, pad1;
+  uint64_t score;
+} or_mb_enc;              /* 864 bytes */
+void or_setup_segment(int q, int dq_y1_dc, int dq_y2_dc, int dq_y2_ac, int dq_uv_dc, int dq_uv_ac, int method,
+                      int sns_strength, or_segment* seg);
+void or_fixed_costs_i4(uint16_t* out /* [10][10][10] */);
+void or_encode_frame_rd(uint8_t* y, uint8_t* u, uint8_t* v, int width, int height, int mbw, int mbh,
+                        const uint8_t* segments, const or_segment* segs, const uint8_t* proba, int method,
+                        int quality, or_mb_enc* out);
+
 /* ---- SharpYUV (sharpyuv.c; sharpyuv/sharpyuv.go, gamma.go) ---- */
 void or_sharpyuv_tables(uint32_t* g2l_out /* 1026 */, uint32_t* l2g_out /* 514 */);
 int or_sharpyuv_convert(const uint8_t* rgb, int width, int height, int rgb_stride, uint8_t* y, int y_stride,

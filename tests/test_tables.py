@@ -22,6 +22,9 @@ def test_tables_match_reference_source():
     srcs = {f: G.strip_comments(open(os.path.join(G.REF, f)).read()) for f in ("constants.go", "proba.go")}
     syms = G.symbols(srcs["constants.go"])
     tabs = [(c, t, G.values(srcs[f], g, syms)) for f, g, c, t in G.TABLES]
+    for f, g, c, t in G.ENC_TABLES:
+        src = G.strip_comments(open(os.path.join(os.path.dirname(G.REF), f)).read())
+        tabs.append((c, t, G.values(src, g, syms)))
     txt = open(os.path.join(ROOT, "webp_amd", "csrc", "vp8_tables.h")).read()
     for cname, ctype, vals in tabs:
         start = txt.index(f"{cname}[")
