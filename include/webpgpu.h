@@ -144,6 +144,48 @@ int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int32_t filter
 int wg_vp8_parse(const uint8_t* data, size_t size, int32_t* dims, wg_mb_info* mb, int16_t* coeffs,
                  int64_t max_mbs);
 
+/* Encoder macroblock RD loop: Phase A of encodeFrameParallel
+ * (internal/lossy/encode_parallel.go:168-1495; encodeRow :252-338), method
+ * >= 4 (methods 4-6 run the same Phase A; method 3 returns WG_EINVAL).
+ * y/u/v: the encoder's padded planes (importImage output: Y stride 16*mbw,
+ * U/V 8*mbw), pitches per image.  segments: per-MB segment id (NULL = all 0).
+ * segs: 4 x wg_segment (device).  proba: the 4x8x3x11 coefficient
+ * probabilities Phase A prices tokens with (device; ResetProba gives
+ * CoeffsProba0).  out: n_images*mbw*mbh wg_mb_enc.  ry/ru/rv receive the
+ * reconstruction (exportParallel writes it over the source planes; passing
+ * the source pointers does the same).  work: wg_encode_work_bytes(). */
+typedef struct wg_squant {  /* SegmentQuant, internal/lossy/encode.go:311-323 */
+  int32_t quant, iquant, bias, zthresh;
+  int32_t dc_quant, dc_iquant, dc_bias, dc_zthresh;
+  int16_t sharpen[16];
+} wg_squant;
+typedef struct wg_segment { /* SegmentInfo fields Phase A reads, encode.go:278-309 */
+  wg_squant y1, y2, uv;
+  int32_t lambda_i4, lambda_i16, lambda_uv, lambda_mode;
+  int32_t tlambda_i4, tlambda_i16, tlambda_uv, tlambda_sd;
+} wg_segment;
+typedef struct wg_mb_enc {  /* MBEncInfo, encode.go:241-276 (Phase A outputs) */
+  int16_t coeffs[400];      /* levels: 16 Y, 4 U, 4 V blocks (raster), then the I16 WHT block */
+  uint8_t modes[16];        /* I4 modes */
+  uint8_t nz_y[16];         /* zigzag nz count per block */
+  uint8_t nz_uv[8];
+  uint32_t non_zero_y;      /* bit b: Y block b non-zero; bit 24: WHT block */
+  uint32_t non_zero_uv;
+  uint8_t mb_type;          /* 0 I16, 1 I4 */
+  uint8_t i16_mode, uv_mode, nz_dc, skip, segment, pad0, pad1;
+  uint64_t score;
+} wg_mb_enc;
+/* setupSegment (encode.go:1085-1181) for quantiser index q and the frame's
+ * dq deltas {y1_dc, y2_dc, y2_ac, uv_dc, uv_ac}; host memory. */
+int wg_setup_segment(int32_t q, const int32_t* dq5, int32_t method, int32_t sns_strength, wg_segment* out);
+size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images);
+int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t y_pitch, int64_t uv_pitch,
+                  int32_t width, int32_t height, int32_t n_images, const uint8_t* segments, const void* segs,
+                  const uint8_t* proba, int32_t method, int32_t quality, void* out, uint8_t* ry, uint8_t* ru,
+                  uint8_t* rv, void* work, void* stream);
+/* After wg_encode_mbs on the same stream: WG_OK or WG_EHIP on a row-wait timeout.  Synchronises. */
+int wg_encode_status(const void* work, int32_t mbw, int32_t n_images, void* stream);
+
 /* After wg_decode_frames on the same stream: WG_OK, or WG_EHIP if a row
  * dependency wait timed out inside the kernel (output invalid).  Synchronises
  * the stream. */

@@ -63,10 +63,15 @@ SIGNATURES = {
     "wg_sharpyuv_work_bytes": [_i32, _i32, _i32],
     "wg_sharpyuv_convert": [_vp, _i32, _i32, _i32, _i64, _vp, _i32, _vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _vp],
     "wg_sharpyuv_tables_host": [_vp, _vp],
+    "wg_setup_segment": [_i32, _vp, _i32, _i32, _vp],
+    "wg_encode_work_bytes": [_i32, _i32, _i32],
+    "wg_encode_mbs": [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
+                      _vp],
+    "wg_encode_status": [_vp, _i32, _i32, _vp],
 }
 _RES = {"wg_last_error": ctypes.c_char_p, "wg_decode_work_bytes": ctypes.c_size_t,
         "wg_plane_ssim_work_bytes": ctypes.c_size_t, "wg_vp8l_inverse_work_bytes": ctypes.c_size_t,
-        "wg_sharpyuv_work_bytes": ctypes.c_size_t}
+        "wg_sharpyuv_work_bytes": ctypes.c_size_t, "wg_encode_work_bytes": ctypes.c_size_t}
 
 for _name, _args in SIGNATURES.items():
     _f = getattr(lib, _name)

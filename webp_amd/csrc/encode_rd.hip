@@ -1,0 +1,1141 @@
+// encode_rd.hip -- the encoder's macroblock RD loop on gfx950 (SURVEY.md
+// 8(a) A20): Phase A of encodeFrameParallel (internal/lossy/
+// encode_parallel.go:168-1495), method >= 4, for whole frames.
+//
+// Schedule: like decode.hip, one persistent launch; each 64-lane workgroup
+// dequeues a macroblock ROW (ordered counter over (row, image)) and walks it
+// left to right exactly as the reference's encodeRow does, with row y
+// allowed to start MB x once row y-1 has finished MB x+1 (:286-295).  The
+// shared top arrays of the reference (topY/U/V, topModes, topNz, topNzDC)
+// become one 48-byte record per MB column, handed down with sc1 stores +
+// a progress counter; the left context stays in LDS.
+//
+// Inside a macroblock the lanes take the reference's independent loops:
+//   I16 RD     lane = (mode, block): 4 x 16 blocks predicted, transformed,
+//              quantised, costed and reconstructed at once; contexts from the
+//              neighbours' nz (exchanged in LDS); one lane per mode runs the
+//              DC WHT path; per-mode sums reduced with lane shuffles
+//   UV RD      lane = (mode, plane, block): 4 x 8 blocks
+//   I4 RD      the 16 blocks stay sequential (each predicts from its
+//              reconstructed neighbours); per block, lanes 0-9 pre-screen the
+//              10 modes, lanes 0..K-1 run the K trellis candidates at once
+//   final      I16 AC blocks trellis-quantised along the 7 block diagonals
+//              (each needs its left / top neighbour's nz), DC and chroma in
+//              parallel, then reconstruction and export
+// All integer; bit-exact with the C restatement (oracle/lossy_rd.c).
+#include "vp8_tables.h"
+#include "wg_common.h"
+#include "wg_dsp.h"
+
+namespace {
+
+using namespace wg;
+
+constexpr int BPS = 32;
+constexpr int YOFF = BPS * 1 + 8;
+constexpr int UOFF = YOFF + BPS * 16 + BPS;
+constexpr int VOFF = UOFF + 16;
+constexpr int YUV = BPS * 17 + BPS * 9;
+constexpr int REC = 48;  // per MB column hand-off record
+
+struct SQuant {  // SegmentQuant (encode.go:311-323); layout = wg_squant
+  int32_t quant, iquant, bias, zthresh;
+  int32_t dc_quant, dc_iquant, dc_bias, dc_zthresh;
+  int16_t sharpen[16];
+};
+struct Segment {  // = wg_segment
+  SQuant y1, y2, uv;
+  int32_t lambda_i4, lambda_i16, lambda_uv, lambda_mode;
+  int32_t tlambda_i4, tlambda_i16, tlambda_uv, tlambda_sd;
+};
+static_assert(sizeof(SQuant) == 64 && sizeof(Segment) == 224, "segment layout");
+
+struct MbEnc {  // = wg_mb_enc (MBEncInfo subset)
+  int16_t coeffs[400];
+  uint8_t modes[16];
+  uint8_t nz_y[16];
+  uint8_t nz_uv[8];
+  uint32_t non_zero_y, non_zero_uv;
+  uint8_t mb_type, i16_mode, uv_mode, nz_dc;
+  uint8_t skip, segment, pad0, pad1;
+  uint64_t score;
+};
+static_assert(sizeof(MbEnc) == 864, "MbEnc layout");
+
+// zigzag scan as a compile-time table: with the coefficient loops unrolled
+// every co[zig] / q[zig] index is a constant (no scratch-memory arrays)
+constexpr int kZig[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+constexpr int kBand[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
+
+__constant__ uint16_t c_level_codes[134];
+__constant__ uint16_t c_fixed_i4[1000];
+__constant__ uint8_t c_zigzag[16], c_bands[17], c_rzig[16];
+__constant__ int32_t c_wtrellis[16];
+
+// ------------------------------------------------------------------ LDS state
+struct Shared {
+  uint8_t proba[4 * 8 * 3 * 11];
+  uint16_t ecost[256];
+  uint16_t lfixed[2048];
+  Segment seg[4];
+  uint8_t yin[YUV], yout[YUV], yout2[YUV];
+  alignas(16) int16_t coeffs[400];
+  uint8_t modes4[16];
+  uint8_t nzy[16], nzuv[8];
+  int dcin[4][16];
+  int dcq[4][16];  // per mode: quantised WHT levels (I16 RD), then block DCs after the inverse WHT
+  int dcout[4][16];
+  int mode_rate[4], mode_disto[4];
+  int sse10[10];
+  int word;
+};
+
+__device__ __forceinline__ int ecost(const Shared& s, int p) { return s.ecost[p]; }
+__device__ __forceinline__ int bit_cost(const Shared& s, int bit, int p) { return s.ecost[bit ? 255 - p : p]; }
+__device__ __forceinline__ const uint8_t* proba_p(const Shared& s, int type, int band, int ctx) {
+  return s.proba + ((type * 8 + band) * 3 + ctx) * 11;
+}
+
+// QuantizeCoeffs (encode_quant.go:16-80): returns the zigzag nz count
+__device__ int quantize(const int co[16], int16_t q[16], const SQuant& sq, int first) {
+  int max_zz = -1;
+#pragma unroll
+  for (int n = 0; n < 16; n++) {
+    if (n < first) {
+      q[n] = 0;
+      continue;
+    }
+    int v = co[n];
+    const int sign = v < 0 ? -1 : 1;
+    v = abs(v) + sq.sharpen[n];
+    v = max(v, 0);
+    const uint32_t iq = n == 0 ? (uint32_t)sq.dc_iquant : (uint32_t)sq.iquant;
+    const uint32_t bias = n == 0 ? (uint32_t)sq.dc_bias : (uint32_t)sq.bias;
+    const int c = min((int)(((uint32_t)v * iq + bias) >> 17), 2047);
+    q[n] = (int16_t)(sign * c);
+    if (c != 0) max_zz = max(max_zz, (int)c_rzig[n]);
+  }
+  return max_zz + 1;
+}
+
+__device__ __forceinline__ int variable_level_cost(const Shared& s, int level, const uint8_t* p) {
+  const int idx = min(level - 1, 66);
+  int pattern = c_level_codes[2 * idx], bits = c_level_codes[2 * idx + 1], cost = 0;
+  for (int i = 2; pattern != 0; i++) {
+    if (pattern & 1) cost += bit_cost(s, bits & 1, p[i]);
+    bits >>= 1;
+    pattern >>= 1;
+  }
+  return cost;
+}
+
+// TokenCostForCoeffs (encode_quant.go:154-223), unrolled (no early break)
+__device__ int token_cost(const Shared& s, const int16_t q[16], int nz_count, int type, int ctx0, int first) {
+  if (nz_count <= first) return ecost(s, proba_p(s, type, first == 0 ? 0 : 1, ctx0)[0]);
+  const int last = nz_count - 1;
+  int cost = 0, ctx = ctx0;
+  bool done = false;
+#pragma unroll
+  for (int n = 0; n < 16; n++) {
+    if (n < first || done) continue;
+    const uint8_t* pp = proba_p(s, type, kBand[n], ctx);
+    if (n > last) {
+      cost += ecost(s, pp[0]);
+      done = true;
+      continue;
+    }
+    const int v = abs((int)q[kZig[n]]);
+    cost += ecost(s, 255 - pp[0]);
+    if (v == 0) {
+      cost += ecost(s, pp[1]);
+      ctx = 0;
+    } else {
+      cost += ecost(s, 255 - pp[1]);
+      if (v == 1) {
+        cost += s.lfixed[1] + ecost(s, pp[2]);
+        ctx = 1;
+      } else if (v == 2) {
+        cost += s.lfixed[2] + ecost(s, 255 - pp[2]) + ecost(s, pp[3]) + ecost(s, pp[4]);
+        ctx = 2;
+      } else {
+        cost += s.lfixed[v] + variable_level_cost(s, v, pp);
+        ctx = 2;
+      }
+    }
+  }
+  return cost;
+}
+
+// TrellisQuantizeBlock (encode_trellis.go:23-301).  Path kept packed per
+// position: levels of the three end contexts + their predecessor context.
+__device__ int trellis(const Shared& s, const int co[16], int16_t q[16], const SQuant& sq, int first, int ctx_type,
+                       int init_ctx, int lambda) {
+  {  // pre-scan: all levels zero under the neutral bias?
+    bool nonzero = false;
+#pragma unroll
+    for (int n = 0; n < 16; n++) {
+      if (n < first) continue;
+      const int zig = kZig[n];
+      const int c0 = max(abs(co[zig]) + sq.sharpen[zig], 0);
+      const int iq = n == 0 ? sq.dc_iquant : sq.iquant;
+      nonzero |= ((c0 * iq) >> 17) > 0;
+    }
+    if (!nonzero) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) q[i] = 0;
+      return 0;
+    }
+  }
+  init_ctx = min(init_ctx, 2);
+  int64_t ps[3];
+  bool pv[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    pv[c] = c == init_ctx;
+    ps[c] = 0;
+  }
+  // path per position: A = level(ctx0) | level(ctx1) << 16, B = level(ctx2) |
+  // pred ctx 0/1/2 at bits 16/18/20 | valid mask at bit 22
+  uint32_t pathA[16], pathB[16];
+  const int64_t lam = lambda;
+  int64_t best_terminal = (int64_t)bit_cost(s, 0, proba_p(s, ctx_type, first == 0 ? 0 : 1, init_ctx)[0]) * lam;
+  int best_n = -1, best_c = -1;
+#pragma unroll
+  for (int n = 0; n < 16; n++) {
+    if (n < first) {
+      pathA[n] = 0;
+      pathB[n] = 0;
+      continue;
+    }
+    const int zig = kZig[n];
+    const int band = kBand[n + 1];
+    int raw = co[zig];
+    const int sign = raw < 0 ? -1 : 1;
+    raw = abs(raw);
+    const int c0 = max(raw + sq.sharpen[zig], 0);
+    const int quant = n == 0 ? sq.dc_quant : sq.quant;
+    const int iquant = n == 0 ? sq.dc_iquant : sq.iquant;
+    const int L0 = min((c0 * iquant) >> 17, 2047);
+    const int thresh = min((int)(((uint32_t)c0 * (uint32_t)iquant + 65536u) >> 17), 2047);
+    const int64_t weight = c_wtrellis[zig];
+    const int64_t c0sq = (int64_t)(c0 * c0);
+    const bool has0 = L0 > 0 && L0 <= thresh;
+    const bool has1 = L0 + 1 <= 2047 && L0 + 1 <= thresh;
+    int64_t d0 = 0, d1 = 0;
+    int fixed0 = 0, fixed1 = 0;
+    if (has0) {
+      const int err = c0 - L0 * quant;
+      d0 = 256 * (weight * ((int64_t)(err * err) - c0sq));
+      fixed0 = s.lfixed[L0];
+    }
+    if (has1) {
+      const int err = c0 - (L0 + 1) * quant;
+      d1 = 256 * (weight * ((int64_t)(err * err) - c0sq));
+      fixed1 = s.lfixed[L0 + 1];
+    }
+    const int nctx0 = min(L0, 2), nctx1 = min(L0 + 1, 2);
+    int64_t cs[3] = {0, 0, 0};
+    bool cv[3] = {false, false, false};
+    int16_t cl[3] = {0, 0, 0};
+    uint8_t cp[3] = {0, 0, 0};
+#pragma unroll
+    for (int pc = 0; pc < 3; pc++) {
+      if (!pv[pc]) continue;
+      const int64_t base = ps[pc];
+      const uint8_t* p = proba_p(s, ctx_type, band, pc);
+      const int not_eob = ecost(s, 255 - p[0]);
+      const int64_t t0 = base + (int64_t)(not_eob + ecost(s, p[1])) * lam;
+      if (!cv[0] || t0 < cs[0]) {
+        cs[0] = t0;
+        cl[0] = 0;
+        cp[0] = (uint8_t)pc;
+        cv[0] = true;
+      }
+      if (has0 || has1) {
+        const int nzc = not_eob + ecost(s, 255 - p[1]);
+        if (has0) {
+          const int64_t t = base + (int64_t)(nzc + fixed0 + variable_level_cost(s, L0, p)) * lam + d0;
+#pragma unroll
+          for (int k = 0; k < 3; k++)
+            if (k == nctx0 && (!cv[k] || t < cs[k])) {
+              cs[k] = t;
+              cl[k] = (int16_t)(sign * L0);
+              cp[k] = (uint8_t)pc;
+              cv[k] = true;
+            }
+        }
+        if (has1) {
+          const int64_t t = base + (int64_t)(nzc + fixed1 + variable_level_cost(s, L0 + 1, p)) * lam + d1;
+#pragma unroll
+          for (int k = 0; k < 3; k++)
+            if (k == nctx1 && (!cv[k] || t < cs[k])) {
+              cs[k] = t;
+              cl[k] = (int16_t)(sign * (L0 + 1));
+              cp[k] = (uint8_t)pc;
+              cv[k] = true;
+            }
+        }
+      }
+    }
+    pathA[n] = (uint32_t)(uint16_t)cl[0] | ((uint32_t)(uint16_t)cl[1] << 16);
+    pathB[n] = (uint32_t)(uint16_t)cl[2] | ((uint32_t)cp[0] << 16) | ((uint32_t)cp[1] << 18) | ((uint32_t)cp[2] << 20) |
+               ((uint32_t)((cv[0] ? 1 : 0) | (cv[1] ? 2 : 0) | (cv[2] ? 4 : 0)) << 22);
+#pragma unroll
+    for (int c = 1; c < 3; c++) {
+      if (!cv[c]) continue;
+      int64_t eob = cs[c];
+      if (n < 15) eob += (int64_t)ecost(s, proba_p(s, ctx_type, band, c)[0]) * lam;
+      if (eob < best_terminal) {
+        best_terminal = eob;
+        best_n = n;
+        best_c = c;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      ps[c] = cs[c];
+      pv[c] = cv[c];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) q[i] = 0;
+  if (best_n < 0) return 0;
+  int ctx = best_c, last = 0;
+#pragma unroll
+  for (int n = 15; n >= 0; n--) {
+    if (n > best_n || n < first) continue;
+    if ((pathB[n] >> (22 + ctx)) & 1) {
+      const int16_t lv = (int16_t)(ctx == 0 ? pathA[n] : (ctx == 1 ? pathA[n] >> 16 : pathB[n]));
+      const int pcx = (int)((pathB[n] >> (16 + 2 * ctx)) & 3);
+      q[kZig[n]] = lv;
+      if (lv != 0 && last == 0) last = n + 1;
+      ctx = pcx;
+    }
+  }
+  return last;
+}
+
+// residual + reconstruction of one 4x4 block: rec = clip(pred + IDCT(dq))
+__device__ __forceinline__ void dequant(const int16_t q[16], int dq[16], const SQuant& sq) {
+  dq[0] = (int16_t)(q[0] * sq.dc_quant);
+#pragma unroll
+  for (int i = 1; i < 16; i++) dq[i] = (int16_t)(q[i] * sq.quant);
+}
+__device__ __forceinline__ void recon4(const int pred[16], const int dq[16], int rec[16]) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    int res[4];
+    idct_row(dq, r, res);
+#pragma unroll
+    for (int c = 0; c < 4; c++) rec[4 * r + c] = clip8(pred[4 * r + c] + res[c]);
+  }
+}
+__device__ __forceinline__ int sse16(const int a[16], const int b[16]) {
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) s += (a[i] - b[i]) * (a[i] - b[i]);
+  return s;
+}
+__device__ __forceinline__ int ttrans(const int px[16]) {  // tTransform (ssim.go:266-304)
+  const int kw[16] = {38, 32, 20, 9, 32, 28, 17, 7, 20, 17, 10, 4, 9, 7, 4, 2};
+  int tmp[16];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int* r = px + 4 * i;
+    const int a0 = r[0] + r[2], a1 = r[1] + r[3], a2 = r[1] - r[3], a3 = r[0] - r[2];
+    tmp[4 * i] = a0 + a1;
+    tmp[4 * i + 1] = a3 + a2;
+    tmp[4 * i + 2] = a3 - a2;
+    tmp[4 * i + 3] = a0 - a1;
+  }
+  int sum = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int a0 = tmp[i] + tmp[8 + i], a1 = tmp[4 + i] + tmp[12 + i];
+    const int a2 = tmp[4 + i] - tmp[12 + i], a3 = tmp[i] - tmp[8 + i];
+    sum += kw[i] * abs(a0 + a1) + kw[4 + i] * abs(a3 + a2) + kw[8 + i] * abs(a3 - a2) + kw[12 + i] * abs(a0 - a1);
+  }
+  return sum;
+}
+__device__ __forceinline__ int tdisto(const int a[16], const int b[16]) { return abs(ttrans(b) - ttrans(a)) >> 5; }
+__device__ __forceinline__ void fdct(const int src[16], const int pred[16], int co[16]) {
+  int d[16];
+  int16_t o[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) d[i] = src[i] - pred[i];
+  fdct4x4(d, o);
+#pragma unroll
+  for (int i = 0; i < 16; i++) co[i] = o[i];
+}
+__device__ __forceinline__ void load4x4(const uint8_t* p, int v[16]) {
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) v[4 * r + c] = p[r * BPS + c];
+}
+__device__ __forceinline__ void store4x4(uint8_t* p, const int v[16]) {
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+    *reinterpret_cast<uint32_t*>(p + r * BPS) = pack4(v[4 * r], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
+}
+__device__ __forceinline__ void unpack_rows(uint32_t w, int* d) {
+#pragma unroll
+  for (int c = 0; c < 4; c++) d[c] = byte_of(w, c);
+}
+// 16x16 / 8x8 square prediction of the 4x4 block at (px, py) of `base`
+__device__ __forceinline__ void predsq_block(int mode, const uint8_t* base, int size, int px, int py, int pred[16]) {
+  const int dc = predsq_dc(mode, base, size);
+#pragma unroll
+  for (int r = 0; r < 4; r++) unpack_rows(predsq_row4(mode, base, px, py + r, dc), pred + 4 * r);
+}
+__device__ __forceinline__ void pred4_block(int mode, const uint8_t* buf, int off, int pred[16]) {
+  int X, T[8], L[4];
+  pred4_ctx(buf, off, X, T, L);
+#pragma unroll
+  for (int r = 0; r < 4; r++) unpack_rows(pred4_row(mode, r, X, T, L), pred + 4 * r);
+}
+__device__ __forceinline__ int check_mode(int mbx, int mby, int mode) {
+  const int edge = (mbx == 0) ? ((mby == 0) ? 6 : 5) : ((mby == 0) ? 4 : 0);
+  return mode == 0 ? edge : mode;
+}
+__device__ __forceinline__ bool needs_top4(int m) { return m == 1 || m == 2 || m == 4 || m == 5 || m == 6 || m == 7 || m == 8; }
+__device__ __forceinline__ bool needs_left4(int m) { return m == 1 || m == 3 || m == 4 || m == 8 || m == 9; }
+__device__ __forceinline__ uint64_t rd_score(int disto, int rate, int lambda) {
+  return (uint64_t)(int64_t)rate * (uint64_t)(int64_t)lambda + 256ull * (uint64_t)(int64_t)disto;
+}
+template <typename T>
+__device__ __forceinline__ T group_sum(T v, int width) {  // sum over aligned groups of `width` lanes
+  for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ void lds_sync() { __syncthreads(); }
+
+// sc1 hand-off helpers (see decode.hip)
+__device__ __forceinline__ uint32_t ld_sc1_32(const uint8_t* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_32(uint8_t* p, uint32_t v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct EncArgs {
+  const uint8_t* y;  // source planes (stride 16*mbw / 8*mbw), pitch per image
+  const uint8_t* u;
+  const uint8_t* v;
+  uint8_t* ry;  // reconstruction (may alias the source)
+  uint8_t* ru;
+  uint8_t* rv;
+  const uint8_t* segments;  // per MB segment id, n_img * mbw * mbh
+  const Segment* segs;      // 4
+  const uint8_t* proba;     // 1056
+  MbEnc* out;
+  uint8_t* top;   // [n_img][mbw][REC]
+  int* progress;  // [n_img][mbh]
+  int* ctl;       // [0] dequeue, [1] error
+  int64_t y_pitch, uv_pitch;
+  int width, height, mbw, mbh, n_img, quality;
+};
+
+constexpr uint64_t SPIN_TICKS = 200000000ull;
+
+__global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
+  __shared__ Shared s;
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 1056; i += 64) s.proba[i] = a.proba[i];
+  for (int i = lane; i < 256; i += 64) s.ecost[i] = vp8_entropy_cost[i];
+  for (int i = lane; i < 2048; i += 64) s.lfixed[i] = vp8_level_fixed_costs[i];
+  for (int i = lane; i < (int)(4 * sizeof(Segment) / 4); i += 64)
+    reinterpret_cast<int*>(s.seg)[i] = reinterpret_cast<const int*>(a.segs)[i];
+  const int mbw = a.mbw, mbh = a.mbh;
+  const int ys = 16 * mbw, uvs = 8 * mbw;
+  const int max_modes = a.quality < 50 ? 2 : 3;
+  const int total_rows = a.n_img * mbh;
+  lds_sync();
+
+  for (;;) {
+    if (lane == 0) s.word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lds_sync();
+    const int row = __builtin_amdgcn_readfirstlane(s.word);
+    lds_sync();
+    if (row >= total_rows) break;
+    const int mby = row / a.n_img, img = row % a.n_img;
+    const uint8_t* Y = a.y + img * a.y_pitch;
+    const uint8_t* U = a.u + img * a.uv_pitch;
+    const uint8_t* V = a.v + img * a.uv_pitch;
+    uint8_t* RY = a.ry + img * a.y_pitch;
+    uint8_t* RU = a.ru + img * a.uv_pitch;
+    uint8_t* RV = a.rv + img * a.uv_pitch;
+    uint8_t* top = a.top + (int64_t)img * mbw * REC;
+    int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
+    int* prog_mine = a.progress + (int64_t)img * mbh + mby;
+    // left context (encodeRow :257-282)
+    if (lane < 16) s.yout[YOFF - 1 + lane * BPS] = 129;
+    else if (lane < 24) s.yout[UOFF - 1 + (lane - 16) * BPS] = 129;
+    else if (lane < 32) s.yout[VOFF - 1 + (lane - 24) * BPS] = 129;
+    uint32_t left_nz = 0;
+    int left_nz_dc = 0;
+    uint32_t left_modes = 0;  // 4 x 8 bits, B_DC_PRED = 0
+    int tl_y = 127, tl_u = 127, tl_v = 127;
+    int seen = 0;
+
+    for (int mbx = 0; mbx < mbw; mbx++) {
+      const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
+      // ---- wait for the row above (MB x+1 done) ----
+      if (mby > 0) {
+        const int need = min(mbx + 2, mbw);
+        if (seen < need) {
+          int v = 0;
+          if (lane == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t it = 0;; it++) {
+              v = __hip_atomic_load(prog_above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (v >= need) break;
+              if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+                                      __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v = mbw;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(2);
+            }
+          }
+          seen = __shfl(v, 0, 64);
+        }
+      }
+      const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
+      const Segment& sg = s.seg[segid];
+      // ---- import (importBlockParallel :433-452) with edge replication ----
+      {
+        const int x = 16 * mbx, y = 16 * mby;
+        const int ww = min(a.width - x, 16), hh = min(a.height - y, 16);
+        if (lane < 16) {
+          const int r = min(lane, hh - 1);
+          for (int c = 0; c < 16; c++) s.yin[YOFF + lane * BPS + c] = Y[(int64_t)(y + r) * ys + x + min(c, ww - 1)];
+        } else if (lane < 32) {
+          const int k = lane - 16, pl = k >> 3, j = k & 7;
+          const int uvw = (ww + 1) >> 1, uvh = (hh + 1) >> 1;
+          const int r = min(j, uvh - 1);
+          const uint8_t* P = pl ? V : U;
+          for (int c = 0; c < 8; c++)
+            s.yin[(pl ? VOFF : UOFF) + j * BPS + c] = P[(int64_t)(8 * mby + r) * uvs + 8 * mbx + min(c, uvw - 1)];
+        }
+      }
+      // ---- prediction context (fillPredContextParallel :455-562) ----
+      uint32_t top_nz = 0, top_modes = 0;
+      int top_nz_dc = 0;
+      {
+        const uint8_t* rec = top + mbx * REC;
+        if (mby > 0) {
+          if (lane < 8) {  // Y16 U8 V8 of the row above
+            const uint32_t w = ld_sc1_32(rec + 4 * lane);
+            const int o = lane < 4 ? YOFF - BPS + 4 * lane : (lane < 6 ? UOFF - BPS + 4 * (lane - 4) : VOFF - BPS + 4 * (lane - 6));
+            *reinterpret_cast<uint32_t*>(s.yout + o) = w;
+          } else if (lane == 8) {  // top-right
+            const uint32_t tr = mbx < mbw - 1 ? ld_sc1_32(rec + REC) : 0x01010101u * (ld_sc1_32(rec + 12) >> 24);
+            *reinterpret_cast<uint32_t*>(s.yout + YOFF - BPS + 16) = tr;
+          }
+          top_nz = ld_sc1_32(rec + 32);
+          top_modes = ld_sc1_32(rec + 36);
+          top_nz_dc = (int)ld_sc1_32(rec + 40);
+        } else {
+          if (lane < 21) s.yout[YOFF - BPS + lane] = 127;  // cols 0..20 (top-right incl.)
+          else if (lane < 29) s.yout[UOFF - BPS + lane - 21] = 127;
+          else if (lane < 37) s.yout[VOFF - BPS + lane - 29] = 127;
+        }
+        if (lane == 37) s.yout[YOFF - BPS - 1] = (mbx > 0 && mby > 0) ? tl_y : (mby > 0 ? 129 : 127);
+        if (lane == 38) s.yout[UOFF - BPS - 1] = (mbx > 0 && mby > 0) ? tl_u : (mby > 0 ? 129 : 127);
+        if (lane == 39) s.yout[VOFF - BPS - 1] = (mbx > 0 && mby > 0) ? tl_v : (mby > 0 ? 129 : 127);
+      }
+      lds_sync();
+      if (lane < 12) {  // replicate the top-right into rows 3, 7, 11
+        const int r = 4 * (lane / 4 + 1) - 1, i = lane & 3;
+        s.yout[YOFF - BPS + 16 + (r + 1) * BPS + i] = s.yout[YOFF - BPS + 16 + i];
+      }
+      lds_sync();
+      // scalar copies of the neighbour context
+      top_nz = __builtin_amdgcn_readfirstlane(top_nz);
+      top_modes = __builtin_amdgcn_readfirstlane(top_modes);
+      top_nz_dc = __builtin_amdgcn_readfirstlane(top_nz_dc);
+
+      // ================= I16 RD (pickBestI16ModeRDParallel :624-737) =================
+      bool src_flat;
+      {
+        // isFlatSource16 (encode_analysis.go:358)
+        const uint8_t v0 = s.yin[YOFF];
+        bool mine = true;
+        for (int i = lane; i < 256; i += 64) mine &= s.yin[YOFF + (i >> 4) * BPS + (i & 15)] == v0;
+        src_flat = __all(mine);
+      }
+      const int m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
+      const bool mvalid = !((m == 2 && mby == 0) || (m == 3 && mbx == 0) || (m == 1 && (mbx == 0 || mby == 0)));
+      int src16[16], pred16[16], rec16[16];
+      int16_t q16[16];
+      int nz16 = 0;
+      {
+        const int off = YOFF + 4 * by * BPS + 4 * bx;
+        load4x4(s.yin + off, src16);
+        predsq_block(check_mode(mbx, mby, m), s.yout + YOFF, 16, 4 * bx, 4 * by, pred16);
+        int co[16];
+        fdct(src16, pred16, co);
+        s.dcin[m][b] = co[0];
+        co[0] = 0;
+        nz16 = quantize(co, q16, sg.y1, 1);
+      }
+      // contexts from the neighbours' nz within the same mode
+      const int nz_left = __shfl(nz16, (lane - 1) & 63, 64), nz_top = __shfl(nz16, (lane - 4) & 63, 64);
+      {
+        const int l = bx > 0 ? (nz_left > 0) : (int)((left_nz >> by) & 1);
+        const int t = by > 0 ? (nz_top > 0) : (int)((top_nz >> bx) & 1);
+        const int ctx = min(l + t, 2);
+        int rate = mvalid ? token_cost(s, q16, nz16, 0, ctx, 1) : 0;
+        bool acnz = false;
+#pragma unroll
+        for (int i = 1; i < 16; i++) acnz |= q16[i] != 0;
+        lds_sync();
+        // one lane per mode: WHT path
+        if (b == 0 && mvalid) {
+          int dcv[16], qdc_i[16];
+          int16_t wht[16], qdc[16];
+#pragma unroll
+          for (int i = 0; i < 16; i++) dcv[i] = s.dcin[m][i];
+          fwht(dcv, wht);
+#pragma unroll
+          for (int i = 0; i < 16; i++) qdc_i[i] = wht[i];
+          const int nzdc = quantize(qdc_i, qdc, sg.y2, 0);
+          const int dc_ctx = min(top_nz_dc + left_nz_dc, 2);
+          s.mode_rate[m] = vp8_mode_fixed_cost16[m] + token_cost(s, qdc, nzdc, 1, dc_ctx, 0);
+          int dq[16];
+          dequant(qdc, dq, sg.y2);
+          int16_t whto[16];
+          iwht(dq, whto);
+#pragma unroll
+          for (int i = 0; i < 16; i++) s.dcout[m][i] = whto[i];
+        }
+        lds_sync();
+        int dq[16];
+        dequant(q16, dq, sg.y1);
+        dq[0] = s.dcout[m][b];
+        recon4(pred16, dq, rec16);
+        const int sse = sse16(src16, rec16);
+        const int td = sg.tlambda_sd > 0 ? tdisto(src16, rec16) : 0;
+        const int rsum = group_sum(rate, 16), ssum = group_sum(sse, 16), tsum = group_sum(td, 16);
+        const unsigned long long acmask = __ballot(acnz);
+        if (b == 0 && mvalid) {
+          const int total_rate = s.mode_rate[m] + rsum;
+          int disto = ssum;
+          if (sg.tlambda_sd > 0) disto += (sg.tlambda_sd * tsum + 128) >> 8;
+          if (src_flat && ((acmask >> (16 * m)) & 0xffffull) == 0) disto *= 2;
+          s.mode_rate[m] = total_rate;
+          s.mode_disto[m] = disto;
+        }
+        lds_sync();
+      }
+      int best16 = 0, rate16 = 0, disto16 = 0;
+      {
+        uint64_t best = ~0ull;
+        for (int mm = 0; mm < 4; mm++) {
+          if ((mm == 2 && mby == 0) || (mm == 3 && mbx == 0) || (mm == 1 && (mbx == 0 || mby == 0))) continue;
+          const uint64_t sc = rd_score(s.mode_disto[mm], s.mode_rate[mm], sg.lambda_i16);
+          if (sc < best) {
+            best = sc;
+            best16 = mm;
+            rate16 = s.mode_rate[mm];
+            disto16 = s.mode_disto[mm];
+          }
+        }
+      }
+      const uint64_t s16 = rd_score(disto16, rate16, sg.lambda_mode);
+
+      // ================= I4 RD (tryI4ModesRDParallel :739-846) =================
+      for (int i = lane; i < YUV / 4; i += 64)
+        reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
+      lds_sync();
+      uint64_t s4;
+      {
+        int total_rate = 0, total_disto = 0, total_header = 0;
+        bool early = false;
+        for (int blk = 0; blk < 16 && !early; blk++) {
+          const int bx4 = blk & 3, by4 = blk >> 2;
+          const int top_mode = by4 == 0 ? (int)((top_modes >> (8 * bx4)) & 0xff) : s.modes4[blk - 4];
+          const int left_mode = bx4 == 0 ? (int)((left_modes >> (8 * by4)) & 0xff) : s.modes4[blk - 1];
+          const int off = YOFF + 4 * by4 * BPS + 4 * bx4;
+          const bool has_top = mby > 0 || by4 > 0, has_left = mbx > 0 || bx4 > 0;
+          const int l = bx4 > 0 ? (s.nzy[blk - 1] > 0) : (int)((left_nz >> by4) & 1);
+          const int t = by4 > 0 ? (s.nzy[blk - 4] > 0) : (int)((top_nz >> bx4) & 1);
+          const int nz_ctx = min(l + t, 2);
+          int src[16];
+          load4x4(s.yin + off, src);
+          // pre-screen all eligible modes by prediction SSE
+          if (lane < 10) {
+            const bool ok = !(!has_top && needs_top4(lane)) && !(!has_left && needs_left4(lane));
+            int pred[16];
+            pred4_block(lane, s.yout2, off, pred);
+            s.sse10[lane] = ok ? sse16(src, pred) : -1;
+          }
+          lds_sync();
+          // partial selection sort of the candidates, in the reference's order (:869-886)
+          int cm[10], cs[10], nc = 0;
+          for (int k = 0; k < 10; k++)
+            if (s.sse10[k] >= 0) {
+              cm[nc] = k;
+              cs[nc] = s.sse10[k];
+              nc++;
+            }
+          const int K = min(max_modes, nc);
+          for (int i = 0; i < K; i++) {
+            int mi = i;
+            for (int j = i + 1; j < nc; j++)
+              if (cs[j] < cs[mi]) mi = j;
+            if (mi != i) {
+              int t2 = cm[i];
+              cm[i] = cm[mi];
+              cm[mi] = t2;
+              t2 = cs[i];
+              cs[i] = cs[mi];
+              cs[mi] = t2;
+            }
+          }
+          // candidates in parallel (lane i = candidate i)
+          uint64_t score = ~0ull;
+          int rate = 0, disto = 0, nz = 0, mode = cm[0];
+          int16_t q[16];
+          int dq[16];
+          int pred[16];
+          if (lane < K) {
+            mode = lane == 0 ? cm[0] : (lane == 1 ? cm[1] : cm[2]);
+            pred4_block(mode, s.yout2, off, pred);
+            int co[16];
+            fdct(src, pred, co);
+            nz = trellis(s, co, q, sg.y1, 0, 3, nz_ctx, sg.tlambda_i4);
+            dequant(q, dq, sg.y1);
+            int rec[16];
+            recon4(pred, dq, rec);
+            disto = sse16(src, rec);
+            if (sg.tlambda_sd > 0) disto += (sg.tlambda_sd * tdisto(src, rec) + 128) >> 8;
+            bool flat = true;
+            int cnt = 0;
+#pragma unroll
+            for (int i = 1; i < 16; i++) cnt += q[i] != 0;
+            flat = cnt <= 3;
+            rate = (mode > 0 && flat) ? 140 : 0;
+            rate += token_cost(s, q, nz, 3, nz_ctx, 0);
+            rate += c_fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
+            score = rd_score(disto, rate, sg.lambda_i4);
+          }
+          // first minimum over candidates (strict '<' in candidate order)
+          int win = 0;
+          uint64_t wsc = __shfl(score, 0, 64);
+          for (int i = 1; i < K; i++) {
+            const uint64_t sc = __shfl(score, i, 64);
+            if (sc < wsc) {
+              wsc = sc;
+              win = i;
+            }
+          }
+          const int wmode = __shfl(mode, win, 64), wrate = __shfl(rate, win, 64), wdisto = __shfl(disto, win, 64);
+          const int wnz = __shfl(nz, win, 64);
+          if (lane == win) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) s.coeffs[blk * 16 + i] = q[i];
+            s.modes4[blk] = (uint8_t)wmode;
+            s.nzy[blk] = (uint8_t)wnz;
+          }
+          total_rate += wrate;
+          total_disto += wdisto;
+          total_header += c_fixed_i4[(top_mode * 10 + left_mode) * 10 + wmode];
+          if (rd_score(total_disto, total_rate + 211, sg.lambda_mode) >= s16 || total_header > 15000) {
+            early = true;
+          } else if (lane == win) {  // reconstruct the chosen block into yout2
+            int rec[16];
+            recon4(pred, dq, rec);
+            store4x4(s.yout2 + off, rec);
+          }
+          lds_sync();
+        }
+        s4 = early ? ~0ull : rd_score(total_disto, total_rate + 211, sg.lambda_mode);
+      }
+      const bool is_i4 = s4 < s16;
+
+      // ================= UV RD (pickBestUVModeRDParallel :1030-1114) =================
+      int best_uv = 0;
+      {
+        const int um = lane >> 3, k = lane & 7, pl = k >> 2, ub = k & 3, ubx = ub & 1, uby = ub >> 1;
+        const bool act = lane < 32;
+        const bool uvalid = act && !((um == 2 && mby == 0) || (um == 3 && mbx == 0) || (um == 1 && (mbx == 0 || mby == 0)));
+        const int base = pl ? VOFF : UOFF;
+        int src[16], pred[16];
+        int16_t q[16];
+        int nz = 0;
+        if (act) {
+          load4x4(s.yin + base + 4 * uby * BPS + 4 * ubx, src);
+          predsq_block(check_mode(mbx, mby, um), s.yout + base, 8, 4 * ubx, 4 * uby, pred);
+          int co[16];
+          fdct(src, pred, co);
+          nz = quantize(co, q, sg.uv, 0);
+        }
+        const int nzl = __shfl(nz, (lane - 1) & 63, 64), nzt = __shfl(nz, (lane - 2) & 63, 64);
+        int rate = 0, sse = 0, acn = 0;
+        if (act) {
+          const int l = ubx > 0 ? (nzl > 0) : (int)((left_nz >> (4 + 2 * pl + uby)) & 1);
+          const int t = uby > 0 ? (nzt > 0) : (int)((top_nz >> (4 + 2 * pl + ubx)) & 1);
+          rate = uvalid ? token_cost(s, q, nz, 2, min(l + t, 2), 0) : 0;
+          int dq[16], rec[16];
+          dequant(q, dq, sg.uv);
+          recon4(pred, dq, rec);
+          sse = sse16(src, rec);
+#pragma unroll
+          for (int i = 1; i < 16; i++) acn += q[i] != 0;
+        }
+        const int rsum = group_sum(rate, 8), ssum = group_sum(sse, 8), asum = group_sum(acn, 8);
+        if (act && k == 0) {
+          int total = vp8_mode_fixed_cost_uv[um] + rsum;
+          if (um > 0 && asum <= 2) total += 140 * 8;
+          s.mode_rate[um] = total;
+          s.mode_disto[um] = ssum;
+        }
+        lds_sync();
+        uint64_t best = ~0ull;
+        for (int mm = 0; mm < 4; mm++) {
+          if ((mm == 2 && mby == 0) || (mm == 3 && mbx == 0) || (mm == 1 && (mbx == 0 || mby == 0))) continue;
+          const uint64_t sc = rd_score(s.mode_disto[mm], s.mode_rate[mm], sg.lambda_uv);
+          if (sc < best) {
+            best = sc;
+            best_uv = mm;
+          }
+        }
+        lds_sync();
+      }
+
+      // ================= predictions into yout (pickBestModeParallel :586-604) =================
+      // (the square predictors read only the borders, so lanes write their blocks directly)
+      if (is_i4) {  // I4 reconstruction from the RD pass (I4Cached)
+        if (lane < 16)
+          *reinterpret_cast<uint4*>(s.yout + YOFF + lane * BPS) = *reinterpret_cast<const uint4*>(s.yout2 + YOFF + lane * BPS);
+        else if (lane < 32)
+          s.coeffs[384 + lane - 16] = 0;  // no WHT block for I4
+      } else if (lane < 16) {
+        int p[16];
+        predsq_block(check_mode(mbx, mby, best16), s.yout + YOFF, 16, 4 * bx, 4 * by, p);
+        store4x4(s.yout + YOFF + 4 * by * BPS + 4 * bx, p);
+      }
+      if (lane >= 32 && lane < 40) {
+        const int k = lane - 32, pl = k >> 2, ub = k & 3;
+        int p[16];
+        predsq_block(check_mode(mbx, mby, best_uv), s.yout + (pl ? VOFF : UOFF), 8, 4 * (ub & 1), 4 * (ub >> 1), p);
+        store4x4(s.yout + (pl ? VOFF : UOFF) + 4 * (ub >> 1) * BPS + 4 * (ub & 1), p);
+      }
+      lds_sync();
+
+      // ================= final residuals (encodeResidualsParallel :1166-1356) =================
+      uint32_t nzy_mask = 0, nzuv_mask = 0;
+      int nz_dc = 0;
+      if (!is_i4) {
+        int src[16], pred[16], co[16];
+        int16_t q[16];
+        if (lane < 16) {
+          const int off = YOFF + 4 * by * BPS + 4 * bx;
+          load4x4(s.yin + off, src);
+          load4x4(s.yout + off, pred);
+          fdct(src, pred, co);
+          s.dcin[0][lane] = co[0];
+          co[0] = 0;
+        }
+        // trellis along block diagonals: block (bx, by) needs its left / top nz
+        for (int d = 0; d < 7; d++) {
+          if (lane < 16 && bx + by == d) {
+            const int l = bx > 0 ? (s.nzy[lane - 1] > 0) : (int)((left_nz >> by) & 1);
+            const int t = by > 0 ? (s.nzy[lane - 4] > 0) : (int)((top_nz >> bx) & 1);
+            const int nz = trellis(s, co, q, sg.y1, 1, 0, min(l + t, 2), sg.tlambda_i16);
+            s.nzy[lane] = (uint8_t)nz;
+#pragma unroll
+            for (int i = 0; i < 16; i++) s.coeffs[lane * 16 + i] = q[i];
+          }
+          lds_sync();
+        }
+        if (lane == 0) {
+          int dcv[16], qi[16];
+          int16_t wht[16], qdc[16];
+#pragma unroll
+          for (int i = 0; i < 16; i++) dcv[i] = s.dcin[0][i];
+          fwht(dcv, wht);
+#pragma unroll
+          for (int i = 0; i < 16; i++) qi[i] = wht[i];
+          const int nzdc = quantize(qi, qdc, sg.y2, 0);
+#pragma unroll
+          for (int i = 0; i < 16; i++) s.coeffs[384 + i] = qdc[i];
+          s.word = nzdc;
+        }
+        lds_sync();
+        nz_dc = s.word;
+      }
+      for (int i = 0; i < 16; i++) nzy_mask |= (s.nzy[i] > 0 ? 1u : 0u) << i;
+      if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
+      if (lane < 8) {  // chroma
+        const int pl = lane >> 2, ub = lane & 3;
+        const int off = (pl ? VOFF : UOFF) + 4 * (ub >> 1) * BPS + 4 * (ub & 1);
+        int src[16], pred[16], co[16];
+        int16_t q[16];
+        load4x4(s.yin + off, src);
+        load4x4(s.yout + off, pred);
+        fdct(src, pred, co);
+        const int nz = quantize(co, q, sg.uv, 0);
+        s.nzuv[lane] = (uint8_t)nz;
+#pragma unroll
+        for (int i = 0; i < 16; i++) s.coeffs[(16 + lane) * 16 + i] = q[i];
+      }
+      lds_sync();
+      for (int i = 0; i < 8; i++) nzuv_mask |= (s.nzuv[i] > 0 ? 1u : 0u) << i;
+
+      // ================= reconstruction (reconstructMBParallel :1358-1410) =================
+      if (!is_i4) {
+        if (lane == 0) {
+          int dq[16];
+          int16_t qdc[16], whto[16];
+#pragma unroll
+          for (int i = 0; i < 16; i++) qdc[i] = s.coeffs[384 + i];
+          dequant(qdc, dq, sg.y2);
+          iwht(dq, whto);
+#pragma unroll
+          for (int i = 0; i < 16; i++) s.dcout[0][i] = whto[i];
+        }
+        lds_sync();
+        if (lane < 16) {
+          const int off = YOFF + 4 * by * BPS + 4 * bx;
+          int16_t q[16];
+          int dq[16], pred[16], rec[16];
+#pragma unroll
+          for (int i = 0; i < 16; i++) q[i] = s.coeffs[lane * 16 + i];
+          dequant(q, dq, sg.y1);
+          dq[0] = s.dcout[0][lane];
+          load4x4(s.yout + off, pred);
+          recon4(pred, dq, rec);
+          store4x4(s.yout + off, rec);
+        }
+      }
+      if (lane >= 16 && lane < 24) {
+        const int k = lane - 16, pl = k >> 2, ub = k & 3;
+        const int off = (pl ? VOFF : UOFF) + 4 * (ub >> 1) * BPS + 4 * (ub & 1);
+        int16_t q[16];
+        int dq[16], pred[16], rec[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) q[i] = s.coeffs[(16 + k) * 16 + i];
+        dequant(q, dq, sg.uv);
+        load4x4(s.yout + off, pred);
+        recon4(pred, dq, rec);
+        store4x4(s.yout + off, rec);
+      }
+      lds_sync();
+
+      // ================= outputs, export, contexts (exportParallel :1412-1495) =================
+      MbEnc* o = a.out + mbi;
+      {
+        uint4* dst = reinterpret_cast<uint4*>(o->coeffs);
+        const uint4* srcv = reinterpret_cast<const uint4*>(s.coeffs);
+        for (int i = lane; i < 50; i += 64) dst[i] = srcv[i];
+        if (lane < 16) {
+          o->modes[lane] = is_i4 ? s.modes4[lane] : 0;
+          o->nz_y[lane] = s.nzy[lane];
+        } else if (lane < 24) {
+          o->nz_uv[lane - 16] = s.nzuv[lane - 16];
+        } else if (lane == 24) {
+          o->non_zero_y = nzy_mask;
+          o->non_zero_uv = nzuv_mask;
+          o->mb_type = is_i4 ? 1 : 0;
+          o->i16_mode = is_i4 ? 0 : (uint8_t)best16;
+          o->uv_mode = (uint8_t)best_uv;
+          o->nz_dc = (uint8_t)nz_dc;
+          o->skip = (nzy_mask == 0 && nzuv_mask == 0) ? 1 : 0;
+          o->segment = (uint8_t)segid;
+          o->pad0 = o->pad1 = 0;
+          o->score = is_i4 ? s4 : s16;
+        }
+      }
+      {
+        const int x = 16 * mbx, y = 16 * mby;
+        const int wy = min(a.width - x, 16), hy = min(a.height - y, 16);
+        if (lane < hy)
+          for (int c = 0; c < wy; c++) RY[(int64_t)(y + lane) * ys + x + c] = s.yout[YOFF + lane * BPS + c];
+        if (lane >= 16 && lane < 32) {
+          const int k = lane - 16, pl = k >> 3, j = k & 7;
+          uint8_t* P = pl ? RV : RU;
+          for (int c = 0; c < 8; c++) P[(int64_t)(8 * mby + j) * uvs + 8 * mbx + c] = s.yout[(pl ? VOFF : UOFF) + j * BPS + c];
+        }
+      }
+      // new top-left: the row above's bottom-right of this column (before we overwrite it)
+      tl_y = s.yout[YOFF - BPS + 15];
+      tl_u = s.yout[UOFF - BPS + 7];
+      tl_v = s.yout[VOFF - BPS + 7];
+      // NZ context update (updateNZContextParallel :343-430)
+      uint32_t out_t, out_l;
+      {
+        const int first = is_i4 ? 0 : 1;
+        uint32_t tnz = top_nz & 0x0f, lnz = left_nz & 0x0f;
+        for (int yy = 0; yy < 4; yy++) {
+          uint32_t l = lnz & 1;
+          for (int xx = 0; xx < 4; xx++) {
+            l = s.nzy[yy * 4 + xx] > first;
+            tnz = (tnz >> 1) | (l << 7);
+          }
+          tnz >>= 4;
+          lnz = (lnz >> 1) | (l << 7);
+        }
+        out_t = tnz;
+        out_l = lnz >> 4;
+        for (int ch = 0; ch < 4; ch += 2) {
+          tnz = (top_nz >> (4 + ch)) & 0x0f;
+          lnz = (left_nz >> (4 + ch)) & 0x0f;
+          for (int yy = 0; yy < 2; yy++) {
+            uint32_t l = lnz & 1;
+            for (int xx = 0; xx < 2; xx++) {
+              l = s.nzuv[(ch / 2) * 4 + yy * 2 + xx] > 0;
+              tnz = (tnz >> 1) | (l << 3);
+            }
+            tnz >>= 2;
+            lnz = (lnz >> 1) | (l << 5);
+          }
+          out_t |= (tnz << 4) << ch;
+          out_l |= (lnz & 0xf0) << ch;
+        }
+      }
+      int new_top_dc = top_nz_dc;
+      if (!is_i4) {
+        new_top_dc = nz_dc > 0;
+        left_nz_dc = nz_dc > 0;
+      }
+      uint32_t new_top_modes;
+      if (is_i4) {
+        new_top_modes = (uint32_t)s.modes4[12] | ((uint32_t)s.modes4[13] << 8) | ((uint32_t)s.modes4[14] << 16) |
+                        ((uint32_t)s.modes4[15] << 24);
+        left_modes = (uint32_t)s.modes4[3] | ((uint32_t)s.modes4[7] << 8) | ((uint32_t)s.modes4[11] << 16) |
+                     ((uint32_t)s.modes4[15] << 24);
+      } else {
+        new_top_modes = 0;
+        left_modes = 0;
+      }
+      left_nz = out_l;
+      // hand-off record for the row below (sc1 stores), then publish
+      if (mby < mbh - 1) {
+        uint8_t* rec = top + mbx * REC;
+        if (lane < 8) {
+          const int so = lane < 4 ? YOFF + 15 * BPS + 4 * lane : (lane < 6 ? UOFF + 7 * BPS + 4 * (lane - 4) : VOFF + 7 * BPS + 4 * (lane - 6));
+          st_sc1_32(rec + 4 * lane, *reinterpret_cast<const uint32_t*>(s.yout + so));
+        } else if (lane == 8) {
+          st_sc1_32(rec + 32, out_t);
+        } else if (lane == 9) {
+          st_sc1_32(rec + 36, new_top_modes);
+        } else if (lane == 10) {
+          st_sc1_32(rec + 40, (uint32_t)new_top_dc);
+        }
+      }
+      // rotate the left context: column 15 / 7 becomes column -1
+      lds_sync();
+      if (lane < 16) s.yout[YOFF - 1 + lane * BPS] = s.yout[YOFF + 15 + lane * BPS];
+      else if (lane < 24) s.yout[UOFF - 1 + (lane - 16) * BPS] = s.yout[UOFF + 7 + (lane - 16) * BPS];
+      else if (lane < 32) s.yout[VOFF - 1 + (lane - 24) * BPS] = s.yout[VOFF + 7 + (lane - 24) * BPS];
+      if (lane < 16) s.nzy[lane] = 0;
+      lds_sync();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+int g_tables_ready_dev = -1;
+
+}  // namespace
+
+extern "C" size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images) {
+  if (mbw <= 0 || mbh <= 0 || n_images <= 0) return 0;
+  return (size_t)n_images * mbw * REC + sizeof(int) * ((size_t)n_images * mbh + 4);
+}
+
+extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t y_pitch, int64_t uv_pitch,
+                             int32_t width, int32_t height, int32_t n_images, const uint8_t* segments,
+                             const void* segs, const uint8_t* proba, int32_t method, int32_t quality, void* out,
+                             uint8_t* ry, uint8_t* ru, uint8_t* rv, void* work, void* stream) {
+  WG_REQUIRE(y && u && v && segs && proba && out && ry && ru && rv && work);
+  WG_REQUIRE(width > 0 && height > 0 && n_images > 0);
+  if (method < 4) return wg::invalid("wg_encode_mbs implements method >= 4 (the default); method 3 is not built");
+  const int mbw = (width + 15) >> 4, mbh = (height + 15) >> 4;
+  hipStream_t s = wg::as_stream(stream);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return wg::check_launch("hipGetDevice");
+  if (g_tables_ready_dev != dev) {  // constant tables: level codes, fixed I4 mode costs, scan orders
+    uint16_t fixed[1000];
+    for (int t = 0; t < 10; t++)
+      for (int l = 0; l < 10; l++) {
+        const uint8_t* prob = vp8_bmodes_proba + (t * 10 + l) * 9;
+        for (int m = 0; m < 10; m++) {
+          // walk the mode tree (i4ModeCost, encode_analysis.go:1505)
+          auto contains = [](int node, int mode, auto&& self) -> bool {
+            if (node <= 0) return -node == mode;
+            return self(vp8_ymodes_intra4[2 * node], mode, self) || self(vp8_ymodes_intra4[2 * node + 1], mode, self);
+          };
+          int cost = 0, bit = contains(vp8_ymodes_intra4[0], m, contains) ? 0 : 1;
+          cost += bit ? vp8_entropy_cost[255 - prob[0]] : vp8_entropy_cost[prob[0]];
+          int i = vp8_ymodes_intra4[bit];
+          while (i > 0) {
+            bit = contains(vp8_ymodes_intra4[2 * i], m, contains) ? 0 : 1;
+            cost += bit ? vp8_entropy_cost[255 - prob[i]] : vp8_entropy_cost[prob[i]];
+            i = vp8_ymodes_intra4[2 * i + bit];
+          }
+          fixed[(t * 10 + l) * 10 + m] = (uint16_t)cost;
+        }
+      }
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_fixed_i4), fixed, sizeof(fixed)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_level_codes), vp8_level_codes, sizeof(vp8_level_codes)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_zigzag), vp8_zigzag, sizeof(vp8_zigzag)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_bands), vp8_bands, sizeof(vp8_bands)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_rzig), vp8_reverse_zigzag, sizeof(vp8_reverse_zigzag)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_wtrellis), vp8_weight_trellis, sizeof(vp8_weight_trellis)) != hipSuccess)
+      return wg::check_launch("encode tables");
+    g_tables_ready_dev = dev;
+  }
+  EncArgs a;
+  a.y = y;
+  a.u = u;
+  a.v = v;
+  a.ry = ry;
+  a.ru = ru;
+  a.rv = rv;
+  a.segments = segments;
+  a.segs = static_cast<const Segment*>(segs);
+  a.proba = proba;
+  a.out = static_cast<MbEnc*>(out);
+  a.top = static_cast<uint8_t*>(work);
+  a.ctl = reinterpret_cast<int*>(a.top + (size_t)n_images * mbw * REC);
+  a.progress = a.ctl + 4;
+  a.y_pitch = y_pitch;
+  a.uv_pitch = uv_pitch;
+  a.width = width;
+  a.height = height;
+  a.mbw = mbw;
+  a.mbh = mbh;
+  a.n_img = n_images;
+  a.quality = quality;
+  if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
+    return wg::check_launch("hipMemsetAsync(encode ctl)");
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows, 64, 0) != hipSuccess || per_cu <= 0)
+    return wg::check_launch("encode occupancy query");
+  const int rows = n_images * mbh;
+  const int grid = rows < per_cu * cus ? rows : per_cu * cus;
+  hipLaunchKernelGGL(k_encode_rows, dim3((unsigned)grid), dim3(64), 0, s, a);
+  return wg::check_launch("k_encode_rows");
+}
+
+extern "C" int wg_encode_status(const void* work, int32_t mbw, int32_t n_images, void* stream) {
+  WG_REQUIRE(work && mbw > 0 && n_images > 0);
+  const int* ctl = reinterpret_cast<const int*>(static_cast<const uint8_t*>(work) + (size_t)n_images * mbw * REC);
+  int flag = 0;
+  hipStream_t s = wg::as_stream(stream);
+  if (hipMemcpyAsync(&flag, ctl + 1, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return wg::check_launch("wg_encode_status");
+  if (flag) {
+    wg::set_error("encode: a row dependency wait timed out (output invalid)");
+    return WG_EHIP;
+  }
+  return WG_OK;
+}

@@ -153,3 +153,54 @@ def sharpyuv_convert(rgb, matrix=WEBP_MATRIX, out=None, work=None):
     call("wg_sharpyuv_convert", rgb.data_ptr(), w, h, 3 * w, 3 * w * h, m.ctypes.data, n, Y.data_ptr(), w, h * w,
          U.data_ptr(), V.data_ptr(), cw, cw * ch, work.data_ptr(), _stream())
     return Y, U, V
+
+
+# ---------------- encoder macroblock RD loop (Phase A) ----------------
+
+SQUANT_DTYPE = np.dtype([("quant", "<i4"), ("iquant", "<i4"), ("bias", "<i4"), ("zthresh", "<i4"),
+                         ("dc_quant", "<i4"), ("dc_iquant", "<i4"), ("dc_bias", "<i4"), ("dc_zthresh", "<i4"),
+                         ("sharpen", "<i2", (16,))])  # wg_squant
+SEGMENT_DTYPE = np.dtype([("y1", SQUANT_DTYPE), ("y2", SQUANT_DTYPE), ("uv", SQUANT_DTYPE),
+                          ("lambda_i4", "<i4"), ("lambda_i16", "<i4"), ("lambda_uv", "<i4"), ("lambda_mode", "<i4"),
+                          ("tlambda_i4", "<i4"), ("tlambda_i16", "<i4"), ("tlambda_uv", "<i4"),
+                          ("tlambda_sd", "<i4")])  # wg_segment
+MB_ENC_DTYPE = np.dtype([("coeffs", "<i2", (400,)), ("modes", "u1", (16,)), ("nz_y", "u1", (16,)),
+                         ("nz_uv", "u1", (8,)), ("non_zero_y", "<u4"), ("non_zero_uv", "<u4"),
+                         ("mb_type", "u1"), ("i16_mode", "u1"), ("uv_mode", "u1"), ("nz_dc", "u1"),
+                         ("skip", "u1"), ("segment", "u1"), ("pad", "u1", (2,)), ("score", "<u8")])  # wg_mb_enc
+assert SEGMENT_DTYPE.itemsize == 224 and MB_ENC_DTYPE.itemsize == 864
+
+
+def setup_segment(q, dq=(0, 0, 0, 0, 0), method=4, sns_strength=50):
+    """setupSegment (encode.go:1085) on the host -> SEGMENT_DTYPE record."""
+    seg = np.zeros(1, SEGMENT_DTYPE)
+    d = np.asarray(dq, np.int32)
+    call("wg_setup_segment", q, d.ctypes.data, method, sns_strength, seg.ctypes.data)
+    return seg[0]
+
+
+def encode_mbs(Y, U, V, width, height, segments, segs, proba, method=4, quality=75, recon=None, work=None,
+               out=None, check=False):
+    """Phase A over n frames: Y (n, 16*mbh, 16*mbw) / U, V planes (CUDA uint8),
+    segments (n, mbh*mbw) uint8, segs (4,) SEGMENT_DTYPE, proba (1056,) uint8.
+    Returns (out uint8 tensor viewed as (n*mbw*mbh, 864) wg_mb_enc bytes, (RY, RU, RV))."""
+    n = Y.shape[0]
+    mbw, mbh = mb_dims(width, height)
+    dev = Y.device
+    if recon is None:
+        recon = (torch.empty_like(Y), torch.empty_like(U), torch.empty_like(V))
+    if out is None:
+        out = torch.empty((n * mbw * mbh, MB_ENC_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    if work is None:
+        work = torch.empty(lib.wg_encode_work_bytes(mbw, mbh, n), dtype=torch.uint8, device=dev)
+    if not torch.is_tensor(segs):
+        segs = torch.from_numpy(np.ascontiguousarray(segs, SEGMENT_DTYPE).view(np.uint8).copy()).to(dev)
+    if not torch.is_tensor(proba):
+        proba = torch.from_numpy(np.ascontiguousarray(proba, np.uint8)).to(dev)
+    seg_ptr = None if segments is None else segments.data_ptr()
+    call("wg_encode_mbs", Y.data_ptr(), U.data_ptr(), V.data_ptr(), Y[0].numel(), U[0].numel(), width, height, n,
+         seg_ptr, segs.data_ptr(), proba.data_ptr(), method, quality, out.data_ptr(), recon[0].data_ptr(),
+         recon[1].data_ptr(), recon[2].data_ptr(), work.data_ptr(), _stream())
+    if check:
+        call("wg_encode_status", work.data_ptr(), mbw, n, _stream())
+    return out, recon
