@@ -3,11 +3,13 @@
 One step = one pass of the hot path over this rank's batch of synthetic
 1920x1080 frames, all inputs resident in HBM before timing starts:
   encode side  import RGBA->YUV420 (k_import)  ->  analysis alphas (k_analysis)
+               ->  macroblock RD loop, Phase A of encodeFrameParallel (k_encode_rows)
   decode side  reconstruct + loop filter of parsed macroblocks (k_decode_rows)
                ->  fancy upsample to NRGBA (k_upsample)
-The decode side consumes seeded synthetic macroblock data (tools/synth.py,
-SURVEY.md 8(d) C3 recipe) because the encoder's RD/quantiser stage that would
-produce it is not part of this round.
+The decode side consumes seeded synthetic parsed-macroblock data (tools/synth.py,
+SURVEY.md 8(d) C3 recipe).  Segment ids for the RD loop come from the analysis
+alphas (quartiles, standing in for the CPU-side AssignSegments k-means) with
+q75-range quantisers per segment.
 
 Multi-GPU: one process per GPU (torch.distributed.run), frames sharded across
 ranks with no data-path collective ("weak" scaling); value = all pixels / max
@@ -33,12 +35,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 BYTES_PER_PX = {
     "import": 4.0 + 1.5,              # RGBA in, Y + U/V out
     "analysis": 1.5,                  # Y/U/V planes in (alphas out ~0)
+    "encode": 1.5 + 864 / 256.0 + 1.5,  # YUV in, MBEncInfo (800 B levels + info) + reconstruction out
     "decode": (384 * 2 + 32 + 384) / 256.0,  # coeffs + mb info in, YUV out (recon and filter fused)
     "upsample": 1.5 + 4.0,            # YUV in, NRGBA out
 }
 
 
-KERNELS = {"import": "k_import", "analysis": "k_analysis", "decode": "k_decode_rows", "upsample": "k_upsample"}
+KERNELS = {"import": "k_import", "analysis": "k_analysis", "encode": "k_encode_rows", "decode": "k_decode_rows",
+           "upsample": "k_upsample"}
+SEG_Q = (22, 25, 28, 31)  # quantiser index per segment: q75 (index 26) +- SNS-style offsets
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -51,6 +56,16 @@ def pmc_traffic(kernel):
         return int(rec["hbm_bytes_per_launch"]), os.path.relpath(PMC_FILE, ROOT)
     except (OSError, KeyError, ValueError):
         return None, None
+
+
+def default_proba():
+    """CoeffsProba0 (internal/lossy/proba.go:45): the token probabilities
+    Phase A prices with after ResetProba; read from the generated table."""
+    import re
+    txt = open(os.path.join(ROOT, "webp_amd", "csrc", "vp8_tables.h")).read()
+    body = txt[txt.index("vp8_coeffs_proba0["):]
+    body = body[body.index("{") + 1:body.index("};")]
+    return np.array([int(x) for x in re.findall(r"\d+", body)], np.uint8)
 
 
 def parse():
@@ -97,6 +112,12 @@ class Pipeline:
         self.V = torch.empty_like(self.U)
         self.alphas = torch.empty((batch, MBW * MBH), dtype=torch.int32, device=device)
         self.uv_sum = torch.empty((batch,), dtype=torch.int32, device=device)
+        self.segs = torch.from_numpy(np.stack([frames.setup_segment(q) for q in SEG_Q]).view(np.uint8).copy()).to(device)
+        self.proba = torch.from_numpy(default_proba()).to(device)
+        self.seg_ids = torch.empty((batch, MBW * MBH), dtype=torch.uint8, device=device)
+        self.enc_out = torch.empty((batch * MBW * MBH, frames.MB_ENC_DTYPE.itemsize), dtype=torch.uint8, device=device)
+        self.rY, self.rU, self.rV = torch.empty_like(self.Y), torch.empty_like(self.U), torch.empty_like(self.U)
+        self.enc_work = torch.empty(_lib.lib.wg_encode_work_bytes(MBW, MBH, batch), dtype=torch.uint8, device=device)
         self.dY = torch.empty_like(self.Y)
         self.dU = torch.empty_like(self.U)
         self.dV = torch.empty_like(self.U)
@@ -115,6 +136,12 @@ class Pipeline:
         if record:
             ev.append(torch.cuda.Event(enable_timing=True)); ev[-1].record()
         f.analysis_alphas(self.Y, self.U, self.V, W, H, out=(self.alphas, self.uv_sum, None, None))
+        if record:
+            ev.append(torch.cuda.Event(enable_timing=True)); ev[-1].record()
+        torch.clamp(self.alphas >> 6, max=3, out=self.alphas)
+        self.seg_ids.copy_(self.alphas)
+        f.encode_mbs(self.Y, self.U, self.V, W, H, self.seg_ids, self.segs, self.proba, out=self.enc_out,
+                     recon=(self.rY, self.rU, self.rV), work=self.enc_work)
         if record:
             ev.append(torch.cuda.Event(enable_timing=True)); ev[-1].record()
         f.decode_frames(self.mb, self.co, 2, MBW, MBH, self.batch, out=(self.dY, self.dU, self.dV), work=self.work)
@@ -145,9 +172,13 @@ def cpu_baseline(seconds, mb_co):
     per = MBW * MBH
     mb1, co1 = mb[:per], co[:per]
     frames_done, t0 = 0, time.perf_counter()
+    segs = np.stack([O.setup_segment(q) for q in SEG_Q])
+    proba = default_proba()
     while True:
         Y, U, V = O.import_rgba(img, has_alpha=False)
-        O.compute_alphas(Y, U, V, W, H)
+        alphas, _, _, _ = O.compute_alphas(Y, U, V, W, H)
+        seg_ids = np.minimum(np.asarray(alphas) >> 6, 3).astype(np.uint8)
+        O.encode_frame_rd(Y, U, V, W, H, seg_ids, segs, proba, method=4, quality=75)
         dy, du, dv = O.decode_frame(mb1, co1, 2, MBW, MBH)
         O.build_nrgba(dy, du, dv, W, H)
         frames_done += 1
@@ -155,7 +186,7 @@ def cpu_baseline(seconds, mb_co):
         if el >= seconds:
             break
     return {"value": round(frames_done * W * H / el / 1e6, 2), "unit": "MPixels/s", "cores": 1, "kind": "port",
-            "sample": f"{frames_done} x 1920x1080 frames (import+analysis+decode+upsample), C restatement of the "
+            "sample": f"{frames_done} x 1920x1080 frames (import+analysis+MB RD+decode+upsample), C restatement of the "
                       "reference Go CPU path, single thread"}
 
 
@@ -212,9 +243,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (gradient/noise/blobs RGBA; seeded parsed-macroblock data)",
+            "data": "synthetic (gradient/noise/blobs RGBA; seeded parsed-macroblock data for the decode side)",
             "config": {"workload": f"{args.batch} x 1920x1080 frames per GPU per step (C2 frame, C4 per-GPU share): "
-                                   "import+analysis (encode DSP) + reconstruct+loopfilter+upsample (decode DSP)",
+                                   "import+analysis+MB RD loop (encode DSP, method 4) + reconstruct+loopfilter+upsample (decode DSP)",
                        "frames_per_gpu": args.batch, "width": W, "height": H, "parallelism": f"frames sharded x{world}"},
             "stage_ms": {k: round(v, 3) for k, v in stage.items()},
             "roofline": {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -40,6 +40,8 @@ def main():
     px = B * W * H
     if os.environ.get("DECODE_ONLY"):
         return decode_cases(Y, U, V, px, dev)
+    if os.environ.get("ENCODE_ONLY"):
+        return encode_cases(Y, U, V, px, dev)
     t = timeit(lambda: frames.import_rgba(rgba, has_alpha=False, out=(Y, U, V)))
     print(f"import      {t:8.3f} ms  {px / t / 1e3:9.1f} MPix/s  {5.5 * px / t / 1e6:7.1f} GB/s")
     al = torch.empty((B, MBW * MBH), dtype=torch.int32, device=dev)
@@ -50,6 +52,18 @@ def main():
     t = timeit(lambda: frames.build_nrgba(Y, U, V, W, H, out=out))
     print(f"upsample    {t:8.3f} ms  {px / t / 1e3:9.1f} MPix/s  {5.5 * px / t / 1e6:7.1f} GB/s")
     decode_cases(Y, U, V, px, dev)
+    encode_cases(Y, U, V, px, dev)
+
+
+def encode_cases(Y, U, V, px, dev):
+    segs = np.stack([frames.setup_segment(q) for q in (20, 24, 28, 32)])
+    mbs = MBW * MBH
+    seg_ids = torch.from_numpy((np.arange(B * mbs) % 4).astype(np.uint8)).to(dev)
+    import oracle as O
+    proba = O.default_proba()
+    out, rec = frames.encode_mbs(Y, U, V, W, H, seg_ids, segs, proba)
+    t = timeit(lambda: frames.encode_mbs(Y, U, V, W, H, seg_ids, segs, proba, out=out, recon=rec))
+    print(f"encode_rd   {t:8.3f} ms  {px / t / 1e3:9.1f} MPix/s  ({B} frames)")
 
 
 def decode_cases(Y, U, V, px, dev):

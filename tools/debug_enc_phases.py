@@ -1,0 +1,25 @@
+"""Diagnostic: cycles per phase of k_encode_rows (stamped build, see tools/gpu_enc_phases.sh)."""
+import ctypes, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+import oracle as O
+from webp_amd import _lib, frames
+from tools import synth
+B, W, H = int(os.environ.get("BATCH", "64")), 1920, 1080
+MBW, MBH = 120, 68
+names = ["wait", "import+ctx", "i16rd", "i4rd", "uvrd", "final", "recon+export", "-", "i4:prescreen", "i4:select", "i4:candidates", "i4:winner"]
+_lib.lib.wg_debug_enc_phases.argtypes = [ctypes.c_void_p, ctypes.c_int]
+buf = (ctypes.c_ulonglong * 16)()
+Y, U, V = O.import_rgba(synth.blobs_rgba(W, H, seed=3), has_alpha=False)
+Yt = torch.from_numpy(np.stack([Y] * B)).cuda(); Ut = torch.from_numpy(np.stack([U] * B)).cuda(); Vt = torch.from_numpy(np.stack([V] * B)).cuda()
+segs = np.stack([frames.setup_segment(q) for q in (20, 24, 28, 32)])
+seg_ids = torch.from_numpy((np.arange(B * MBW * MBH) % 4).astype(np.uint8)).cuda()
+out, rec = frames.encode_mbs(Yt, Ut, Vt, W, H, seg_ids, segs, O.default_proba())
+torch.cuda.synchronize()
+_lib.lib.wg_debug_enc_phases(ctypes.addressof(buf), 16)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(); frames.encode_mbs(Yt, Ut, Vt, W, H, seg_ids, segs, O.default_proba(), out=out, recon=rec); e1.record()
+torch.cuda.synchronize()
+_lib.lib.wg_debug_enc_phases(ctypes.addressof(buf), 16)
+v = np.frombuffer(buf, dtype=np.uint64)[:12].astype(np.float64) / (MBW * MBH * B)
+print(f"{e0.elapsed_time(e1):.3f} ms; cycles per MB: " + ", ".join(f"{n}={x:.0f}" for n, x in zip(names, v)) + f"; total={v[:7].sum():.0f}")

@@ -77,6 +77,10 @@ struct Shared {
   uint8_t proba[4 * 8 * 3 * 11];
   uint16_t ecost[256];
   uint16_t lfixed[2048];
+  // probability-dependent part of the level cost for every (type, band, ctx)
+  // and level 1..67 (variableLevelCost, encode_quant.go:258-273; levels past
+  // 67 share entry 67), built once per workgroup from `proba`
+  uint16_t vcost[4 * 8 * 3][68];
   Segment seg[4];
   uint8_t yin[YUV], yout[YUV], yout2[YUV];
   alignas(16) int16_t coeffs[400];
@@ -97,7 +101,7 @@ __device__ __forceinline__ const uint8_t* proba_p(const Shared& s, int type, int
 }
 
 // QuantizeCoeffs (encode_quant.go:16-80): returns the zigzag nz count
-__device__ int quantize(const int co[16], int16_t q[16], const SQuant& sq, int first) {
+__device__ __forceinline__ int quantize(const int co[16], int16_t q[16], const SQuant& sq, int first) {
   int max_zz = -1;
 #pragma unroll
   for (int n = 0; n < 16; n++) {
@@ -129,8 +133,12 @@ __device__ __forceinline__ int variable_level_cost(const Shared& s, int level, c
   return cost;
 }
 
+__device__ __forceinline__ int level_cost(const Shared& s, int tbc, int level) {  // fixed + variable, level >= 1
+  return s.lfixed[level] + s.vcost[tbc][min(level, 67)];
+}
+
 // TokenCostForCoeffs (encode_quant.go:154-223), unrolled (no early break)
-__device__ int token_cost(const Shared& s, const int16_t q[16], int nz_count, int type, int ctx0, int first) {
+__device__ __forceinline__ int token_cost(const Shared& s, const int16_t q[16], int nz_count, int type, int ctx0, int first) {
   if (nz_count <= first) return ecost(s, proba_p(s, type, first == 0 ? 0 : 1, ctx0)[0]);
   const int last = nz_count - 1;
   int cost = 0, ctx = ctx0;
@@ -150,17 +158,8 @@ __device__ int token_cost(const Shared& s, const int16_t q[16], int nz_count, in
       cost += ecost(s, pp[1]);
       ctx = 0;
     } else {
-      cost += ecost(s, 255 - pp[1]);
-      if (v == 1) {
-        cost += s.lfixed[1] + ecost(s, pp[2]);
-        ctx = 1;
-      } else if (v == 2) {
-        cost += s.lfixed[2] + ecost(s, 255 - pp[2]) + ecost(s, pp[3]) + ecost(s, pp[4]);
-        ctx = 2;
-      } else {
-        cost += s.lfixed[v] + variable_level_cost(s, v, pp);
-        ctx = 2;
-      }
+      cost += ecost(s, 255 - pp[1]) + level_cost(s, (type * 8 + kBand[n]) * 3 + ctx, v);
+      ctx = v == 1 ? 1 : 2;
     }
   }
   return cost;
@@ -168,7 +167,7 @@ __device__ int token_cost(const Shared& s, const int16_t q[16], int nz_count, in
 
 // TrellisQuantizeBlock (encode_trellis.go:23-301).  Path kept packed per
 // position: levels of the three end contexts + their predecessor context.
-__device__ int trellis(const Shared& s, const int co[16], int16_t q[16], const SQuant& sq, int first, int ctx_type,
+__device__ __forceinline__ int trellis(const Shared& s, const int co[16], int16_t q[16], const SQuant& sq, int first, int ctx_type,
                        int init_ctx, int lambda) {
   {  // pre-scan: all levels zero under the neutral bias?
     bool nonzero = false;
@@ -254,7 +253,7 @@ __device__ int trellis(const Shared& s, const int co[16], int16_t q[16], const S
       if (has0 || has1) {
         const int nzc = not_eob + ecost(s, 255 - p[1]);
         if (has0) {
-          const int64_t t = base + (int64_t)(nzc + fixed0 + variable_level_cost(s, L0, p)) * lam + d0;
+          const int64_t t = base + (int64_t)(nzc + fixed0 + s.vcost[(ctx_type * 8 + band) * 3 + pc][min(L0, 67)]) * lam + d0;
 #pragma unroll
           for (int k = 0; k < 3; k++)
             if (k == nctx0 && (!cv[k] || t < cs[k])) {
@@ -265,7 +264,7 @@ __device__ int trellis(const Shared& s, const int co[16], int16_t q[16], const S
             }
         }
         if (has1) {
-          const int64_t t = base + (int64_t)(nzc + fixed1 + variable_level_cost(s, L0 + 1, p)) * lam + d1;
+          const int64_t t = base + (int64_t)(nzc + fixed1 + s.vcost[(ctx_type * 8 + band) * 3 + pc][min(L0 + 1, 67)]) * lam + d1;
 #pragma unroll
           for (int k = 0; k < 3; k++)
             if (k == nctx1 && (!cv[k] || t < cs[k])) {
@@ -438,6 +437,41 @@ struct EncArgs {
 
 constexpr uint64_t SPIN_TICKS = 200000000ull;
 
+#ifdef WG_STAMPS
+// Diagnostic build only: cycles per phase summed over macroblocks.
+__device__ unsigned long long g_enc_phase[16];
+#define ESTAMP_DECL unsigned long long st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0, sub_prev = 0
+#define ESTAMP(k)                                                                  \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long ts_;                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");   \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    if ((k) > 0) st_acc[(k)-1] += ts_ - st_prev;                                   \
+    st_prev = ts_;                                                                 \
+  } while (0)
+#define ESTAMP_FLUSH()                                                              \
+  do {                                                                              \
+    if (lane == 0)                                                                  \
+      for (int k_ = 0; k_ < 12; k_++) atomicAdd(&g_enc_phase[k_], st_acc[k_]);      \
+  } while (0)
+// sub-phase stamps (inside a phase): accumulate into st_acc[8 + k], k >= 0
+#define SSTAMP(k)                                                                  \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long ts_;                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");   \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    if ((k) >= 0) st_acc[8 + (k)] += ts_ - sub_prev;                              \
+    sub_prev = ts_;                                                                \
+  } while (0)
+#else
+#define SSTAMP(k) (void)0
+#define ESTAMP_DECL int st_unused_ = 0
+#define ESTAMP(k) (void)st_unused_
+#define ESTAMP_FLUSH() (void)st_unused_
+#endif
+
 __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
   __shared__ Shared s;
   const int lane = threadIdx.x;
@@ -446,10 +480,16 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
   for (int i = lane; i < 2048; i += 64) s.lfixed[i] = vp8_level_fixed_costs[i];
   for (int i = lane; i < (int)(4 * sizeof(Segment) / 4); i += 64)
     reinterpret_cast<int*>(s.seg)[i] = reinterpret_cast<const int*>(a.segs)[i];
+  __syncthreads();
+  for (int i = lane; i < 4 * 8 * 3 * 68; i += 64) {
+    const int tbc = i / 68, level = i % 68;
+    s.vcost[tbc][level] = level == 0 ? 0 : (uint16_t)variable_level_cost(s, level, s.proba + tbc * 11);
+  }
   const int mbw = a.mbw, mbh = a.mbh;
   const int ys = 16 * mbw, uvs = 8 * mbw;
   const int max_modes = a.quality < 50 ? 2 : 3;
   const int total_rows = a.n_img * mbh;
+  ESTAMP_DECL;
   lds_sync();
 
   for (;;) {
@@ -480,6 +520,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
 
     for (int mbx = 0; mbx < mbw; mbx++) {
       const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
+      ESTAMP(0);
       // ---- wait for the row above (MB x+1 done) ----
       if (mby > 0) {
         const int need = min(mbx + 2, mbw);
@@ -502,6 +543,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
           seen = __shfl(v, 0, 64);
         }
       }
+      ESTAMP(1);
       const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
       const Segment& sg = s.seg[segid];
       // ---- import (importBlockParallel :433-452) with edge replication ----
@@ -557,6 +599,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
       top_modes = __builtin_amdgcn_readfirstlane(top_modes);
       top_nz_dc = __builtin_amdgcn_readfirstlane(top_nz_dc);
 
+      ESTAMP(2);
       // ================= I16 RD (pickBestI16ModeRDParallel :624-737) =================
       bool src_flat;
       {
@@ -646,6 +689,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
       }
       const uint64_t s16 = rd_score(disto16, rate16, sg.lambda_mode);
 
+      ESTAMP(3);
       // ================= I4 RD (tryI4ModesRDParallel :739-846) =================
       for (int i = lane; i < YUV / 4; i += 64)
         reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
@@ -665,6 +709,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
           const int nz_ctx = min(l + t, 2);
           int src[16];
           load4x4(s.yin + off, src);
+          SSTAMP(-1);
           // pre-screen all eligible modes by prediction SSE
           if (lane < 10) {
             const bool ok = !(!has_top && needs_top4(lane)) && !(!has_left && needs_left4(lane));
@@ -673,28 +718,57 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
             s.sse10[lane] = ok ? sse16(src, pred) : -1;
           }
           lds_sync();
-          // partial selection sort of the candidates, in the reference's order (:869-886)
-          int cm[10], cs[10], nc = 0;
-          for (int k = 0; k < 10; k++)
-            if (s.sse10[k] >= 0) {
-              cm[nc] = k;
-              cs[nc] = s.sse10[k];
+          SSTAMP(0);
+          // partial selection sort of the candidates, in the reference's order
+          // (:869-886): compact the eligible modes, then K rounds of argmin +
+          // swap.  Every index is a compile-time slot (selects, no scratch).
+          int cm[10], cs[10];
+#pragma unroll
+          for (int p = 0; p < 10; p++) {
+            cm[p] = 0;
+            cs[p] = 0x7fffffff;
+          }
+          int nc = 0;
+#pragma unroll
+          for (int mm = 0; mm < 10; mm++) {
+            const int v = s.sse10[mm];
+            if (v >= 0) {
+#pragma unroll
+              for (int p = 0; p < 10; p++)
+                if (p == nc) {
+                  cm[p] = mm;
+                  cs[p] = v;
+                }
               nc++;
             }
+          }
           const int K = min(max_modes, nc);
-          for (int i = 0; i < K; i++) {
-            int mi = i;
-            for (int j = i + 1; j < nc; j++)
-              if (cs[j] < cs[mi]) mi = j;
-            if (mi != i) {
-              int t2 = cm[i];
-              cm[i] = cm[mi];
-              cm[mi] = t2;
-              t2 = cs[i];
-              cs[i] = cs[mi];
-              cs[mi] = t2;
+#pragma unroll
+          for (int i = 0; i < 3; i++) {
+            if (i < K) {
+              int mi = i, bsse = cs[i];
+#pragma unroll
+              for (int j = i + 1; j < 10; j++)
+                if (j < nc && cs[j] < bsse) {
+                  bsse = cs[j];
+                  mi = j;
+                }
+              int mmode = cm[i];
+#pragma unroll
+              for (int p = i + 1; p < 10; p++)
+                if (p == mi) mmode = cm[p];
+              const int im = cm[i], is = cs[i];
+#pragma unroll
+              for (int p = i + 1; p < 10; p++)
+                if (p == mi) {
+                  cm[p] = im;
+                  cs[p] = is;
+                }
+              cm[i] = mmode;
+              cs[i] = bsse;
             }
           }
+          SSTAMP(1);
           // candidates in parallel (lane i = candidate i)
           uint64_t score = ~0ull;
           int rate = 0, disto = 0, nz = 0, mode = cm[0];
@@ -722,6 +796,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
             rate += c_fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
             score = rd_score(disto, rate, sg.lambda_i4);
           }
+          SSTAMP(2);
           // first minimum over candidates (strict '<' in candidate order)
           int win = 0;
           uint64_t wsc = __shfl(score, 0, 64);
@@ -751,11 +826,13 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
             store4x4(s.yout2 + off, rec);
           }
           lds_sync();
+          SSTAMP(3);
         }
         s4 = early ? ~0ull : rd_score(total_disto, total_rate + 211, sg.lambda_mode);
       }
       const bool is_i4 = s4 < s16;
 
+      ESTAMP(4);
       // ================= UV RD (pickBestUVModeRDParallel :1030-1114) =================
       int best_uv = 0;
       {
@@ -826,6 +903,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
       }
       lds_sync();
 
+      ESTAMP(5);
       // ================= final residuals (encodeResidualsParallel :1166-1356) =================
       uint32_t nzy_mask = 0, nzuv_mask = 0;
       int nz_dc = 0;
@@ -886,6 +964,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
       lds_sync();
       for (int i = 0; i < 8; i++) nzuv_mask |= (s.nzuv[i] > 0 ? 1u : 0u) << i;
 
+      ESTAMP(6);
       // ================= reconstruction (reconstructMBParallel :1358-1410) =================
       if (!is_i4) {
         if (lane == 0) {
@@ -1036,13 +1115,23 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
       lds_sync();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ESTAMP(7);
     }
   }
+  ESTAMP_FLUSH();
 }
 
 int g_tables_ready_dev = -1;
 
 }  // namespace
+
+#ifdef WG_STAMPS
+extern "C" int wg_debug_enc_phases(unsigned long long* host, int n) {
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_enc_phase), sizeof(unsigned long long) * n);
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_enc_phase), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 extern "C" size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images) {
   if (mbw <= 0 || mbh <= 0 || n_images <= 0) return 0;
