@@ -73,14 +73,23 @@ __constant__ uint8_t c_zigzag[16], c_bands[17], c_rzig[16];
 __constant__ int32_t c_wtrellis[16];
 
 // ------------------------------------------------------------------ LDS state
+// token costs of one (type, band) row, per context 0..2: `zero` = not-EOB +
+// zero token, `nz` = not-EOB + non-zero token prefix, `eob` = EOB
+// (the bit-cost sums TokenCostForCoeffs / TrellisQuantizeBlock take per
+// position, encode_quant.go:154-223, encode_trellis.go:150-230)
+struct alignas(16) TokRow {
+  uint16_t zero[4], nz[4], eob[4], pad[4];
+};
 struct Shared {
   uint8_t proba[4 * 8 * 3 * 11];
   uint16_t ecost[256];
   uint16_t lfixed[2048];
-  // probability-dependent part of the level cost for every (type, band, ctx)
-  // and level 1..67 (variableLevelCost, encode_quant.go:258-273; levels past
-  // 67 share entry 67), built once per workgroup from `proba`
-  uint16_t vcost[4 * 8 * 3][68];
+  TokRow tok[4 * 8];
+  // probability-dependent part of the level cost for every (type, band),
+  // level 1..67 and context (levels past 67 share entry 67;
+  // variableLevelCost, encode_quant.go:258-273): the three contexts of one
+  // level sit in one 8-byte word so one ds_read_b64 serves a trellis step
+  uint64_t vcost[4 * 8][68];
   Segment seg[4];
   uint8_t yin[YUV], yout[YUV], yout2[YUV];
   alignas(16) int16_t coeffs[400];
@@ -90,7 +99,9 @@ struct Shared {
   int dcq[4][16];  // per mode: quantised WHT levels (I16 RD), then block DCs after the inverse WHT
   int dcout[4][16];
   int mode_rate[4], mode_disto[4];
-  int sse10[10];
+  int sse10[2][10];
+  int blk_rate[16], blk_disto[16], blk_hdr[16];
+  uint16_t fixed_i4[1000];
   int word;
 };
 
@@ -99,6 +110,8 @@ __device__ __forceinline__ int bit_cost(const Shared& s, int bit, int p) { retur
 __device__ __forceinline__ const uint8_t* proba_p(const Shared& s, int type, int band, int ctx) {
   return s.proba + ((type * 8 + band) * 3 + ctx) * 11;
 }
+__device__ __forceinline__ int pick3(int c, int a0, int a1, int a2) { return c == 0 ? a0 : (c == 1 ? a1 : a2); }
+__device__ __forceinline__ int vc_of(uint64_t w, int c) { return (int)((w >> (16 * c)) & 0xffff); }
 
 // QuantizeCoeffs (encode_quant.go:16-80): returns the zigzag nz count
 __device__ __forceinline__ int quantize(const int co[16], int16_t q[16], const SQuant& sq, int first) {
@@ -133,47 +146,46 @@ __device__ __forceinline__ int variable_level_cost(const Shared& s, int level, c
   return cost;
 }
 
-__device__ __forceinline__ int level_cost(const Shared& s, int tbc, int level) {  // fixed + variable, level >= 1
-  return s.lfixed[level] + s.vcost[tbc][min(level, 67)];
-}
-
-// TokenCostForCoeffs (encode_quant.go:154-223), unrolled (no early break)
+// TokenCostForCoeffs (encode_quant.go:154-223), branch-free: the context of
+// every position follows from the levels alone (min(|q|, 2) of the previous
+// one), so all table reads are independent and issue back to back.
 __device__ __forceinline__ int token_cost(const Shared& s, const int16_t q[16], int nz_count, int type, int ctx0, int first) {
-  if (nz_count <= first) return ecost(s, proba_p(s, type, first == 0 ? 0 : 1, ctx0)[0]);
-  const int last = nz_count - 1;
   int cost = 0, ctx = ctx0;
-  bool done = false;
+  const int eob_at = max(nz_count, first);
 #pragma unroll
   for (int n = 0; n < 16; n++) {
-    if (n < first || done) continue;
-    const uint8_t* pp = proba_p(s, type, kBand[n], ctx);
-    if (n > last) {
-      cost += ecost(s, pp[0]);
-      done = true;
-      continue;
-    }
+    if (n < first) continue;
+    const TokRow& t = s.tok[type * 8 + kBand[n]];
     const int v = abs((int)q[kZig[n]]);
-    cost += ecost(s, 255 - pp[0]);
-    if (v == 0) {
-      cost += ecost(s, pp[1]);
-      ctx = 0;
-    } else {
-      cost += ecost(s, 255 - pp[1]) + level_cost(s, (type * 8 + kBand[n]) * 3 + ctx, v);
-      ctx = v == 1 ? 1 : 2;
-    }
+    const uint64_t vw = s.vcost[type * 8 + kBand[n]][min(v, 67)];
+    const int tokc = v == 0 ? pick3(ctx, t.zero[0], t.zero[1], t.zero[2])
+                            : pick3(ctx, t.nz[0], t.nz[1], t.nz[2]) + s.lfixed[min(v, 2047)] + vc_of(vw, ctx);
+    const int eob = pick3(ctx, t.eob[0], t.eob[1], t.eob[2]);
+    cost += n < nz_count ? tokc : (n == eob_at ? eob : 0);
+    ctx = min(v, 2);
   }
   return cost;
 }
 
-// TrellisQuantizeBlock (encode_trellis.go:23-301).  Path kept packed per
-// position: levels of the three end contexts + their predecessor context.
-__device__ __forceinline__ int trellis(const Shared& s, const int co[16], int16_t q[16], const SQuant& sq, int first, int ctx_type,
-                       int init_ctx, int lambda) {
+// TrellisQuantizeBlock (encode_trellis.go:23-301), branch-free.
+//
+// Scores are kept x16 so the low 4 bits of a 64-bit key can carry the
+// candidate's position in the reference's update order; "first strict
+// minimum in order" then is a plain min over keys.  Candidates per position
+// and end context: level 0 from predecessor pc (key idx = pc, end ctx 0),
+// level L0 (idx 2pc) and L0 + 1 (idx 2pc + 1), whose end context is
+// min(level, 2).  Invalid states carry scores >= 2^58 (valid ones stay below
+// 2^51), so they never win against a valid candidate.  The path keeps the
+// winning idx per end context (4 bits each, 16 bits per position); levels
+// are re-derived from `co` when walking back.
+template <int FIRST, int CTX_TYPE>
+__device__ __forceinline__ int trellis(const Shared& s, const int co[16], int16_t q[16], const SQuant& sq, int init_ctx,
+                                       int lambda) {
+  constexpr int64_t BIG = 1ll << 59, VALID = 1ll << 58;
   {  // pre-scan: all levels zero under the neutral bias?
     bool nonzero = false;
 #pragma unroll
-    for (int n = 0; n < 16; n++) {
-      if (n < first) continue;
+    for (int n = FIRST; n < 16; n++) {
       const int zig = kZig[n];
       const int c0 = max(abs(co[zig]) + sq.sharpen[zig], 0);
       const int iq = n == 0 ? sq.dc_iquant : sq.iquant;
@@ -186,130 +198,92 @@ __device__ __forceinline__ int trellis(const Shared& s, const int co[16], int16_
     }
   }
   init_ctx = min(init_ctx, 2);
-  int64_t ps[3];
-  bool pv[3];
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    pv[c] = c == init_ctx;
-    ps[c] = 0;
-  }
-  // path per position: A = level(ctx0) | level(ctx1) << 16, B = level(ctx2) |
-  // pred ctx 0/1/2 at bits 16/18/20 | valid mask at bit 22
-  uint32_t pathA[16], pathB[16];
-  const int64_t lam = lambda;
-  int64_t best_terminal = (int64_t)bit_cost(s, 0, proba_p(s, ctx_type, first == 0 ? 0 : 1, init_ctx)[0]) * lam;
-  int best_n = -1, best_c = -1;
+  int64_t ps0 = init_ctx == 0 ? 0 : BIG, ps1 = init_ctx == 1 ? 0 : BIG, ps2 = init_ctx == 2 ? 0 : BIG;
+  uint32_t path[8];
+  const int lam16 = lambda * 16;
+  const TokRow& t_init = s.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
+  int64_t best_terminal = (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16;
+  int best = -1;  // n << 2 | end context
 #pragma unroll
   for (int n = 0; n < 16; n++) {
-    if (n < first) {
-      pathA[n] = 0;
-      pathB[n] = 0;
+    if (n < FIRST) {
+      if (!(n & 1)) path[n >> 1] = 0;
       continue;
     }
     const int zig = kZig[n];
     const int band = kBand[n + 1];
-    int raw = co[zig];
-    const int sign = raw < 0 ? -1 : 1;
-    raw = abs(raw);
-    const int c0 = max(raw + sq.sharpen[zig], 0);
+    const int c0 = max(abs(co[zig]) + sq.sharpen[zig], 0);
     const int quant = n == 0 ? sq.dc_quant : sq.quant;
     const int iquant = n == 0 ? sq.dc_iquant : sq.iquant;
     const int L0 = min((c0 * iquant) >> 17, 2047);
     const int thresh = min((int)(((uint32_t)c0 * (uint32_t)iquant + 65536u) >> 17), 2047);
-    const int64_t weight = c_wtrellis[zig];
-    const int64_t c0sq = (int64_t)(c0 * c0);
+    const int w4096 = c_wtrellis[zig] * 4096;
     const bool has0 = L0 > 0 && L0 <= thresh;
     const bool has1 = L0 + 1 <= 2047 && L0 + 1 <= thresh;
-    int64_t d0 = 0, d1 = 0;
-    int fixed0 = 0, fixed1 = 0;
-    if (has0) {
-      const int err = c0 - L0 * quant;
-      d0 = 256 * (weight * ((int64_t)(err * err) - c0sq));
-      fixed0 = s.lfixed[L0];
-    }
-    if (has1) {
-      const int err = c0 - (L0 + 1) * quant;
-      d1 = 256 * (weight * ((int64_t)(err * err) - c0sq));
-      fixed1 = s.lfixed[L0 + 1];
-    }
-    const int nctx0 = min(L0, 2), nctx1 = min(L0 + 1, 2);
-    int64_t cs[3] = {0, 0, 0};
-    bool cv[3] = {false, false, false};
-    int16_t cl[3] = {0, 0, 0};
-    uint8_t cp[3] = {0, 0, 0};
+    const int e0 = c0 - L0 * quant, e1 = c0 - (L0 + 1) * quant;
+    // per-level parts (fixed level cost, distortion delta 256 * w * (err^2 -
+    // c0^2), both squares < 2^27), x16, + BIG when not a candidate
+    const int64_t A0 = (int64_t)s.lfixed[L0] * lam16 + (int64_t)w4096 * (e0 * e0 - c0 * c0) + (has0 ? 0 : BIG);
+    const int64_t A1 = (int64_t)s.lfixed[min(L0 + 1, 2047)] * lam16 + (int64_t)w4096 * (e1 * e1 - c0 * c0) + (has1 ? 0 : BIG);
+    const TokRow& t = s.tok[CTX_TYPE * 8 + band];
+    const uint64_t v0 = s.vcost[CTX_TYPE * 8 + band][min(L0, 67)], v1 = s.vcost[CTX_TYPE * 8 + band][min(L0 + 1, 67)];
+    int64_t kz = BIG * 2, ka = BIG * 2, kb = BIG * 2;
 #pragma unroll
     for (int pc = 0; pc < 3; pc++) {
-      if (!pv[pc]) continue;
-      const int64_t base = ps[pc];
-      const uint8_t* p = proba_p(s, ctx_type, band, pc);
-      const int not_eob = ecost(s, 255 - p[0]);
-      const int64_t t0 = base + (int64_t)(not_eob + ecost(s, p[1])) * lam;
-      if (!cv[0] || t0 < cs[0]) {
-        cs[0] = t0;
-        cl[0] = 0;
-        cp[0] = (uint8_t)pc;
-        cv[0] = true;
-      }
-      if (has0 || has1) {
-        const int nzc = not_eob + ecost(s, 255 - p[1]);
-        if (has0) {
-          const int64_t t = base + (int64_t)(nzc + fixed0 + s.vcost[(ctx_type * 8 + band) * 3 + pc][min(L0, 67)]) * lam + d0;
-#pragma unroll
-          for (int k = 0; k < 3; k++)
-            if (k == nctx0 && (!cv[k] || t < cs[k])) {
-              cs[k] = t;
-              cl[k] = (int16_t)(sign * L0);
-              cp[k] = (uint8_t)pc;
-              cv[k] = true;
-            }
-        }
-        if (has1) {
-          const int64_t t = base + (int64_t)(nzc + fixed1 + s.vcost[(ctx_type * 8 + band) * 3 + pc][min(L0 + 1, 67)]) * lam + d1;
-#pragma unroll
-          for (int k = 0; k < 3; k++)
-            if (k == nctx1 && (!cv[k] || t < cs[k])) {
-              cs[k] = t;
-              cl[k] = (int16_t)(sign * (L0 + 1));
-              cp[k] = (uint8_t)pc;
-              cv[k] = true;
-            }
-        }
-      }
+      const int64_t base = pc == 0 ? ps0 : (pc == 1 ? ps1 : ps2);
+      const int64_t z = base + pc + (int64_t)t.zero[pc] * lam16;
+      const int64_t ca = base + 2 * pc + A0 + (int64_t)(t.nz[pc] + vc_of(v0, pc)) * lam16;
+      const int64_t cb = base + 2 * pc + 1 + A1 + (int64_t)(t.nz[pc] + vc_of(v1, pc)) * lam16;
+      kz = z < kz ? z : kz;
+      ka = ca < ka ? ca : ka;
+      kb = cb < kb ? cb : kb;
     }
-    pathA[n] = (uint32_t)(uint16_t)cl[0] | ((uint32_t)(uint16_t)cl[1] << 16);
-    pathB[n] = (uint32_t)(uint16_t)cl[2] | ((uint32_t)cp[0] << 16) | ((uint32_t)cp[1] << 18) | ((uint32_t)cp[2] << 20) |
-               ((uint32_t)((cv[0] ? 1 : 0) | (cv[1] ? 2 : 0) | (cv[2] ? 4 : 0)) << 22);
-#pragma unroll
-    for (int c = 1; c < 3; c++) {
-      if (!cv[c]) continue;
-      int64_t eob = cs[c];
-      if (n < 15) eob += (int64_t)ecost(s, proba_p(s, ctx_type, band, c)[0]) * lam;
-      if (eob < best_terminal) {
-        best_terminal = eob;
-        best_n = n;
-        best_c = c;
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-      ps[c] = cs[c];
-      pv[c] = cv[c];
-    }
+    // route L0 / L0 + 1 to their end contexts min(level, 2)
+    const int64_t kab = kb < ka ? kb : ka;
+    const int64_t k1 = L0 == 0 ? kb : (L0 == 1 ? ka : BIG);
+    const int64_t k2 = L0 == 0 ? BIG : (L0 == 1 ? kb : kab);
+    const uint32_t rec = ((uint32_t)kz & 15) | (((uint32_t)k1 & 15) << 4) | (((uint32_t)k2 & 15) << 8);
+    if (n & 1)
+      path[n >> 1] |= rec << 16;
+    else
+      path[n >> 1] = rec;
+    ps0 = kz & ~15ll;
+    ps1 = k1 & ~15ll;
+    ps2 = k2 & ~15ll;
+    // terminal (EOB after this position) from end contexts 1 and 2
+    const int64_t eob1 = ps1 + (n < 15 ? (int64_t)t.eob[1] * lam16 : 0);
+    const bool w1 = ps1 < VALID && eob1 < best_terminal;
+    best_terminal = w1 ? eob1 : best_terminal;
+    best = w1 ? (n << 2 | 1) : best;
+    const int64_t eob2 = ps2 + (n < 15 ? (int64_t)t.eob[2] * lam16 : 0);
+    const bool w2 = ps2 < VALID && eob2 < best_terminal;
+    best_terminal = w2 ? eob2 : best_terminal;
+    best = w2 ? (n << 2 | 2) : best;
   }
+  if (best < 0) {
 #pragma unroll
-  for (int i = 0; i < 16; i++) q[i] = 0;
-  if (best_n < 0) return 0;
-  int ctx = best_c, last = 0;
+    for (int i = 0; i < 16; i++) q[i] = 0;
+    return 0;
+  }
+  const int best_n = best >> 2;
+  int ctx = best & 3, last = 0;
 #pragma unroll
   for (int n = 15; n >= 0; n--) {
-    if (n > best_n || n < first) continue;
-    if ((pathB[n] >> (22 + ctx)) & 1) {
-      const int16_t lv = (int16_t)(ctx == 0 ? pathA[n] : (ctx == 1 ? pathA[n] >> 16 : pathB[n]));
-      const int pcx = (int)((pathB[n] >> (16 + 2 * ctx)) & 3);
-      q[kZig[n]] = lv;
-      if (lv != 0 && last == 0) last = n + 1;
-      ctx = pcx;
+    const int zig = kZig[n];
+    if (n < FIRST) {
+      q[zig] = 0;
+      continue;
     }
+    const bool act = n <= best_n;
+    const int idx = (int)(((path[n >> 1] >> (16 * (n & 1))) >> (4 * ctx)) & 15);
+    const int c0 = max(abs(co[zig]) + sq.sharpen[zig], 0);
+    const int iquant = n == 0 ? sq.dc_iquant : sq.iquant;
+    const int L0 = min((c0 * iquant) >> 17, 2047);
+    const int mag = ctx == 0 ? 0 : L0 + (idx & 1);
+    const int lv = act ? (co[zig] < 0 ? -mag : mag) : 0;
+    q[zig] = (int16_t)lv;
+    last = (lv != 0 && last == 0) ? n + 1 : last;
+    ctx = act ? (ctx == 0 ? idx : idx >> 1) : ctx;
   }
   return last;
 }
@@ -440,7 +414,7 @@ constexpr uint64_t SPIN_TICKS = 200000000ull;
 #ifdef WG_STAMPS
 // Diagnostic build only: cycles per phase summed over macroblocks.
 __device__ unsigned long long g_enc_phase[16];
-#define ESTAMP_DECL unsigned long long st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0, sub_prev = 0
+#define ESTAMP_DECL unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0, sub_prev = 0, cst_prev = 0
 #define ESTAMP(k)                                                                  \
   do {                                                                             \
     __builtin_amdgcn_sched_barrier(0);                                             \
@@ -453,7 +427,7 @@ __device__ unsigned long long g_enc_phase[16];
 #define ESTAMP_FLUSH()                                                              \
   do {                                                                              \
     if (lane == 0)                                                                  \
-      for (int k_ = 0; k_ < 12; k_++) atomicAdd(&g_enc_phase[k_], st_acc[k_]);      \
+      for (int k_ = 0; k_ < 16; k_++) atomicAdd(&g_enc_phase[k_], st_acc[k_]);      \
   } while (0)
 // sub-phase stamps (inside a phase): accumulate into st_acc[8 + k], k >= 0
 #define SSTAMP(k)                                                                  \
@@ -465,7 +439,18 @@ __device__ unsigned long long g_enc_phase[16];
     if ((k) >= 0) st_acc[8 + (k)] += ts_ - sub_prev;                              \
     sub_prev = ts_;                                                                \
   } while (0)
+// candidate-internal stamps: accumulate into st_acc[12 + k], k >= 0
+#define CSTAMP(k)                                                                  \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long ts_;                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");   \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    if ((k) >= 0) st_acc[12 + (k)] += ts_ - cst_prev;                             \
+    cst_prev = ts_;                                                                \
+  } while (0)
 #else
+#define CSTAMP(k) (void)0
 #define SSTAMP(k) (void)0
 #define ESTAMP_DECL int st_unused_ = 0
 #define ESTAMP(k) (void)st_unused_
@@ -478,12 +463,26 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
   for (int i = lane; i < 1056; i += 64) s.proba[i] = a.proba[i];
   for (int i = lane; i < 256; i += 64) s.ecost[i] = vp8_entropy_cost[i];
   for (int i = lane; i < 2048; i += 64) s.lfixed[i] = vp8_level_fixed_costs[i];
+  for (int i = lane; i < 1000; i += 64) s.fixed_i4[i] = c_fixed_i4[i];
   for (int i = lane; i < (int)(4 * sizeof(Segment) / 4); i += 64)
     reinterpret_cast<int*>(s.seg)[i] = reinterpret_cast<const int*>(a.segs)[i];
   __syncthreads();
-  for (int i = lane; i < 4 * 8 * 3 * 68; i += 64) {
-    const int tbc = i / 68, level = i % 68;
-    s.vcost[tbc][level] = level == 0 ? 0 : (uint16_t)variable_level_cost(s, level, s.proba + tbc * 11);
+  for (int i = lane; i < 4 * 8 * 68; i += 64) {
+    const int tb = i / 68, level = i % 68;
+    uint64_t w = 0;
+    for (int c = 0; c < 3; c++)
+      if (level > 0) w |= (uint64_t)variable_level_cost(s, level, s.proba + (tb * 3 + c) * 11) << (16 * c);
+    s.vcost[tb][level] = w;
+  }
+  if (lane < 4 * 8) {
+    TokRow r = {};
+    for (int c = 0; c < 3; c++) {
+      const uint8_t* p = s.proba + (lane * 3 + c) * 11;
+      r.zero[c] = (uint16_t)(ecost(s, 255 - p[0]) + ecost(s, p[1]));
+      r.nz[c] = (uint16_t)(ecost(s, 255 - p[0]) + ecost(s, 255 - p[1]));
+      r.eob[c] = (uint16_t)ecost(s, p[0]);
+    }
+    s.tok[lane] = r;
   }
   const int mbw = a.mbw, mbh = a.mbh;
   const int ys = 16 * mbw, uvs = 8 * mbw;
@@ -691,31 +690,45 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
 
       ESTAMP(3);
       // ================= I4 RD (tryI4ModesRDParallel :739-846) =================
+      // The 16 blocks run as a wavefront, step st = bx + 2 by: a block's left,
+      // top and top-right neighbours (the LD/VL context) all finish in earlier
+      // steps, so the (up to) two blocks of a step run at once, one per
+      // half-wave.  The reference's raster-order early exit (:820-833) is
+      // applied afterwards from the per-block results: a block reads only
+      // reconstructions of raster-earlier blocks, so every block evaluated
+      // before the exit point sees exactly the reference's inputs.
       for (int i = lane; i < YUV / 4; i += 64)
         reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
       lds_sync();
       uint64_t s4;
       {
-        int total_rate = 0, total_disto = 0, total_header = 0;
+        const int half = lane >> 5, hl = lane & 31;
+        // running totals over the finished blocks: rate, distortion and header
+        // bits only grow, so once the finished blocks alone reach the exit
+        // condition the reference exits too (at some block) and I4 loses
+        int run_rate = 0, run_disto = 0, run_header = 0;
         bool early = false;
-        for (int blk = 0; blk < 16 && !early; blk++) {
-          const int bx4 = blk & 3, by4 = blk >> 2;
-          const int top_mode = by4 == 0 ? (int)((top_modes >> (8 * bx4)) & 0xff) : s.modes4[blk - 4];
-          const int left_mode = bx4 == 0 ? (int)((left_modes >> (8 * by4)) & 0xff) : s.modes4[blk - 1];
+        for (int st = 0; st < 10 && !early; st++) {
+          const int wy = (st <= 3 ? 0 : (st - 2) >> 1) + half, wx = st - 2 * wy;
+          const bool bvalid = wy <= 3 && wx >= 0 && wx <= 3;
+          const int by4 = bvalid ? wy : 0, bx4 = bvalid ? wx : 0;  // an idle half works on block 0 (discarded)
+          const int blk = by4 * 4 + bx4;
+          const int top_mode = by4 == 0 ? (int)((top_modes >> (8 * bx4)) & 0xff) : s.modes4[max(blk - 4, 0)];
+          const int left_mode = bx4 == 0 ? (int)((left_modes >> (8 * by4)) & 0xff) : s.modes4[max(blk - 1, 0)];
           const int off = YOFF + 4 * by4 * BPS + 4 * bx4;
           const bool has_top = mby > 0 || by4 > 0, has_left = mbx > 0 || bx4 > 0;
-          const int l = bx4 > 0 ? (s.nzy[blk - 1] > 0) : (int)((left_nz >> by4) & 1);
-          const int t = by4 > 0 ? (s.nzy[blk - 4] > 0) : (int)((top_nz >> bx4) & 1);
+          const int l = bx4 > 0 ? (s.nzy[max(blk - 1, 0)] > 0) : (int)((left_nz >> by4) & 1);
+          const int t = by4 > 0 ? (s.nzy[max(blk - 4, 0)] > 0) : (int)((top_nz >> bx4) & 1);
           const int nz_ctx = min(l + t, 2);
           int src[16];
-          load4x4(s.yin + off, src);
+          if (bvalid) load4x4(s.yin + off, src);
           SSTAMP(-1);
-          // pre-screen all eligible modes by prediction SSE
-          if (lane < 10) {
-            const bool ok = !(!has_top && needs_top4(lane)) && !(!has_left && needs_left4(lane));
+          // pre-screen all eligible modes by prediction SSE (lanes 0-9 of the half)
+          if (bvalid && hl < 10) {
+            const bool ok = !(!has_top && needs_top4(hl)) && !(!has_left && needs_left4(hl));
             int pred[16];
-            pred4_block(lane, s.yout2, off, pred);
-            s.sse10[lane] = ok ? sse16(src, pred) : -1;
+            pred4_block(hl, s.yout2, off, pred);
+            s.sse10[half][hl] = ok ? sse16(src, pred) : -1;
           }
           lds_sync();
           SSTAMP(0);
@@ -731,7 +744,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
           int nc = 0;
 #pragma unroll
           for (int mm = 0; mm < 10; mm++) {
-            const int v = s.sse10[mm];
+            const int v = s.sse10[half][mm];
             if (v >= 0) {
 #pragma unroll
               for (int p = 0; p < 10; p++)
@@ -769,66 +782,78 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
             }
           }
           SSTAMP(1);
-          // candidates in parallel (lane i = candidate i)
+          // candidates in parallel (lane hl = candidate hl of this half's block)
           uint64_t score = ~0ull;
-          int rate = 0, disto = 0, nz = 0, mode = cm[0];
+          int rate = 0, disto = 0, nz = 0, mode = 0;
           int16_t q[16];
-          int dq[16];
-          int pred[16];
-          if (lane < K) {
-            mode = lane == 0 ? cm[0] : (lane == 1 ? cm[1] : cm[2]);
+          uint32_t recp[4] = {0, 0, 0, 0};
+          if (bvalid && hl < K) {
+            CSTAMP(-1);
+            mode = hl == 0 ? cm[0] : (hl == 1 ? cm[1] : cm[2]);
+            int pred[16];
             pred4_block(mode, s.yout2, off, pred);
             int co[16];
             fdct(src, pred, co);
-            nz = trellis(s, co, q, sg.y1, 0, 3, nz_ctx, sg.tlambda_i4);
+            CSTAMP(0);
+            nz = trellis<0, 3>(s, co, q, sg.y1, nz_ctx, sg.tlambda_i4);
+            CSTAMP(1);
+            int dq[16], rec[16];
             dequant(q, dq, sg.y1);
-            int rec[16];
             recon4(pred, dq, rec);
+#pragma unroll
+            for (int r = 0; r < 4; r++) recp[r] = pack4(rec[4 * r], rec[4 * r + 1], rec[4 * r + 2], rec[4 * r + 3]);
             disto = sse16(src, rec);
             if (sg.tlambda_sd > 0) disto += (sg.tlambda_sd * tdisto(src, rec) + 128) >> 8;
-            bool flat = true;
+            CSTAMP(2);
             int cnt = 0;
 #pragma unroll
             for (int i = 1; i < 16; i++) cnt += q[i] != 0;
-            flat = cnt <= 3;
-            rate = (mode > 0 && flat) ? 140 : 0;
+            rate = (mode > 0 && cnt <= 3) ? 140 : 0;
             rate += token_cost(s, q, nz, 3, nz_ctx, 0);
-            rate += c_fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
+            rate += s.fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
             score = rd_score(disto, rate, sg.lambda_i4);
+            CSTAMP(3);
           }
           SSTAMP(2);
-          // first minimum over candidates (strict '<' in candidate order)
+          // first minimum over this half's candidates (strict '<' in candidate order)
           int win = 0;
-          uint64_t wsc = __shfl(score, 0, 64);
-          for (int i = 1; i < K; i++) {
-            const uint64_t sc = __shfl(score, i, 64);
-            if (sc < wsc) {
+          uint64_t wsc = __shfl(score, half * 32, 64);
+#pragma unroll
+          for (int i = 1; i < 3; i++) {
+            const uint64_t sc = __shfl(score, half * 32 + i, 64);
+            if (i < K && sc < wsc) {
               wsc = sc;
               win = i;
             }
           }
-          const int wmode = __shfl(mode, win, 64), wrate = __shfl(rate, win, 64), wdisto = __shfl(disto, win, 64);
-          const int wnz = __shfl(nz, win, 64);
-          if (lane == win) {
+          if (bvalid && hl == win) {
 #pragma unroll
             for (int i = 0; i < 16; i++) s.coeffs[blk * 16 + i] = q[i];
-            s.modes4[blk] = (uint8_t)wmode;
-            s.nzy[blk] = (uint8_t)wnz;
-          }
-          total_rate += wrate;
-          total_disto += wdisto;
-          total_header += c_fixed_i4[(top_mode * 10 + left_mode) * 10 + wmode];
-          if (rd_score(total_disto, total_rate + 211, sg.lambda_mode) >= s16 || total_header > 15000) {
-            early = true;
-          } else if (lane == win) {  // reconstruct the chosen block into yout2
-            int rec[16];
-            recon4(pred, dq, rec);
-            store4x4(s.yout2 + off, rec);
+#pragma unroll
+            for (int r = 0; r < 4; r++) *reinterpret_cast<uint32_t*>(s.yout2 + off + r * BPS) = recp[r];
+            s.modes4[blk] = (uint8_t)mode;
+            s.nzy[blk] = (uint8_t)nz;
+            s.blk_rate[blk] = rate;
+            s.blk_disto[blk] = disto;
+            s.blk_hdr[blk] = s.fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
           }
           lds_sync();
+          {
+            const int b0 = st <= 3 ? st : 4 * ((st - 2) >> 1) + (st & 1) + 2;  // half 0's block
+            run_rate += s.blk_rate[b0];
+            run_disto += s.blk_disto[b0];
+            run_header += s.blk_hdr[b0];
+            if (st >= 2 && st <= 7) {  // half 1's block: (st & 1, by of half 0 + 1)
+              const int b1 = b0 + 4 - 2;
+              run_rate += s.blk_rate[b1];
+              run_disto += s.blk_disto[b1];
+              run_header += s.blk_hdr[b1];
+            }
+            early = rd_score(run_disto, run_rate + 211, sg.lambda_mode) >= s16 || run_header > 15000;
+          }
           SSTAMP(3);
         }
-        s4 = early ? ~0ull : rd_score(total_disto, total_rate + 211, sg.lambda_mode);
+        s4 = early ? ~0ull : rd_score(run_disto, run_rate + 211, sg.lambda_mode);
       }
       const bool is_i4 = s4 < s16;
 
@@ -923,7 +948,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
           if (lane < 16 && bx + by == d) {
             const int l = bx > 0 ? (s.nzy[lane - 1] > 0) : (int)((left_nz >> by) & 1);
             const int t = by > 0 ? (s.nzy[lane - 4] > 0) : (int)((top_nz >> bx) & 1);
-            const int nz = trellis(s, co, q, sg.y1, 1, 0, min(l + t, 2), sg.tlambda_i16);
+            const int nz = trellis<1, 0>(s, co, q, sg.y1, min(l + t, 2), sg.tlambda_i16);
             s.nzy[lane] = (uint8_t)nz;
 #pragma unroll
             for (int i = 0; i < 16; i++) s.coeffs[lane * 16 + i] = q[i];
