@@ -67,6 +67,30 @@ static_assert(sizeof(MbEnc) == 864, "MbEnc layout");
 constexpr int kZig[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
 constexpr int kBand[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
 
+constexpr uint64_t pack_zig() {
+  uint64_t v = 0;
+  for (int n = 0; n < 16; n++) v |= (uint64_t)kZig[n] << (4 * n);
+  return v;
+}
+constexpr uint64_t pack_band() {
+  uint64_t v = 0;
+  for (int n = 0; n < 17; n++) v |= (uint64_t)kBand[n] << (3 * n);
+  return v;
+}
+// lane-varying scan lookups (a position per lane) without a memory access
+__device__ __forceinline__ int zig_of(int n) { return (int)((pack_zig() >> (4 * n)) & 15); }
+__device__ __forceinline__ int band_of(int n) { return (int)((pack_band() >> (3 * n)) & 7); }
+
+// One trellis position, prepared by a lane of its own (trellis_prep) and
+// consumed by the lane running the serial DP (trellis_dp).
+struct alignas(16) TRec {
+  int64_t na[3];  // from predecessor pc to level L0: (nz token + level cost) * lam16 + distortion + order idx 2pc
+  int64_t nb[3];  // ... to level L0 + 1 (order idx 2pc + 1); + BIG when that level is not a candidate
+  int32_t l0s;    // L0 << 3 | negative << 2 | min(L0, 2)
+  int32_t pad[3];
+};
+static_assert(sizeof(TRec) == 64, "TRec layout");
+
 __constant__ uint16_t c_level_codes[134];
 __constant__ uint16_t c_fixed_i4[1000];
 __constant__ uint8_t c_zigzag[16], c_bands[17], c_rzig[16];
@@ -99,8 +123,12 @@ struct Shared {
   int dcq[4][16];  // per mode: quantised WHT levels (I16 RD), then block DCs after the inverse WHT
   int dcout[4][16];
   int mode_rate[4], mode_disto[4];
-  int sse10[2][10];
   int blk_rate[16], blk_disto[16], blk_hdr[16];
+  int wtr[16];             // trellis distortion weights (kWeightTrellis)
+  int co_buf[16][16];      // transform coefficients handed to the trellis prep lanes
+  TRec trec[6][16];        // trellis position records: I4 (half, candidate) / final I16 (diagonal slot)
+  int16_t cand_q[6][16];   // I4 candidates' levels for the lane-parallel token cost
+  int cand_nz[6], cand_rate[6];
   uint16_t fixed_i4[1000];
   int word;
 };
@@ -167,7 +195,7 @@ __device__ __forceinline__ int token_cost(const Shared& s, const int16_t q[16], 
   return cost;
 }
 
-// TrellisQuantizeBlock (encode_trellis.go:23-301), branch-free.
+// TrellisQuantizeBlock (encode_trellis.go:23-301), split across lanes.
 //
 // Scores are kept x16 so the low 4 bits of a 64-bit key can carry the
 // candidate's position in the reference's update order; "first strict
@@ -177,80 +205,86 @@ __device__ __forceinline__ int token_cost(const Shared& s, const int16_t q[16], 
 // min(level, 2).  Invalid states carry scores >= 2^58 (valid ones stay below
 // 2^51), so they never win against a valid candidate.  The path keeps the
 // winning idx per end context (4 bits each, 16 bits per position); levels
-// are re-derived from `co` when walking back.
-template <int FIRST, int CTX_TYPE>
-__device__ __forceinline__ int trellis(const Shared& s, const int co[16], int16_t q[16], const SQuant& sq, int init_ctx,
-                                       int lambda) {
-  constexpr int64_t BIG = 1ll << 59, VALID = 1ll << 58;
-  {  // pre-scan: all levels zero under the neutral bias?
-    bool nonzero = false;
+// are re-derived from the position records when walking back.
+//
+// ---- TrellisQuantizeBlock split across lanes ----------------------------
+// Everything a trellis position needs that does not depend on the DP state
+// (level candidates, distortion deltas, token + level costs per predecessor
+// context) is computed by one lane per position into a TRec; the lane that
+// runs the serial DP then does only the 3 x 3 transitions per position.
+// Returns whether the position has a non-zero level under the neutral bias
+// (the reference's all-zero pre-scan).
+template <int CTX_TYPE>
+__device__ __forceinline__ bool trellis_prep(const Shared& s, int co_z, int n, const SQuant& sq, int lam16, TRec& out) {
+  constexpr int64_t BIG = 1ll << 59;
+  const int zig = zig_of(n), band = band_of(n + 1);
+  const int c0 = max(abs(co_z) + sq.sharpen[zig], 0);
+  const int quant = n == 0 ? sq.dc_quant : sq.quant;
+  const int iquant = n == 0 ? sq.dc_iquant : sq.iquant;
+  const int L0raw = (c0 * iquant) >> 17;
+  const int L0 = min(L0raw, 2047);
+  const int thresh = min((int)(((uint32_t)c0 * (uint32_t)iquant + 65536u) >> 17), 2047);
+  const bool has0 = L0 > 0 && L0 <= thresh;
+  const bool has1 = L0 + 1 <= 2047 && L0 + 1 <= thresh;
+  const int w4096 = s.wtr[zig] * 4096;
+  const int e0 = c0 - L0 * quant, e1 = c0 - (L0 + 1) * quant;
+  const int64_t A0 = (int64_t)s.lfixed[L0] * lam16 + (int64_t)w4096 * (e0 * e0 - c0 * c0) + (has0 ? 0 : BIG);
+  const int64_t A1 = (int64_t)s.lfixed[min(L0 + 1, 2047)] * lam16 + (int64_t)w4096 * (e1 * e1 - c0 * c0) + (has1 ? 0 : BIG);
+  const TokRow& t = s.tok[CTX_TYPE * 8 + band];
+  const uint64_t v0 = s.vcost[CTX_TYPE * 8 + band][min(L0, 67)], v1 = s.vcost[CTX_TYPE * 8 + band][min(L0 + 1, 67)];
 #pragma unroll
-    for (int n = FIRST; n < 16; n++) {
-      const int zig = kZig[n];
-      const int c0 = max(abs(co[zig]) + sq.sharpen[zig], 0);
-      const int iq = n == 0 ? sq.dc_iquant : sq.iquant;
-      nonzero |= ((c0 * iq) >> 17) > 0;
-    }
-    if (!nonzero) {
-#pragma unroll
-      for (int i = 0; i < 16; i++) q[i] = 0;
-      return 0;
-    }
+  for (int pc = 0; pc < 3; pc++) {
+    out.na[pc] = (int64_t)(t.nz[pc] + vc_of(v0, pc)) * lam16 + A0 + 2 * pc;
+    out.nb[pc] = (int64_t)(t.nz[pc] + vc_of(v1, pc)) * lam16 + A1 + 2 * pc + 1;
   }
+  out.l0s = L0 << 3 | (co_z < 0 ? 4 : 0) | min(L0, 2);
+  return L0raw > 0;
+}
+
+// The serial DP + walk back over prepared positions (key encoding above).  Returns the zigzag nz count; q in raster order.
+template <int FIRST, int CTX_TYPE>
+__device__ __forceinline__ int trellis_dp(const Shared& s, const TRec* rec, int init_ctx, int lam16, int16_t q[16]) {
+  constexpr int64_t BIG = 1ll << 59, VALID = 1ll << 58;
   init_ctx = min(init_ctx, 2);
   int64_t ps0 = init_ctx == 0 ? 0 : BIG, ps1 = init_ctx == 1 ? 0 : BIG, ps2 = init_ctx == 2 ? 0 : BIG;
   uint32_t path[8];
-  const int lam16 = lambda * 16;
   const TokRow& t_init = s.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
   int64_t best_terminal = (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16;
   int best = -1;  // n << 2 | end context
+  TRec r = rec[FIRST];
 #pragma unroll
   for (int n = 0; n < 16; n++) {
     if (n < FIRST) {
       if (!(n & 1)) path[n >> 1] = 0;
       continue;
     }
-    const int zig = kZig[n];
-    const int band = kBand[n + 1];
-    const int c0 = max(abs(co[zig]) + sq.sharpen[zig], 0);
-    const int quant = n == 0 ? sq.dc_quant : sq.quant;
-    const int iquant = n == 0 ? sq.dc_iquant : sq.iquant;
-    const int L0 = min((c0 * iquant) >> 17, 2047);
-    const int thresh = min((int)(((uint32_t)c0 * (uint32_t)iquant + 65536u) >> 17), 2047);
-    const int w4096 = c_wtrellis[zig] * 4096;
-    const bool has0 = L0 > 0 && L0 <= thresh;
-    const bool has1 = L0 + 1 <= 2047 && L0 + 1 <= thresh;
-    const int e0 = c0 - L0 * quant, e1 = c0 - (L0 + 1) * quant;
-    // per-level parts (fixed level cost, distortion delta 256 * w * (err^2 -
-    // c0^2), both squares < 2^27), x16, + BIG when not a candidate
-    const int64_t A0 = (int64_t)s.lfixed[L0] * lam16 + (int64_t)w4096 * (e0 * e0 - c0 * c0) + (has0 ? 0 : BIG);
-    const int64_t A1 = (int64_t)s.lfixed[min(L0 + 1, 2047)] * lam16 + (int64_t)w4096 * (e1 * e1 - c0 * c0) + (has1 ? 0 : BIG);
-    const TokRow& t = s.tok[CTX_TYPE * 8 + band];
-    const uint64_t v0 = s.vcost[CTX_TYPE * 8 + band][min(L0, 67)], v1 = s.vcost[CTX_TYPE * 8 + band][min(L0 + 1, 67)];
+    const TRec cur = r;
+    if (n < 15) r = rec[n + 1];  // one position ahead
+    asm volatile("" ::: "memory");  // keep the loads of later positions below this point
+    const TokRow& t = s.tok[CTX_TYPE * 8 + kBand[n + 1]];
     int64_t kz = BIG * 2, ka = BIG * 2, kb = BIG * 2;
 #pragma unroll
     for (int pc = 0; pc < 3; pc++) {
       const int64_t base = pc == 0 ? ps0 : (pc == 1 ? ps1 : ps2);
-      const int64_t z = base + pc + (int64_t)t.zero[pc] * lam16;
-      const int64_t ca = base + 2 * pc + A0 + (int64_t)(t.nz[pc] + vc_of(v0, pc)) * lam16;
-      const int64_t cb = base + 2 * pc + 1 + A1 + (int64_t)(t.nz[pc] + vc_of(v1, pc)) * lam16;
+      const int64_t z = (base | pc) + (int64_t)t.zero[pc] * lam16;
+      const int64_t ca = base + cur.na[pc];
+      const int64_t cb = base + cur.nb[pc];
       kz = z < kz ? z : kz;
       ka = ca < ka ? ca : ka;
       kb = cb < kb ? cb : kb;
     }
-    // route L0 / L0 + 1 to their end contexts min(level, 2)
+    const int cls = cur.l0s & 3;
     const int64_t kab = kb < ka ? kb : ka;
-    const int64_t k1 = L0 == 0 ? kb : (L0 == 1 ? ka : BIG);
-    const int64_t k2 = L0 == 0 ? BIG : (L0 == 1 ? kb : kab);
-    const uint32_t rec = ((uint32_t)kz & 15) | (((uint32_t)k1 & 15) << 4) | (((uint32_t)k2 & 15) << 8);
+    const int64_t k1 = cls == 0 ? kb : (cls == 1 ? ka : BIG);
+    const int64_t k2 = cls == 0 ? BIG : (cls == 1 ? kb : kab);
+    const uint32_t pr = ((uint32_t)kz & 15) | (((uint32_t)k1 & 15) << 4) | (((uint32_t)k2 & 15) << 8);
     if (n & 1)
-      path[n >> 1] |= rec << 16;
+      path[n >> 1] |= pr << 16;
     else
-      path[n >> 1] = rec;
+      path[n >> 1] = pr;
     ps0 = kz & ~15ll;
     ps1 = k1 & ~15ll;
     ps2 = k2 & ~15ll;
-    // terminal (EOB after this position) from end contexts 1 and 2
     const int64_t eob1 = ps1 + (n < 15 ? (int64_t)t.eob[1] * lam16 : 0);
     const bool w1 = ps1 < VALID && eob1 < best_terminal;
     best_terminal = w1 ? eob1 : best_terminal;
@@ -260,12 +294,7 @@ __device__ __forceinline__ int trellis(const Shared& s, const int co[16], int16_
     best_terminal = w2 ? eob2 : best_terminal;
     best = w2 ? (n << 2 | 2) : best;
   }
-  if (best < 0) {
-#pragma unroll
-    for (int i = 0; i < 16; i++) q[i] = 0;
-    return 0;
-  }
-  const int best_n = best >> 2;
+  const int best_n = best >> 2;  // -1 when no terminal beat the all-zero block
   int ctx = best & 3, last = 0;
 #pragma unroll
   for (int n = 15; n >= 0; n--) {
@@ -276,16 +305,61 @@ __device__ __forceinline__ int trellis(const Shared& s, const int co[16], int16_
     }
     const bool act = n <= best_n;
     const int idx = (int)(((path[n >> 1] >> (16 * (n & 1))) >> (4 * ctx)) & 15);
-    const int c0 = max(abs(co[zig]) + sq.sharpen[zig], 0);
-    const int iquant = n == 0 ? sq.dc_iquant : sq.iquant;
-    const int L0 = min((c0 * iquant) >> 17, 2047);
-    const int mag = ctx == 0 ? 0 : L0 + (idx & 1);
-    const int lv = act ? (co[zig] < 0 ? -mag : mag) : 0;
+    const int l0s = rec[n].l0s;
+    const int mag = ctx == 0 ? 0 : (l0s >> 3) + (idx & 1);
+    const int lv = act ? ((l0s & 4) ? -mag : mag) : 0;
     q[zig] = (int16_t)lv;
     last = (lv != 0 && last == 0) ? n + 1 : last;
     ctx = act ? (ctx == 0 ? idx : idx >> 1) : ctx;
   }
-  return last;
+  return best < 0 ? 0 : last;
+}
+
+// TokenCostForCoeffs's term for position n alone (lane-parallel form of
+// token_cost(); the caller sums over n).  q: raster levels in LDS.
+template <int TYPE>
+__device__ __forceinline__ int token_cost_pos(const Shared& s, const int16_t* q, int n, int nz_count, int ctx0, int first) {
+  if (n < first) return 0;
+  const int band = band_of(n);
+  const TokRow& t = s.tok[TYPE * 8 + band];
+  const int v = abs((int)q[zig_of(n)]);
+  const int ctx = n == first ? ctx0 : min(abs((int)q[zig_of(max(n - 1, 0))]), 2);
+  const uint64_t vw = s.vcost[TYPE * 8 + band][min(v, 67)];
+  const int tokc = v == 0 ? pick3(ctx, t.zero[0], t.zero[1], t.zero[2])
+                          : pick3(ctx, t.nz[0], t.nz[1], t.nz[2]) + s.lfixed[min(v, 2047)] + vc_of(vw, ctx);
+  return n < nz_count ? tokc : (n == max(nz_count, first) ? pick3(ctx, t.eob[0], t.eob[1], t.eob[2]) : 0);
+}
+
+// min over the 16 lanes of a DPP row, result in every lane of the row
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false));  // row_mirror
+  return v;
+}
+
+// The reference's candidate pick for one I4 block (tryI4ModesRDParallel
+// :869-886): compact the eligible modes, then K rounds of first-argmin +
+// swap.  Lane m (< 10) of a 16-lane row holds mode m's key
+// sse << 8 | compacted position << 4 | m (sse <= 16 * 255^2 < 2^21), so the
+// first minimum is a row min; the swap moves the element at position i to
+// the winner's position.  Returns candidate i's mode in cm[i], uniform over
+// the row.  `eligible`: bit m set when mode m is allowed for this block.
+__device__ __forceinline__ void select_i4_modes(int sse, int m, uint32_t eligible, int K, int cm[3]) {
+  const bool ok = m < 10 && ((eligible >> m) & 1);
+  uint32_t key = ok ? ((uint32_t)sse << 8 | (uint32_t)__builtin_popcount(eligible & ((1u << m) - 1)) << 4 | (uint32_t)m) : ~0u;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const uint32_t kmin = row_min_u32(key);
+    cm[i] = (int)(kmin & 15);
+    if (i + 1 < 3) {
+      const uint32_t wpos = (kmin >> 4) & 15;
+      const bool at_i = ((key >> 4) & 15) == (uint32_t)i;
+      key = key == kmin ? ~0u : (at_i && key != ~0u ? ((key & ~0xf0u) | wpos << 4) : key);
+    }
+  }
+  (void)K;
 }
 
 // residual + reconstruction of one 4x4 block: rec = clip(pred + IDCT(dq))
@@ -371,8 +445,6 @@ __device__ __forceinline__ int check_mode(int mbx, int mby, int mode) {
   const int edge = (mbx == 0) ? ((mby == 0) ? 6 : 5) : ((mby == 0) ? 4 : 0);
   return mode == 0 ? edge : mode;
 }
-__device__ __forceinline__ bool needs_top4(int m) { return m == 1 || m == 2 || m == 4 || m == 5 || m == 6 || m == 7 || m == 8; }
-__device__ __forceinline__ bool needs_left4(int m) { return m == 1 || m == 3 || m == 4 || m == 8 || m == 9; }
 __device__ __forceinline__ uint64_t rd_score(int disto, int rate, int lambda) {
   return (uint64_t)(int64_t)rate * (uint64_t)(int64_t)lambda + 256ull * (uint64_t)(int64_t)disto;
 }
@@ -382,6 +454,18 @@ __device__ __forceinline__ T group_sum(T v, int width) {  // sum over aligned gr
   return v;
 }
 __device__ __forceinline__ void lds_sync() { __syncthreads(); }
+
+// An opaque copy of the LDS base (still typed as LDS, so accesses stay
+// ds_read/ds_write).  Re-taken at the top of a loop body it stops the
+// compiler from hoisting loop-invariant table reads (token-cost rows,
+// segment fields) out of the loop and pinning them in registers for the
+// whole loop -- which is what drove this kernel past 256 VGPRs.
+typedef __attribute__((address_space(3))) Shared LdsShared;
+__device__ __forceinline__ Shared& launder(Shared& s) {
+  LdsShared* p = (LdsShared*)&s;
+  asm volatile("" : "+s"(p));
+  return *(Shared*)p;
+}
 
 // sc1 hand-off helpers (see decode.hip)
 __device__ __forceinline__ uint32_t ld_sc1_32(const uint8_t* p) {
@@ -458,12 +542,14 @@ __device__ unsigned long long g_enc_phase[16];
 #endif
 
 __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
-  __shared__ Shared s;
+  __shared__ Shared s_lds;
+  Shared& s = s_lds;
   const int lane = threadIdx.x;
   for (int i = lane; i < 1056; i += 64) s.proba[i] = a.proba[i];
   for (int i = lane; i < 256; i += 64) s.ecost[i] = vp8_entropy_cost[i];
   for (int i = lane; i < 2048; i += 64) s.lfixed[i] = vp8_level_fixed_costs[i];
   for (int i = lane; i < 1000; i += 64) s.fixed_i4[i] = c_fixed_i4[i];
+  if (lane < 16) s.wtr[lane] = c_wtrellis[lane];
   for (int i = lane; i < (int)(4 * sizeof(Segment) / 4); i += 64)
     reinterpret_cast<int*>(s.seg)[i] = reinterpret_cast<const int*>(a.segs)[i];
   __syncthreads();
@@ -518,6 +604,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
     int seen = 0;
 
     for (int mbx = 0; mbx < mbw; mbx++) {
+      Shared& s = launder(s_lds);
       const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
       ESTAMP(0);
       // ---- wait for the row above (MB x+1 done) ----
@@ -709,6 +796,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
         int run_rate = 0, run_disto = 0, run_header = 0;
         bool early = false;
         for (int st = 0; st < 10 && !early; st++) {
+          Shared& s = launder(s_lds);
           const int wy = (st <= 3 ? 0 : (st - 2) >> 1) + half, wx = st - 2 * wy;
           const bool bvalid = wy <= 3 && wx >= 0 && wx <= 3;
           const int by4 = bvalid ? wy : 0, bx4 = bvalid ? wx : 0;  // an idle half works on block 0 (discarded)
@@ -721,95 +809,97 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
           const int t = by4 > 0 ? (s.nzy[max(blk - 4, 0)] > 0) : (int)((top_nz >> bx4) & 1);
           const int nz_ctx = min(l + t, 2);
           int src[16];
-          if (bvalid) load4x4(s.yin + off, src);
+          load4x4(s.yin + off, src);
           SSTAMP(-1);
-          // pre-screen all eligible modes by prediction SSE (lanes 0-9 of the half)
+          // pre-screen all eligible modes by prediction SSE (lanes 0-9 of each half)
+          int sse_lane = 0;
           if (bvalid && hl < 10) {
-            const bool ok = !(!has_top && needs_top4(hl)) && !(!has_left && needs_left4(hl));
             int pred[16];
             pred4_block(hl, s.yout2, off, pred);
-            s.sse10[half][hl] = ok ? sse16(src, pred) : -1;
+            sse_lane = sse16(src, pred);
+          }
+          SSTAMP(0);
+          // eligible modes (no top / no left context rules out some), candidates
+          uint32_t eligible = 0x3ff;
+          if (!has_top) eligible &= ~0x1f6u;  // TM VE RD VR LD VL HD need the top row
+          if (!has_left) eligible &= ~0x31au;  // TM HE RD HD HU need the left column
+          const int K = bvalid ? min(max_modes, __builtin_popcount(eligible)) : 0;
+          int cm[3];
+          select_i4_modes(sse_lane, hl, eligible, K, cm);
+          const bool cand = bvalid && hl < K;
+          const int mode = pick3(hl, cm[0], cm[1], cm[2]);
+          const int slot = half * 3 + min(hl, 2);  // candidate slot in the trellis / level buffers
+          SSTAMP(1);
+          // candidates: prediction + transform (lane hl = candidate hl)
+          uint32_t predp[4] = {0, 0, 0, 0};
+          if (cand) {
+            CSTAMP(-1);
+            int pred[16], co[16];
+            pred4_block(mode, s.yout2, off, pred);
+#pragma unroll
+            for (int r = 0; r < 4; r++) predp[r] = pack4(pred[4 * r], pred[4 * r + 1], pred[4 * r + 2], pred[4 * r + 3]);
+            fdct(src, pred, co);
+#pragma unroll
+            for (int i = 0; i < 16; i++) s.co_buf[slot][i] = co[i];
+            CSTAMP(0);
           }
           lds_sync();
-          SSTAMP(0);
-          // partial selection sort of the candidates, in the reference's order
-          // (:869-886): compact the eligible modes, then K rounds of argmin +
-          // swap.  Every index is a compile-time slot (selects, no scratch).
-          int cm[10], cs[10];
+          // trellis positions: lane (candidate c, pair pp) prepares positions 2pp, 2pp + 1
+          const int lam16 = sg.tlambda_i4 * 16;
+          bool pnz = false;
+          if (bvalid && hl < 8 * K) {
+            const int c = hl >> 3, n0 = 2 * (hl & 7), sl = half * 3 + c;
 #pragma unroll
-          for (int p = 0; p < 10; p++) {
-            cm[p] = 0;
-            cs[p] = 0x7fffffff;
+            for (int j = 0; j < 2; j++)
+              pnz |= trellis_prep<3>(s, s.co_buf[sl][zig_of(n0 + j)], n0 + j, sg.y1, lam16, s.trec[sl][n0 + j]);
           }
-          int nc = 0;
-#pragma unroll
-          for (int mm = 0; mm < 10; mm++) {
-            const int v = s.sse10[half][mm];
-            if (v >= 0) {
-#pragma unroll
-              for (int p = 0; p < 10; p++)
-                if (p == nc) {
-                  cm[p] = mm;
-                  cs[p] = v;
-                }
-              nc++;
-            }
-          }
-          const int K = min(max_modes, nc);
-#pragma unroll
-          for (int i = 0; i < 3; i++) {
-            if (i < K) {
-              int mi = i, bsse = cs[i];
-#pragma unroll
-              for (int j = i + 1; j < 10; j++)
-                if (j < nc && cs[j] < bsse) {
-                  bsse = cs[j];
-                  mi = j;
-                }
-              int mmode = cm[i];
-#pragma unroll
-              for (int p = i + 1; p < 10; p++)
-                if (p == mi) mmode = cm[p];
-              const int im = cm[i], is = cs[i];
-#pragma unroll
-              for (int p = i + 1; p < 10; p++)
-                if (p == mi) {
-                  cm[p] = im;
-                  cs[p] = is;
-                }
-              cm[i] = mmode;
-              cs[i] = bsse;
-            }
-          }
-          SSTAMP(1);
-          // candidates in parallel (lane hl = candidate hl of this half's block)
-          uint64_t score = ~0ull;
-          int rate = 0, disto = 0, nz = 0, mode = 0;
+          const uint64_t pnz_mask = __ballot(pnz);
+          lds_sync();
+          // candidates: DP, reconstruction, distortion
           int16_t q[16];
+          int nz = 0, disto = 0, cnt = 0;
           uint32_t recp[4] = {0, 0, 0, 0};
-          if (bvalid && hl < K) {
-            CSTAMP(-1);
-            mode = hl == 0 ? cm[0] : (hl == 1 ? cm[1] : cm[2]);
-            int pred[16];
-            pred4_block(mode, s.yout2, off, pred);
-            int co[16];
-            fdct(src, pred, co);
-            CSTAMP(0);
-            nz = trellis<0, 3>(s, co, q, sg.y1, nz_ctx, sg.tlambda_i4);
+          if (cand) {
+            if ((pnz_mask >> (32 * half + 8 * hl)) & 0xff) {
+              nz = trellis_dp<0, 3>(s, s.trec[slot], nz_ctx, lam16, q);
+            } else {
+#pragma unroll
+              for (int i = 0; i < 16; i++) q[i] = 0;
+            }
             CSTAMP(1);
-            int dq[16], rec[16];
+            int pred[16], dq[16], rec[16];
+#pragma unroll
+            for (int r = 0; r < 4; r++) unpack_rows(predp[r], pred + 4 * r);
             dequant(q, dq, sg.y1);
             recon4(pred, dq, rec);
 #pragma unroll
             for (int r = 0; r < 4; r++) recp[r] = pack4(rec[4 * r], rec[4 * r + 1], rec[4 * r + 2], rec[4 * r + 3]);
             disto = sse16(src, rec);
             if (sg.tlambda_sd > 0) disto += (sg.tlambda_sd * tdisto(src, rec) + 128) >> 8;
-            CSTAMP(2);
-            int cnt = 0;
 #pragma unroll
             for (int i = 1; i < 16; i++) cnt += q[i] != 0;
+#pragma unroll
+            for (int i = 0; i < 16; i++) s.cand_q[slot][i] = q[i];
+            s.cand_nz[slot] = nz;
+            CSTAMP(2);
+          }
+          lds_sync();
+          // token cost, lane-parallel over positions, summed over each candidate's 8 lanes
+          int part = 0;
+          if (bvalid && hl < 8 * K) {
+            const int c = hl >> 3, n0 = 2 * (hl & 7), sl = half * 3 + c;
+            const int nzc = s.cand_nz[sl];
+            part = token_cost_pos<3>(s, s.cand_q[sl], n0, nzc, nz_ctx, 0) + token_cost_pos<3>(s, s.cand_q[sl], n0 + 1, nzc, nz_ctx, 0);
+          }
+          part += __shfl_xor(part, 1, 64);
+          part += __shfl_xor(part, 2, 64);
+          part += __shfl_xor(part, 4, 64);
+          const int tok_rate = __shfl(part, 32 * half + 8 * min(hl, 2), 64);
+          uint64_t score = ~0ull;
+          int rate = 0;
+          if (cand) {
             rate = (mode > 0 && cnt <= 3) ? 140 : 0;
-            rate += token_cost(s, q, nz, 3, nz_ctx, 0);
+            rate += tok_rate;
             rate += s.fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
             score = rd_score(disto, rate, sg.lambda_i4);
             CSTAMP(3);
@@ -933,22 +1023,45 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
       uint32_t nzy_mask = 0, nzuv_mask = 0;
       int nz_dc = 0;
       if (!is_i4) {
-        int src[16], pred[16], co[16];
-        int16_t q[16];
         if (lane < 16) {
           const int off = YOFF + 4 * by * BPS + 4 * bx;
+          int src[16], pred[16], co[16];
           load4x4(s.yin + off, src);
           load4x4(s.yout + off, pred);
           fdct(src, pred, co);
           s.dcin[0][lane] = co[0];
-          co[0] = 0;
+#pragma unroll
+          for (int i = 1; i < 16; i++) s.co_buf[lane][i] = co[i];
         }
-        // trellis along block diagonals: block (bx, by) needs its left / top nz
+        lds_sync();
+        // trellis along block diagonals (each block needs its left / top nz):
+        // lane (diagonal slot j, pair pp) prepares positions 2pp, 2pp + 1 of
+        // block j on the diagonal, then the block's lane runs the DP
+        const int lam16 = sg.tlambda_i16 * 16;
         for (int d = 0; d < 7; d++) {
+          Shared& s = launder(s_lds);
+          const int by_lo = max(0, d - 3), nblk = min(d, 3) - by_lo + 1;
+          bool pnz = false;
+          if (lane < 8 * nblk) {
+            const int j = lane >> 3, n0 = 2 * (lane & 7), pb = (by_lo + j) * 4 + d - (by_lo + j);
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+              if (n0 + k >= 1) pnz |= trellis_prep<0>(s, s.co_buf[pb][zig_of(n0 + k)], n0 + k, sg.y1, lam16, s.trec[j][n0 + k]);
+          }
+          const uint64_t pnz_mask = __ballot(pnz);
+          lds_sync();
           if (lane < 16 && bx + by == d) {
+            const int j = by - by_lo;
             const int l = bx > 0 ? (s.nzy[lane - 1] > 0) : (int)((left_nz >> by) & 1);
             const int t = by > 0 ? (s.nzy[lane - 4] > 0) : (int)((top_nz >> bx) & 1);
-            const int nz = trellis<1, 0>(s, co, q, sg.y1, min(l + t, 2), sg.tlambda_i16);
+            int16_t q[16];
+            int nz = 0;
+            if ((pnz_mask >> (8 * j)) & 0xff) {
+              nz = trellis_dp<1, 0>(s, s.trec[j], min(l + t, 2), lam16, q);
+            } else {
+#pragma unroll
+              for (int i = 0; i < 16; i++) q[i] = 0;
+            }
             s.nzy[lane] = (uint8_t)nz;
 #pragma unroll
             for (int i = 0; i < 16; i++) s.coeffs[lane * 16 + i] = q[i];
