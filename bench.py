@@ -90,7 +90,7 @@ def make_inputs(batch, rank, device):
         rgba[i].copy_(torch.from_numpy(base[(i + rank) % 3]))
     mb, co = synth.random_macroblocks(MBW * MBH * 4, seed=100 + rank, levels=(20, 32))
     per = MBW * MBH
-    mb_t = frames.mb_info_tensor(mb).view(4, per, 32)
+    mb_t = frames.mb_info_tensor(mb, device).view(4, per, 32)
     co_t = torch.from_numpy(co).to(device).view(4, per, 384)
     mb_all = torch.empty((batch, per, 32), dtype=torch.uint8, device=device)
     co_all = torch.empty((batch, per, 384), dtype=torch.int16, device=device)
@@ -190,6 +190,37 @@ def cpu_baseline(seconds, mb_co):
                       "reference Go CPU path, single thread"}
 
 
+def timed_region(step, steps, warmup, world, sync, device):
+    """W untimed steps, then exactly K timed steps bracketed by a barrier and
+    a device sync on both sides; returns the MAX over ranks of the elapsed
+    seconds (all_reduce MAX on the process group: RCCL on the GPU box, gloo
+    in tests/test_multi_rank.py)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        torch.distributed.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(record=True)
+    sync()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def aggregate_mpix_s(world, batch, steps, elapsed):
+    """Whole-job throughput: every rank's pixels over the slowest rank's time
+    (weak scaling: each rank owns `batch` frames)."""
+    return world * batch * W * H * steps / elapsed / 1e6
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -204,28 +235,11 @@ def main():
 
     rgba, mb, co, mb_co = make_inputs(args.batch, rank, device)
     pipe = Pipeline(rgba, mb, co, args.batch, device)
-    for _ in range(args.warmup):
-        pipe.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pipe.step(record=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_region(pipe.step, args.steps, args.warmup, world, torch.cuda.synchronize, device)
     stage = pipe.collect()
 
     if rank == 0:
-        px_total = world * args.batch * W * H * args.steps
-        value = px_total / elapsed / 1e6
+        value = aggregate_mpix_s(world, args.batch, args.steps, elapsed)
         dominant = max(stage, key=stage.get)
         px_rank_step = args.batch * W * H
         kernel = KERNELS[dominant]
