@@ -260,7 +260,11 @@ __device__ __forceinline__ int trellis_dp(const Shared& s, const TRec* rec, int 
     }
     const TRec cur = r;
     if (n < 15) r = rec[n + 1];  // one position ahead
-    asm volatile("" ::: "memory");  // keep the loads of later positions below this point
+    // Tie the previous position's state into the memory chain: later loads
+    // cannot be issued before it is computed, so at most two positions of
+    // records are in flight (otherwise every position's loads are hoisted
+    // to the top and the DP alone needs 250 VGPRs).
+    asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
     const TokRow& t = s.tok[CTX_TYPE * 8 + kBand[n + 1]];
     int64_t kz = BIG * 2, ka = BIG * 2, kb = BIG * 2;
 #pragma unroll
@@ -460,6 +464,14 @@ __device__ __forceinline__ void lds_sync() { __syncthreads(); }
 // compiler from hoisting loop-invariant table reads (token-cost rows,
 // segment fields) out of the loop and pinning them in registers for the
 // whole loop -- which is what drove this kernel past 256 VGPRs.
+// threadIdx.x through an opaque move: lane-derived values (addresses,
+// block coordinates) are then re-derived where used instead of being
+// hoisted out of the row loop and pinned in registers for the whole kernel
+__device__ __forceinline__ int opaque_lane() {
+  int l;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"((int)threadIdx.x));
+  return l;
+}
 typedef __attribute__((address_space(3))) Shared LdsShared;
 __device__ __forceinline__ Shared& launder(Shared& s) {
   LdsShared* p = (LdsShared*)&s;
@@ -605,6 +617,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
 
     for (int mbx = 0; mbx < mbw; mbx++) {
       Shared& s = launder(s_lds);
+      const int lane = opaque_lane();
       const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
       ESTAMP(0);
       // ---- wait for the row above (MB x+1 done) ----
@@ -797,6 +810,8 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
         bool early = false;
         for (int st = 0; st < 10 && !early; st++) {
           Shared& s = launder(s_lds);
+          const int lane = opaque_lane();
+          const int half = lane >> 5, hl = lane & 31;
           const int wy = (st <= 3 ? 0 : (st - 2) >> 1) + half, wx = st - 2 * wy;
           const bool bvalid = wy <= 3 && wx >= 0 && wx <= 3;
           const int by4 = bvalid ? wy : 0, bx4 = bvalid ? wx : 0;  // an idle half works on block 0 (discarded)
