@@ -104,7 +104,8 @@ __constant__ int32_t c_wtrellis[16];
 struct alignas(16) TokRow {
   uint16_t zero[4], nz[4], eob[4], pad[4];
 };
-struct Shared {
+// Tables shared by the workgroup's waves (filled once per launch)
+struct Tables {
   uint8_t proba[4 * 8 * 3 * 11];
   uint16_t ecost[256];
   uint16_t lfixed[2048];
@@ -115,28 +116,31 @@ struct Shared {
   // level sit in one 8-byte word so one ds_read_b64 serves a trellis step
   uint64_t vcost[4 * 8][68];
   Segment seg[4];
+  uint16_t fixed_i4[1000];
+  int wtr[16];  // trellis distortion weights (kWeightTrellis)
+};
+// Per-wave state: each wave of the workgroup encodes its own macroblock row
+struct Shared {
   uint8_t yin[YUV], yout[YUV], yout2[YUV];
   alignas(16) int16_t coeffs[400];
   uint8_t modes4[16];
   uint8_t nzy[16], nzuv[8];
   int dcin[4][16];
-  int dcq[4][16];  // per mode: quantised WHT levels (I16 RD), then block DCs after the inverse WHT
   int dcout[4][16];
   int mode_rate[4], mode_disto[4];
   int blk_rate[16], blk_disto[16], blk_hdr[16];
-  int wtr[16];             // trellis distortion weights (kWeightTrellis)
   int co_buf[16][16];      // transform coefficients handed to the trellis prep lanes
   TRec trec[6][16];        // trellis position records: I4 (half, candidate) / final I16 (diagonal slot)
   int16_t cand_q[6][16];   // I4 candidates' levels for the lane-parallel token cost
   int cand_nz[6], cand_rate[6];
-  uint16_t fixed_i4[1000];
   int word;
 };
+constexpr int WAVES = 4;  // waves (macroblock rows in flight) per workgroup
 
-__device__ __forceinline__ int ecost(const Shared& s, int p) { return s.ecost[p]; }
-__device__ __forceinline__ int bit_cost(const Shared& s, int bit, int p) { return s.ecost[bit ? 255 - p : p]; }
-__device__ __forceinline__ const uint8_t* proba_p(const Shared& s, int type, int band, int ctx) {
-  return s.proba + ((type * 8 + band) * 3 + ctx) * 11;
+__device__ __forceinline__ int ecost(const Tables& t, int p) { return t.ecost[p]; }
+__device__ __forceinline__ int bit_cost(const Tables& t, int bit, int p) { return t.ecost[bit ? 255 - p : p]; }
+__device__ __forceinline__ const uint8_t* proba_p(const Tables& t, int type, int band, int ctx) {
+  return t.proba + ((type * 8 + band) * 3 + ctx) * 11;
 }
 __device__ __forceinline__ int pick3(int c, int a0, int a1, int a2) { return c == 0 ? a0 : (c == 1 ? a1 : a2); }
 __device__ __forceinline__ int vc_of(uint64_t w, int c) { return (int)((w >> (16 * c)) & 0xffff); }
@@ -163,11 +167,11 @@ __device__ __forceinline__ int quantize(const int co[16], int16_t q[16], const S
   return max_zz + 1;
 }
 
-__device__ __forceinline__ int variable_level_cost(const Shared& s, int level, const uint8_t* p) {
+__device__ __forceinline__ int variable_level_cost(const Tables& t, int level, const uint8_t* p) {
   const int idx = min(level - 1, 66);
   int pattern = c_level_codes[2 * idx], bits = c_level_codes[2 * idx + 1], cost = 0;
   for (int i = 2; pattern != 0; i++) {
-    if (pattern & 1) cost += bit_cost(s, bits & 1, p[i]);
+    if (pattern & 1) cost += bit_cost(t, bits & 1, p[i]);
     bits >>= 1;
     pattern >>= 1;
   }
@@ -177,18 +181,18 @@ __device__ __forceinline__ int variable_level_cost(const Shared& s, int level, c
 // TokenCostForCoeffs (encode_quant.go:154-223), branch-free: the context of
 // every position follows from the levels alone (min(|q|, 2) of the previous
 // one), so all table reads are independent and issue back to back.
-__device__ __forceinline__ int token_cost(const Shared& s, const int16_t q[16], int nz_count, int type, int ctx0, int first) {
+__device__ __forceinline__ int token_cost(const Tables& t, const int16_t q[16], int nz_count, int type, int ctx0, int first) {
   int cost = 0, ctx = ctx0;
   const int eob_at = max(nz_count, first);
 #pragma unroll
   for (int n = 0; n < 16; n++) {
     if (n < first) continue;
-    const TokRow& t = s.tok[type * 8 + kBand[n]];
+    const TokRow& tr = t.tok[type * 8 + kBand[n]];
     const int v = abs((int)q[kZig[n]]);
-    const uint64_t vw = s.vcost[type * 8 + kBand[n]][min(v, 67)];
-    const int tokc = v == 0 ? pick3(ctx, t.zero[0], t.zero[1], t.zero[2])
-                            : pick3(ctx, t.nz[0], t.nz[1], t.nz[2]) + s.lfixed[min(v, 2047)] + vc_of(vw, ctx);
-    const int eob = pick3(ctx, t.eob[0], t.eob[1], t.eob[2]);
+    const uint64_t vw = t.vcost[type * 8 + kBand[n]][min(v, 67)];
+    const int tokc = v == 0 ? pick3(ctx, tr.zero[0], tr.zero[1], tr.zero[2])
+                            : pick3(ctx, tr.nz[0], tr.nz[1], tr.nz[2]) + t.lfixed[min(v, 2047)] + vc_of(vw, ctx);
+    const int eob = pick3(ctx, tr.eob[0], tr.eob[1], tr.eob[2]);
     cost += n < nz_count ? tokc : (n == eob_at ? eob : 0);
     ctx = min(v, 2);
   }
@@ -215,7 +219,7 @@ __device__ __forceinline__ int token_cost(const Shared& s, const int16_t q[16], 
 // Returns whether the position has a non-zero level under the neutral bias
 // (the reference's all-zero pre-scan).
 template <int CTX_TYPE>
-__device__ __forceinline__ bool trellis_prep(const Shared& s, int co_z, int n, const SQuant& sq, int lam16, TRec& out) {
+__device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, const SQuant& sq, int lam16, TRec& out) {
   constexpr int64_t BIG = 1ll << 59;
   const int zig = zig_of(n), band = band_of(n + 1);
   const int c0 = max(abs(co_z) + sq.sharpen[zig], 0);
@@ -226,16 +230,16 @@ __device__ __forceinline__ bool trellis_prep(const Shared& s, int co_z, int n, c
   const int thresh = min((int)(((uint32_t)c0 * (uint32_t)iquant + 65536u) >> 17), 2047);
   const bool has0 = L0 > 0 && L0 <= thresh;
   const bool has1 = L0 + 1 <= 2047 && L0 + 1 <= thresh;
-  const int w4096 = s.wtr[zig] * 4096;
+  const int w4096 = t.wtr[zig] * 4096;
   const int e0 = c0 - L0 * quant, e1 = c0 - (L0 + 1) * quant;
-  const int64_t A0 = (int64_t)s.lfixed[L0] * lam16 + (int64_t)w4096 * (e0 * e0 - c0 * c0) + (has0 ? 0 : BIG);
-  const int64_t A1 = (int64_t)s.lfixed[min(L0 + 1, 2047)] * lam16 + (int64_t)w4096 * (e1 * e1 - c0 * c0) + (has1 ? 0 : BIG);
-  const TokRow& t = s.tok[CTX_TYPE * 8 + band];
-  const uint64_t v0 = s.vcost[CTX_TYPE * 8 + band][min(L0, 67)], v1 = s.vcost[CTX_TYPE * 8 + band][min(L0 + 1, 67)];
+  const int64_t A0 = (int64_t)t.lfixed[L0] * lam16 + (int64_t)w4096 * (e0 * e0 - c0 * c0) + (has0 ? 0 : BIG);
+  const int64_t A1 = (int64_t)t.lfixed[min(L0 + 1, 2047)] * lam16 + (int64_t)w4096 * (e1 * e1 - c0 * c0) + (has1 ? 0 : BIG);
+  const TokRow& tr = t.tok[CTX_TYPE * 8 + band];
+  const uint64_t v0 = t.vcost[CTX_TYPE * 8 + band][min(L0, 67)], v1 = t.vcost[CTX_TYPE * 8 + band][min(L0 + 1, 67)];
 #pragma unroll
   for (int pc = 0; pc < 3; pc++) {
-    out.na[pc] = (int64_t)(t.nz[pc] + vc_of(v0, pc)) * lam16 + A0 + 2 * pc;
-    out.nb[pc] = (int64_t)(t.nz[pc] + vc_of(v1, pc)) * lam16 + A1 + 2 * pc + 1;
+    out.na[pc] = (int64_t)(tr.nz[pc] + vc_of(v0, pc)) * lam16 + A0 + 2 * pc;
+    out.nb[pc] = (int64_t)(tr.nz[pc] + vc_of(v1, pc)) * lam16 + A1 + 2 * pc + 1;
   }
   out.l0s = L0 << 3 | (co_z < 0 ? 4 : 0) | min(L0, 2);
   return L0raw > 0;
@@ -243,12 +247,12 @@ __device__ __forceinline__ bool trellis_prep(const Shared& s, int co_z, int n, c
 
 // The serial DP + walk back over prepared positions (key encoding above).  Returns the zigzag nz count; q in raster order.
 template <int FIRST, int CTX_TYPE>
-__device__ __forceinline__ int trellis_dp(const Shared& s, const TRec* rec, int init_ctx, int lam16, int16_t q[16]) {
+__device__ __forceinline__ int trellis_dp(const Tables& t, const TRec* rec, int init_ctx, int lam16, int16_t q[16]) {
   constexpr int64_t BIG = 1ll << 59, VALID = 1ll << 58;
   init_ctx = min(init_ctx, 2);
   int64_t ps0 = init_ctx == 0 ? 0 : BIG, ps1 = init_ctx == 1 ? 0 : BIG, ps2 = init_ctx == 2 ? 0 : BIG;
   uint32_t path[8];
-  const TokRow& t_init = s.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
+  const TokRow& t_init = t.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
   int64_t best_terminal = (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16;
   int best = -1;  // n << 2 | end context
   TRec r = rec[FIRST];
@@ -265,12 +269,12 @@ __device__ __forceinline__ int trellis_dp(const Shared& s, const TRec* rec, int 
     // records are in flight (otherwise every position's loads are hoisted
     // to the top and the DP alone needs 250 VGPRs).
     asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
-    const TokRow& t = s.tok[CTX_TYPE * 8 + kBand[n + 1]];
+    const TokRow& tr = t.tok[CTX_TYPE * 8 + kBand[n + 1]];
     int64_t kz = BIG * 2, ka = BIG * 2, kb = BIG * 2;
 #pragma unroll
     for (int pc = 0; pc < 3; pc++) {
       const int64_t base = pc == 0 ? ps0 : (pc == 1 ? ps1 : ps2);
-      const int64_t z = (base | pc) + (int64_t)t.zero[pc] * lam16;
+      const int64_t z = (base | pc) + (int64_t)tr.zero[pc] * lam16;
       const int64_t ca = base + cur.na[pc];
       const int64_t cb = base + cur.nb[pc];
       kz = z < kz ? z : kz;
@@ -289,11 +293,11 @@ __device__ __forceinline__ int trellis_dp(const Shared& s, const TRec* rec, int 
     ps0 = kz & ~15ll;
     ps1 = k1 & ~15ll;
     ps2 = k2 & ~15ll;
-    const int64_t eob1 = ps1 + (n < 15 ? (int64_t)t.eob[1] * lam16 : 0);
+    const int64_t eob1 = ps1 + (n < 15 ? (int64_t)tr.eob[1] * lam16 : 0);
     const bool w1 = ps1 < VALID && eob1 < best_terminal;
     best_terminal = w1 ? eob1 : best_terminal;
     best = w1 ? (n << 2 | 1) : best;
-    const int64_t eob2 = ps2 + (n < 15 ? (int64_t)t.eob[2] * lam16 : 0);
+    const int64_t eob2 = ps2 + (n < 15 ? (int64_t)tr.eob[2] * lam16 : 0);
     const bool w2 = ps2 < VALID && eob2 < best_terminal;
     best_terminal = w2 ? eob2 : best_terminal;
     best = w2 ? (n << 2 | 2) : best;
@@ -322,16 +326,16 @@ __device__ __forceinline__ int trellis_dp(const Shared& s, const TRec* rec, int 
 // TokenCostForCoeffs's term for position n alone (lane-parallel form of
 // token_cost(); the caller sums over n).  q: raster levels in LDS.
 template <int TYPE>
-__device__ __forceinline__ int token_cost_pos(const Shared& s, const int16_t* q, int n, int nz_count, int ctx0, int first) {
+__device__ __forceinline__ int token_cost_pos(const Tables& t, const int16_t* q, int n, int nz_count, int ctx0, int first) {
   if (n < first) return 0;
   const int band = band_of(n);
-  const TokRow& t = s.tok[TYPE * 8 + band];
+  const TokRow& tr = t.tok[TYPE * 8 + band];
   const int v = abs((int)q[zig_of(n)]);
   const int ctx = n == first ? ctx0 : min(abs((int)q[zig_of(max(n - 1, 0))]), 2);
-  const uint64_t vw = s.vcost[TYPE * 8 + band][min(v, 67)];
-  const int tokc = v == 0 ? pick3(ctx, t.zero[0], t.zero[1], t.zero[2])
-                          : pick3(ctx, t.nz[0], t.nz[1], t.nz[2]) + s.lfixed[min(v, 2047)] + vc_of(vw, ctx);
-  return n < nz_count ? tokc : (n == max(nz_count, first) ? pick3(ctx, t.eob[0], t.eob[1], t.eob[2]) : 0);
+  const uint64_t vw = t.vcost[TYPE * 8 + band][min(v, 67)];
+  const int tokc = v == 0 ? pick3(ctx, tr.zero[0], tr.zero[1], tr.zero[2])
+                          : pick3(ctx, tr.nz[0], tr.nz[1], tr.nz[2]) + t.lfixed[min(v, 2047)] + vc_of(vw, ctx);
+  return n < nz_count ? tokc : (n == max(nz_count, first) ? pick3(ctx, tr.eob[0], tr.eob[1], tr.eob[2]) : 0);
 }
 
 // min over the 16 lanes of a DPP row, result in every lane of the row
@@ -457,7 +461,14 @@ __device__ __forceinline__ T group_sum(T v, int width) {  // sum over aligned gr
   for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-__device__ __forceinline__ void lds_sync() { __syncthreads(); }
+// Each wave works on its own macroblock row, so the cross-lane hand-offs
+// through LDS need a wave-level sync only: LDS executes one wave's
+// instructions in order, so draining this wave's LDS queue before the next
+// access (and keeping the compiler from moving accesses across) suffices.
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // An opaque copy of the LDS base (still typed as LDS, so accesses stay
 // ds_read/ds_write).  Re-taken at the top of a loop body it stops the
@@ -469,14 +480,15 @@ __device__ __forceinline__ void lds_sync() { __syncthreads(); }
 // hoisted out of the row loop and pinned in registers for the whole kernel
 __device__ __forceinline__ int opaque_lane() {
   int l;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"((int)threadIdx.x));
+  asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"((int)threadIdx.x & 63));
   return l;
 }
-typedef __attribute__((address_space(3))) Shared LdsShared;
-__device__ __forceinline__ Shared& launder(Shared& s) {
-  LdsShared* p = (LdsShared*)&s;
+template <typename T>
+__device__ __forceinline__ T& launder(T& s) {
+  typedef __attribute__((address_space(3))) T LdsT;
+  LdsT* p = (LdsT*)&s;
   asm volatile("" : "+s"(p));
-  return *(Shared*)p;
+  return *(T*)p;
 }
 
 // sc1 hand-off helpers (see decode.hip)
@@ -553,41 +565,46 @@ __device__ unsigned long long g_enc_phase[16];
 #define ESTAMP_FLUSH() (void)st_unused_
 #endif
 
-__global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
-  __shared__ Shared s_lds;
-  Shared& s = s_lds;
-  const int lane = threadIdx.x;
-  for (int i = lane; i < 1056; i += 64) s.proba[i] = a.proba[i];
-  for (int i = lane; i < 256; i += 64) s.ecost[i] = vp8_entropy_cost[i];
-  for (int i = lane; i < 2048; i += 64) s.lfixed[i] = vp8_level_fixed_costs[i];
-  for (int i = lane; i < 1000; i += 64) s.fixed_i4[i] = c_fixed_i4[i];
-  if (lane < 16) s.wtr[lane] = c_wtrellis[lane];
-  for (int i = lane; i < (int)(4 * sizeof(Segment) / 4); i += 64)
-    reinterpret_cast<int*>(s.seg)[i] = reinterpret_cast<const int*>(a.segs)[i];
+__global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
+  __shared__ Tables t_lds;
+  __shared__ Shared s_waves[WAVES];
+  Tables& t = t_lds;
+  const int tid = threadIdx.x;
+  constexpr int NT = 64 * WAVES;
+  for (int i = tid; i < 1056; i += NT) t.proba[i] = a.proba[i];
+  for (int i = tid; i < 256; i += NT) t.ecost[i] = vp8_entropy_cost[i];
+  for (int i = tid; i < 2048; i += NT) t.lfixed[i] = vp8_level_fixed_costs[i];
+  for (int i = tid; i < 1000; i += NT) t.fixed_i4[i] = c_fixed_i4[i];
+  if (tid < 16) t.wtr[tid] = c_wtrellis[tid];
+  for (int i = tid; i < (int)(4 * sizeof(Segment) / 4); i += NT)
+    reinterpret_cast<int*>(t.seg)[i] = reinterpret_cast<const int*>(a.segs)[i];
   __syncthreads();
-  for (int i = lane; i < 4 * 8 * 68; i += 64) {
+  for (int i = tid; i < 4 * 8 * 68; i += NT) {
     const int tb = i / 68, level = i % 68;
     uint64_t w = 0;
     for (int c = 0; c < 3; c++)
-      if (level > 0) w |= (uint64_t)variable_level_cost(s, level, s.proba + (tb * 3 + c) * 11) << (16 * c);
-    s.vcost[tb][level] = w;
+      if (level > 0) w |= (uint64_t)variable_level_cost(t, level, t.proba + (tb * 3 + c) * 11) << (16 * c);
+    t.vcost[tb][level] = w;
   }
-  if (lane < 4 * 8) {
+  if (tid < 4 * 8) {
     TokRow r = {};
     for (int c = 0; c < 3; c++) {
-      const uint8_t* p = s.proba + (lane * 3 + c) * 11;
-      r.zero[c] = (uint16_t)(ecost(s, 255 - p[0]) + ecost(s, p[1]));
-      r.nz[c] = (uint16_t)(ecost(s, 255 - p[0]) + ecost(s, 255 - p[1]));
-      r.eob[c] = (uint16_t)ecost(s, p[0]);
+      const uint8_t* p = t.proba + (tid * 3 + c) * 11;
+      r.zero[c] = (uint16_t)(ecost(t, 255 - p[0]) + ecost(t, p[1]));
+      r.nz[c] = (uint16_t)(ecost(t, 255 - p[0]) + ecost(t, 255 - p[1]));
+      r.eob[c] = (uint16_t)ecost(t, p[0]);
     }
-    s.tok[lane] = r;
+    t.tok[tid] = r;
   }
+  __syncthreads();  // the tables are read-only from here; the waves run independently
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  Shared& s = s_waves[wave];
   const int mbw = a.mbw, mbh = a.mbh;
   const int ys = 16 * mbw, uvs = 8 * mbw;
   const int max_modes = a.quality < 50 ? 2 : 3;
   const int total_rows = a.n_img * mbh;
   ESTAMP_DECL;
-  lds_sync();
 
   for (;;) {
     if (lane == 0) s.word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -616,7 +633,8 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
     int seen = 0;
 
     for (int mbx = 0; mbx < mbw; mbx++) {
-      Shared& s = launder(s_lds);
+      Shared& s = launder(s_waves[wave]);
+      Tables& t = launder(t_lds);
       const int lane = opaque_lane();
       const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
       ESTAMP(0);
@@ -644,7 +662,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
       }
       ESTAMP(1);
       const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
-      const Segment& sg = s.seg[segid];
+      const Segment& sg = t.seg[segid];
       // ---- import (importBlockParallel :433-452) with edge replication ----
       {
         const int x = 16 * mbx, y = 16 * mby;
@@ -727,9 +745,9 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
       const int nz_left = __shfl(nz16, (lane - 1) & 63, 64), nz_top = __shfl(nz16, (lane - 4) & 63, 64);
       {
         const int l = bx > 0 ? (nz_left > 0) : (int)((left_nz >> by) & 1);
-        const int t = by > 0 ? (nz_top > 0) : (int)((top_nz >> bx) & 1);
-        const int ctx = min(l + t, 2);
-        int rate = mvalid ? token_cost(s, q16, nz16, 0, ctx, 1) : 0;
+        const int tp = by > 0 ? (nz_top > 0) : (int)((top_nz >> bx) & 1);
+        const int ctx = min(l + tp, 2);
+        int rate = mvalid ? token_cost(t, q16, nz16, 0, ctx, 1) : 0;
         bool acnz = false;
 #pragma unroll
         for (int i = 1; i < 16; i++) acnz |= q16[i] != 0;
@@ -745,7 +763,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
           for (int i = 0; i < 16; i++) qdc_i[i] = wht[i];
           const int nzdc = quantize(qdc_i, qdc, sg.y2, 0);
           const int dc_ctx = min(top_nz_dc + left_nz_dc, 2);
-          s.mode_rate[m] = vp8_mode_fixed_cost16[m] + token_cost(s, qdc, nzdc, 1, dc_ctx, 0);
+          s.mode_rate[m] = vp8_mode_fixed_cost16[m] + token_cost(t, qdc, nzdc, 1, dc_ctx, 0);
           int dq[16];
           dequant(qdc, dq, sg.y2);
           int16_t whto[16];
@@ -809,7 +827,8 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
         int run_rate = 0, run_disto = 0, run_header = 0;
         bool early = false;
         for (int st = 0; st < 10 && !early; st++) {
-          Shared& s = launder(s_lds);
+          Shared& s = launder(s_waves[wave]);
+          Tables& t = launder(t_lds);
           const int lane = opaque_lane();
           const int half = lane >> 5, hl = lane & 31;
           const int wy = (st <= 3 ? 0 : (st - 2) >> 1) + half, wx = st - 2 * wy;
@@ -821,8 +840,8 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
           const int off = YOFF + 4 * by4 * BPS + 4 * bx4;
           const bool has_top = mby > 0 || by4 > 0, has_left = mbx > 0 || bx4 > 0;
           const int l = bx4 > 0 ? (s.nzy[max(blk - 1, 0)] > 0) : (int)((left_nz >> by4) & 1);
-          const int t = by4 > 0 ? (s.nzy[max(blk - 4, 0)] > 0) : (int)((top_nz >> bx4) & 1);
-          const int nz_ctx = min(l + t, 2);
+          const int tp = by4 > 0 ? (s.nzy[max(blk - 4, 0)] > 0) : (int)((top_nz >> bx4) & 1);
+          const int nz_ctx = min(l + tp, 2);
           int src[16];
           load4x4(s.yin + off, src);
           SSTAMP(-1);
@@ -866,7 +885,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
             const int c = hl >> 3, n0 = 2 * (hl & 7), sl = half * 3 + c;
 #pragma unroll
             for (int j = 0; j < 2; j++)
-              pnz |= trellis_prep<3>(s, s.co_buf[sl][zig_of(n0 + j)], n0 + j, sg.y1, lam16, s.trec[sl][n0 + j]);
+              pnz |= trellis_prep<3>(t, s.co_buf[sl][zig_of(n0 + j)], n0 + j, sg.y1, lam16, s.trec[sl][n0 + j]);
           }
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
@@ -876,7 +895,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
           uint32_t recp[4] = {0, 0, 0, 0};
           if (cand) {
             if ((pnz_mask >> (32 * half + 8 * hl)) & 0xff) {
-              nz = trellis_dp<0, 3>(s, s.trec[slot], nz_ctx, lam16, q);
+              nz = trellis_dp<0, 3>(t, s.trec[slot], nz_ctx, lam16, q);
             } else {
 #pragma unroll
               for (int i = 0; i < 16; i++) q[i] = 0;
@@ -904,7 +923,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
           if (bvalid && hl < 8 * K) {
             const int c = hl >> 3, n0 = 2 * (hl & 7), sl = half * 3 + c;
             const int nzc = s.cand_nz[sl];
-            part = token_cost_pos<3>(s, s.cand_q[sl], n0, nzc, nz_ctx, 0) + token_cost_pos<3>(s, s.cand_q[sl], n0 + 1, nzc, nz_ctx, 0);
+            part = token_cost_pos<3>(t, s.cand_q[sl], n0, nzc, nz_ctx, 0) + token_cost_pos<3>(t, s.cand_q[sl], n0 + 1, nzc, nz_ctx, 0);
           }
           part += __shfl_xor(part, 1, 64);
           part += __shfl_xor(part, 2, 64);
@@ -915,7 +934,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
           if (cand) {
             rate = (mode > 0 && cnt <= 3) ? 140 : 0;
             rate += tok_rate;
-            rate += s.fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
+            rate += t.fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
             score = rd_score(disto, rate, sg.lambda_i4);
             CSTAMP(3);
           }
@@ -940,7 +959,7 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
             s.nzy[blk] = (uint8_t)nz;
             s.blk_rate[blk] = rate;
             s.blk_disto[blk] = disto;
-            s.blk_hdr[blk] = s.fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
+            s.blk_hdr[blk] = t.fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
           }
           lds_sync();
           {
@@ -984,8 +1003,8 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
         int rate = 0, sse = 0, acn = 0;
         if (act) {
           const int l = ubx > 0 ? (nzl > 0) : (int)((left_nz >> (4 + 2 * pl + uby)) & 1);
-          const int t = uby > 0 ? (nzt > 0) : (int)((top_nz >> (4 + 2 * pl + ubx)) & 1);
-          rate = uvalid ? token_cost(s, q, nz, 2, min(l + t, 2), 0) : 0;
+          const int tp = uby > 0 ? (nzt > 0) : (int)((top_nz >> (4 + 2 * pl + ubx)) & 1);
+          rate = uvalid ? token_cost(t, q, nz, 2, min(l + tp, 2), 0) : 0;
           int dq[16], rec[16];
           dequant(q, dq, sg.uv);
           recon4(pred, dq, rec);
@@ -1054,25 +1073,26 @@ __global__ __launch_bounds__(64) void k_encode_rows(EncArgs a) {
         // block j on the diagonal, then the block's lane runs the DP
         const int lam16 = sg.tlambda_i16 * 16;
         for (int d = 0; d < 7; d++) {
-          Shared& s = launder(s_lds);
+          Shared& s = launder(s_waves[wave]);
+          Tables& t = launder(t_lds);
           const int by_lo = max(0, d - 3), nblk = min(d, 3) - by_lo + 1;
           bool pnz = false;
           if (lane < 8 * nblk) {
             const int j = lane >> 3, n0 = 2 * (lane & 7), pb = (by_lo + j) * 4 + d - (by_lo + j);
 #pragma unroll
             for (int k = 0; k < 2; k++)
-              if (n0 + k >= 1) pnz |= trellis_prep<0>(s, s.co_buf[pb][zig_of(n0 + k)], n0 + k, sg.y1, lam16, s.trec[j][n0 + k]);
+              if (n0 + k >= 1) pnz |= trellis_prep<0>(t, s.co_buf[pb][zig_of(n0 + k)], n0 + k, sg.y1, lam16, s.trec[j][n0 + k]);
           }
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
           if (lane < 16 && bx + by == d) {
             const int j = by - by_lo;
             const int l = bx > 0 ? (s.nzy[lane - 1] > 0) : (int)((left_nz >> by) & 1);
-            const int t = by > 0 ? (s.nzy[lane - 4] > 0) : (int)((top_nz >> bx) & 1);
+            const int tp = by > 0 ? (s.nzy[lane - 4] > 0) : (int)((top_nz >> bx) & 1);
             int16_t q[16];
             int nz = 0;
             if ((pnz_mask >> (8 * j)) & 0xff) {
-              nz = trellis_dp<1, 0>(s, s.trec[j], min(l + t, 2), lam16, q);
+              nz = trellis_dp<1, 0>(t, s.trec[j], min(l + tp, 2), lam16, q);
             } else {
 #pragma unroll
               for (int i = 0; i < 16; i++) q[i] = 0;
@@ -1359,11 +1379,12 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
     return wg::check_launch("hipMemsetAsync(encode ctl)");
   int cus = 0, per_cu = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows, 64, 0) != hipSuccess || per_cu <= 0)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows, 64 * WAVES, 0) != hipSuccess || per_cu <= 0)
     return wg::check_launch("encode occupancy query");
   const int rows = n_images * mbh;
-  const int grid = rows < per_cu * cus ? rows : per_cu * cus;
-  hipLaunchKernelGGL(k_encode_rows, dim3((unsigned)grid), dim3(64), 0, s, a);
+  const int wgs = (rows + WAVES - 1) / WAVES;  // each wave dequeues rows on its own
+  const int grid = wgs < per_cu * cus ? wgs : per_cu * cus;
+  hipLaunchKernelGGL(k_encode_rows, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
   return wg::check_launch("k_encode_rows");
 }
 
