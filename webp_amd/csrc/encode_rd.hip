@@ -82,7 +82,7 @@ __device__ __forceinline__ int zig_of(int n) { return (int)((pack_zig() >> (4 * 
 __device__ __forceinline__ int band_of(int n) { return (int)((pack_band() >> (3 * n)) & 7); }
 
 // One trellis position, prepared by a lane of its own (trellis_prep) and
-// consumed by the lane running the serial DP (trellis_dp).
+// consumed by the lane quad running the DP (trellis_dp4).
 struct alignas(16) TRec {
   int64_t na[3];  // from predecessor pc to level L0: (nz token + level cost) * lam16 + distortion + order idx 2pc
   int64_t nb[3];  // ... to level L0 + 1 (order idx 2pc + 1); + BIG when that level is not a candidate
@@ -104,6 +104,28 @@ __constant__ int32_t c_wtrellis[16];
 struct alignas(16) TokRow {
   uint16_t zero[4], nz[4], eob[4], pad[4];
 };
+// Table-driven 4x4 intra prediction for lane-varying modes.  Every pixel of
+// every PredLuma4 mode (predict_lossy.go:185-424) is one entry of a 64-byte
+// per-block value table V built from the 13 context pixels:
+//   V[0..14]  edge E = L L K J I X A B C D E F G H H (L and H repeated)
+//   V[16+i]   avg2(E[i], E[i+1])          V[32+i]  avg3(E[i-1], E[i], E[i+1])
+//   V[47]     the DC value                V[48+p]  the TM value of pixel p
+// kPred4Code[mode][pixel] is the V index (checked against pred4_row on
+// random contexts by tools-side derivation; pinned on the GPU by the
+// encoder parity tests).
+constexpr uint8_t kPred4Code[10][16] = {
+  {47, 47, 47, 47, 47, 47, 47, 47, 47, 47, 47, 47, 47, 47, 47, 47},
+  {48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 63},
+  {38, 39, 40, 41, 38, 39, 40, 41, 38, 39, 40, 41, 38, 39, 40, 41},
+  {36, 36, 36, 36, 35, 35, 35, 35, 34, 34, 34, 34, 33, 33, 33, 33},
+  {37, 38, 39, 40, 36, 37, 38, 39, 35, 36, 37, 38, 34, 35, 36, 37},
+  {21, 22, 23, 24, 37, 38, 39, 40, 36, 21, 22, 23, 35, 37, 38, 39},
+  {39, 40, 41, 42, 40, 41, 42, 43, 41, 42, 43, 44, 42, 43, 44, 45},
+  {22, 23, 24, 25, 39, 40, 41, 42, 23, 24, 25, 43, 40, 41, 42, 44},
+  {20, 37, 38, 39, 19, 36, 20, 37, 18, 35, 19, 36, 17, 34, 18, 35},
+  {19, 35, 18, 34, 18, 34, 17, 33, 17, 33, 1, 1, 1, 1, 1, 1}
+};
+
 // Tables shared by the workgroup's waves (filled once per launch)
 struct Tables {
   uint8_t proba[4 * 8 * 3 * 11];
@@ -118,6 +140,7 @@ struct Tables {
   Segment seg[4];
   uint16_t fixed_i4[1000];
   int wtr[16];  // trellis distortion weights (kWeightTrellis)
+  alignas(16) uint8_t pcode[10][16];  // kPred4Code
 };
 // Per-wave state: each wave of the workgroup encodes its own macroblock row
 struct Shared {
@@ -133,6 +156,7 @@ struct Shared {
   TRec trec[6][16];        // trellis position records: I4 (half, candidate) / final I16 (diagonal slot)
   int16_t cand_q[6][16];   // I4 candidates' levels for the lane-parallel token cost
   int cand_nz[6], cand_rate[6];
+  alignas(16) uint8_t pv[2][64];  // per half-wave: the I4 block's prediction value table
   int word;
 };
 constexpr int WAVES = 4;  // waves (macroblock rows in flight) per workgroup
@@ -245,82 +269,122 @@ __device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, c
   return L0raw > 0;
 }
 
-// The serial DP + walk back over prepared positions (key encoding above).  Returns the zigzag nz count; q in raster order.
+// 64-bit value of lane j of this lane's quad (DPP quad_perm broadcast)
+template <int J>
+__device__ __forceinline__ int64_t quad_bcast(int64_t v) {
+  constexpr int perm = J | J << 2 | J << 4 | J << 6;
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, perm, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)v >> 32), perm, 0xf, 0xf, false);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int J>
+__device__ __forceinline__ int quad_bcast32(int v) {
+  return __builtin_amdgcn_mov_dpp(v, J | J << 2 | J << 4 | J << 6, 0xf, 0xf, false);
+}
+
+// The trellis DP on a quad of lanes: lane k (0..2) of the quad owns end
+// context k and computes its min over the (up to 6) candidates per
+// position; the three states are exchanged by DPP broadcasts.  Lane 3
+// shadows lane 2.  The keys and their order are those of the sequential DP; the
+// quad's lane 0 walks the path back and writes the levels (raster) to q and
+// the zigzag nz count to *nz.  (The DP alone on one lane took ~112 VALU
+// instructions per position; on the quad ~55.)
 template <int FIRST, int CTX_TYPE>
-__device__ __forceinline__ int trellis_dp(const Tables& t, const TRec* rec, int init_ctx, int lam16, int16_t q[16]) {
+__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, int init_ctx, int lam16, int k, int16_t* q,
+                                            int* nz) {
   constexpr int64_t BIG = 1ll << 59, VALID = 1ll << 58;
   init_ctx = min(init_ctx, 2);
-  int64_t ps0 = init_ctx == 0 ? 0 : BIG, ps1 = init_ctx == 1 ? 0 : BIG, ps2 = init_ctx == 2 ? 0 : BIG;
-  uint32_t path[8];
+  const int kk = min(k, 2);
+  int64_t ps = kk == init_ctx ? 0 : BIG;
+  uint32_t path0 = 0, path1 = 0;  // 4 bits (key idx) per position: positions 0-7, 8-15
   const TokRow& t_init = t.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
   int64_t best_terminal = (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16;
-  int best = -1;  // n << 2 | end context
+  int best_n = -1;
   TRec r = rec[FIRST];
 #pragma unroll
-  for (int n = 0; n < 16; n++) {
-    if (n < FIRST) {
-      if (!(n & 1)) path[n >> 1] = 0;
-      continue;
-    }
+  for (int n = FIRST; n < 16; n++) {
     const TRec cur = r;
-    if (n < 15) r = rec[n + 1];  // one position ahead
-    // Tie the previous position's state into the memory chain: later loads
-    // cannot be issued before it is computed, so at most two positions of
-    // records are in flight (otherwise every position's loads are hoisted
-    // to the top and the DP alone needs 250 VGPRs).
-    asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
+    if (n < 15) r = rec[n + 1];
+    asm volatile("" : "+v"(ps), "+v"(best_terminal)::"memory");
     const TokRow& tr = t.tok[CTX_TYPE * 8 + kBand[n + 1]];
-    int64_t kz = BIG * 2, ka = BIG * 2, kb = BIG * 2;
+    const int64_t p0 = quad_bcast<0>(ps), p1 = quad_bcast<1>(ps), p2 = quad_bcast<2>(ps);
+    const int cls = cur.l0s & 3;
+    const bool isZ = kk == 0;
+    const bool useA = (kk == 1 && cls == 1) || (kk == 2 && cls == 2);
+    const bool useB = (kk == 1 && cls == 0) || (kk == 2 && cls >= 1);
+    // every lane evaluates every operand (selects, no divergent branches)
+    uint64_t zw = *reinterpret_cast<const uint64_t*>(tr.zero);
+    asm volatile("" : "+v"(zw));  // keep it per-lane: a uniform operand turns the selects below into branches
+    int64_t best = BIG * 2;
 #pragma unroll
     for (int pc = 0; pc < 3; pc++) {
-      const int64_t base = pc == 0 ? ps0 : (pc == 1 ? ps1 : ps2);
-      const int64_t z = (base | pc) + (int64_t)tr.zero[pc] * lam16;
-      const int64_t ca = base + cur.na[pc];
-      const int64_t cb = base + cur.nb[pc];
-      kz = z < kz ? z : kz;
-      ka = ca < ka ? ca : ka;
-      kb = cb < kb ? cb : kb;
+      const int64_t base = pc == 0 ? p0 : (pc == 1 ? p1 : p2);
+      int64_t z = (int64_t)(int)((zw >> (16 * pc)) & 0xffff) * lam16 + pc;
+      asm volatile("" : "+v"(z));  // materialised before the select (else it is sunk into a branch)
+      const int64_t na = cur.na[pc], nb = cur.nb[pc];
+      const int64_t xa = isZ ? z : (useA ? na : BIG);
+      const int64_t xb = useB ? nb : BIG;
+      const int64_t ca = base + xa, cb = base + xb;
+      best = ca < best ? ca : best;
+      best = cb < best ? cb : best;
     }
-    const int cls = cur.l0s & 3;
-    const int64_t kab = kb < ka ? kb : ka;
-    const int64_t k1 = cls == 0 ? kb : (cls == 1 ? ka : BIG);
-    const int64_t k2 = cls == 0 ? BIG : (cls == 1 ? kb : kab);
-    const uint32_t pr = ((uint32_t)kz & 15) | (((uint32_t)k1 & 15) << 4) | (((uint32_t)k2 & 15) << 8);
-    if (n & 1)
-      path[n >> 1] |= pr << 16;
+    const uint32_t idx = (uint32_t)best & 15;
+    if (n < 8)
+      path0 |= idx << (4 * n);
     else
-      path[n >> 1] = pr;
-    ps0 = kz & ~15ll;
-    ps1 = k1 & ~15ll;
-    ps2 = k2 & ~15ll;
-    const int64_t eob1 = ps1 + (n < 15 ? (int64_t)tr.eob[1] * lam16 : 0);
-    const bool w1 = ps1 < VALID && eob1 < best_terminal;
-    best_terminal = w1 ? eob1 : best_terminal;
-    best = w1 ? (n << 2 | 1) : best;
-    const int64_t eob2 = ps2 + (n < 15 ? (int64_t)tr.eob[2] * lam16 : 0);
-    const bool w2 = ps2 < VALID && eob2 < best_terminal;
-    best_terminal = w2 ? eob2 : best_terminal;
-    best = w2 ? (n << 2 | 2) : best;
+      path1 |= idx << (4 * (n - 8));
+    ps = best & ~15ll;
+    // terminal (EOB after this position) from end contexts 1 and 2
+    uint64_t ew = *reinterpret_cast<const uint64_t*>(tr.eob);
+    asm volatile("" : "+v"(ew));
+    int64_t ecost_k = n < 15 ? (int64_t)(int)((ew >> (16 * kk)) & 0xffff) * lam16 : 0;
+    asm volatile("" : "+v"(ecost_k));
+    const int64_t eob = ps + ecost_k;
+    const bool w = kk >= 1 && ps < VALID && eob < best_terminal;
+    best_terminal = w ? eob : best_terminal;
+    best_n = w ? n : best_n;
   }
-  const int best_n = best >> 2;  // -1 when no terminal beat the all-zero block
-  int ctx = best & 3, last = 0;
+  // combine the terminals of contexts 1 and 2: lower score, then earlier
+  // position, then context 1 (the reference's scan order)
+  const int64_t bt1 = quad_bcast<1>(best_terminal), bt2 = quad_bcast<2>(best_terminal);
+  const int bn1 = quad_bcast32<1>(best_n), bn2 = quad_bcast32<2>(best_n);
+  const uint32_t pa0 = quad_bcast32<0>(path0), pb0 = quad_bcast32<0>(path1);
+  const uint32_t pa1 = quad_bcast32<1>(path0), pb1 = quad_bcast32<1>(path1);
+  const uint32_t pa2 = quad_bcast32<2>(path0), pb2 = quad_bcast32<2>(path1);
+  if (k != 0) return;
+  int bn, bc;
+  if (bn1 < 0 && bn2 < 0) {
+    bn = -1;
+    bc = 0;
+  } else if (bn2 < 0 || (bn1 >= 0 && (bt1 < bt2 || (bt1 == bt2 && bn1 <= bn2)))) {
+    bn = bn1;
+    bc = 1;
+  } else {
+    bn = bn2;
+    bc = 2;
+  }
+  int ctx = bc, last = 0;
+  int16_t lv_out[16];
 #pragma unroll
   for (int n = 15; n >= 0; n--) {
     const int zig = kZig[n];
     if (n < FIRST) {
-      q[zig] = 0;
+      lv_out[zig] = 0;
       continue;
     }
-    const bool act = n <= best_n;
-    const int idx = (int)(((path[n >> 1] >> (16 * (n & 1))) >> (4 * ctx)) & 15);
+    const bool act = n <= bn;
+    const uint32_t w = n < 8 ? (ctx == 0 ? pa0 : (ctx == 1 ? pa1 : pa2)) : (ctx == 0 ? pb0 : (ctx == 1 ? pb1 : pb2));
+    const int idx = (int)((w >> (4 * (n & 7))) & 15);
     const int l0s = rec[n].l0s;
     const int mag = ctx == 0 ? 0 : (l0s >> 3) + (idx & 1);
     const int lv = act ? ((l0s & 4) ? -mag : mag) : 0;
-    q[zig] = (int16_t)lv;
+    lv_out[zig] = (int16_t)lv;
     last = (lv != 0 && last == 0) ? n + 1 : last;
     ctx = act ? (ctx == 0 ? idx : idx >> 1) : ctx;
   }
-  return best < 0 ? 0 : last;
+#pragma unroll
+  for (int i = 0; i < 16; i++) q[i] = lv_out[i];
+  *nz = bn < 0 ? 0 : last;
 }
 
 // TokenCostForCoeffs's term for position n alone (lane-parallel form of
@@ -449,6 +513,39 @@ __device__ __forceinline__ void pred4_block(int mode, const uint8_t* buf, int of
 #pragma unroll
   for (int r = 0; r < 4; r++) unpack_rows(pred4_row(mode, r, X, T, L), pred + 4 * r);
 }
+// Build the block's value table V (see kPred4Code) from the context around
+// buf + off: lane i (< 32 of the caller's half-wave) fills its entries in
+// two LDS passes.  The caller syncs after each pass (`pass` 0 then 1).
+__device__ __forceinline__ void pred4_values(const uint8_t* buf, int off, int i, uint8_t* v, int pass) {
+  const uint8_t* d = buf + off;
+  if (pass == 0) {
+    if (i < 15) {  // E: L L K J I X A..H H
+      const int src = i <= 1 ? -1 + 3 * BPS : (i <= 4 ? -1 + (4 - i) * BPS : (i == 5 ? -1 - BPS : -BPS + min(i - 6, 7)));
+      v[i] = d[src];
+    } else if (i == 15) {
+      int sum = 4;
+#pragma unroll
+      for (int k = 0; k < 4; k++) sum += d[k - BPS] + d[-1 + k * BPS];
+      v[47] = (uint8_t)(sum >> 3);
+    } else {  // TM of pixel p = i - 16
+      const int p = i - 16, x = p & 3, y = p >> 2;
+      v[48 + p] = (uint8_t)clip8(d[-1 + y * BPS] + d[x - BPS] - d[-1 - BPS]);
+    }
+  } else {
+    if (i < 14) {
+      v[16 + i] = (uint8_t)avg2(v[i], v[i + 1]);
+    } else if (i >= 16 && i < 29) {
+      const int c = i - 15;  // 1..13
+      v[32 + c] = (uint8_t)avg3(v[c - 1], v[c], v[c + 1]);
+    }
+  }
+}
+__device__ __forceinline__ void pred4_lut(const uint8_t* code, const uint8_t* v, int pred[16]) {
+  const uint4 c = *reinterpret_cast<const uint4*>(code);
+  const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+  for (int p = 0; p < 16; p++) pred[p] = v[(w[p >> 2] >> (8 * (p & 3))) & 0xff];
+}
 __device__ __forceinline__ int check_mode(int mbx, int mby, int mode) {
   const int edge = (mbx == 0) ? ((mby == 0) ? 6 : 5) : ((mby == 0) ? 4 : 0);
   return mode == 0 ? edge : mode;
@@ -576,6 +673,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
   for (int i = tid; i < 2048; i += NT) t.lfixed[i] = vp8_level_fixed_costs[i];
   for (int i = tid; i < 1000; i += NT) t.fixed_i4[i] = c_fixed_i4[i];
   if (tid < 16) t.wtr[tid] = c_wtrellis[tid];
+  if (tid < 160) t.pcode[tid >> 4][tid & 15] = kPred4Code[tid >> 4][tid & 15];
   for (int i = tid; i < (int)(4 * sizeof(Segment) / 4); i += NT)
     reinterpret_cast<int*>(t.seg)[i] = reinterpret_cast<const int*>(a.segs)[i];
   __syncthreads();
@@ -846,10 +944,14 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           load4x4(s.yin + off, src);
           SSTAMP(-1);
           // pre-screen all eligible modes by prediction SSE (lanes 0-9 of each half)
+          pred4_values(s.yout2, off, hl, s.pv[half], 0);
+          lds_sync();
+          pred4_values(s.yout2, off, hl, s.pv[half], 1);
+          lds_sync();
           int sse_lane = 0;
           if (bvalid && hl < 10) {
             int pred[16];
-            pred4_block(hl, s.yout2, off, pred);
+            pred4_lut(t.pcode[hl], s.pv[half], pred);
             sse_lane = sse16(src, pred);
           }
           SSTAMP(0);
@@ -869,7 +971,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           if (cand) {
             CSTAMP(-1);
             int pred[16], co[16];
-            pred4_block(mode, s.yout2, off, pred);
+            pred4_lut(t.pcode[mode], s.pv[half], pred);
 #pragma unroll
             for (int r = 0; r < 4; r++) predp[r] = pack4(pred[4 * r], pred[4 * r + 1], pred[4 * r + 2], pred[4 * r + 3]);
             fdct(src, pred, co);
@@ -889,18 +991,27 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           }
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
-          // candidates: DP, reconstruction, distortion
+          // the trellis DP: one lane quad per candidate (lane 4c + k owns end context k)
+          if (bvalid && hl < 4 * K) {
+            const int c = hl >> 2, sl = half * 3 + c;
+            if ((pnz_mask >> (32 * half + 8 * c)) & 0xff) {
+              trellis_dp4<0, 3>(t, s.trec[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
+            } else if ((hl & 3) == 0) {
+#pragma unroll
+              for (int i = 0; i < 16; i++) s.cand_q[sl][i] = 0;
+              s.cand_nz[sl] = 0;
+            }
+          }
+          lds_sync();
+          // candidates: reconstruction, distortion
           int16_t q[16];
           int nz = 0, disto = 0, cnt = 0;
           uint32_t recp[4] = {0, 0, 0, 0};
           if (cand) {
-            if ((pnz_mask >> (32 * half + 8 * hl)) & 0xff) {
-              nz = trellis_dp<0, 3>(t, s.trec[slot], nz_ctx, lam16, q);
-            } else {
-#pragma unroll
-              for (int i = 0; i < 16; i++) q[i] = 0;
-            }
             CSTAMP(1);
+#pragma unroll
+            for (int i = 0; i < 16; i++) q[i] = s.cand_q[slot][i];
+            nz = s.cand_nz[slot];
             int pred[16], dq[16], rec[16];
 #pragma unroll
             for (int r = 0; r < 4; r++) unpack_rows(predp[r], pred + 4 * r);
@@ -912,12 +1023,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
             if (sg.tlambda_sd > 0) disto += (sg.tlambda_sd * tdisto(src, rec) + 128) >> 8;
 #pragma unroll
             for (int i = 1; i < 16; i++) cnt += q[i] != 0;
-#pragma unroll
-            for (int i = 0; i < 16; i++) s.cand_q[slot][i] = q[i];
-            s.cand_nz[slot] = nz;
             CSTAMP(2);
           }
-          lds_sync();
           // token cost, lane-parallel over positions, summed over each candidate's 8 lanes
           int part = 0;
           if (bvalid && hl < 8 * K) {
@@ -1085,21 +1192,18 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           }
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
-          if (lane < 16 && bx + by == d) {
-            const int j = by - by_lo;
-            const int l = bx > 0 ? (s.nzy[lane - 1] > 0) : (int)((left_nz >> by) & 1);
-            const int tp = by > 0 ? (s.nzy[lane - 4] > 0) : (int)((top_nz >> bx) & 1);
-            int16_t q[16];
-            int nz = 0;
+          if (lane < 4 * nblk) {  // one lane quad per block of the diagonal
+            const int j = lane >> 2, qby = by_lo + j, qbx = d - qby, qb = qby * 4 + qbx;
+            const int l = qbx > 0 ? (s.nzy[qb - 1] > 0) : (int)((left_nz >> qby) & 1);
+            const int tp = qby > 0 ? (s.nzy[qb - 4] > 0) : (int)((top_nz >> qbx) & 1);
+            int nzv = 0;
             if ((pnz_mask >> (8 * j)) & 0xff) {
-              nz = trellis_dp<1, 0>(t, s.trec[j], min(l + tp, 2), lam16, q);
-            } else {
+              trellis_dp4<1, 0>(t, s.trec[j], min(l + tp, 2), lam16, lane & 3, s.coeffs + qb * 16, &nzv);
+            } else if ((lane & 3) == 0) {
 #pragma unroll
-              for (int i = 0; i < 16; i++) q[i] = 0;
+              for (int i = 0; i < 16; i++) s.coeffs[qb * 16 + i] = 0;
             }
-            s.nzy[lane] = (uint8_t)nz;
-#pragma unroll
-            for (int i = 0; i < 16; i++) s.coeffs[lane * 16 + i] = q[i];
+            if ((lane & 3) == 0) s.nzy[qb] = (uint8_t)nzv;
           }
           lds_sync();
         }
