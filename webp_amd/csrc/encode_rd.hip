@@ -83,13 +83,16 @@ __device__ __forceinline__ int band_of(int n) { return (int)((pack_band() >> (3 
 
 // One trellis position, prepared by a lane of its own (trellis_prep) and
 // consumed by the lane quad running the DP (trellis_dp4).
-struct alignas(16) TRec {
-  int64_t na[3];  // from predecessor pc to level L0: (nz token + level cost) * lam16 + distortion + order idx 2pc
-  int64_t nb[3];  // ... to level L0 + 1 (order idx 2pc + 1); + BIG when that level is not a candidate
-  int32_t l0s;    // L0 << 3 | negative << 2 | min(L0, 2)
-  int32_t pad[3];
+struct alignas(8) TRec {
+  // x[role][pc]: the transition from predecessor context pc, as a key
+  // (score x16 + order idx) to add to that predecessor's state:
+  //   role 0  level 0 (end context 0): zero-token cost * lam16 + idx pc
+  //   role 1  level L0: (nz token + level cost) * lam16 + distortion + idx 2pc
+  //   role 2  level L0 + 1: likewise, idx 2pc + 1
+  // + BIG when that level is not a candidate
+  int64_t x[3][3];
 };
-static_assert(sizeof(TRec) == 64, "TRec layout");
+static_assert(sizeof(TRec) == 72, "TRec layout");
 
 __constant__ uint16_t c_level_codes[134];
 __constant__ uint16_t c_fixed_i4[1000];
@@ -154,6 +157,7 @@ struct Shared {
   int blk_rate[16], blk_disto[16], blk_hdr[16];
   int co_buf[16][16];      // transform coefficients handed to the trellis prep lanes
   TRec trec[6][16];        // trellis position records: I4 (half, candidate) / final I16 (diagonal slot)
+  int l0s[6][16];          // per position: L0 << 3 | negative << 2 | min(L0, 2)
   int16_t cand_q[6][16];   // I4 candidates' levels for the lane-parallel token cost
   int cand_nz[6], cand_rate[6];
   alignas(16) uint8_t pv[2][64];  // per half-wave: the I4 block's prediction value table
@@ -243,7 +247,8 @@ __device__ __forceinline__ int token_cost(const Tables& t, const int16_t q[16], 
 // Returns whether the position has a non-zero level under the neutral bias
 // (the reference's all-zero pre-scan).
 template <int CTX_TYPE>
-__device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, const SQuant& sq, int lam16, TRec& out) {
+__device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, const SQuant& sq, int lam16, TRec& out,
+                                             int& l0s) {
   constexpr int64_t BIG = 1ll << 59;
   const int zig = zig_of(n), band = band_of(n + 1);
   const int c0 = max(abs(co_z) + sq.sharpen[zig], 0);
@@ -262,10 +267,11 @@ __device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, c
   const uint64_t v0 = t.vcost[CTX_TYPE * 8 + band][min(L0, 67)], v1 = t.vcost[CTX_TYPE * 8 + band][min(L0 + 1, 67)];
 #pragma unroll
   for (int pc = 0; pc < 3; pc++) {
-    out.na[pc] = (int64_t)(tr.nz[pc] + vc_of(v0, pc)) * lam16 + A0 + 2 * pc;
-    out.nb[pc] = (int64_t)(tr.nz[pc] + vc_of(v1, pc)) * lam16 + A1 + 2 * pc + 1;
+    out.x[0][pc] = (int64_t)tr.zero[pc] * lam16 + pc;
+    out.x[1][pc] = (int64_t)(tr.nz[pc] + vc_of(v0, pc)) * lam16 + A0 + 2 * pc;
+    out.x[2][pc] = (int64_t)(tr.nz[pc] + vc_of(v1, pc)) * lam16 + A1 + 2 * pc + 1;
   }
-  out.l0s = L0 << 3 | (co_z < 0 ? 4 : 0) | min(L0, 2);
+  l0s = L0 << 3 | (co_z < 0 ? 4 : 0) | min(L0, 2);
   return L0raw > 0;
 }
 
@@ -282,88 +288,72 @@ __device__ __forceinline__ int quad_bcast32(int v) {
   return __builtin_amdgcn_mov_dpp(v, J | J << 2 | J << 4 | J << 6, 0xf, 0xf, false);
 }
 
-// The trellis DP on a quad of lanes: lane k (0..2) of the quad owns end
-// context k and computes its min over the (up to 6) candidates per
-// position; the three states are exchanged by DPP broadcasts.  Lane 3
-// shadows lane 2.  The keys and their order are those of the sequential DP; the
-// quad's lane 0 walks the path back and writes the levels (raster) to q and
-// the zigzag nz count to *nz.  (The DP alone on one lane took ~112 VALU
-// instructions per position; on the quad ~55.)
+// The trellis DP on a quad of lanes.  Lane r (0..2) of the quad owns one
+// transition role (level 0 / L0 / L0 + 1, see TRec): it adds its row of the
+// position record to the three predecessor states and takes the min; the
+// three minima are exchanged by DPP broadcasts and routed to the end
+// contexts (min(level, 2)) in every lane, so all lanes carry the same
+// states.  Lane 3 shadows lane 2.  Keys and order are those of the
+// sequential DP; the quad's lane 0 walks the path back and writes the
+// levels (raster) to q and the zigzag nz count to *nz.
 template <int FIRST, int CTX_TYPE>
-__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, int init_ctx, int lam16, int k, int16_t* q,
-                                            int* nz) {
+__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int* l0s, int init_ctx, int lam16,
+                                            int k, int16_t* q, int* nz) {
   constexpr int64_t BIG = 1ll << 59, VALID = 1ll << 58;
   init_ctx = min(init_ctx, 2);
-  const int kk = min(k, 2);
-  int64_t ps = kk == init_ctx ? 0 : BIG;
-  uint32_t path0 = 0, path1 = 0;  // 4 bits (key idx) per position: positions 0-7, 8-15
+  const int role = min(k, 2);
+  int64_t ps0 = init_ctx == 0 ? 0 : BIG, ps1 = init_ctx == 1 ? 0 : BIG, ps2 = init_ctx == 2 ? 0 : BIG;
+  uint32_t path[8];
   const TokRow& t_init = t.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
   int64_t best_terminal = (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16;
-  int best_n = -1;
-  TRec r = rec[FIRST];
+  int best = -1;  // n << 2 | end context
+  const int64_t* mine = &rec[0].x[role][0];
+  constexpr int STRIDE = sizeof(TRec) / sizeof(int64_t);
+  int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
+  int cls_next = l0s[FIRST] & 3;
 #pragma unroll
-  for (int n = FIRST; n < 16; n++) {
-    const TRec cur = r;
-    if (n < 15) r = rec[n + 1];
-    asm volatile("" : "+v"(ps), "+v"(best_terminal)::"memory");
-    const TokRow& tr = t.tok[CTX_TYPE * 8 + kBand[n + 1]];
-    const int64_t p0 = quad_bcast<0>(ps), p1 = quad_bcast<1>(ps), p2 = quad_bcast<2>(ps);
-    const int cls = cur.l0s & 3;
-    const bool isZ = kk == 0;
-    const bool useA = (kk == 1 && cls == 1) || (kk == 2 && cls == 2);
-    const bool useB = (kk == 1 && cls == 0) || (kk == 2 && cls >= 1);
-    // every lane evaluates every operand (selects, no divergent branches)
-    uint64_t zw = *reinterpret_cast<const uint64_t*>(tr.zero);
-    asm volatile("" : "+v"(zw));  // keep it per-lane: a uniform operand turns the selects below into branches
-    int64_t best = BIG * 2;
-#pragma unroll
-    for (int pc = 0; pc < 3; pc++) {
-      const int64_t base = pc == 0 ? p0 : (pc == 1 ? p1 : p2);
-      int64_t z = (int64_t)(int)((zw >> (16 * pc)) & 0xffff) * lam16 + pc;
-      asm volatile("" : "+v"(z));  // materialised before the select (else it is sunk into a branch)
-      const int64_t na = cur.na[pc], nb = cur.nb[pc];
-      const int64_t xa = isZ ? z : (useA ? na : BIG);
-      const int64_t xb = useB ? nb : BIG;
-      const int64_t ca = base + xa, cb = base + xb;
-      best = ca < best ? ca : best;
-      best = cb < best ? cb : best;
+  for (int n = 0; n < 16; n++) {
+    if (n < FIRST) {
+      if (!(n & 1)) path[n >> 1] = 0;
+      continue;
     }
-    const uint32_t idx = (uint32_t)best & 15;
-    if (n < 8)
-      path0 |= idx << (4 * n);
+    const int64_t c0 = ps0 + x0, c1 = ps1 + x1, c2 = ps2 + x2;
+    const int cls = cls_next;
+    if (n < 15) {  // one position ahead
+      x0 = mine[(n + 1) * STRIDE];
+      x1 = mine[(n + 1) * STRIDE + 1];
+      x2 = mine[(n + 1) * STRIDE + 2];
+      cls_next = l0s[n + 1] & 3;
+    }
+    asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
+    int64_t m = c1 < c0 ? c1 : c0;
+    m = c2 < m ? c2 : m;
+    const int64_t kz = quad_bcast<0>(m), ka = quad_bcast<1>(m), kb = quad_bcast<2>(m);
+    const int64_t kab = kb < ka ? kb : ka;
+    const int64_t k1 = cls == 0 ? kb : (cls == 1 ? ka : BIG);
+    const int64_t k2 = cls == 0 ? BIG : (cls == 1 ? kb : kab);
+    const uint32_t pr = ((uint32_t)kz & 15) | (((uint32_t)k1 & 15) << 4) | (((uint32_t)k2 & 15) << 8);
+    if (n & 1)
+      path[n >> 1] |= pr << 16;
     else
-      path1 |= idx << (4 * (n - 8));
-    ps = best & ~15ll;
+      path[n >> 1] = pr;
+    ps0 = kz & ~15ll;
+    ps1 = k1 & ~15ll;
+    ps2 = k2 & ~15ll;
     // terminal (EOB after this position) from end contexts 1 and 2
-    uint64_t ew = *reinterpret_cast<const uint64_t*>(tr.eob);
-    asm volatile("" : "+v"(ew));
-    int64_t ecost_k = n < 15 ? (int64_t)(int)((ew >> (16 * kk)) & 0xffff) * lam16 : 0;
-    asm volatile("" : "+v"(ecost_k));
-    const int64_t eob = ps + ecost_k;
-    const bool w = kk >= 1 && ps < VALID && eob < best_terminal;
-    best_terminal = w ? eob : best_terminal;
-    best_n = w ? n : best_n;
+    const TokRow& tr = t.tok[CTX_TYPE * 8 + kBand[n + 1]];
+    const int64_t eob1 = ps1 + (n < 15 ? (int64_t)tr.eob[1] * lam16 : 0);
+    const bool w1 = ps1 < VALID && eob1 < best_terminal;
+    best_terminal = w1 ? eob1 : best_terminal;
+    best = w1 ? (n << 2 | 1) : best;
+    const int64_t eob2 = ps2 + (n < 15 ? (int64_t)tr.eob[2] * lam16 : 0);
+    const bool w2 = ps2 < VALID && eob2 < best_terminal;
+    best_terminal = w2 ? eob2 : best_terminal;
+    best = w2 ? (n << 2 | 2) : best;
   }
-  // combine the terminals of contexts 1 and 2: lower score, then earlier
-  // position, then context 1 (the reference's scan order)
-  const int64_t bt1 = quad_bcast<1>(best_terminal), bt2 = quad_bcast<2>(best_terminal);
-  const int bn1 = quad_bcast32<1>(best_n), bn2 = quad_bcast32<2>(best_n);
-  const uint32_t pa0 = quad_bcast32<0>(path0), pb0 = quad_bcast32<0>(path1);
-  const uint32_t pa1 = quad_bcast32<1>(path0), pb1 = quad_bcast32<1>(path1);
-  const uint32_t pa2 = quad_bcast32<2>(path0), pb2 = quad_bcast32<2>(path1);
   if (k != 0) return;
-  int bn, bc;
-  if (bn1 < 0 && bn2 < 0) {
-    bn = -1;
-    bc = 0;
-  } else if (bn2 < 0 || (bn1 >= 0 && (bt1 < bt2 || (bt1 == bt2 && bn1 <= bn2)))) {
-    bn = bn1;
-    bc = 1;
-  } else {
-    bn = bn2;
-    bc = 2;
-  }
-  int ctx = bc, last = 0;
+  const int best_n = best >> 2;  // -1 when no terminal beat the all-zero block
+  int ctx = best & 3, last = 0;
   int16_t lv_out[16];
 #pragma unroll
   for (int n = 15; n >= 0; n--) {
@@ -372,19 +362,18 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, in
       lv_out[zig] = 0;
       continue;
     }
-    const bool act = n <= bn;
-    const uint32_t w = n < 8 ? (ctx == 0 ? pa0 : (ctx == 1 ? pa1 : pa2)) : (ctx == 0 ? pb0 : (ctx == 1 ? pb1 : pb2));
-    const int idx = (int)((w >> (4 * (n & 7))) & 15);
-    const int l0s = rec[n].l0s;
-    const int mag = ctx == 0 ? 0 : (l0s >> 3) + (idx & 1);
-    const int lv = act ? ((l0s & 4) ? -mag : mag) : 0;
+    const bool act = n <= best_n;
+    const int idx = (int)(((path[n >> 1] >> (16 * (n & 1))) >> (4 * ctx)) & 15);
+    const int ls = l0s[n];
+    const int mag = ctx == 0 ? 0 : (ls >> 3) + (idx & 1);
+    const int lv = act ? ((ls & 4) ? -mag : mag) : 0;
     lv_out[zig] = (int16_t)lv;
     last = (lv != 0 && last == 0) ? n + 1 : last;
     ctx = act ? (ctx == 0 ? idx : idx >> 1) : ctx;
   }
 #pragma unroll
   for (int i = 0; i < 16; i++) q[i] = lv_out[i];
-  *nz = bn < 0 ? 0 : last;
+  *nz = best < 0 ? 0 : last;
 }
 
 // TokenCostForCoeffs's term for position n alone (lane-parallel form of
@@ -987,7 +976,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
             const int c = hl >> 3, n0 = 2 * (hl & 7), sl = half * 3 + c;
 #pragma unroll
             for (int j = 0; j < 2; j++)
-              pnz |= trellis_prep<3>(t, s.co_buf[sl][zig_of(n0 + j)], n0 + j, sg.y1, lam16, s.trec[sl][n0 + j]);
+              pnz |= trellis_prep<3>(t, s.co_buf[sl][zig_of(n0 + j)], n0 + j, sg.y1, lam16, s.trec[sl][n0 + j], s.l0s[sl][n0 + j]);
           }
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
@@ -995,7 +984,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           if (bvalid && hl < 4 * K) {
             const int c = hl >> 2, sl = half * 3 + c;
             if ((pnz_mask >> (32 * half + 8 * c)) & 0xff) {
-              trellis_dp4<0, 3>(t, s.trec[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
+              trellis_dp4<0, 3>(t, s.trec[sl], s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
             } else if ((hl & 3) == 0) {
 #pragma unroll
               for (int i = 0; i < 16; i++) s.cand_q[sl][i] = 0;
@@ -1188,7 +1177,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
             const int j = lane >> 3, n0 = 2 * (lane & 7), pb = (by_lo + j) * 4 + d - (by_lo + j);
 #pragma unroll
             for (int k = 0; k < 2; k++)
-              if (n0 + k >= 1) pnz |= trellis_prep<0>(t, s.co_buf[pb][zig_of(n0 + k)], n0 + k, sg.y1, lam16, s.trec[j][n0 + k]);
+              if (n0 + k >= 1) pnz |= trellis_prep<0>(t, s.co_buf[pb][zig_of(n0 + k)], n0 + k, sg.y1, lam16, s.trec[j][n0 + k], s.l0s[j][n0 + k]);
           }
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
@@ -1198,7 +1187,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
             const int tp = qby > 0 ? (s.nzy[qb - 4] > 0) : (int)((top_nz >> qbx) & 1);
             int nzv = 0;
             if ((pnz_mask >> (8 * j)) & 0xff) {
-              trellis_dp4<1, 0>(t, s.trec[j], min(l + tp, 2), lam16, lane & 3, s.coeffs + qb * 16, &nzv);
+              trellis_dp4<1, 0>(t, s.trec[j], s.l0s[j], min(l + tp, 2), lam16, lane & 3, s.coeffs + qb * 16, &nzv);
             } else if ((lane & 3) == 0) {
 #pragma unroll
               for (int i = 0; i < 16; i++) s.coeffs[qb * 16 + i] = 0;
