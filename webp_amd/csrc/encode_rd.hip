@@ -283,6 +283,12 @@ __device__ __forceinline__ int64_t quad_bcast(int64_t v) {
   const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)v >> 32), perm, 0xf, 0xf, false);
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
+// sum over the 4 lanes of a quad, in every lane of it
+__device__ __forceinline__ int quad_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+  return v;
+}
 template <int J>
 __device__ __forceinline__ int quad_bcast32(int v) {
   return __builtin_amdgcn_mov_dpp(v, J | J << 2 | J << 4 | J << 6, 0xf, 0xf, false);
@@ -956,13 +962,10 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           const int slot = half * 3 + min(hl, 2);  // candidate slot in the trellis / level buffers
           SSTAMP(1);
           // candidates: prediction + transform (lane hl = candidate hl)
-          uint32_t predp[4] = {0, 0, 0, 0};
           if (cand) {
             CSTAMP(-1);
             int pred[16], co[16];
             pred4_lut(t.pcode[mode], s.pv[half], pred);
-#pragma unroll
-            for (int r = 0; r < 4; r++) predp[r] = pack4(pred[4 * r], pred[4 * r + 1], pred[4 * r + 2], pred[4 * r + 3]);
             fdct(src, pred, co);
 #pragma unroll
             for (int i = 0; i < 16; i++) s.co_buf[slot][i] = co[i];
@@ -992,28 +995,77 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
             }
           }
           lds_sync();
-          // candidates: reconstruction, distortion
-          int16_t q[16];
-          int nz = 0, disto = 0, cnt = 0;
-          uint32_t recp[4] = {0, 0, 0, 0};
-          if (cand) {
+          // candidates: reconstruction + distortion on the candidate's lane quad
+          // (lane 4c + r owns row r; the TDisto column pass reads the row pass
+          // results back from LDS; sums are quad reductions)
+          const bool qact = bvalid && hl < 4 * K;
+          const int qc = min(hl >> 2, 2), qr = hl & 3, qsl = half * 3 + qc;
+          const int qmode = pick3(qc, cm[0], cm[1], cm[2]);
+          int16_t qv[16];
+          int qnz = 0, sse_r = 0, cnt = 0;
+          uint32_t rec_row = 0;
+          if (qact) {
             CSTAMP(1);
 #pragma unroll
-            for (int i = 0; i < 16; i++) q[i] = s.cand_q[slot][i];
-            nz = s.cand_nz[slot];
-            int pred[16], dq[16], rec[16];
+            for (int i = 0; i < 16; i++) qv[i] = s.cand_q[qsl][i];
+            qnz = s.cand_nz[qsl];
+            int dq[16], res[4], pr[4], sr[4], rr[4];
+            dequant(qv, dq, sg.y1);
+            idct_row(dq, qr, res);
+            const uint32_t cw = reinterpret_cast<const uint32_t*>(t.pcode[qmode])[qr];
 #pragma unroll
-            for (int r = 0; r < 4; r++) unpack_rows(predp[r], pred + 4 * r);
-            dequant(q, dq, sg.y1);
-            recon4(pred, dq, rec);
+            for (int k = 0; k < 4; k++) {
+              pr[k] = s.pv[half][(cw >> (8 * k)) & 0xff];
+              sr[k] = s.yin[off + qr * BPS + k];
+              rr[k] = clip8(pr[k] + res[k]);
+              sse_r += (sr[k] - rr[k]) * (sr[k] - rr[k]);
+            }
+            rec_row = pack4(rr[0], rr[1], rr[2], rr[3]);
+            // tTransform row pass (ssim.go:266-304) of the reconstruction and the source
+            int* th = &s.co_buf[2 * qsl][0] + 8 * qr;  // co_buf is free again after the trellis prep
+            {
+              const int a0 = rr[0] + rr[2], a1 = rr[1] + rr[3], a2 = rr[1] - rr[3], a3 = rr[0] - rr[2];
+              th[0] = a0 + a1;
+              th[1] = a3 + a2;
+              th[2] = a3 - a2;
+              th[3] = a0 - a1;
+            }
+            {
+              const int a0 = sr[0] + sr[2], a1 = sr[1] + sr[3], a2 = sr[1] - sr[3], a3 = sr[0] - sr[2];
+              th[4] = a0 + a1;
+              th[5] = a3 + a2;
+              th[6] = a3 - a2;
+              th[7] = a0 - a1;
+            }
 #pragma unroll
-            for (int r = 0; r < 4; r++) recp[r] = pack4(rec[4 * r], rec[4 * r + 1], rec[4 * r + 2], rec[4 * r + 3]);
-            disto = sse16(src, rec);
-            if (sg.tlambda_sd > 0) disto += (sg.tlambda_sd * tdisto(src, rec) + 128) >> 8;
-#pragma unroll
-            for (int i = 1; i < 16; i++) cnt += q[i] != 0;
-            CSTAMP(2);
+            for (int i = 1; i < 16; i++) cnt += qv[i] != 0;
           }
+          lds_sync();
+          int wrec = 0, wsrc = 0;  // weighted column sums of column qr
+          if (qact) {
+            const int* tx = &s.co_buf[2 * qsl][0];
+            int cr[4], cs[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              cr[j] = tx[8 * j + qr];
+              cs[j] = tx[8 * j + 4 + qr];
+            }
+            // kWeightY (ssim.go:257) column qr, one byte per row
+            const uint32_t wcol = qr == 0 ? 0x09142026u : (qr == 1 ? 0x07111c20u : (qr == 2 ? 0x040a1114u : 0x02040709u));
+            const int w0 = wcol & 0xff, w1 = (wcol >> 8) & 0xff, w2 = (wcol >> 16) & 0xff, w3 = wcol >> 24;
+            {
+              const int a0 = cr[0] + cr[2], a1 = cr[1] + cr[3], a2 = cr[1] - cr[3], a3 = cr[0] - cr[2];
+              wrec = w0 * abs(a0 + a1) + w1 * abs(a3 + a2) + w2 * abs(a3 - a2) + w3 * abs(a0 - a1);
+            }
+            {
+              const int a0 = cs[0] + cs[2], a1 = cs[1] + cs[3], a2 = cs[1] - cs[3], a3 = cs[0] - cs[2];
+              wsrc = w0 * abs(a0 + a1) + w1 * abs(a3 + a2) + w2 * abs(a3 - a2) + w3 * abs(a0 - a1);
+            }
+          }
+          const int sse_q = quad_sum(sse_r), wrec_q = quad_sum(wrec), wsrc_q = quad_sum(wsrc);
+          int disto = sse_q;
+          if (sg.tlambda_sd > 0) disto += (sg.tlambda_sd * (abs(wrec_q - wsrc_q) >> 5) + 128) >> 8;
+          CSTAMP(2);
           // token cost, lane-parallel over positions, summed over each candidate's 8 lanes
           int part = 0;
           if (bvalid && hl < 8 * K) {
@@ -1024,13 +1076,13 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           part += __shfl_xor(part, 1, 64);
           part += __shfl_xor(part, 2, 64);
           part += __shfl_xor(part, 4, 64);
-          const int tok_rate = __shfl(part, 32 * half + 8 * min(hl, 2), 64);
+          const int tok_rate = __shfl(part, 32 * half + 8 * qc, 64);
           uint64_t score = ~0ull;
           int rate = 0;
-          if (cand) {
-            rate = (mode > 0 && cnt <= 3) ? 140 : 0;
+          if (qact) {
+            rate = (qmode > 0 && cnt <= 3) ? 140 : 0;
             rate += tok_rate;
-            rate += t.fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
+            rate += t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];
             score = rd_score(disto, rate, sg.lambda_i4);
             CSTAMP(3);
           }
@@ -1040,22 +1092,23 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           uint64_t wsc = __shfl(score, half * 32, 64);
 #pragma unroll
           for (int i = 1; i < 3; i++) {
-            const uint64_t sc = __shfl(score, half * 32 + i, 64);
+            const uint64_t sc = __shfl(score, half * 32 + 4 * i, 64);
             if (i < K && sc < wsc) {
               wsc = sc;
               win = i;
             }
           }
-          if (bvalid && hl == win) {
+          if (qact && qc == win) {  // the winning quad: row qr of the reconstruction, 4 levels each
+            *reinterpret_cast<uint32_t*>(s.yout2 + off + qr * BPS) = rec_row;
 #pragma unroll
-            for (int i = 0; i < 16; i++) s.coeffs[blk * 16 + i] = q[i];
-#pragma unroll
-            for (int r = 0; r < 4; r++) *reinterpret_cast<uint32_t*>(s.yout2 + off + r * BPS) = recp[r];
-            s.modes4[blk] = (uint8_t)mode;
-            s.nzy[blk] = (uint8_t)nz;
-            s.blk_rate[blk] = rate;
-            s.blk_disto[blk] = disto;
-            s.blk_hdr[blk] = t.fixed_i4[(top_mode * 10 + left_mode) * 10 + mode];
+            for (int k = 0; k < 4; k++) s.coeffs[blk * 16 + 4 * qr + k] = qv[4 * qr + k];
+            if (qr == 0) {
+              s.modes4[blk] = (uint8_t)qmode;
+              s.nzy[blk] = (uint8_t)qnz;
+              s.blk_rate[blk] = rate;
+              s.blk_disto[blk] = disto;
+              s.blk_hdr[blk] = t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];
+            }
           }
           lds_sync();
           {
