@@ -66,6 +66,9 @@ static_assert(sizeof(MbEnc) == 864, "MbEnc layout");
 // every co[zig] / q[zig] index is a constant (no scratch-memory arrays)
 constexpr int kZig[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
 constexpr int kBand[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
+// raster index -> zigzag position (kRZig[kZig[n]] == n); immediates, not
+// constant-memory loads (those landed in SGPRs and spilled)
+constexpr int kRZig[16] = {0, 1, 5, 6, 2, 4, 7, 12, 3, 8, 11, 13, 9, 10, 14, 15};
 
 constexpr uint64_t pack_zig() {
   uint64_t v = 0;
@@ -96,7 +99,6 @@ static_assert(sizeof(TRec) == 72, "TRec layout");
 
 __constant__ uint16_t c_level_codes[134];
 __constant__ uint16_t c_fixed_i4[1000];
-__constant__ uint8_t c_zigzag[16], c_bands[17], c_rzig[16];
 __constant__ int32_t c_wtrellis[16];
 
 // ------------------------------------------------------------------ LDS state
@@ -190,7 +192,7 @@ __device__ __forceinline__ int quantize(const int co[16], int16_t q[16], const S
     const uint32_t bias = n == 0 ? (uint32_t)sq.dc_bias : (uint32_t)sq.bias;
     const int c = min((int)(((uint32_t)v * iq + bias) >> 17), 2047);
     q[n] = (int16_t)(sign * c);
-    if (c != 0) max_zz = max(max_zz, (int)c_rzig[n]);
+    if (c != 0) max_zz = max(max_zz, kRZig[n]);
   }
   return max_zz + 1;
 }
@@ -816,7 +818,11 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
         // isFlatSource16 (encode_analysis.go:358)
         const uint8_t v0 = s.yin[YOFF];
         bool mine = true;
-        for (int i = lane; i < 256; i += 64) mine &= s.yin[YOFF + (i >> 4) * BPS + (i & 15)] == v0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {  // fixed trip count (lane is opaque to the compiler)
+          const int i = lane + 64 * k;
+          mine &= s.yin[YOFF + (i >> 4) * BPS + (i & 15)] == v0;
+        }
         src_flat = __all(mine);
       }
       const int m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
@@ -908,8 +914,11 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
       // applied afterwards from the per-block results: a block reads only
       // reconstructions of raster-earlier blocks, so every block evaluated
       // before the exit point sees exactly the reference's inputs.
-      for (int i = lane; i < YUV / 4; i += 64)
-        reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
+#pragma unroll
+      for (int k = 0; k < (YUV / 4 + 63) / 64; k++) {
+        const int i = lane + 64 * k;
+        if (i < YUV / 4) reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
+      }
       lds_sync();
       uint64_t s4;
       {
@@ -1329,7 +1338,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
       {
         uint4* dst = reinterpret_cast<uint4*>(o->coeffs);
         const uint4* srcv = reinterpret_cast<const uint4*>(s.coeffs);
-        for (int i = lane; i < 50; i += 64) dst[i] = srcv[i];
+        if (lane < 50) dst[lane] = srcv[lane];
         if (lane < 16) {
           o->modes[lane] = is_i4 ? s.modes4[lane] : 0;
           o->nz_y[lane] = s.nzy[lane];
@@ -1492,9 +1501,6 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
       }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_fixed_i4), fixed, sizeof(fixed)) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(c_level_codes), vp8_level_codes, sizeof(vp8_level_codes)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_zigzag), vp8_zigzag, sizeof(vp8_zigzag)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_bands), vp8_bands, sizeof(vp8_bands)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_rzig), vp8_reverse_zigzag, sizeof(vp8_reverse_zigzag)) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(c_wtrellis), vp8_weight_trellis, sizeof(vp8_weight_trellis)) != hipSuccess)
       return wg::check_launch("encode tables");
     g_tables_ready_dev = dev;
