@@ -483,12 +483,6 @@ __device__ __forceinline__ void fdct(const int src[16], const int pred[16], int 
 #pragma unroll
   for (int i = 0; i < 16; i++) co[i] = o[i];
 }
-__device__ __forceinline__ void load4x4(const uint8_t* p, int v[16]) {
-#pragma unroll
-  for (int r = 0; r < 4; r++)
-#pragma unroll
-    for (int c = 0; c < 4; c++) v[4 * r + c] = p[r * BPS + c];
-}
 __device__ __forceinline__ void store4x4(uint8_t* p, const int v[16]) {
 #pragma unroll
   for (int r = 0; r < 4; r++)
@@ -497,6 +491,10 @@ __device__ __forceinline__ void store4x4(uint8_t* p, const int v[16]) {
 __device__ __forceinline__ void unpack_rows(uint32_t w, int* d) {
 #pragma unroll
   for (int c = 0; c < 4; c++) d[c] = byte_of(w, c);
+}
+__device__ __forceinline__ void load4x4(const uint8_t* p, int v[16]) {  // p 4-byte aligned (all block origins are)
+#pragma unroll
+  for (int r = 0; r < 4; r++) unpack_rows(*reinterpret_cast<const uint32_t*>(p + r * BPS), v + 4 * r);
 }
 // 16x16 / 8x8 square prediction of the 4x4 block at (px, py) of `base`
 __device__ __forceinline__ void predsq_block(int mode, const uint8_t* base, int size, int px, int py, int pred[16]) {
