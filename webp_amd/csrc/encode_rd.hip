@@ -208,6 +208,18 @@ __device__ __forceinline__ int variable_level_cost(const Tables& t, int level, c
   return cost;
 }
 
+// One row of token costs for context ctx, read as two wide LDS loads:
+// returns the zero-token cost (v == 0) or the non-zero prefix, and the EOB
+// cost in *eob.
+__device__ __forceinline__ int tok_costs(const TokRow& tr, int ctx, bool zero, int* eob) {
+  const uint4 zn = *reinterpret_cast<const uint4*>(tr.zero);  // zero[0..3], nz[0..3]
+  const uint2 ew = *reinterpret_cast<const uint2*>(tr.eob);
+  const int sh = 16 * ctx;
+  const uint64_t zw = (uint64_t)zn.y << 32 | zn.x, nw = (uint64_t)zn.w << 32 | zn.z, e64 = (uint64_t)ew.y << 32 | ew.x;
+  *eob = (int)((e64 >> sh) & 0xffff);
+  return (int)(((zero ? zw : nw) >> sh) & 0xffff);
+}
+
 // TokenCostForCoeffs (encode_quant.go:154-223), branch-free: the context of
 // every position follows from the levels alone (min(|q|, 2) of the previous
 // one), so all table reads are independent and issue back to back.
@@ -220,9 +232,9 @@ __device__ __forceinline__ int token_cost(const Tables& t, const int16_t q[16], 
     const TokRow& tr = t.tok[type * 8 + kBand[n]];
     const int v = abs((int)q[kZig[n]]);
     const uint64_t vw = t.vcost[type * 8 + kBand[n]][min(v, 67)];
-    const int tokc = v == 0 ? pick3(ctx, tr.zero[0], tr.zero[1], tr.zero[2])
-                            : pick3(ctx, tr.nz[0], tr.nz[1], tr.nz[2]) + t.lfixed[min(v, 2047)] + vc_of(vw, ctx);
-    const int eob = pick3(ctx, tr.eob[0], tr.eob[1], tr.eob[2]);
+    int eob;
+    const int base = tok_costs(tr, ctx, v == 0, &eob);
+    const int tokc = v == 0 ? base : base + t.lfixed[min(v, 2047)] + vc_of(vw, ctx);
     cost += n < nz_count ? tokc : (n == eob_at ? eob : 0);
     ctx = min(v, 2);
   }
@@ -394,9 +406,10 @@ __device__ __forceinline__ int token_cost_pos(const Tables& t, const int16_t* q,
   const int v = abs((int)q[zig_of(n)]);
   const int ctx = n == first ? ctx0 : min(abs((int)q[zig_of(max(n - 1, 0))]), 2);
   const uint64_t vw = t.vcost[TYPE * 8 + band][min(v, 67)];
-  const int tokc = v == 0 ? pick3(ctx, tr.zero[0], tr.zero[1], tr.zero[2])
-                          : pick3(ctx, tr.nz[0], tr.nz[1], tr.nz[2]) + t.lfixed[min(v, 2047)] + vc_of(vw, ctx);
-  return n < nz_count ? tokc : (n == max(nz_count, first) ? pick3(ctx, tr.eob[0], tr.eob[1], tr.eob[2]) : 0);
+  int eob;
+  const int base = tok_costs(tr, ctx, v == 0, &eob);
+  const int tokc = v == 0 ? base : base + t.lfixed[min(v, 2047)] + vc_of(vw, ctx);
+  return n < nz_count ? tokc : (n == max(nz_count, first) ? eob : 0);
 }
 
 // min over the 16 lanes of a DPP row, result in every lane of the row
