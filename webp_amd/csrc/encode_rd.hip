@@ -178,6 +178,11 @@ __device__ __forceinline__ int vc_of(uint64_t w, int c) { return (int)((w >> (16
 // QuantizeCoeffs (encode_quant.go:16-80): returns the zigzag nz count
 __device__ __forceinline__ int quantize(const int co[16], int16_t q[16], const SQuant& sq, int first) {
   int max_zz = -1;
+  // the quantiser as four 16-byte LDS reads (SQuant is 64 B, 16-B aligned)
+  const uint4 h0 = *reinterpret_cast<const uint4*>(&sq.quant);     // quant iquant bias zthresh
+  const uint4 h1 = *reinterpret_cast<const uint4*>(&sq.dc_quant);  // the DC ones
+  const uint4 s0 = *reinterpret_cast<const uint4*>(&sq.sharpen[0]), s1 = *reinterpret_cast<const uint4*>(&sq.sharpen[8]);
+  const uint32_t sw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
   for (int n = 0; n < 16; n++) {
     if (n < first) {
@@ -186,10 +191,10 @@ __device__ __forceinline__ int quantize(const int co[16], int16_t q[16], const S
     }
     int v = co[n];
     const int sign = v < 0 ? -1 : 1;
-    v = abs(v) + sq.sharpen[n];
+    v = abs(v) + (int)(int16_t)(sw[n >> 1] >> (16 * (n & 1)));
     v = max(v, 0);
-    const uint32_t iq = n == 0 ? (uint32_t)sq.dc_iquant : (uint32_t)sq.iquant;
-    const uint32_t bias = n == 0 ? (uint32_t)sq.dc_bias : (uint32_t)sq.bias;
+    const uint32_t iq = n == 0 ? h1.y : h0.y;
+    const uint32_t bias = n == 0 ? h1.z : h0.z;
     const int c = min((int)(((uint32_t)v * iq + bias) >> 17), 2047);
     q[n] = (int16_t)(sign * c);
     if (c != 0) max_zz = max(max_zz, kRZig[n]);
@@ -446,9 +451,10 @@ __device__ __forceinline__ void select_i4_modes(int sse, int m, uint32_t eligibl
 
 // residual + reconstruction of one 4x4 block: rec = clip(pred + IDCT(dq))
 __device__ __forceinline__ void dequant(const int16_t q[16], int dq[16], const SQuant& sq) {
-  dq[0] = (int16_t)(q[0] * sq.dc_quant);
+  const int2 qq = make_int2(sq.quant, sq.dc_quant);
+  dq[0] = (int16_t)(q[0] * qq.y);
 #pragma unroll
-  for (int i = 1; i < 16; i++) dq[i] = (int16_t)(q[i] * sq.quant);
+  for (int i = 1; i < 16; i++) dq[i] = (int16_t)(q[i] * qq.x);
 }
 __device__ __forceinline__ void recon4(const int pred[16], const int dq[16], int rec[16]) {
 #pragma unroll
