@@ -252,6 +252,24 @@ int wg_vp8l_green(uint32_t* argb, int64_t n, int32_t add, void* stream);
 /* The fastSLog2 table (encode_histogram.go:359-368) the selection uses, host copy. */
 int wg_vp8l_slog2_lut_host(double* out, int32_t n);
 
+/* ColorSpaceTransform (internal/lossless/encode_predictor.go:727-770): per
+ * 2^bits tile the green->red, green->blue and red->blue multipliers
+ * (findBestMultipliers :514-585), written as g2r | g2b << 8 | r2b << 16
+ * (packMultipliers :489) to data[n_images][tiles_y*tiles_x], and the forward
+ * transform applied to argb IN PLACE.  bits in [2, 9]. */
+int wg_vp8l_color_space_transform(uint32_t* argb, int32_t width, int32_t height, int64_t image_pitch, int32_t bits,
+                                  int32_t n_images, uint32_t* data, void* stream);
+/* colorSpaceInverseTransform (internal/lossless/decode_transform.go:454-520). */
+int wg_vp8l_color_space_inverse(const uint32_t* data, int32_t bits, int32_t width, int32_t height, int64_t image_pitch,
+                                int32_t n_images, const uint32_t* src, uint32_t* dst, void* stream);
+/* colorIndexInverseTransform (internal/lossless/decode_transform.go:560-612):
+ * src rows hold (width + 2^xbits - 1) >> xbits packed index words (index in
+ * the green byte, 8 >> xbits bits per pixel), palette (<= 256 entries, shared
+ * by the n images); indices past the palette leave dst untouched. */
+int wg_vp8l_color_index_inverse(const uint32_t* palette, int32_t palette_size, int32_t xbits, int32_t width,
+                                int32_t height, int32_t n_images, const uint32_t* src, int64_t src_pitch, uint32_t* dst,
+                                int64_t dst_pitch, void* stream);
+
 /* ===================================================================== *
  * 4. SharpYUV: sharpyuv.Convert with SharpEnabled and the
  *    sRGB transfer (sharpyuv/sharpyuv.go:39-64, convertSharp :170-269).

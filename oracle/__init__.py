@@ -104,6 +104,9 @@ _SIGS = {
     "or_vp8l_inverse_predictor": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
     "or_vp8l_subtract_green": (None, [ctypes.c_void_p, ctypes.c_size_t]),
     "or_vp8l_add_green": (None, [ctypes.c_void_p, ctypes.c_size_t]),
+    "or_vp8l_color_space_transform": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p]),
+    "or_vp8l_color_space_inverse": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
+    "or_vp8l_color_index_inverse": (None, [ctypes.c_void_p, _i, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
     "or_sharpyuv_tables": (None, [ctypes.c_void_p, ctypes.c_void_p]),
     "or_setup_segment": (None, [_i] * 8 + [ctypes.c_void_p]),
     "or_fixed_costs_i4": (None, [ctypes.c_void_p]),
@@ -242,6 +245,34 @@ def vp8l_subtract_green(argb):
     a = np.ascontiguousarray(argb, np.uint32).copy()
     lib.or_vp8l_subtract_green(a.ctypes.data, a.size)
     return a
+
+
+def vp8l_color_space_transform(argb, bits):
+    """ColorSpaceTransform: (h, w) uint32 -> (multiplier words (tiles_y, tiles_x), transformed argb)."""
+    a = np.ascontiguousarray(argb, np.uint32).copy()
+    h, w = a.shape
+    data = np.zeros((vp8l_subsample(h, bits), vp8l_subsample(w, bits)), np.uint32)
+    lib.or_vp8l_color_space_transform(a.ctypes.data, w, h, bits, data.ctypes.data)
+    return data, a
+
+
+def vp8l_color_space_inverse(data, bits, src):
+    src = np.ascontiguousarray(src, np.uint32)
+    h, w = src.shape
+    data = np.ascontiguousarray(data, np.uint32)
+    out = np.empty_like(src)
+    lib.or_vp8l_color_space_inverse(data.ctypes.data, bits, w, h, src.ctypes.data, out.ctypes.data)
+    return out
+
+
+def vp8l_color_index_inverse(palette, xbits, width, src, fill=0):
+    """colorIndexInverseTransform: src (h, subsample(width, xbits)) packed index words -> (h, width)."""
+    src = np.ascontiguousarray(src, np.uint32)
+    pal = np.ascontiguousarray(palette, np.uint32)
+    h = src.shape[0]
+    out = np.full((h, width), fill, np.uint32)
+    lib.or_vp8l_color_index_inverse(pal.ctypes.data, len(pal), xbits, width, h, src.ctypes.data, out.ctypes.data)
+    return out
 
 
 # ---------------- SharpYUV ----------------

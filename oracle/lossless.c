@@ -278,3 +278,126 @@ void or_vp8l_add_green(uint32_t* argb, size_t n) {
     argb[i] = (p & 0xff00ff00u) | ((((p >> 16) & 0xff) + g) & 0xff) << 16 | (((p & 0xff) + g) & 0xff);
   }
 }
+
+/* ---------------------------------------------------------------------------
+ * Cross-colour transform.
+ * ColorSpaceTransform   internal/lossless/encode_predictor.go:727-770
+ * findBestMultipliers   :514-585,  findBestMultiplier :590-619,
+ * multiplierCost        :645-718 (the threshold early exit returns a partial
+ *                       sum above the running best, which never changes the
+ *                       argmin, so the full sum is used here),
+ * applyColorTransformPixel :497-507, encColorTransformDelta :478-480,
+ * packMultipliers       :489-493 (no alpha byte).
+ * ------------------------------------------------------------------------- */
+static uint8_t cc_delta(int m, uint8_t c) { return (uint8_t)((m * (int)(int8_t)c) >> 5); }
+
+static int64_t cc_cost(int m, const uint8_t* src, const uint8_t* dst, int n) {
+  int64_t total = 0;
+  for (int i = 0; i < n; i++) {
+    uint8_t r = (uint8_t)(dst[i] - cc_delta(m, src[i]));
+    if (r > 128) r = (uint8_t)(-r);
+    total += r;
+  }
+  return total;
+}
+
+static int cc_best_multiplier(const uint8_t* src, const uint8_t* dst, int n) {
+  int best_m = 0;
+  int64_t best = INT64_MAX;
+  for (int m = -128; m <= 127; m += 8) {
+    const int64_t c = cc_cost(m, src, dst, n);
+    if (c < best) {
+      best = c;
+      best_m = m;
+    }
+  }
+  const int coarse = best_m;
+  for (int m = coarse - 7; m <= coarse + 7; m++) {
+    if (m < -128 || m > 127) continue;
+    const int64_t c = cc_cost(m, src, dst, n);
+    if (c < best) {
+      best = c;
+      best_m = m;
+    }
+  }
+  return best_m;
+}
+
+void or_vp8l_color_space_transform(uint32_t* argb, int width, int height, int bits, uint32_t* data) {
+  const int tw = subsample(width, bits), th = subsample(height, bits), ts = 1 << bits;
+  uint8_t* buf = (uint8_t*)malloc((size_t)5 * ts * ts);
+  uint8_t *g = buf, *r = buf + ts * ts, *b = buf + 2 * ts * ts, *ar = buf + 3 * ts * ts, *ab = buf + 4 * ts * ts;
+  for (int ty = 0; ty < th; ty++)
+    for (int tx = 0; tx < tw; tx++) {
+      const int x0 = tx * ts, y0 = ty * ts;
+      const int x1 = x0 + ts < width ? x0 + ts : width, y1 = y0 + ts < height ? y0 + ts : height;
+      int n = 0;
+      for (int y = y0; y < y1; y++)
+        for (int x = x0; x < x1; x++) {
+          const uint32_t px = argb[(size_t)y * width + x];
+          g[n] = (uint8_t)(px >> 8);
+          r[n] = (uint8_t)(px >> 16);
+          b[n] = (uint8_t)px;
+          n++;
+        }
+      int g2r = 0, g2b = 0, r2b = 0;
+      if (n > 0) {
+        g2r = cc_best_multiplier(g, r, n);
+        for (int i = 0; i < n; i++) ar[i] = (uint8_t)(r[i] - cc_delta(g2r, g[i]));
+        g2b = cc_best_multiplier(g, b, n);
+        for (int i = 0; i < n; i++) ab[i] = (uint8_t)(b[i] - cc_delta(g2b, g[i]));
+        r2b = cc_best_multiplier(ar, ab, n);
+      }
+      data[ty * tw + tx] = (uint32_t)(uint8_t)g2r | (uint32_t)(uint8_t)g2b << 8 | (uint32_t)(uint8_t)r2b << 16;
+      for (int y = y0; y < y1; y++)
+        for (int x = x0; x < x1; x++) {
+          const uint32_t px = argb[(size_t)y * width + x];
+          const uint8_t gr = (uint8_t)(px >> 8), rd = (uint8_t)(px >> 16), bl = (uint8_t)px;
+          const int nr = (rd - (int)(int8_t)cc_delta(g2r, gr)) & 0xff;
+          int nb = (bl - (int)(int8_t)cc_delta(g2b, gr)) & 0xff;
+          nb = (nb - (int)(int8_t)cc_delta(r2b, rd)) & 0xff;
+          argb[(size_t)y * width + x] = (px & 0xff00ff00u) | ((uint32_t)nr << 16) | (uint32_t)nb;
+        }
+    }
+  free(buf);
+}
+
+/* colorSpaceInverseTransform (internal/lossless/decode_transform.go:454-520) */
+void or_vp8l_color_space_inverse(const uint32_t* data, int bits, int width, int height, const uint32_t* src,
+                                 uint32_t* dst) {
+  const int tw = subsample(width, bits);
+  for (int y = 0; y < height; y++)
+    for (int x = 0; x < width; x++) {
+      const uint32_t code = data[(y >> bits) * tw + (x >> bits)];
+      const int g2r = (int8_t)code, g2b = (int8_t)(code >> 8), r2b = (int8_t)(code >> 16);
+      const uint32_t px = src[(size_t)y * width + x];
+      const int green = (int8_t)(px >> 8);
+      int red = (px >> 16) & 0xff, blue = px & 0xff;
+      red += (g2r * green) >> 5;
+      red &= 0xff;
+      blue += (g2b * green) >> 5;
+      blue += (r2b * (int)(int8_t)red) >> 5;
+      blue &= 0xff;
+      dst[(size_t)y * width + x] = (px & 0xff00ff00u) | ((uint32_t)red << 16) | (uint32_t)blue;
+    }
+}
+
+/* colorIndexInverseTransform (internal/lossless/decode_transform.go:560-612):
+ * xbits = the transform's Bits (0..3: 8 >> xbits bits per index); src rows
+ * hold subsample(width, xbits) packed words; out-of-palette indices leave
+ * dst untouched. */
+void or_vp8l_color_index_inverse(const uint32_t* palette, int palette_size, int xbits, int width, int height,
+                                 const uint32_t* src, uint32_t* dst) {
+  const int bpp = 8 >> xbits, ppb = 1 << xbits, packed_w = subsample(width, xbits);
+  const uint32_t mask = (1u << bpp) - 1;
+  for (int y = 0; y < height; y++) {
+    const uint32_t* s = src + (size_t)y * packed_w;
+    uint32_t packed = 0;
+    for (int x = 0; x < width; x++) {
+      if ((x & (ppb - 1)) == 0) packed = (s[x >> xbits] >> 8) & 0xff;
+      const uint32_t idx = bpp < 8 ? (packed & mask) : packed;
+      if ((int)idx < palette_size) dst[(size_t)y * width + x] = palette[idx];
+      if (bpp < 8) packed >>= bpp;
+    }
+  }
+}

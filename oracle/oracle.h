@@ -156,6 +156,11 @@ void or_vp8l_inverse_predictor(const uint32_t* modes, int bits, int width, int h
                                uint32_t* out);
 void or_vp8l_subtract_green(uint32_t* argb, size_t n);
 void or_vp8l_add_green(uint32_t* argb, size_t n);
+void or_vp8l_color_space_transform(uint32_t* argb, int width, int height, int bits, uint32_t* data);
+void or_vp8l_color_space_inverse(const uint32_t* data, int bits, int width, int height, const uint32_t* src,
+                                 uint32_t* dst);
+void or_vp8l_color_index_inverse(const uint32_t* palette, int palette_size, int xbits, int width, int height,
+                                 const uint32_t* src, uint32_t* dst);
 
 /* ---- Encoder MB RD loop (lossy_rd.c; encode_parallel.go Phase A) ---- */
 typedef struct {          /* SegmentQuant (encode.go:311-323) */

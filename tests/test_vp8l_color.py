@@ -1,0 +1,149 @@
+"""VP8L cross-colour transform and colour inverse transforms.
+
+CPU: the C restatement (oracle/lossless.c) -- round trips (the inverse is the
+normative decoder step, decode_transform.go:454-520), the multiplier search's
+scan order on crafted tiles, and the colour-index unpacking for every xbits.
+Parity status: the multiplier choice is the reference's own heuristic (no
+third-party library shares it), so it is pinned by restatement + these
+properties.
+GPU (-m gpu): wg_vp8l_color_space_transform / _inverse / wg_vp8l_color_index_inverse
+== oracle, bit-exact, on odd sizes, all tile sizes staged in LDS and not, and batches."""
+import numpy as np
+import pytest
+
+import oracle as O
+from tools import synth
+
+
+def argb_of(rgba):
+    rgba = np.asarray(rgba, np.uint32)
+    return (rgba[..., 3] << 24) | (rgba[..., 0] << 16) | (rgba[..., 1] << 8) | rgba[..., 2]
+
+
+def images():
+    rng = np.random.default_rng(2)
+    yield "noise", rng.integers(0, 2 ** 32, (37, 53), dtype=np.uint64).astype(np.uint32)
+    yield "grad", argb_of(synth.gradient_rgba(70, 45))
+    yield "blobs", argb_of(synth.blobs_rgba(64, 64, seed=2, alpha=True))
+    yield "flat", np.full((20, 33), 0xff336699, np.uint32)
+    yield "1x1", np.array([[0x12345678]], np.uint32)
+    # green-correlated red / blue: the search must find non-zero multipliers
+    g = rng.integers(0, 256, (48, 40)).astype(np.int64)
+    r = (g * 3 // 2 + rng.integers(-3, 4, g.shape)) & 0xff
+    b = (255 - g + rng.integers(-2, 3, g.shape)) & 0xff
+    yield "correlated", ((0xff << 24) | (r << 16) | (g << 8) | b).astype(np.uint32)
+
+
+@pytest.mark.parametrize("bits", [2, 3, 5])
+def test_round_trip(bits):
+    for name, a in images():
+        data, t = O.vp8l_color_space_transform(a, bits)
+        assert data.shape == (O.vp8l_subsample(a.shape[0], bits), O.vp8l_subsample(a.shape[1], bits))
+        assert ((data >> 24) == 0).all(), name  # packMultipliers has no alpha byte
+        assert (O.vp8l_color_space_inverse(data, bits, t) == a).all(), name
+        assert ((t & 0xff00ff00) == (a & 0xff00ff00)).all(), name  # alpha and green untouched
+
+
+def test_correlated_tiles_pick_nonzero_multipliers():
+    a = dict(images())["correlated"]
+    data, _ = O.vp8l_color_space_transform(a, 3)
+    g2r = (data & 0xff).astype(np.int8)
+    assert (g2r != 0).mean() > 0.9
+
+
+def _cost(m, src, dst):
+    d = ((m * src.astype(np.int8).astype(np.int64)) >> 5) & 0xff
+    r = (dst.astype(np.int64) - d) & 0xff
+    return np.where(r > 128, 256 - r, r).sum()
+
+
+def test_search_matches_scan_order():
+    """findBestMultiplier (:590-619) by brute force in the same order."""
+    rng = np.random.default_rng(9)
+    for _ in range(20):
+        g = rng.integers(0, 256, 16).astype(np.uint8)
+        r = rng.integers(0, 256, 16).astype(np.uint8)
+        best, bm = None, 0
+        for m in range(-128, 128, 8):
+            c = _cost(m, g, r)
+            if best is None or c < best:
+                best, bm = c, m
+        coarse = bm
+        for m in range(coarse - 7, coarse + 8):
+            if -128 <= m <= 127:
+                c = _cost(m, g, r)
+                if c < best:
+                    best, bm = c, m
+        px = ((0xff << 24) | (r.astype(np.uint32) << 16) | (g.astype(np.uint32) << 8)).reshape(4, 4)
+        data, _ = O.vp8l_color_space_transform(px, 2)
+        assert int(data[0, 0] & 0xff) == (bm & 0xff)
+
+
+@pytest.mark.parametrize("xbits", [0, 1, 2, 3])
+def test_color_index_inverse(xbits):
+    rng = np.random.default_rng(xbits)
+    w, h = 29, 7
+    bpp = 8 >> xbits
+    npal = min(1 << bpp, 200)
+    pal = rng.integers(0, 2 ** 32, npal, dtype=np.uint64).astype(np.uint32)
+    idx = rng.integers(0, 1 << bpp, (h, w))
+    pw = O.vp8l_subsample(w, xbits)
+    packed = np.zeros((h, pw), np.uint32)
+    for x in range(w):
+        packed[:, x >> xbits] |= (idx[:, x].astype(np.uint32) << (bpp * (x & ((1 << xbits) - 1)))) << 8
+    packed |= 0xff000000
+    out = O.vp8l_color_index_inverse(pal, xbits, w, packed, fill=0xdeadbeef)
+    exp = np.where(idx < npal, pal[np.minimum(idx, npal - 1)], 0xdeadbeef).astype(np.uint32)
+    assert (out == exp).all()
+
+
+# ---------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [2, 4, 5, 6, 7])
+def test_gpu_color_space_transform(cuda, bits):
+    from webp_amd import lossless as L
+    for name, a in list(images()) + [("big", argb_of(synth.noise_rgba(300, 170, seed=4, alpha=True)))]:
+        data, t = O.vp8l_color_space_transform(a, bits)
+        g = L.to_argb_tensor(a[None])
+        gd = L.ColorSpaceTransform(g, bits)
+        assert (L.from_argb_tensor(gd)[0] == data).all(), (name, bits)
+        assert (L.from_argb_tensor(g)[0] == t).all(), (name, bits)
+        back = L.color_space_inverse(gd, bits, g)
+        assert (L.from_argb_tensor(back)[0] == a).all(), (name, bits)
+
+
+@pytest.mark.gpu
+def test_gpu_color_space_batch_and_4096_row(cuda):
+    from webp_amd import lossless as L
+    imgs = np.stack([argb_of(synth.blobs_rgba(96, 64, seed=s, alpha=True)) for s in range(3)])
+    g = L.to_argb_tensor(imgs)
+    gd = L.ColorSpaceTransform(g, 5)
+    got_d, got_t = L.from_argb_tensor(gd), L.from_argb_tensor(g)
+    for i in range(3):
+        data, t = O.vp8l_color_space_transform(imgs[i], 5)
+        assert (got_d[i] == data).all() and (got_t[i] == t).all()
+    row = argb_of(synth.noise_rgba(4096, 3, seed=1))
+    data, t = O.vp8l_color_space_transform(row, 5)
+    g = L.to_argb_tensor(row[None])
+    gd = L.ColorSpaceTransform(g, 5)
+    assert (L.from_argb_tensor(gd)[0] == data).all() and (L.from_argb_tensor(g)[0] == t).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("xbits", [0, 1, 2, 3])
+def test_gpu_color_index_inverse(cuda, xbits):
+    import torch
+    from webp_amd import lossless as L
+    rng = np.random.default_rng(10 + xbits)
+    w, h, n = 301, 13, 2
+    bpp = 8 >> xbits
+    npal = min(1 << bpp, 200)
+    pal = rng.integers(0, 2 ** 32, npal, dtype=np.uint64).astype(np.uint32)
+    pw = O.vp8l_subsample(w, xbits)
+    packed = (rng.integers(0, 2 ** 32, (n, h, pw), dtype=np.uint64).astype(np.uint32))
+    out = L.color_index_inverse(L.to_argb_tensor(pal), xbits, w, L.to_argb_tensor(packed),
+                                out=torch.full((n, h, w), 0x0badbeef, dtype=torch.int32, device="cuda"))
+    got = L.from_argb_tensor(out)
+    for i in range(n):
+        exp = O.vp8l_color_index_inverse(pal, xbits, w, packed[i], fill=0x0badbeef)
+        assert (got[i] == exp).all()

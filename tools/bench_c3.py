@@ -1,0 +1,74 @@
+"""C3 (BASELINE.json configs[2]) and single-frame latencies on one GPU.
+
+  C3: one 4096x4096 lossy decode = reconstruct + loop filter (k_decode_rows)
+      + fancy upsample to NRGBA (k_upsample), from seeded synthetic parsed
+      macroblocks (SURVEY.md 8(d) recipe, normal filter, half I4);
+  C2: one 1920x1080 q75 encode RD pass (k_encode_rows) on each content type;
+  plus the same decode at batch 4 / 16 to show where a single image stops
+  filling the chip.
+Prints one line per case (ms, MPix/s).  Not the driver bench."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import oracle as O  # noqa: E402
+from tools import synth  # noqa: E402
+from webp_amd import frames  # noqa: E402
+
+REPS = int(os.environ.get("REPS", "5"))
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(REPS):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts))
+
+
+def decode_case(n_img, w, h):
+    mbw, mbh = (w + 15) >> 4, (h + 15) >> 4
+    mb, co = synth.random_macroblocks(mbw * mbh, seed=5, levels=(20, 32))
+    mbt = frames.mb_info_tensor(np.tile(mb, n_img))
+    cot = torch.from_numpy(np.tile(co, (n_img, 1))).cuda()
+    Y, U, V = frames.decode_frames(mbt, cot, 2, mbw, mbh, n_img, check=True)
+    out = frames.build_nrgba(Y, U, V, w, h)
+    t_dec = timed(lambda: frames.decode_frames(mbt, cot, 2, mbw, mbh, n_img, out=(Y, U, V)))
+    t_up = timed(lambda: frames.build_nrgba(Y, U, V, w, h, out=out))
+    px = n_img * w * h
+    print(f"decode {n_img}x{w}x{h}: reconstruct+filter {t_dec:.3f} ms, upsample {t_up:.3f} ms, "
+          f"total {t_dec + t_up:.3f} ms = {px / (t_dec + t_up) / 1e3:.1f} MPix/s")
+
+
+def encode_case(kind, w=1920, h=1080):
+    mbw, mbh = (w + 15) >> 4, (h + 15) >> 4
+    gen = {"gradient": lambda: synth.gradient_rgba(w, h), "noise": lambda: synth.noise_rgba(w, h, seed=3),
+           "blobs": lambda: synth.blobs_rgba(w, h, seed=3)}[kind]
+    y, u, v = O.import_rgba(gen(), has_alpha=False)
+    Y, U, V = (torch.from_numpy(a[None]).cuda() for a in (y, u, v))
+    segs = np.stack([frames.setup_segment(q) for q in (22, 25, 28, 31)])
+    seg_ids = torch.from_numpy((np.arange(mbw * mbh) % 4).astype(np.uint8)[None]).cuda()
+    proba = O.default_proba()
+    out, rec = frames.encode_mbs(Y, U, V, w, h, seg_ids, segs, proba, check=True)
+    t = timed(lambda: frames.encode_mbs(Y, U, V, w, h, seg_ids, segs, proba, out=out, recon=rec))
+    print(f"encode RD 1x{w}x{h} {kind}: {t:.3f} ms = {w * h / t / 1e3:.1f} MPix/s")
+
+
+def main():
+    for n in (1, 4, 16):
+        decode_case(n, 4096, 4096)
+    for kind in ("gradient", "blobs", "noise"):
+        encode_case(kind)
+
+
+if __name__ == "__main__":
+    main()

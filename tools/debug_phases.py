@@ -1,18 +1,21 @@
-"""Diagnostic: cycles per phase of k_decode_rows (build with OPT='-O3 -DWG_STAMPS')."""
+"""Diagnostic: cycles per phase of k_decode_rows (stamped build: make -C webp_amd
+libwebpgpu_stamps.so; WEBPGPU_LIB=webp_amd/libwebpgpu_stamps.so).  BATCH frames of
+SIZE (1080p default, "4096" for the C3 frame)."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from tools import synth
 from webp_amd import _lib, frames
 B = int(os.environ.get("BATCH", "64"))
-MBW, MBH = 120, 68
+MBW, MBH = (256, 256) if os.environ.get("SIZE") == "4096" else (120, 68)
 names = ["wait", "loads", "luma", "chroma", "ctx+tile", "filter", "stores", "publish"]
 _lib.lib.wg_debug_phases.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = (ctypes.c_ulonglong * 16)()
 for p_i4, ft in ((0.5, 2), (0.0, 0), (1.0, 2)):
-    mb, co = synth.random_macroblocks(MBW * MBH * 4, seed=11, levels=(20, 32), p_i4=p_i4)
-    mbt = frames.mb_info_tensor(mb).view(4, -1, 32).repeat(B // 4, 1, 1).reshape(-1, 32).contiguous()
-    cot = torch.from_numpy(co).cuda().view(4, -1, 384).repeat(B // 4, 1, 1).reshape(-1, 384).contiguous()
+    nv = min(B, 4)
+    mb, co = synth.random_macroblocks(MBW * MBH * nv, seed=11, levels=(20, 32), p_i4=p_i4)
+    mbt = frames.mb_info_tensor(mb).view(nv, -1, 32).repeat(B // nv, 1, 1).reshape(-1, 32).contiguous()
+    cot = torch.from_numpy(co).cuda().view(nv, -1, 384).repeat(B // nv, 1, 1).reshape(-1, 384).contiguous()
     frames.decode_frames(mbt, cot, ft, MBW, MBH, B)
     torch.cuda.synchronize()
     _lib.lib.wg_debug_phases(ctypes.addressof(buf), 16)  # reset after warmup

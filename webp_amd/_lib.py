@@ -60,6 +60,9 @@ SIGNATURES = {
     "wg_vp8l_inverse_status": [_vp, _vp],
     "wg_vp8l_green": [_vp, _i64, _i32, _vp],
     "wg_vp8l_slog2_lut_host": [_vp, _i32],
+    "wg_vp8l_color_space_transform": [_vp, _i32, _i32, _i64, _i32, _i32, _vp, _vp],
+    "wg_vp8l_color_space_inverse": [_vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _vp],
+    "wg_vp8l_color_index_inverse": [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp],
     "wg_sharpyuv_work_bytes": [_i32, _i32, _i32],
     "wg_sharpyuv_convert": [_vp, _i32, _i32, _i32, _i64, _vp, _i32, _vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _vp],
     "wg_sharpyuv_tables_host": [_vp, _vp],

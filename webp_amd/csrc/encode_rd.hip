@@ -939,7 +939,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
       lds_sync();
       uint64_t s4;
       {
-        const int half = lane >> 5, hl = lane & 31;
         // running totals over the finished blocks: rate, distortion and header
         // bits only grow, so once the finished blocks alone reach the exit
         // condition the reference exits too (at some block) and I4 loses

@@ -1,0 +1,296 @@
+// vp8l_color.hip -- the VP8L cross-colour transform and the colour inverse
+// transforms on gfx950.
+//
+//   k_cc_select   ColorSpaceTransform (internal/lossless/encode_predictor.go:
+//                 727-770): per tile, the three multipliers
+//                 (findBestMultipliers :514-585) and the forward transform of
+//                 the tile in place (applyColorTransformTile :774-792)
+//   k_cc_inverse  colorSpaceInverseTransform (decode_transform.go:454-520)
+//   k_ci_inverse  colorIndexInverseTransform (decode_transform.go:560-612)
+//
+// k_cc_select: one 256-lane workgroup per tile.  A multiplier search is a
+// first-minimum over candidate multipliers of sum_i |t_i - (m * int8(s_i)) >> 5|
+// (mod 256, folded at 128; multiplierCost :645-718 -- its threshold early exit
+// returns a partial sum above the running best, which never changes the
+// argmin, so the full sums are used).  Each pass gives a lane one candidate and
+// a strided share of the tile's pixels; the per-candidate sums are reduced in
+// LDS and one lane then applies the reference's scan order (coarse m = -128,
+// -120, ..., 120 with strict '<', then m = best-7..best+7 with strict '<'
+// against the running best).  Passes: coarse green->red and green->blue
+// together (64 candidates), their fine searches (2 x 15), coarse red->blue on
+// the adjusted red / blue (32), its fine search (15), then the transform.
+// All integer; bit-exact with oracle/lossless.c.
+#include "wg_common.h"
+
+namespace {
+
+constexpr int CC_THREADS = 256;
+constexpr int CC_LDS_PIXELS = 64 * 64;  // tiles up to bits = 6 are staged in LDS
+
+__device__ __forceinline__ int cc_delta(int m, int c) { return (m * (int)(int8_t)c) >> 5; }
+// |t - delta| folded as the reference does: r = uint8(t - delta); r > 128 ? 256 - r : r
+__device__ __forceinline__ int cc_term(int m, int s, int t) {
+  const int r = (t - cc_delta(m, s)) & 0xff;
+  return r > 128 ? 256 - r : r;
+}
+
+struct CcArgs {
+  uint32_t* argb;
+  uint32_t* data;
+  int64_t pitch;
+  int width, height, bits, tiles_x, tiles_y;
+};
+
+__global__ __launch_bounds__(CC_THREADS) void k_cc_select(CcArgs a) {
+  __shared__ uint32_t px[CC_LDS_PIXELS];
+  __shared__ int part[CC_THREADS];
+  __shared__ int cost[64];
+  __shared__ int best[3];
+  const int tid = threadIdx.x;
+  const int tiles = a.tiles_x * a.tiles_y;
+  const int img = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int tx = tile % a.tiles_x, ty = tile / a.tiles_x, ts = 1 << a.bits;
+  const int x0 = tx * ts, y0 = ty * ts;
+  const int tw = min(ts, a.width - x0), th = min(ts, a.height - y0), n = tw * th;
+  uint32_t* base = a.argb + img * a.pitch + (int64_t)y0 * a.width + x0;
+  const bool staged = n <= CC_LDS_PIXELS;
+  if (staged) {
+    for (int i = tid; i < n; i += CC_THREADS) px[i] = base[(int64_t)(i / tw) * a.width + i % tw];
+    __syncthreads();
+  }
+  auto pixel = [&](int i) -> uint32_t { return staged ? px[i] : base[(int64_t)(i / tw) * a.width + i % tw]; };
+
+  // one search pass: lane = (candidate c < ncand, pixel group g of ngroups)
+  // -> cost[c]; src/dst channel selectors: 0 green, 1 red, 2 blue, 3 adjusted
+  // red, 4 adjusted blue (after the green multipliers in best[0], best[1])
+  auto pass = [&](int ncand, int first_m, int step, int sel_mode) {
+    const int ngroups = CC_THREADS / ncand;  // ncand in {32, 64}
+    const int c = tid % ncand, g = tid / ncand;
+    int sum = 0;
+    // sel_mode 0: c < 32 green->red, c >= 32 green->blue (coarse, 64 candidates)
+    // sel_mode 1: c < 16 green->red fine, 16..31 green->blue fine
+    // sel_mode 2: adjusted red -> adjusted blue (coarse or fine by step)
+    int m, ch;
+    if (sel_mode == 0) {
+      m = -128 + 8 * (c & 31);
+      ch = c >> 5;
+    } else if (sel_mode == 1) {
+      ch = c >> 4;
+      m = best[ch] - 7 + (c & 15);
+    } else {
+      ch = 2;
+      m = step ? -128 + 8 * c : best[2] - 7 + c;
+    }
+    const bool live = (sel_mode == 1 ? (c & 15) < 15 : (sel_mode == 2 && !step ? c < 15 : true)) && m >= -128 && m <= 127;
+    if (live) {
+      const int g2r = best[0], g2b = best[1];
+      for (int i = g; i < n; i += ngroups) {
+        const uint32_t p = pixel(i);
+        const int gr = (p >> 8) & 0xff, rd = (p >> 16) & 0xff, bl = p & 0xff;
+        if (ch == 0) {
+          sum += cc_term(m, gr, rd);
+        } else if (ch == 1) {
+          sum += cc_term(m, gr, bl);
+        } else {
+          sum += cc_term(m, (rd - cc_delta(g2r, gr)) & 0xff, (bl - cc_delta(g2b, gr)) & 0xff);
+        }
+      }
+    }
+    part[tid] = live ? sum : 0x7fffffff;
+    __syncthreads();
+    if (tid < ncand) {
+      int s = 0;
+      bool ok = part[tid] != 0x7fffffff;
+      for (int k = 0; k < ngroups; k++) s += part[tid + k * ncand];
+      cost[tid] = ok ? s : 0x7fffffff;
+    }
+    __syncthreads();
+  };
+
+  // coarse green->red and green->blue
+  if (tid < 3) best[tid] = 0;
+  __syncthreads();
+  pass(64, -128, 8, 0);
+  __shared__ int coarse_cost[3];
+  if (tid < 2) {  // first minimum in the reference's scan order
+    int bm = 0, bc = 0x7fffffff;
+    for (int k = 0; k < 32; k++)
+      if (cost[32 * tid + k] < bc) {
+        bc = cost[32 * tid + k];
+        bm = -128 + 8 * k;
+      }
+    best[tid] = bm;
+    coarse_cost[tid] = bc;
+  }
+  __syncthreads();
+  pass(32, 0, 0, 1);
+  if (tid < 2) {
+    int bm = best[tid], bc = coarse_cost[tid];
+    for (int k = 0; k < 15; k++) {
+      const int m = best[tid] - 7 + k;
+      if (m < -128 || m > 127) continue;
+      const int cst = cost[16 * tid + k];
+      if (cst < bc) {
+        bc = cst;
+        bm = m;
+      }
+    }
+    part[tid] = bm;  // (part is free here)
+  }
+  __syncthreads();
+  if (tid < 2) best[tid] = part[tid];
+  __syncthreads();
+  // red->blue on the adjusted channels
+  pass(32, -128, 1, 2);
+  if (tid == 0) {
+    int bm = 0, bc = 0x7fffffff;
+    for (int k = 0; k < 32; k++)
+      if (cost[k] < bc) {
+        bc = cost[k];
+        bm = -128 + 8 * k;
+      }
+    best[2] = bm;
+    coarse_cost[2] = bc;
+  }
+  __syncthreads();
+  pass(32, 0, 0, 2);
+  if (tid == 0) {
+    int bm = best[2], bc = coarse_cost[2];
+    for (int k = 0; k < 15; k++) {
+      const int m = best[2] - 7 + k;
+      if (m < -128 || m > 127) continue;
+      if (cost[k] < bc) {
+        bc = cost[k];
+        bm = m;
+      }
+    }
+    part[0] = bm;
+  }
+  __syncthreads();
+  const int g2r = best[0], g2b = best[1], r2b = part[0];
+  if (tid == 0)
+    a.data[(int64_t)img * tiles + tile] = (uint32_t)(uint8_t)g2r | (uint32_t)(uint8_t)g2b << 8 | (uint32_t)(uint8_t)r2b << 16;
+  // applyColorTransformPixel (:497-507) over the tile, in place
+  for (int i = tid; i < n; i += CC_THREADS) {
+    const uint32_t p = pixel(i);
+    const int gr = (p >> 8) & 0xff, rd = (p >> 16) & 0xff, bl = p & 0xff;
+    const int nr = (rd - cc_delta(g2r, gr)) & 0xff;
+    const int nb = (bl - cc_delta(g2b, gr) - cc_delta(r2b, rd)) & 0xff;
+    base[(int64_t)(i / tw) * a.width + i % tw] = (p & 0xff00ff00u) | ((uint32_t)nr << 16) | (uint32_t)nb;
+  }
+}
+
+struct CiArgs {
+  const uint32_t* data;
+  const uint32_t* src;
+  uint32_t* dst;
+  int64_t pitch;
+  int width, height, bits, tiles_x;
+};
+
+// one thread per pixel; the tile's multipliers come from the (cached) data row
+__global__ __launch_bounds__(256) void k_cc_inverse(CiArgs a, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t per = (int64_t)a.width * a.height;
+  const int img = (int)(i / per);
+  const int64_t r = i - img * per;
+  const int y = (int)(r / a.width), x = (int)(r % a.width);
+  const int tiles = a.tiles_x * ((a.height + (1 << a.bits) - 1) >> a.bits);
+  const uint32_t code = a.data[(int64_t)img * tiles + (y >> a.bits) * a.tiles_x + (x >> a.bits)];
+  const int g2r = (int8_t)code, g2b = (int8_t)(code >> 8), r2b = (int8_t)(code >> 16);
+  const uint32_t p = a.src[img * a.pitch + r];
+  const int green = (int8_t)(p >> 8);
+  int red = (int)((p >> 16) & 0xff), blue = (int)(p & 0xff);
+  red = (red + ((g2r * green) >> 5)) & 0xff;
+  blue = (blue + ((g2b * green) >> 5) + ((r2b * (int)(int8_t)red) >> 5)) & 0xff;
+  a.dst[img * a.pitch + r] = (p & 0xff00ff00u) | ((uint32_t)red << 16) | (uint32_t)blue;
+}
+
+struct IxArgs {
+  const uint32_t* palette;
+  const uint32_t* src;
+  uint32_t* dst;
+  int64_t src_pitch, dst_pitch;
+  int palette_size, xbits, width, height, packed_w;
+};
+
+// one thread per output pixel: its packed word, its index bits, the palette
+__global__ __launch_bounds__(256) void k_ci_inverse(IxArgs a, int64_t total) {
+  __shared__ uint32_t pal[256];
+  for (int k = threadIdx.x; k < a.palette_size; k += 256) pal[k] = a.palette[k];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t per = (int64_t)a.width * a.height;
+  const int img = (int)(i / per);
+  const int64_t r = i - img * per;
+  const int y = (int)(r / a.width), x = (int)(r % a.width);
+  const int bpp = 8 >> a.xbits;
+  const uint32_t word = (a.src[img * a.src_pitch + (int64_t)y * a.packed_w + (x >> a.xbits)] >> 8) & 0xff;
+  const uint32_t idx = bpp < 8 ? (word >> (bpp * (x & ((1 << a.xbits) - 1)))) & ((1u << bpp) - 1) : word;
+  if ((int)idx < a.palette_size) a.dst[img * a.dst_pitch + r] = pal[idx];
+}
+
+}  // namespace
+
+extern "C" int wg_vp8l_color_space_transform(uint32_t* argb, int32_t width, int32_t height, int64_t image_pitch,
+                                             int32_t bits, int32_t n_images, uint32_t* data, void* stream) {
+  WG_REQUIRE(argb && data && width > 0 && height > 0 && n_images > 0);
+  WG_REQUIRE(bits >= 2 && bits <= 9 && image_pitch >= (int64_t)width * height);
+  CcArgs a;
+  a.argb = argb;
+  a.data = data;
+  a.pitch = image_pitch;
+  a.width = width;
+  a.height = height;
+  a.bits = bits;
+  a.tiles_x = (width + (1 << bits) - 1) >> bits;
+  a.tiles_y = (height + (1 << bits) - 1) >> bits;
+  const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * n_images;
+  WG_REQUIRE(blocks < (1ll << 31));
+  hipLaunchKernelGGL(k_cc_select, dim3((unsigned)blocks), dim3(CC_THREADS), 0, wg::as_stream(stream), a);
+  return wg::check_launch("k_cc_select");
+}
+
+extern "C" int wg_vp8l_color_space_inverse(const uint32_t* data, int32_t bits, int32_t width, int32_t height,
+                                           int64_t image_pitch, int32_t n_images, const uint32_t* src, uint32_t* dst,
+                                           void* stream) {
+  WG_REQUIRE(data && src && dst && width > 0 && height > 0 && n_images > 0);
+  WG_REQUIRE(bits >= 2 && bits <= 9 && image_pitch >= (int64_t)width * height);
+  CiArgs a;
+  a.data = data;
+  a.src = src;
+  a.dst = dst;
+  a.pitch = image_pitch;
+  a.width = width;
+  a.height = height;
+  a.bits = bits;
+  a.tiles_x = (width + (1 << bits) - 1) >> bits;
+  const int64_t total = (int64_t)width * height * n_images;
+  hipLaunchKernelGGL(k_cc_inverse, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, wg::as_stream(stream), a, total);
+  return wg::check_launch("k_cc_inverse");
+}
+
+extern "C" int wg_vp8l_color_index_inverse(const uint32_t* palette, int32_t palette_size, int32_t xbits, int32_t width,
+                                           int32_t height, int32_t n_images, const uint32_t* src, int64_t src_pitch,
+                                           uint32_t* dst, int64_t dst_pitch, void* stream) {
+  WG_REQUIRE(palette && src && dst && width > 0 && height > 0 && n_images > 0);
+  WG_REQUIRE(palette_size >= 1 && palette_size <= 256 && xbits >= 0 && xbits <= 3);
+  const int packed_w = (width + (1 << xbits) - 1) >> xbits;
+  WG_REQUIRE(src_pitch >= (int64_t)packed_w * height && dst_pitch >= (int64_t)width * height);
+  IxArgs a;
+  a.palette = palette;
+  a.src = src;
+  a.dst = dst;
+  a.src_pitch = src_pitch;
+  a.dst_pitch = dst_pitch;
+  a.palette_size = palette_size;
+  a.xbits = xbits;
+  a.width = width;
+  a.height = height;
+  a.packed_w = packed_w;
+  const int64_t total = (int64_t)width * height * n_images;
+  hipLaunchKernelGGL(k_ci_inverse, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, wg::as_stream(stream), a, total);
+  return wg::check_launch("k_ci_inverse");
+}

@@ -5,6 +5,12 @@ internal/lossless entry points:
   predictor_inverse(modes, bits, resid)   decode_transform.go:202-360 (predictorInverseTransform)
   SubtractGreen(argb) / AddGreen(argb)    encode_predictor.go:461, dsp/lossless_dsp.go:12
 
+and the cross-colour / colour-index transforms:
+
+  ColorSpaceTransform(argb, bits)         encode_predictor.go:727-770 (in place)
+  color_space_inverse(data, bits, src)    decode_transform.go:454-520
+  color_index_inverse(palette, xbits, w, src)  decode_transform.go:560-612
+
 ARGB images are (n, h, w) int32 CUDA tensors holding 0xAARRGGBB words (the
 reference's []uint32; torch has no uint32 arithmetic, the bits are the same).
 """
@@ -64,6 +70,39 @@ def SubtractGreen(argb):
 def AddGreen(argb):
     call("wg_vp8l_green", argb.data_ptr(), argb.numel(), 1, _stream())
     return argb
+
+
+def ColorSpaceTransform(argb, bits, data=None):
+    """Forward cross-colour transform in place; -> multiplier words (n, tiles_y, tiles_x)
+    (g2r | g2b << 8 | r2b << 16, packMultipliers)."""
+    a = _batched(argb)
+    n, h, w = a.shape
+    if data is None:
+        data = torch.empty((n, subsample(h, bits), subsample(w, bits)), dtype=torch.int32, device=a.device)
+    call("wg_vp8l_color_space_transform", a.data_ptr(), w, h, h * w, bits, n, data.data_ptr(), _stream())
+    return data
+
+
+def color_space_inverse(data, bits, src, out=None):
+    s = _batched(src)
+    n, h, w = s.shape
+    if out is None:
+        out = torch.empty_like(s)
+    call("wg_vp8l_color_space_inverse", data.data_ptr(), bits, w, h, h * w, n, s.data_ptr(), out.data_ptr(), _stream())
+    return out
+
+
+def color_index_inverse(palette, xbits, width, src, out=None):
+    """src (n, h, subsample(width, xbits)) packed index words; palette (<=256,) int32
+    shared by the n images.  Out-of-palette indices leave `out` untouched."""
+    s = _batched(src)
+    n, h, pw = s.shape
+    assert pw == subsample(width, xbits)
+    if out is None:
+        out = torch.zeros((n, h, width), dtype=torch.int32, device=s.device)
+    call("wg_vp8l_color_index_inverse", palette.data_ptr(), palette.numel(), xbits, width, h, n, s.data_ptr(), h * pw,
+         out.data_ptr(), h * width, _stream())
+    return out
 
 
 def slog2_lut(n=65536):
