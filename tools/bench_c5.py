@@ -46,6 +46,19 @@ def main():
     inv = torch.empty_like(res)
     ms = timed(lambda: L.predictor_inverse(modes, 5, res, out=inv))
     out["inverse_predictor"] = {"ms": ms, "MPix/s": px / ms / 1e3, "GB/s": 8 * px / ms / 1e6}
+    # cross-colour transform (in place; repeated on its own output) and its inverse
+    cc = t.clone()
+    data = L.ColorSpaceTransform(cc, 5)
+    ms = timed(lambda: L.ColorSpaceTransform(cc, 5, data=data))
+    out["cross_color"] = {"ms": ms, "MPix/s": px / ms / 1e3, "GB/s": 8 * px / ms / 1e6}
+    cinv = torch.empty_like(cc)
+    ms = timed(lambda: L.color_space_inverse(data, 5, cc, out=cinv))
+    out["cross_color_inverse"] = {"ms": ms, "MPix/s": px / ms / 1e3, "GB/s": 8 * px / ms / 1e6}
+    pal = L.to_argb_tensor(np.arange(16, dtype=np.uint32) * 0x01010101)
+    packed = torch.randint(0, 2 ** 31 - 1, (1, N, N // 2), dtype=torch.int32, device="cuda")
+    ci = torch.empty_like(t)
+    ms = timed(lambda: L.color_index_inverse(pal, 1, N, packed, out=ci))
+    out["color_index_inverse"] = {"ms": ms, "MPix/s": px / ms / 1e3, "GB/s": 6 * px / ms / 1e6}
     rgb = torch.from_numpy(np.ascontiguousarray(rgba[..., :3].astype(np.uint8))).cuda().unsqueeze(0)
     Ys, Us, Vs = frames.sharpyuv_convert(rgb)
     work = torch.empty(frames.lib.wg_sharpyuv_work_bytes(N, N, 1), dtype=torch.uint8, device="cuda")
