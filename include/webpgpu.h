@@ -271,6 +271,66 @@ int wg_vp8l_color_index_inverse(const uint32_t* palette, int32_t palette_size, i
                                 int64_t dst_pitch, void* stream);
 
 /* ===================================================================== *
+ * 3c. Alpha plane: the ALPH filters of
+ *     internal/lossy/alpha.go and the alpha processing of
+ *     internal/dsp/alpha_proc.go.  Alpha planes are w x h bytes, row stride w,
+ *     images `pitch` bytes apart.  filter: 0 none, 1 horizontal, 2 vertical,
+ *     3 gradient (AlphaFilter* constants).
+ * ===================================================================== */
+
+/* alphaFilterHorizontal / Vertical / Gradient (alpha.go:387-454); filter 0
+ * copies.  in and out must not alias. */
+int wg_alpha_filter(int32_t filter, const uint8_t* in, uint8_t* out, int32_t width, int32_t height, int64_t pitch,
+                    int32_t n_images, void* stream);
+
+/* alphaUnfilterHorizontal / Vertical / Gradient (alpha.go:128-203), in place.
+ * work: wg_alpha_unfilter_work_bytes(height, n_images) device bytes (gradient
+ * only: band dequeue + progress counters; zeroed by the call). */
+size_t wg_alpha_unfilter_work_bytes(int32_t height, int32_t n_images);
+int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, int32_t height, int64_t pitch, int32_t n_images,
+                      void* work, void* stream);
+/* synchronises `stream`; WG_EHIP if a gradient band wait timed out */
+int wg_alpha_unfilter_status(const void* work, void* stream);
+
+/* estimateBestFilter (alpha.go:321-385) and getNumColors (:302-317) per image:
+ * best_filter[n], num_colors[n] (device int32).  work:
+ * wg_alpha_estimate_work_bytes(n_images) device bytes. */
+size_t wg_alpha_estimate_work_bytes(int32_t n_images);
+int wg_alpha_estimate_filter(const uint8_t* data, int32_t width, int32_t height, int64_t pitch, int32_t n_images,
+                             int32_t* best_filter, int32_t* num_colors, void* work, void* stream);
+
+/* ApplyAlphaMultiply (alpha_proc.go:74-104): 4-byte pixels, alpha at byte 0
+ * (alpha_first) or 3; rows `stride` bytes apart; images `pitch` apart. */
+int wg_apply_alpha_multiply(uint8_t* rgba, int32_t alpha_first, int32_t width, int32_t height, int32_t stride,
+                            int64_t pitch, int32_t n_images, int32_t inverse, void* stream);
+/* MultARGBRow (alpha_proc.go:28-46) over n words */
+int wg_mult_argb(uint32_t* argb, int64_t n, int32_t inverse, void* stream);
+/* ApplyAlphaMultiply4444 (alpha_proc.go:106-135): 2-byte RGBA4444 pixels */
+int wg_apply_alpha_multiply_4444(uint8_t* data, int32_t width, int32_t height, int32_t stride, int64_t pitch,
+                                 int32_t n_images, void* stream);
+/* DispatchAlpha (alpha_proc.go:140-155): *has_transparency (device int32)
+ * = 1 when any alpha != 0xff (the Go bool result) */
+int wg_dispatch_alpha(const uint8_t* alpha, int32_t alpha_stride, int32_t width, int32_t height, uint8_t* dst,
+                      int32_t dst_stride, int32_t alpha_off, int32_t* has_transparency, void* stream);
+/* ExtractAlpha (alpha_proc.go:158-176): *all_opaque (device int32) = 1 when
+ * every alpha is 0xff (the Go int result) */
+int wg_extract_alpha(const uint8_t* src, int32_t src_stride, int32_t width, int32_t height, uint8_t* alpha,
+                     int32_t alpha_stride, int32_t alpha_off, int32_t* all_opaque, void* stream);
+/* HasAlpha8b (step 1) / HasAlpha32b (step 4) (alpha_proc.go:178-197):
+ * *any_transparent (device int32) = the Go bool */
+int wg_has_alpha(const uint8_t* src, int64_t length, int32_t step, int32_t* any_transparent, void* stream);
+/* AlphaReplace (alpha_proc.go:199-206) */
+int wg_alpha_replace(uint32_t* argb, int64_t length, uint32_t color, void* stream);
+/* DispatchAlphaToGreen (alpha_proc.go:209-219); dst_stride in pixels */
+int wg_dispatch_alpha_to_green(const uint8_t* alpha, int32_t alpha_stride, int32_t width, int32_t height,
+                               uint32_t* dst, int32_t dst_stride, void* stream);
+/* ExtractGreen (alpha_proc.go:221-226) */
+int wg_extract_green(const uint32_t* argb, uint8_t* alpha, int64_t size, void* stream);
+/* PackRGB (alpha_proc.go:229-238) */
+int wg_pack_rgb(const uint8_t* r, const uint8_t* g, const uint8_t* b, int64_t length, int32_t step, uint32_t* out,
+                void* stream);
+
+/* ===================================================================== *
  * 4. SharpYUV: sharpyuv.Convert with SharpEnabled and the
  *    sRGB transfer (sharpyuv/sharpyuv.go:39-64, convertSharp :170-269).
  * ===================================================================== */

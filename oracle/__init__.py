@@ -107,6 +107,20 @@ _SIGS = {
     "or_vp8l_color_space_transform": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p]),
     "or_vp8l_color_space_inverse": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
     "or_vp8l_color_index_inverse": (None, [ctypes.c_void_p, _i, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
+    "or_alpha_filter": (None, [_i, ctypes.c_void_p, _i, _i, ctypes.c_void_p]),
+    "or_alpha_unfilter": (None, [_i, ctypes.c_void_p, _i, _i]),
+    "or_alpha_estimate_best_filter": (_i, [ctypes.c_void_p, _i, _i]),
+    "or_alpha_num_colors": (_i, [ctypes.c_void_p, _i, _i]),
+    "or_apply_alpha_multiply": (None, [ctypes.c_void_p, _i, _i, _i, _i, _i]),
+    "or_mult_argb": (None, [ctypes.c_void_p, ctypes.c_size_t, _i]),
+    "or_apply_alpha_multiply_4444": (None, [ctypes.c_void_p, _i, _i, _i]),
+    "or_dispatch_alpha": (_i, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i, _i]),
+    "or_extract_alpha": (_i, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i, _i]),
+    "or_has_alpha": (_i, [ctypes.c_void_p, ctypes.c_size_t, _i]),
+    "or_alpha_replace": (None, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32]),
+    "or_dispatch_alpha_to_green": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i]),
+    "or_extract_green": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "or_pack_rgb": (None, [ctypes.c_void_p] * 3 + [ctypes.c_size_t, _i, ctypes.c_void_p]),
     "or_sharpyuv_tables": (None, [ctypes.c_void_p, ctypes.c_void_p]),
     "or_setup_segment": (None, [_i] * 8 + [ctypes.c_void_p]),
     "or_fixed_costs_i4": (None, [ctypes.c_void_p]),
@@ -272,6 +286,107 @@ def vp8l_color_index_inverse(palette, xbits, width, src, fill=0):
     h = src.shape[0]
     out = np.full((h, width), fill, np.uint32)
     lib.or_vp8l_color_index_inverse(pal.ctypes.data, len(pal), xbits, width, h, src.ctypes.data, out.ctypes.data)
+    return out
+
+
+# ---------------- alpha plane ----------------
+
+def alpha_filter(filter_, plane):
+    """alphaFilter{Horizontal,Vertical,Gradient} (filter 1/2/3; 0 copies): (h, w) uint8 -> filtered."""
+    a = np.ascontiguousarray(plane, np.uint8)
+    h, w = a.shape
+    out = np.empty_like(a)
+    lib.or_alpha_filter(filter_, a.ctypes.data, w, h, out.ctypes.data)
+    return out
+
+
+def alpha_unfilter(filter_, plane):
+    a = np.ascontiguousarray(plane, np.uint8).copy()
+    h, w = a.shape
+    lib.or_alpha_unfilter(filter_, a.ctypes.data, w, h)
+    return a
+
+
+def alpha_estimate_best_filter(plane):
+    a = np.ascontiguousarray(plane, np.uint8)
+    return lib.or_alpha_estimate_best_filter(a.ctypes.data, a.shape[1], a.shape[0])
+
+
+def alpha_num_colors(plane):
+    a = np.ascontiguousarray(plane, np.uint8)
+    return lib.or_alpha_num_colors(a.ctypes.data, a.shape[1], a.shape[0])
+
+
+def apply_alpha_multiply(rgba, alpha_first, inverse, width=None):
+    """ApplyAlphaMultiply on (h, stride) uint8 rows of 4-byte pixels (width defaults to stride // 4)."""
+    a = np.ascontiguousarray(rgba, np.uint8).copy()
+    h, stride = a.shape
+    lib.or_apply_alpha_multiply(a.ctypes.data, int(alpha_first), width or stride // 4, h, stride, int(inverse))
+    return a
+
+
+def mult_argb(argb, inverse):
+    a = np.ascontiguousarray(argb, np.uint32).copy()
+    lib.or_mult_argb(a.ctypes.data, a.size, int(inverse))
+    return a
+
+
+def apply_alpha_multiply_4444(data, width=None):
+    a = np.ascontiguousarray(data, np.uint8).copy()
+    h, stride = a.shape
+    lib.or_apply_alpha_multiply_4444(a.ctypes.data, width or stride // 2, h, stride)
+    return a
+
+
+def dispatch_alpha(alpha, dst, alpha_off, width=None):
+    """DispatchAlpha: alpha (h, alpha_stride) into dst (h, dst_stride) bytes -> (dst', any transparent)."""
+    al = np.ascontiguousarray(alpha, np.uint8)
+    d = np.ascontiguousarray(dst, np.uint8).copy()
+    h, astride = al.shape
+    r = lib.or_dispatch_alpha(al.ctypes.data, astride, width or astride, h, d.ctypes.data, d.shape[1], alpha_off)
+    return d, bool(r)
+
+
+def extract_alpha(src, alpha, alpha_off, width=None):
+    """ExtractAlpha: src (h, src_stride) bytes -> (alpha (h, alpha_stride) plane, 1 if all opaque else 0)."""
+    s_ = np.ascontiguousarray(src, np.uint8)
+    al = np.ascontiguousarray(alpha, np.uint8).copy()
+    h, sstride = s_.shape
+    r = lib.or_extract_alpha(s_.ctypes.data, sstride, width or sstride // 4, h, al.ctypes.data, al.shape[1], alpha_off)
+    return al, r
+
+
+def has_alpha(src, step):
+    """HasAlpha8b (step 1) / HasAlpha32b (step 4) over len(src) // step entries."""
+    s_ = np.ascontiguousarray(src, np.uint8)
+    return bool(lib.or_has_alpha(s_.ctypes.data, s_.size // step if step == 4 else s_.size, step))
+
+
+def alpha_replace(argb, color):
+    a = np.ascontiguousarray(argb, np.uint32).copy()
+    lib.or_alpha_replace(a.ctypes.data, a.size, color)
+    return a
+
+
+def dispatch_alpha_to_green(alpha, dst_stride):
+    al = np.ascontiguousarray(alpha, np.uint8)
+    h, w = al.shape
+    out = np.zeros((h, dst_stride), np.uint32)
+    lib.or_dispatch_alpha_to_green(al.ctypes.data, w, w, h, out.ctypes.data, dst_stride)
+    return out
+
+
+def extract_green(argb):
+    a = np.ascontiguousarray(argb, np.uint32)
+    out = np.empty(a.shape, np.uint8)
+    lib.or_extract_green(a.ctypes.data, out.ctypes.data, a.size)
+    return out
+
+
+def pack_rgb(r, g, b, length, step):
+    r, g, b = (np.ascontiguousarray(c, np.uint8) for c in (r, g, b))
+    out = np.empty(length, np.uint32)
+    lib.or_pack_rgb(r.ctypes.data, g.ctypes.data, b.ctypes.data, length, step, out.ctypes.data)
     return out
 
 

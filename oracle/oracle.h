@@ -162,6 +162,25 @@ void or_vp8l_color_space_inverse(const uint32_t* data, int bits, int width, int 
 void or_vp8l_color_index_inverse(const uint32_t* palette, int palette_size, int xbits, int width, int height,
                                  const uint32_t* src, uint32_t* dst);
 
+/* alpha.c: alpha-plane filters and alpha processing */
+void or_alpha_filter(int filter, const uint8_t* in, int width, int height, uint8_t* out);
+void or_alpha_unfilter(int filter, uint8_t* data, int width, int height);
+int or_alpha_estimate_best_filter(const uint8_t* data, int width, int height);
+int or_alpha_num_colors(const uint8_t* data, int width, int height);
+void or_apply_alpha_multiply(uint8_t* rgba, int alpha_first, int width, int height, int stride, int inverse);
+void or_mult_argb(uint32_t* argb, size_t n, int inverse);
+void or_apply_alpha_multiply_4444(uint8_t* data, int width, int height, int stride);
+int or_dispatch_alpha(const uint8_t* alpha, int alpha_stride, int width, int height, uint8_t* dst, int dst_stride,
+                      int alpha_off);
+int or_extract_alpha(const uint8_t* src, int src_stride, int width, int height, uint8_t* alpha, int alpha_stride,
+                     int alpha_off);
+int or_has_alpha(const uint8_t* src, size_t length, int step);
+void or_alpha_replace(uint32_t* argb, size_t length, uint32_t color);
+void or_dispatch_alpha_to_green(const uint8_t* alpha, int alpha_stride, int width, int height, uint32_t* dst,
+                                int dst_stride);
+void or_extract_green(const uint32_t* argb, uint8_t* alpha, size_t size);
+void or_pack_rgb(const uint8_t* r, const uint8_t* g, const uint8_t* b, size_t length, int step, uint32_t* out);
+
 /* ---- Encoder MB RD loop (lossy_rd.c; encode_parallel.go Phase A) ---- */
 typedef struct {          /* SegmentQuant (encode.go:311-323) */
   int32_t quant, iquant, bias, zthresh;

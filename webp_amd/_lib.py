@@ -63,6 +63,22 @@ SIGNATURES = {
     "wg_vp8l_color_space_transform": [_vp, _i32, _i32, _i64, _i32, _i32, _vp, _vp],
     "wg_vp8l_color_space_inverse": [_vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _vp],
     "wg_vp8l_color_index_inverse": [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp],
+    "wg_alpha_filter": [_i32, _vp, _vp, _i32, _i32, _i64, _i32, _vp],
+    "wg_alpha_unfilter_work_bytes": [_i32, _i32],
+    "wg_alpha_unfilter": [_i32, _vp, _i32, _i32, _i64, _i32, _vp, _vp],
+    "wg_alpha_unfilter_status": [_vp, _vp],
+    "wg_alpha_estimate_work_bytes": [_i32],
+    "wg_alpha_estimate_filter": [_vp, _i32, _i32, _i64, _i32, _vp, _vp, _vp, _vp],
+    "wg_apply_alpha_multiply": [_vp, _i32, _i32, _i32, _i32, _i64, _i32, _i32, _vp],
+    "wg_mult_argb": [_vp, _i64, _i32, _vp],
+    "wg_apply_alpha_multiply_4444": [_vp, _i32, _i32, _i32, _i64, _i32, _vp],
+    "wg_dispatch_alpha": [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
+    "wg_extract_alpha": [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
+    "wg_has_alpha": [_vp, _i64, _i32, _vp, _vp],
+    "wg_alpha_replace": [_vp, _i64, ctypes.c_uint32, _vp],
+    "wg_dispatch_alpha_to_green": [_vp, _i32, _i32, _i32, _vp, _i32, _vp],
+    "wg_extract_green": [_vp, _vp, _i64, _vp],
+    "wg_pack_rgb": [_vp, _vp, _vp, _i64, _i32, _vp, _vp],
     "wg_sharpyuv_work_bytes": [_i32, _i32, _i32],
     "wg_sharpyuv_convert": [_vp, _i32, _i32, _i32, _i64, _vp, _i32, _vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _vp],
     "wg_sharpyuv_tables_host": [_vp, _vp],
@@ -74,7 +90,8 @@ SIGNATURES = {
 }
 _RES = {"wg_last_error": ctypes.c_char_p, "wg_decode_work_bytes": ctypes.c_size_t,
         "wg_plane_ssim_work_bytes": ctypes.c_size_t, "wg_vp8l_inverse_work_bytes": ctypes.c_size_t,
-        "wg_sharpyuv_work_bytes": ctypes.c_size_t, "wg_encode_work_bytes": ctypes.c_size_t}
+        "wg_sharpyuv_work_bytes": ctypes.c_size_t, "wg_encode_work_bytes": ctypes.c_size_t,
+        "wg_alpha_unfilter_work_bytes": ctypes.c_size_t, "wg_alpha_estimate_work_bytes": ctypes.c_size_t}
 
 for _name, _args in SIGNATURES.items():
     _f = getattr(lib, _name)

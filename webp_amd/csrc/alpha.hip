@@ -1,0 +1,604 @@
+// alpha.hip -- alpha-plane filters and alpha processing on gfx950
+// (SURVEY.md 8(f)#4).
+//
+//   k_alpha_filter      alphaFilterHorizontal / Vertical / Gradient
+//                       (internal/lossy/alpha.go:387-454): one thread per pixel
+//   unfilters           alphaUnfilterHorizontal / Vertical / Gradient (:128-203),
+//                       in place:
+//     horizontal        value(y, x) = sum_{k<=y} d(k, 0) + sum_{1<=i<=x} d(y, i)
+//                       (mod 256): a scan of column 0, then one wave per row
+//                       scanning 64 columns at a time
+//     vertical          a scan of row 0, then one thread per column walking down
+//     gradient          row 0 scanned; the rows below are a 2-D recurrence
+//                       (left, top, top-left, clamped): one wave per 64-row band
+//                       walks it diagonally (lane k does x = s - k of row
+//                       band*64 + k; the row above comes from lane k-1 by a lane
+//                       shift); bands hand their last row down 64 columns at a
+//                       time (plain stores, vmcnt(0) + release fence, then a
+//                       relaxed progress counter)
+//   k_alpha_estimate    estimateBestFilter (:321-385): one thread per sampled row
+//                       (the running mean is serial along the row); the 4 x 16
+//                       "seen" bins are OR-ed into one 64-bit word per image
+//   k_alpha_colors      getNumColors (:302-317): 256-bit OR per image
+//   premultiply         ApplyAlphaMultiply, MultARGBRow, ApplyAlphaMultiply4444
+//                       (internal/dsp/alpha_proc.go:13-135): one thread per pixel
+//   dispatch / extract  DispatchAlpha / ExtractAlpha (:140-176) with their
+//                       any-transparent / all-opaque results
+// Bit-exact with oracle/alpha.c.
+#include "wg_common.h"
+
+namespace {
+
+__device__ __forceinline__ int clip255(int v) { return min(max(v, 0), 255); }
+
+// -------------------------------------------------------------- filters
+__global__ __launch_bounds__(256) void k_alpha_filter(int filter, const uint8_t* in, uint8_t* out, int w, int h,
+                                                      int64_t pitch, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t per = (int64_t)w * h;
+  const int64_t img = i / per, r = i - img * per;
+  const int y = (int)(r / w), x = (int)(r % w);
+  const uint8_t* src = in + img * pitch;
+  const int v = src[r];
+  int pred = 0;
+  if (filter != 0) {
+    if (y == 0) {
+      pred = x > 0 ? src[r - 1] : 0;
+    } else if (filter == 2) {
+      pred = src[r - w];
+    } else if (x == 0) {
+      pred = src[r - w];
+    } else {
+      pred = filter == 1 ? src[r - 1] : clip255(src[r - 1] + src[r - w] - src[r - w - 1]);
+    }
+  }
+  out[img * pitch + r] = (uint8_t)(v - pred);
+}
+
+// inclusive scan (mod 256, carried in int) of v over the 64 lanes
+__device__ __forceinline__ int wave_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// scan of n bytes at p, stride `step` (in place): one wave
+__device__ __forceinline__ void scan_line(uint8_t* p, int64_t step, int n, int lane) {
+  int carry = 0;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const int i = c0 + lane;
+    const int v = i < n ? p[i * step] : 0;
+    const int s = wave_scan(v, lane) + carry;
+    if (i < n) p[i * step] = (uint8_t)s;
+    carry = __shfl(s, 63, 64);
+  }
+}
+
+// one wave per (image, line): kind 0 = column 0 of the image, kind 1 = row 0
+__global__ __launch_bounds__(64) void k_alpha_scan_edge(uint8_t* data, int w, int h, int64_t pitch, int kind) {
+  uint8_t* img = data + (int64_t)blockIdx.x * pitch;
+  if (kind == 0)
+    scan_line(img, w, h, threadIdx.x);
+  else
+    scan_line(img, 1, w, threadIdx.x);
+}
+
+// horizontal unfilter, rows: one wave per (image, row); column 0 already holds
+// its prefix, x >= 1 add the row's running sum
+__global__ __launch_bounds__(64) void k_alpha_hrows(uint8_t* data, int w, int h, int64_t pitch) {
+  const int lane = threadIdx.x;
+  const int img = blockIdx.x / h, y = blockIdx.x % h;
+  uint8_t* row = data + img * pitch + (int64_t)y * w;
+  int carry = row[0];
+  for (int c0 = 1; c0 < w; c0 += 64) {
+    const int i = c0 + lane;
+    const int v = i < w ? row[i] : 0;
+    const int s = wave_scan(v, lane) + carry;
+    if (i < w) row[i] = (uint8_t)s;
+    carry = __shfl(s, 63, 64);
+  }
+}
+
+// vertical unfilter below row 0: one thread per column
+__global__ __launch_bounds__(256) void k_alpha_vcols(uint8_t* data, int w, int h, int64_t pitch, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t img = i / w;
+  const int x = (int)(i % w);
+  uint8_t* p = data + img * pitch + x;
+  int acc = p[0];
+  for (int y = 1; y < h; y++) {
+    acc += p[(int64_t)y * w];
+    p[(int64_t)y * w] = (uint8_t)acc;
+  }
+}
+
+struct GArgs {
+  uint8_t* data;
+  int* ctl;       // [0] band dequeue, [1] error
+  int* progress;  // [n_img][bands]
+  int64_t pitch;
+  int w, h, bands, n_img;
+};
+constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
+
+// gradient unfilter below row 0 (row 0 already scanned).  Rows 1.. are cut
+// into bands of 64; band b holds rows 1 + 64b .. 64 + 64b.
+__global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
+  __shared__ uint8_t up_buf[65];  // the band above's last row, columns c0-1 .. c0+63
+  __shared__ int sh_band;
+  const int lane = threadIdx.x;
+  const int w = a.w;
+  const int total = a.bands * a.n_img;
+  for (;;) {
+    if (lane == 0) sh_band = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int idx = __builtin_amdgcn_readfirstlane(sh_band);
+    __syncthreads();
+    if (idx >= total) break;
+    const int band = idx / a.n_img, img = idx % a.n_img;
+    const int y = 1 + band * 64 + lane;
+    const bool live = y < a.h;
+    uint8_t* d = a.data + img * a.pitch;
+    const int* prog_above = a.progress + img * a.bands + band - 1;
+    int* prog_mine = a.progress + img * a.bands + band;
+    const int last_lane = min(63, a.h - 2 - band * 64);
+    int o1 = 0, o2 = 0;  // this lane's outputs at x-1, x-2 (o2: the value before o1)
+    int first = 0;       // row above's value at x = 0 for lane 0 is read with the rest
+    const int steps = w + last_lane;
+    for (int s = 0; s < steps; s++) {
+      const int x = s - lane;
+      if ((s & 63) == 0 && s < w) {  // next 64 columns of the row above this band
+        if (band > 0) {
+          const int need = min(s + 64, w);
+          if (lane == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t it = 0;; it++) {
+              const int seen = __hip_atomic_load(prog_above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (seen >= need) break;
+              if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+                                      __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
+              __builtin_amdgcn_s_sleep(2);
+            }
+          }
+        }
+        const uint8_t* up = d + (int64_t)(band * 64) * w;  // row band*64 (row 0 for band 0)
+        const int c = s + lane;
+        if (c < w) {
+          // the aligned dword holding the byte, read around L1 (same page as the byte)
+          const uintptr_t addr = reinterpret_cast<uintptr_t>(up + c);
+          const uint32_t word = __hip_atomic_load(reinterpret_cast<const uint32_t*>(addr & ~uintptr_t(3)),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          up_buf[lane + 1] = (uint8_t)(word >> (8 * (addr & 3)));
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      // row above at x (lane k-1's newest output) and x-1 (its previous one)
+      int top = __shfl_up(o1, 1, 64), top_left = __shfl_up(o2, 1, 64);
+      if (lane == 0 && x < w) {
+        const int k = x - (s & ~63);  // x - c0
+        top = up_buf[k + 1];
+        top_left = k > 0 ? up_buf[k] : (x > 0 ? first : top);
+      }
+      if (live && x >= 0 && x < w) {
+        // x == 0: left = top_left = top (alpha.go:177-181)
+        const int left = x == 0 ? top : o1;
+        const int tl = x == 0 ? top : top_left;
+        const int v = (d[(int64_t)y * w + x] + clip255(left + top - tl)) & 0xff;
+        o2 = o1;
+        o1 = v;
+        uint8_t* dst = d + (int64_t)y * w + x;
+        *dst = (uint8_t)v;
+      } else {
+        o2 = o1;
+        o1 = 0;
+      }
+      if (lane == 0 && (s & 63) == 63) first = up_buf[64];  // column c0+63 for the next chunk's x-1
+      // publish the band's last row every 64 columns (and at its end)
+      const int xl = s - last_lane;
+      if (band + 1 < a.bands && xl >= 0 && ((xl & 63) == 63 || xl == w - 1)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == last_lane) __hip_atomic_store(prog_mine, xl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// -------------------------------------------------------------- estimate
+__global__ __launch_bounds__(64) void k_alpha_estimate(const uint8_t* data, int w, int h, int64_t pitch, int n_img,
+                                                       unsigned long long* bins) {
+  const int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int rows = (h - 2) / 2;  // j = 2, 4, .. < h - 1
+  if (rows <= 0 || t >= (int64_t)rows * n_img) return;
+  const int img = (int)(t / rows), j = 2 + 2 * (int)(t % rows);
+  if (j >= h - 1) return;
+  const uint8_t* p = data + img * pitch + (int64_t)j * w;
+  unsigned long long seen = 0;
+  int mean = p[0];
+  for (int i = 2; i < w - 1; i += 2) {
+    const int cur = p[i];
+    const int d0 = abs(cur - mean) >> 4, d1 = abs(cur - p[i - 1]) >> 4, d2 = abs(cur - p[i - w]) >> 4;
+    const int d3 = abs(cur - clip255(p[i - 1] + p[i - w] - p[i - w - 1])) >> 4;
+    if (d0 < 16) seen |= 1ull << d0;
+    if (d1 < 16) seen |= 1ull << (16 + d1);
+    if (d2 < 16) seen |= 1ull << (32 + d2);
+    if (d3 < 16) seen |= 1ull << (48 + d3);
+    mean = (3 * mean + cur + 2) >> 2;
+  }
+  if (seen) atomicOr(&bins[img], seen);
+}
+
+__global__ __launch_bounds__(256) void k_alpha_colors(const uint8_t* data, int w, int h, int64_t pitch,
+                                                      uint32_t* sets, int64_t total) {
+  __shared__ uint32_t set[8];
+  if (threadIdx.x < 8) set[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t per = (int64_t)w * h;
+  const int64_t i0 = (int64_t)blockIdx.x * 256;
+  const int64_t i = i0 + threadIdx.x;
+  const int64_t img0 = i0 / per;  // blocks may straddle two images: track the first, flush others directly
+  if (i < total) {
+    const int64_t img = i / per;
+    const int v = data[img * pitch + (i - img * per)];
+    if (img == img0)
+      atomicOr(&set[v >> 5], 1u << (v & 31));
+    else
+      atomicOr(&sets[img * 8 + (v >> 5)], 1u << (v & 31));
+  }
+  __syncthreads();
+  if (threadIdx.x < 8 && set[threadIdx.x]) atomicOr(&sets[img0 * 8 + threadIdx.x], set[threadIdx.x]);
+}
+
+__global__ void k_alpha_finalize(const unsigned long long* bins, const uint32_t* sets, int n_img, int32_t* best,
+                                 int32_t* colors) {
+  const int img = blockIdx.x * blockDim.x + threadIdx.x;
+  if (img >= n_img) return;
+  const unsigned long long b = bins[img];
+  int bf = 0, bs = 0x7fffffff;
+  for (int f = 0; f < 4; f++) {
+    int score = 0;
+    for (int i = 0; i < 16; i++)
+      if ((b >> (16 * f + i)) & 1) score += i;
+    if (score < bs) {
+      bs = score;
+      bf = f;
+    }
+  }
+  int nc = 0;
+  for (int k = 0; k < 8; k++) nc += __popc(sets[img * 8 + k]);
+  best[img] = bf;
+  colors[img] = nc;
+}
+
+// -------------------------------------------------------------- premultiply
+__device__ __forceinline__ uint32_t a_mult(uint32_t x, uint32_t mult) { return (x * mult + (1u << 23)) >> 24; }
+__device__ __forceinline__ uint32_t a_scale(uint32_t a, int inverse) {
+  return inverse ? (255u << 24) / a : a * ((1u << 24) / 255);
+}
+
+__global__ __launch_bounds__(256) void k_alpha_multiply(uint8_t* rgba, int alpha_first, int w, int h, int stride,
+                                                        int64_t pitch, int inverse, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t per = (int64_t)w * h;
+  const int64_t img = i / per, r = i - img * per;
+  uint8_t* p = rgba + img * pitch + (r / w) * stride + 4 * (r % w);
+  const uint32_t word = *reinterpret_cast<const uint32_t*>(p);
+  const int ao = alpha_first ? 0 : 3, ro = alpha_first ? 1 : 0;
+  const uint32_t a = (word >> (8 * ao)) & 0xff;
+  if (a == 255) return;
+  uint32_t out = word & (0xffu << (8 * ao));
+  if (a != 0) {
+    const uint32_t s = a_scale(a, inverse);
+#pragma unroll
+    for (int c = 0; c < 3; c++) out |= (a_mult((word >> (8 * (ro + c))) & 0xff, s) & 0xff) << (8 * (ro + c));
+  }
+  *reinterpret_cast<uint32_t*>(p) = out;
+}
+
+__global__ __launch_bounds__(256) void k_mult_argb(uint32_t* argb, int64_t n, int inverse) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = argb[i];
+  if (p >= 0xff000000u) return;
+  if (p <= 0x00ffffffu) {
+    argb[i] = 0;
+    return;
+  }
+  const uint32_t s = a_scale((p >> 24) & 0xff, inverse);
+  argb[i] = (p & 0xff000000u) | (a_mult(p & 0xff, s) & 0xff) | (a_mult((p >> 8) & 0xff, s) & 0xff) << 8 |
+            (a_mult((p >> 16) & 0xff, s) & 0xff) << 16;
+}
+
+__global__ __launch_bounds__(256) void k_alpha_4444(uint8_t* data, int w, int h, int stride, int64_t pitch,
+                                                    int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t per = (int64_t)w * h;
+  const int64_t img = i / per, r = i - img * per;
+  uint8_t* p = data + img * pitch + (r / w) * stride + 2 * (r % w);
+  const int rg = p[0], ba = p[1], a = ba & 0x0f;
+  if (a == 0x0f) return;
+  if (a == 0) {
+    p[0] = p[1] = 0;
+    return;
+  }
+  const int rr = (((rg >> 4) & 0x0f) * a + 7) / 15, gg = ((rg & 0x0f) * a + 7) / 15, bb = (((ba >> 4) & 0x0f) * a + 7) / 15;
+  p[0] = (uint8_t)(rr << 4 | gg);
+  p[1] = (uint8_t)(bb << 4 | a);
+}
+
+// -------------------------------------------------------------- dispatch / extract
+__global__ __launch_bounds__(256) void k_dispatch_alpha(const uint8_t* alpha, int alpha_stride, int w, int h,
+                                                        uint8_t* dst, int dst_stride, int alpha_off, int* any_transparent) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool in = i < (int64_t)w * h;
+  int v = 0xff;
+  if (in) {
+    const int y = (int)(i / w), x = (int)(i % w);
+    v = alpha[(int64_t)y * alpha_stride + x];
+    dst[(int64_t)y * dst_stride + 4 * x + alpha_off] = (uint8_t)v;
+  }
+  if (__ballot(v != 0xff) && (threadIdx.x & 63) == 0) atomicOr(any_transparent, 1);
+}
+
+__global__ __launch_bounds__(256) void k_extract_alpha(const uint8_t* src, int src_stride, int w, int h, uint8_t* alpha,
+                                                       int alpha_stride, int alpha_off, int* and_mask) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool in = i < (int64_t)w * h;
+  int v = 0xff;
+  if (in) {
+    const int y = (int)(i / w), x = (int)(i % w);
+    v = src[(int64_t)y * src_stride + 4 * x + alpha_off];
+    alpha[(int64_t)y * alpha_stride + x] = (uint8_t)v;
+  }
+  if (__ballot(v != 0xff) && (threadIdx.x & 63) == 0) atomicAnd(and_mask, 0);
+}
+
+// -------------------------------------------------------------- small row helpers (alpha_proc.go:178-238)
+// HasAlpha8b / HasAlpha32b: any byte at i * step (i < n) other than 0xff
+__global__ __launch_bounds__(256) void k_has_alpha(const uint8_t* src, int64_t n, int step, int* any) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool hit = i < n && src[i * step] != 0xff;
+  if (__ballot(hit) && (threadIdx.x & 63) == 0) atomicOr(any, 1);
+}
+
+__global__ __launch_bounds__(256) void k_alpha_replace(uint32_t* argb, int64_t n, uint32_t color) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n && (argb[i] >> 24) == 0) argb[i] = color;
+}
+
+__global__ __launch_bounds__(256) void k_alpha_to_green(const uint8_t* alpha, int alpha_stride, int w, int h,
+                                                        uint32_t* dst, int dst_stride) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)w * h) return;
+  const int y = (int)(i / w), x = (int)(i % w);
+  dst[(int64_t)y * dst_stride + x] = (uint32_t)alpha[(int64_t)y * alpha_stride + x] << 8;
+}
+
+__global__ __launch_bounds__(256) void k_extract_green(const uint32_t* argb, uint8_t* alpha, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) alpha[i] = (uint8_t)(argb[i] >> 8);
+}
+
+__global__ __launch_bounds__(256) void k_pack_rgb(const uint8_t* r, const uint8_t* g, const uint8_t* b, int64_t n,
+                                                  int step, uint32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t o = i * step;
+  out[i] = 0xff000000u | (uint32_t)r[o] << 16 | (uint32_t)g[o] << 8 | (uint32_t)b[o];
+}
+
+unsigned grid_of(int64_t total, int block) { return (unsigned)((total + block - 1) / block); }
+
+}  // namespace
+
+extern "C" int wg_alpha_filter(int32_t filter, const uint8_t* in, uint8_t* out, int32_t width, int32_t height,
+                               int64_t pitch, int32_t n_images, void* stream) {
+  WG_REQUIRE(in && out && width > 0 && height > 0 && n_images > 0 && filter >= 0 && filter <= 3);
+  WG_REQUIRE(pitch >= (int64_t)width * height);
+  const int64_t total = (int64_t)width * height * n_images;
+  hipLaunchKernelGGL(k_alpha_filter, dim3(grid_of(total, 256)), dim3(256), 0, wg::as_stream(stream), (int)filter, in, out,
+                     (int)width, (int)height, pitch, total);
+  return wg::check_launch("k_alpha_filter");
+}
+
+extern "C" size_t wg_alpha_unfilter_work_bytes(int32_t height, int32_t n_images) {
+  if (height <= 0 || n_images <= 0) return 0;
+  const int bands = (height - 1 + 63) / 64;
+  return sizeof(int) * (4 + (size_t)n_images * (bands > 0 ? bands : 1));
+}
+
+extern "C" int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, int32_t height, int64_t pitch,
+                                 int32_t n_images, void* work, void* stream) {
+  WG_REQUIRE(data && width > 0 && height > 0 && n_images > 0 && filter >= 0 && filter <= 3);
+  WG_REQUIRE(pitch >= (int64_t)width * height);
+  hipStream_t s = wg::as_stream(stream);
+  if (filter == 0) return WG_OK;
+  if (filter == 1) {
+    hipLaunchKernelGGL(k_alpha_scan_edge, dim3(n_images), dim3(64), 0, s, data, (int)width, (int)height, pitch, 0);
+    int rc = wg::check_launch("k_alpha_scan_edge");
+    if (rc != WG_OK) return rc;
+    hipLaunchKernelGGL(k_alpha_hrows, dim3((unsigned)((int64_t)height * n_images)), dim3(64), 0, s, data, (int)width,
+                       (int)height, pitch);
+    return wg::check_launch("k_alpha_hrows");
+  }
+  hipLaunchKernelGGL(k_alpha_scan_edge, dim3(n_images), dim3(64), 0, s, data, (int)width, (int)height, pitch, 1);
+  int rc = wg::check_launch("k_alpha_scan_edge");
+  if (rc != WG_OK || height == 1) return rc;
+  if (filter == 2) {
+    const int64_t total = (int64_t)width * n_images;
+    hipLaunchKernelGGL(k_alpha_vcols, dim3(grid_of(total, 256)), dim3(256), 0, s, data, (int)width, (int)height, pitch,
+                       total);
+    return wg::check_launch("k_alpha_vcols");
+  }
+  WG_REQUIRE(work);
+  GArgs a;
+  a.data = data;
+  a.ctl = static_cast<int*>(work);
+  a.progress = a.ctl + 4;
+  a.pitch = pitch;
+  a.w = width;
+  a.h = height;
+  a.bands = (height - 1 + 63) / 64;
+  a.n_img = n_images;
+  if (hipMemsetAsync(work, 0, wg_alpha_unfilter_work_bytes(height, n_images), s) != hipSuccess)
+    return wg::check_launch("hipMemsetAsync(alpha work)");
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return wg::check_launch("device query");
+  const int total = a.bands * n_images;
+  const int grid = total < 4 * cus ? total : 4 * cus;
+  hipLaunchKernelGGL(k_alpha_gbands, dim3(grid), dim3(64), 0, s, a);
+  return wg::check_launch("k_alpha_gbands");
+}
+
+extern "C" int wg_alpha_unfilter_status(const void* work, void* stream) {
+  WG_REQUIRE(work);
+  int flag = 0;
+  hipStream_t s = wg::as_stream(stream);
+  if (hipMemcpyAsync(&flag, static_cast<const int*>(work) + 1, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return wg::check_launch("wg_alpha_unfilter_status");
+  if (flag) {
+    wg::set_error("alpha unfilter: a band wait timed out (output invalid)");
+    return WG_EHIP;
+  }
+  return WG_OK;
+}
+
+extern "C" size_t wg_alpha_estimate_work_bytes(int32_t n_images) {
+  return n_images > 0 ? (size_t)n_images * (sizeof(unsigned long long) + 8 * sizeof(uint32_t)) : 0;
+}
+
+extern "C" int wg_alpha_estimate_filter(const uint8_t* data, int32_t width, int32_t height, int64_t pitch,
+                                        int32_t n_images, int32_t* best_filter, int32_t* num_colors, void* work,
+                                        void* stream) {
+  WG_REQUIRE(data && best_filter && num_colors && work && width > 0 && height > 0 && n_images > 0);
+  WG_REQUIRE(pitch >= (int64_t)width * height);
+  hipStream_t s = wg::as_stream(stream);
+  unsigned long long* bins = static_cast<unsigned long long*>(work);
+  uint32_t* sets = reinterpret_cast<uint32_t*>(bins + n_images);
+  if (hipMemsetAsync(work, 0, wg_alpha_estimate_work_bytes(n_images), s) != hipSuccess)
+    return wg::check_launch("hipMemsetAsync(alpha estimate)");
+  const int rows = (height - 2) / 2;
+  if (rows > 0) {
+    hipLaunchKernelGGL(k_alpha_estimate, dim3(grid_of((int64_t)rows * n_images, 64)), dim3(64), 0, s, data, (int)width,
+                       (int)height, pitch, (int)n_images, bins);
+    const int rc = wg::check_launch("k_alpha_estimate");
+    if (rc != WG_OK) return rc;
+  }
+  const int64_t total = (int64_t)width * height * n_images;
+  hipLaunchKernelGGL(k_alpha_colors, dim3(grid_of(total, 256)), dim3(256), 0, s, data, (int)width, (int)height, pitch,
+                     sets, total);
+  int rc = wg::check_launch("k_alpha_colors");
+  if (rc != WG_OK) return rc;
+  hipLaunchKernelGGL(k_alpha_finalize, dim3(grid_of(n_images, 64)), dim3(64), 0, s, bins, sets, (int)n_images,
+                     best_filter, num_colors);
+  return wg::check_launch("k_alpha_finalize");
+}
+
+extern "C" int wg_apply_alpha_multiply(uint8_t* rgba, int32_t alpha_first, int32_t width, int32_t height,
+                                       int32_t stride, int64_t pitch, int32_t n_images, int32_t inverse, void* stream) {
+  WG_REQUIRE(rgba && width > 0 && height > 0 && n_images > 0 && stride >= 4 * width);
+  WG_REQUIRE((stride & 3) == 0 && (pitch & 3) == 0 && (reinterpret_cast<uintptr_t>(rgba) & 3) == 0);
+  WG_REQUIRE(pitch >= (int64_t)stride * (height - 1) + 4 * width);
+  const int64_t total = (int64_t)width * height * n_images;
+  hipLaunchKernelGGL(k_alpha_multiply, dim3(grid_of(total, 256)), dim3(256), 0, wg::as_stream(stream), rgba,
+                     (int)(alpha_first != 0), (int)width, (int)height, (int)stride, pitch, (int)(inverse != 0), total);
+  return wg::check_launch("k_alpha_multiply");
+}
+
+extern "C" int wg_mult_argb(uint32_t* argb, int64_t n, int32_t inverse, void* stream) {
+  WG_REQUIRE(argb && n >= 0);
+  if (n == 0) return WG_OK;
+  hipLaunchKernelGGL(k_mult_argb, dim3(grid_of(n, 256)), dim3(256), 0, wg::as_stream(stream), argb, n, (int)(inverse != 0));
+  return wg::check_launch("k_mult_argb");
+}
+
+extern "C" int wg_apply_alpha_multiply_4444(uint8_t* data, int32_t width, int32_t height, int32_t stride,
+                                            int64_t pitch, int32_t n_images, void* stream) {
+  WG_REQUIRE(data && width > 0 && height > 0 && n_images > 0 && stride >= 2 * width);
+  WG_REQUIRE(pitch >= (int64_t)stride * (height - 1) + 2 * width);
+  const int64_t total = (int64_t)width * height * n_images;
+  hipLaunchKernelGGL(k_alpha_4444, dim3(grid_of(total, 256)), dim3(256), 0, wg::as_stream(stream), data, (int)width,
+                     (int)height, (int)stride, pitch, total);
+  return wg::check_launch("k_alpha_4444");
+}
+
+extern "C" int wg_dispatch_alpha(const uint8_t* alpha, int32_t alpha_stride, int32_t width, int32_t height, uint8_t* dst,
+                                 int32_t dst_stride, int32_t alpha_off, int32_t* has_transparency, void* stream) {
+  WG_REQUIRE(alpha && dst && has_transparency && width > 0 && height > 0 && alpha_off >= 0 && alpha_off <= 3);
+  WG_REQUIRE(alpha_stride >= width && dst_stride >= 4 * width);
+  hipStream_t s = wg::as_stream(stream);
+  if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(has_transparency), 0, 1, s) != hipSuccess)
+    return wg::check_launch("hipMemsetD32Async(dispatch flag)");
+  hipLaunchKernelGGL(k_dispatch_alpha, dim3(grid_of((int64_t)width * height, 256)), dim3(256), 0, s, alpha,
+                     (int)alpha_stride, (int)width, (int)height, dst, (int)dst_stride, (int)alpha_off,
+                     reinterpret_cast<int*>(has_transparency));
+  return wg::check_launch("k_dispatch_alpha");
+}
+
+extern "C" int wg_extract_alpha(const uint8_t* src, int32_t src_stride, int32_t width, int32_t height, uint8_t* alpha,
+                                int32_t alpha_stride, int32_t alpha_off, int32_t* all_opaque, void* stream) {
+  WG_REQUIRE(src && alpha && all_opaque && width > 0 && height > 0 && alpha_off >= 0 && alpha_off <= 3);
+  WG_REQUIRE(alpha_stride >= width && src_stride >= 4 * width);
+  hipStream_t s = wg::as_stream(stream);
+  if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(all_opaque), 1, 1, s) != hipSuccess)
+    return wg::check_launch("hipMemsetD32Async(extract flag)");
+  hipLaunchKernelGGL(k_extract_alpha, dim3(grid_of((int64_t)width * height, 256)), dim3(256), 0, s, src,
+                     (int)src_stride, (int)width, (int)height, alpha, (int)alpha_stride, (int)alpha_off,
+                     reinterpret_cast<int*>(all_opaque));
+  return wg::check_launch("k_extract_alpha");
+}
+
+extern "C" int wg_has_alpha(const uint8_t* src, int64_t length, int32_t step, int32_t* any_transparent, void* stream) {
+  WG_REQUIRE(src && any_transparent && length >= 0 && (step == 1 || step == 4));
+  hipStream_t s = wg::as_stream(stream);
+  if (hipMemsetAsync(any_transparent, 0, sizeof(int32_t), s) != hipSuccess)
+    return wg::check_launch("hipMemsetAsync(has_alpha flag)");
+  if (length == 0) return WG_OK;
+  hipLaunchKernelGGL(k_has_alpha, dim3(grid_of(length, 256)), dim3(256), 0, s, src, length, (int)step, any_transparent);
+  return wg::check_launch("k_has_alpha");
+}
+
+extern "C" int wg_alpha_replace(uint32_t* argb, int64_t length, uint32_t color, void* stream) {
+  WG_REQUIRE(argb && length >= 0);
+  if (length == 0) return WG_OK;
+  hipLaunchKernelGGL(k_alpha_replace, dim3(grid_of(length, 256)), dim3(256), 0, wg::as_stream(stream), argb, length,
+                     color);
+  return wg::check_launch("k_alpha_replace");
+}
+
+extern "C" int wg_dispatch_alpha_to_green(const uint8_t* alpha, int32_t alpha_stride, int32_t width, int32_t height,
+                                          uint32_t* dst, int32_t dst_stride, void* stream) {
+  WG_REQUIRE(alpha && dst && width > 0 && height > 0 && alpha_stride >= width && dst_stride >= width);
+  hipLaunchKernelGGL(k_alpha_to_green, dim3(grid_of((int64_t)width * height, 256)), dim3(256), 0,
+                     wg::as_stream(stream), alpha, (int)alpha_stride, (int)width, (int)height, dst, (int)dst_stride);
+  return wg::check_launch("k_alpha_to_green");
+}
+
+extern "C" int wg_extract_green(const uint32_t* argb, uint8_t* alpha, int64_t size, void* stream) {
+  WG_REQUIRE(argb && alpha && size >= 0);
+  if (size == 0) return WG_OK;
+  hipLaunchKernelGGL(k_extract_green, dim3(grid_of(size, 256)), dim3(256), 0, wg::as_stream(stream), argb, alpha, size);
+  return wg::check_launch("k_extract_green");
+}
+
+extern "C" int wg_pack_rgb(const uint8_t* r, const uint8_t* g, const uint8_t* b, int64_t length, int32_t step,
+                           uint32_t* out, void* stream) {
+  WG_REQUIRE(r && g && b && out && length >= 0 && step > 0);
+  if (length == 0) return WG_OK;
+  hipLaunchKernelGGL(k_pack_rgb, dim3(grid_of(length, 256)), dim3(256), 0, wg::as_stream(stream), r, g, b, length,
+                     (int)step, out);
+  return wg::check_launch("k_pack_rgb");
+}
