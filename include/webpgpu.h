@@ -331,6 +331,32 @@ int wg_pack_rgb(const uint8_t* r, const uint8_t* g, const uint8_t* b, int64_t le
                 void* stream);
 
 /* ===================================================================== *
+ * 3d. Row rescaler: internal/dsp/rescale.go's Rescaler
+ *     (RescalerInit :63, RescalerImportRow :110, RescalerExportRow :185),
+ *     driven over whole planes: import a source row while RescalerNeedsSrcRow,
+ *     else export a destination row, until dst_height rows are out or the
+ *     source is exhausted.  The Go arithmetic is kept as written (it is not
+ *     libwebp's: no x_add-1 adjustment, FYScale only when expanding), so for
+ *     some sizes fewer than dst_height rows come out; `rows` reports how many.
+ * ===================================================================== */
+
+/* device bytes of a plan for dst_width x dst_height */
+size_t wg_rescaler_plan_bytes(int32_t dst_width, int32_t dst_height);
+/* Builds the plan (the size-only walk of the Go state machine) on the host
+ * and copies it into `plan` (device memory) on `stream`, synchronising it;
+ * *rows (host) = destination rows the driver writes. */
+int wg_rescaler_plan(int32_t src_width, int32_t src_height, int32_t dst_width, int32_t dst_height, void* plan,
+                     int32_t* rows, void* stream);
+/* the same plan into host memory (no device work; for inspection and tests).
+ * Layout: a 64-byte header, 32 bytes per destination column, 16 per row. */
+int wg_rescaler_plan_host(int32_t src_width, int32_t src_height, int32_t dst_width, int32_t dst_height,
+                          void* plan_host, int32_t* rows);
+/* Rescales n_images planes (images src_pitch / dst_pitch bytes apart) with a
+ * plan built for these sizes; rows and dst_width as returned / planned. */
+int wg_rescale(const void* plan, int32_t dst_width, int32_t rows, const uint8_t* src, int64_t src_stride,
+               int64_t src_pitch, uint8_t* dst, int64_t dst_stride, int64_t dst_pitch, int32_t n_images, void* stream);
+
+/* ===================================================================== *
  * 4. SharpYUV: sharpyuv.Convert with SharpEnabled and the
  *    sRGB transfer (sharpyuv/sharpyuv.go:39-64, convertSharp :170-269).
  * ===================================================================== */

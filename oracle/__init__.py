@@ -121,6 +121,7 @@ _SIGS = {
     "or_dispatch_alpha_to_green": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i]),
     "or_extract_green": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     "or_pack_rgb": (None, [ctypes.c_void_p] * 3 + [ctypes.c_size_t, _i, ctypes.c_void_p]),
+    "or_rescale_plane": (_i, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i, _i, _i]),
     "or_sharpyuv_tables": (None, [ctypes.c_void_p, ctypes.c_void_p]),
     "or_setup_segment": (None, [_i] * 8 + [ctypes.c_void_p]),
     "or_fixed_costs_i4": (None, [ctypes.c_void_p]),
@@ -388,6 +389,16 @@ def pack_rgb(r, g, b, length, step):
     out = np.empty(length, np.uint32)
     lib.or_pack_rgb(r.ctypes.data, g.ctypes.data, b.ctypes.data, length, step, out.ctypes.data)
     return out
+
+
+def rescale_plane(src, dst_width, dst_height):
+    """Drive dsp.Rescaler (rescale.go:63-257) over a (h, w) uint8 plane.
+    -> (dst (dst_height, dst_width) uint8, rows written); unwritten rows are 0."""
+    s = np.ascontiguousarray(src, np.uint8)
+    sh, sw = s.shape
+    out = np.zeros((dst_height, dst_width), np.uint8)
+    rows = lib.or_rescale_plane(s.ctypes.data, sw, sh, sw, out.ctypes.data, dst_width, dst_height, dst_width)
+    return out, rows
 
 
 # ---------------- SharpYUV ----------------

@@ -181,6 +181,25 @@ void or_dispatch_alpha_to_green(const uint8_t* alpha, int alpha_stride, int widt
 void or_extract_green(const uint32_t* argb, uint8_t* alpha, size_t size);
 void or_pack_rgb(const uint8_t* r, const uint8_t* g, const uint8_t* b, size_t length, int step, uint32_t* out);
 
+/* rescale.c: the row rescaler (internal/dsp/rescale.go) */
+typedef struct {          /* dsp.Rescaler (rescale.go:14-41) */
+  int src_width, src_height, dst_width, dst_height;
+  int x_expand, y_expand;
+  int32_t* frow;
+  int32_t* irow;
+  int64_t y_accum;
+  int y_add, y_sub, x_add, x_sub;
+  uint32_t fx_scale, fy_scale, fxy_scale;
+  int src_y, dst_y;
+} or_rescaler;
+void or_rescaler_init(or_rescaler* r, int sw, int sh, int dw, int dh);
+void or_rescaler_free(or_rescaler* r);
+void or_rescaler_import_row(or_rescaler* r, const uint8_t* src);
+int or_rescaler_export_row(or_rescaler* r, uint8_t* dst);
+/* plane driver: returns the number of destination rows written */
+int or_rescale_plane(const uint8_t* src, int sw, int sh, int src_stride, uint8_t* dst, int dw, int dh,
+                     int dst_stride);
+
 /* ---- Encoder MB RD loop (lossy_rd.c; encode_parallel.go Phase A) ---- */
 typedef struct {          /* SegmentQuant (encode.go:311-323) */
   int32_t quant, iquant, bias, zthresh;

@@ -79,6 +79,10 @@ SIGNATURES = {
     "wg_dispatch_alpha_to_green": [_vp, _i32, _i32, _i32, _vp, _i32, _vp],
     "wg_extract_green": [_vp, _vp, _i64, _vp],
     "wg_pack_rgb": [_vp, _vp, _vp, _i64, _i32, _vp, _vp],
+    "wg_rescaler_plan_bytes": [_i32, _i32],
+    "wg_rescaler_plan_host": [_i32, _i32, _i32, _i32, _vp, _vp],
+    "wg_rescaler_plan": [_i32, _i32, _i32, _i32, _vp, _vp, _vp],
+    "wg_rescale": [_vp, _i32, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _vp],
     "wg_sharpyuv_work_bytes": [_i32, _i32, _i32],
     "wg_sharpyuv_convert": [_vp, _i32, _i32, _i32, _i64, _vp, _i32, _vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _vp],
     "wg_sharpyuv_tables_host": [_vp, _vp],
@@ -91,7 +95,8 @@ SIGNATURES = {
 _RES = {"wg_last_error": ctypes.c_char_p, "wg_decode_work_bytes": ctypes.c_size_t,
         "wg_plane_ssim_work_bytes": ctypes.c_size_t, "wg_vp8l_inverse_work_bytes": ctypes.c_size_t,
         "wg_sharpyuv_work_bytes": ctypes.c_size_t, "wg_encode_work_bytes": ctypes.c_size_t,
-        "wg_alpha_unfilter_work_bytes": ctypes.c_size_t, "wg_alpha_estimate_work_bytes": ctypes.c_size_t}
+        "wg_alpha_unfilter_work_bytes": ctypes.c_size_t, "wg_alpha_estimate_work_bytes": ctypes.c_size_t,
+        "wg_rescaler_plan_bytes": ctypes.c_size_t}
 
 for _name, _args in SIGNATURES.items():
     _f = getattr(lib, _name)
