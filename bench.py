@@ -58,6 +58,30 @@ def pmc_traffic(kernel):
         return None, None
 
 
+VALU_FILE = os.path.join(ROOT, "profiles", "pmc_valu.json")
+# VALU issue peak: 256 CUs x 4 SIMDs, one 64-lane VALU instruction per SIMD
+# every 2 cycles (MI355X_MICROARCH.md), at the 2.4 GHz peak clock.
+VALU_PEAK_WINST_S = 256 * 4 * 0.5 * 2.4e9
+
+
+def pmc_valu(kernel, launch_ms):
+    """VALU issue rate of `kernel` from the committed SQ pass (tools/profile.sh:
+    SQ_INSTS_VALU per launch) over this run's measured launch time, against
+    the SIMD issue peak; None if the pass is absent."""
+    try:
+        rec = json.load(open(VALU_FILE))[kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+    insts = rec["SQ_INSTS_VALU"]
+    rate = insts / (launch_ms / 1e3)
+    out = {"kernel": kernel, "insts_valu_per_launch": int(insts), "achieved": round(rate / 1e12, 4),
+           "peak": round(VALU_PEAK_WINST_S / 1e12, 4), "unit": "T wave-instr/s",
+           "frac": round(rate / VALU_PEAK_WINST_S, 4), "source": os.path.relpath(VALU_FILE, ROOT)}
+    if "GRBM_GUI_ACTIVE" in rec:
+        out["effective_clock_ghz"] = round(rec["GRBM_GUI_ACTIVE"] / 8 / (launch_ms / 1e3) / 1e9, 3)
+    return out
+
+
 def default_proba():
     """CoeffsProba0 (internal/lossy/proba.go:45): the token probabilities
     Phase A prices with after ResetProba; read from the generated table."""
@@ -76,6 +100,7 @@ def parse():
     p.add_argument("--batch", type=int, default=64, help="frames per GPU per step (C4: 512 frames / 8 GPUs)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget for the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--slots", type=int, default=1, help="batches in flight (one HIP stream each)")
     return p.parse_args()
 
 
@@ -100,56 +125,78 @@ def make_inputs(batch, rank, device):
     return rgba, mb_all.view(-1, 32), co_all.view(-1, 384), (mb, co)
 
 
-class Pipeline:
-    """Pre-allocated buffers + the 4 stages; optional per-stage HIP events."""
+class Slot:
+    """One in-flight batch: its own HIP stream and every output / work buffer."""
 
-    def __init__(self, rgba, mb, co, batch, device):
-        from webp_amd import _lib, frames
-        self.frames = frames
-        self.rgba, self.mb, self.co, self.batch = rgba, mb, co, batch
+    def __init__(self, batch, device, frames, lib):
+        self.stream = torch.cuda.Stream(device)
         self.Y = torch.empty((batch, 16 * MBH, 16 * MBW), dtype=torch.uint8, device=device)
         self.U = torch.empty((batch, 8 * MBH, 8 * MBW), dtype=torch.uint8, device=device)
         self.V = torch.empty_like(self.U)
         self.alphas = torch.empty((batch, MBW * MBH), dtype=torch.int32, device=device)
         self.uv_sum = torch.empty((batch,), dtype=torch.int32, device=device)
-        self.segs = torch.from_numpy(np.stack([frames.setup_segment(q) for q in SEG_Q]).view(np.uint8).copy()).to(device)
-        self.proba = torch.from_numpy(default_proba()).to(device)
         self.seg_ids = torch.empty((batch, MBW * MBH), dtype=torch.uint8, device=device)
         self.enc_out = torch.empty((batch * MBW * MBH, frames.MB_ENC_DTYPE.itemsize), dtype=torch.uint8, device=device)
         self.rY, self.rU, self.rV = torch.empty_like(self.Y), torch.empty_like(self.U), torch.empty_like(self.U)
-        self.enc_work = torch.empty(_lib.lib.wg_encode_work_bytes(MBW, MBH, batch), dtype=torch.uint8, device=device)
+        self.enc_work = torch.empty(lib.wg_encode_work_bytes(MBW, MBH, batch), dtype=torch.uint8, device=device)
         self.dY = torch.empty_like(self.Y)
         self.dU = torch.empty_like(self.U)
         self.dV = torch.empty_like(self.U)
-        self.work = torch.empty(_lib.lib.wg_decode_work_bytes(MBW, MBH, batch), dtype=torch.uint8, device=device)
+        self.work = torch.empty(lib.wg_decode_work_bytes(MBW, MBH, batch), dtype=torch.uint8, device=device)
         self.out = torch.empty((batch, H, W, 4), dtype=torch.uint8, device=device)
+
+
+class Pipeline:
+    """The 5 stages over pre-allocated buffers, optional per-stage HIP events.
+
+    With `slots` > 1, consecutive steps alternate between slots, each with its
+    own HIP stream and buffers, so step k+1's kernels fill the CUs that step
+    k's encoder RD wavefront leaves idle in its ramp-down.  Every
+    step still runs every stage over its whole batch; the timed region ends
+    with a device-wide synchronisation."""
+
+    def __init__(self, rgba, mb, co, batch, device, slots=1):
+        from webp_amd import _lib, frames
+        self.frames = frames
+        self.rgba, self.mb, self.co, self.batch = rgba, mb, co, batch
+        self.segs = torch.from_numpy(np.stack([frames.setup_segment(q) for q in SEG_Q]).view(np.uint8).copy()).to(device)
+        self.proba = torch.from_numpy(default_proba()).to(device)
+        self.slots = [Slot(batch, device, frames, _lib.lib) for _ in range(slots)]
+        self.k = 0
         self.stage_ms = {k: 0.0 for k in BYTES_PER_PX}
         self.events = []
+        torch.cuda.synchronize(device)  # inputs made on the default stream are ready for every slot stream
 
     def step(self, record=False):
+        sl = self.slots[self.k % len(self.slots)]
+        self.k += 1
+        with torch.cuda.stream(sl.stream):
+            self._stages(sl, record)
+
+    def _stages(self, sl, record):
         f = self.frames
         ev = []
+
+        def mark():
+            if record:
+                ev.append(torch.cuda.Event(enable_timing=True))
+                ev[-1].record()  # on the slot's stream (the current stream here)
+
+        mark()
+        f.import_rgba(self.rgba, has_alpha=False, out=(sl.Y, sl.U, sl.V))
+        mark()
+        f.analysis_alphas(sl.Y, sl.U, sl.V, W, H, out=(sl.alphas, sl.uv_sum, None, None))
+        mark()
+        torch.clamp(sl.alphas >> 6, max=3, out=sl.alphas)
+        sl.seg_ids.copy_(sl.alphas)
+        f.encode_mbs(sl.Y, sl.U, sl.V, W, H, sl.seg_ids, self.segs, self.proba, out=sl.enc_out,
+                     recon=(sl.rY, sl.rU, sl.rV), work=sl.enc_work)
+        mark()
+        f.decode_frames(self.mb, self.co, 2, MBW, MBH, self.batch, out=(sl.dY, sl.dU, sl.dV), work=sl.work)
+        mark()
+        f.build_nrgba(sl.dY, sl.dU, sl.dV, W, H, out=sl.out)
+        mark()
         if record:
-            ev.append(torch.cuda.Event(enable_timing=True))
-            ev[-1].record()
-        f.import_rgba(self.rgba, has_alpha=False, out=(self.Y, self.U, self.V))
-        if record:
-            ev.append(torch.cuda.Event(enable_timing=True)); ev[-1].record()
-        f.analysis_alphas(self.Y, self.U, self.V, W, H, out=(self.alphas, self.uv_sum, None, None))
-        if record:
-            ev.append(torch.cuda.Event(enable_timing=True)); ev[-1].record()
-        torch.clamp(self.alphas >> 6, max=3, out=self.alphas)
-        self.seg_ids.copy_(self.alphas)
-        f.encode_mbs(self.Y, self.U, self.V, W, H, self.seg_ids, self.segs, self.proba, out=self.enc_out,
-                     recon=(self.rY, self.rU, self.rV), work=self.enc_work)
-        if record:
-            ev.append(torch.cuda.Event(enable_timing=True)); ev[-1].record()
-        f.decode_frames(self.mb, self.co, 2, MBW, MBH, self.batch, out=(self.dY, self.dU, self.dV), work=self.work)
-        if record:
-            ev.append(torch.cuda.Event(enable_timing=True)); ev[-1].record()
-        f.build_nrgba(self.dY, self.dU, self.dV, W, H, out=self.out)
-        if record:
-            ev.append(torch.cuda.Event(enable_timing=True)); ev[-1].record()
             self.events.append(ev)
 
     def collect(self):
@@ -162,32 +209,66 @@ class Pipeline:
         return {k: v / n for k, v in self.stage_ms.items()}
 
 
+def cpu_threads():
+    """Host cores this run may use: the box's CPU share (OMP_NUM_THREADS is set
+    to it on the GPU box) capped by the affinity mask."""
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(env))) if env and env.isdigit() else max(1, min(n, 16))
+
+
 def cpu_baseline(seconds, mb_co):
-    """C restatement of the reference Go CPU path (oracle/), 1 thread, on a
-    bounded sample of the same per-frame workload."""
+    """C restatement of the reference Go CPU path (oracle/) on a bounded sample
+    of the same per-frame workload: first one thread, then one frame per
+    thread on every host core this run may use (ctypes releases the GIL for
+    the C calls).  The reference parallelises inside a frame (row workers,
+    encode_parallel.go:176); across independent frames is the same work with
+    no synchronisation, so the threaded figure is an upper bound of what its
+    CPU path reaches on these cores."""
+    import concurrent.futures as cf
+
     import oracle as O
     from tools import synth
     img = synth.blobs_rgba(W, H, seed=1)
     mb, co = mb_co
     per = MBW * MBH
     mb1, co1 = mb[:per], co[:per]
-    frames_done, t0 = 0, time.perf_counter()
     segs = np.stack([O.setup_segment(q) for q in SEG_Q])
     proba = default_proba()
-    while True:
+
+    def one_frame():
         Y, U, V = O.import_rgba(img, has_alpha=False)
         alphas, _, _, _ = O.compute_alphas(Y, U, V, W, H)
         seg_ids = np.minimum(np.asarray(alphas) >> 6, 3).astype(np.uint8)
         O.encode_frame_rd(Y, U, V, W, H, seg_ids, segs, proba, method=4, quality=75)
         dy, du, dv = O.decode_frame(mb1, co1, 2, MBW, MBH)
         O.build_nrgba(dy, du, dv, W, H)
-        frames_done += 1
+
+    def run(budget):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            one_frame()
+            done += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return done, el
+
+    f1, e1 = run(seconds / 3)  # also initialises the oracle's lazily built tables before threading
+    single = f1 * W * H / e1 / 1e6
+    threads = cpu_threads()
+    if threads > 1:
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            res = list(ex.map(lambda _: run(seconds * 2 / 3), range(threads)))
         el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": round(frames_done * W * H / el / 1e6, 2), "unit": "MPixels/s", "cores": 1, "kind": "port",
-            "sample": f"{frames_done} x 1920x1080 frames (import+analysis+MB RD+decode+upsample), C restatement of the "
-                      "reference Go CPU path, single thread"}
+        fn = sum(r[0] for r in res)
+        value = fn * W * H / el / 1e6
+    else:
+        fn, value = f1, single
+    return {"value": round(value, 2), "unit": "MPixels/s", "cores": threads, "kind": "port",
+            "single_thread_value": round(single, 2),
+            "sample": f"{fn} x 1920x1080 frames on {threads} threads (one frame per thread; {f1} frames on 1 thread "
+                      "before it) of import+analysis+MB RD+decode+upsample, C restatement of the reference Go CPU path"}
 
 
 def timed_region(step, steps, warmup, world, sync, device):
@@ -234,7 +315,7 @@ def main():
     webp_amd.device_check()
 
     rgba, mb, co, mb_co = make_inputs(args.batch, rank, device)
-    pipe = Pipeline(rgba, mb, co, args.batch, device)
+    pipe = Pipeline(rgba, mb, co, args.batch, device, slots=args.slots)
     elapsed = timed_region(pipe.step, args.steps, args.warmup, world, torch.cuda.synchronize, device)
     stage = pipe.collect()
 
@@ -260,7 +341,7 @@ def main():
             "data": "synthetic (gradient/noise/blobs RGBA; seeded parsed-macroblock data for the decode side)",
             "config": {"workload": f"{args.batch} x 1920x1080 frames per GPU per step (C2 frame, C4 per-GPU share): "
                                    "import+analysis+MB RD loop (encode DSP, method 4) + reconstruct+loopfilter+upsample (decode DSP)",
-                       "frames_per_gpu": args.batch, "width": W, "height": H, "parallelism": f"frames sharded x{world}"},
+                       "frames_per_gpu": args.batch, "width": W, "height": H, "parallelism": f"frames sharded x{world}", "batches_in_flight": args.slots},
             "stage_ms": {k: round(v, 3) for k, v in stage.items()},
             "roofline": {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -271,6 +352,9 @@ def main():
                                    "frac": round(BYTES_PER_PX[k] * px_rank_step / (v / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
                                for k, v in stage.items()},
         }
+        valu = pmc_valu(kernel, stage[dominant])
+        if valu is not None:
+            rec["valu"] = valu
         if not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds, mb_co)
         print(json.dumps(rec), flush=True)

@@ -23,8 +23,27 @@ def load(paths):
     return agg
 
 
+SQ_COUNTERS = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVES",
+               "SQ_INSTS_LDS", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE")
+
+
+def valu_json(out, paths):
+    """Per-kernel averages of the SQ / GRBM pass (one launch each)."""
+    agg = load(paths)
+    rec = {}
+    for name, ctrs in agg.items():
+        if not name.startswith("k_") or "SQ_INSTS_VALU" not in ctrs:
+            continue
+        rec[name] = {c: sum(ctrs[c]) / len(ctrs[c]) for c in SQ_COUNTERS if c in ctrs}
+        rec[name]["launches"] = len(ctrs["SQ_INSTS_VALU"])
+    json.dump(rec, open(out, "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
 def main(argv):
     out = None
+    if argv and argv[0] == "--valu-json":
+        return valu_json(argv[1], argv[2:])
     if argv and argv[0] == "--json":
         out, argv = argv[1], argv[2:]
     agg = load(argv)

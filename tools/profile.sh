@@ -10,4 +10,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1
 python3 tools/pmc_summary.py --json $OUT/pmc_traffic.json $(find $OUT/fetch $OUT/write -name "*counter_collection.csv")
-find $OUT -name "*.csv" | head -20
+# SQ / GRBM pass (8 SQ + 1 GRBM counters, within the per-pass slots): VALU issue
+# rate of the latency-bound kernels against the SIMD issue peak.
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- python3 bench.py $ARGS > $OUT/sq.log 2>&1
+python3 tools/pmc_summary.py --valu-json $OUT/pmc_valu.json $(find $OUT/sq -name "*counter_collection.csv")
+find $OUT -name "*.csv"
