@@ -64,7 +64,7 @@ VALU_FILE = os.path.join(ROOT, "profiles", "pmc_valu.json")
 VALU_PEAK_WINST_S = 256 * 4 * 0.5 * 2.4e9
 
 
-def pmc_valu(kernel, launch_ms):
+def pmc_valu(kernel, launch_ms, step_ms):
     """VALU issue rate of `kernel` from the committed SQ pass (tools/profile.sh:
     SQ_INSTS_VALU per launch) over this run's measured launch time, against
     the SIMD issue peak; None if the pass is absent."""
@@ -76,7 +76,8 @@ def pmc_valu(kernel, launch_ms):
     rate = insts / (launch_ms / 1e3)
     out = {"kernel": kernel, "insts_valu_per_launch": int(insts), "achieved": round(rate / 1e12, 4),
            "peak": round(VALU_PEAK_WINST_S / 1e12, 4), "unit": "T wave-instr/s",
-           "frac": round(rate / VALU_PEAK_WINST_S, 4), "source": os.path.relpath(VALU_FILE, ROOT)}
+           "frac": round(rate / VALU_PEAK_WINST_S, 4), "source": os.path.relpath(VALU_FILE, ROOT),
+           "frac_per_step": round(insts / (step_ms / 1e3) / VALU_PEAK_WINST_S, 4)}
     if "GRBM_GUI_ACTIVE" in rec:
         out["effective_clock_ghz"] = round(rec["GRBM_GUI_ACTIVE"] / 8 / (launch_ms / 1e3) / 1e9, 3)
     return out
@@ -100,7 +101,7 @@ def parse():
     p.add_argument("--batch", type=int, default=64, help="frames per GPU per step (C4: 512 frames / 8 GPUs)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget for the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--slots", type=int, default=1, help="batches in flight (one HIP stream each)")
+    p.add_argument("--slots", type=int, default=3, help="batches in flight (one HIP stream each)")
     return p.parse_args()
 
 
@@ -347,12 +348,15 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src, "bytes_per_px": BYTES_PER_PX[dominant],
                          "algorithmic_bytes_per_launch": int(BYTES_PER_PX[dominant] * px_rank_step),
-                         "avg_launch_ms": round(stage[dominant], 4), "launches_per_step": 1},
+                         "avg_launch_ms": round(stage[dominant], 4), "launches_per_step": 1,
+                         # with batches in flight the launches overlap: bytes per step over the step time
+                         "achieved_per_step": round(BYTES_PER_PX[dominant] * px_rank_step / (elapsed / args.steps) / 1e9, 1),
+                         "launches_in_flight": args.slots},
             "stage_roofline": {k: {"kernel": KERNELS[k], "GB/s": round(BYTES_PER_PX[k] * px_rank_step / (v / 1e3) / 1e9, 1),
                                    "frac": round(BYTES_PER_PX[k] * px_rank_step / (v / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
                                for k, v in stage.items()},
         }
-        valu = pmc_valu(kernel, stage[dominant])
+        valu = pmc_valu(kernel, stage[dominant], elapsed / args.steps * 1e3)
         if valu is not None:
             rec["valu"] = valu
         if not args.no_cpu_baseline:
