@@ -78,8 +78,6 @@ def pmc_valu(kernel, launch_ms, step_ms):
            "peak": round(VALU_PEAK_WINST_S / 1e12, 4), "unit": "T wave-instr/s",
            "frac": round(rate / VALU_PEAK_WINST_S, 4), "source": os.path.relpath(VALU_FILE, ROOT),
            "frac_per_step": round(insts / (step_ms / 1e3) / VALU_PEAK_WINST_S, 4)}
-    if "GRBM_GUI_ACTIVE" in rec:
-        out["effective_clock_ghz"] = round(rec["GRBM_GUI_ACTIVE"] / 8 / (launch_ms / 1e3) / 1e9, 3)
     return out
 
 
