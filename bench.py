@@ -4,7 +4,7 @@ One step = one pass of the hot path over this rank's batch of synthetic
 1920x1080 frames, all inputs resident in HBM before timing starts:
   encode side  import RGBA->YUV420 (k_import)  ->  analysis alphas (k_analysis)
                ->  macroblock RD loop, Phase A of encodeFrameParallel (k_encode_rows)
-  decode side  reconstruct + loop filter of parsed macroblocks (k_decode_rows)
+  decode side  reconstruct + loop filter of parsed macroblocks (k_decode_bands)
                ->  fancy upsample to NRGBA (k_upsample)
 The decode side consumes seeded synthetic parsed-macroblock data (tools/synth.py,
 SURVEY.md 8(d) C3 recipe).  Segment ids for the RD loop come from the analysis
@@ -41,7 +41,7 @@ BYTES_PER_PX = {
 }
 
 
-KERNELS = {"import": "k_import", "analysis": "k_analysis", "encode": "k_encode_rows", "decode": "k_decode_rows",
+KERNELS = {"import": "k_import", "analysis": "k_analysis", "encode": "k_encode_rows", "decode": "k_decode_bands",
            "upsample": "k_upsample"}
 SEG_Q = (22, 25, 28, 31)  # quantiser index per segment: q75 (index 26) +- SNS-style offsets
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")

@@ -338,3 +338,65 @@ def test_gpu_dispatch_extract_helpers(cuda):
     po = torch.empty(5000, dtype=torch.int32, device=cuda)
     A.PackRGB(_t(r, cuda), _t(gg, cuda), _t(bb, cuda), 5000, 3, po)
     assert (po.cpu().numpy().view(np.uint32) == O.pack_rgb(r, gg, bb, 5000, 3)).all()
+
+
+def _bins_np(p):
+    """estimateBestFilter's 4 x 16 'seen' bins (alpha.go:321-375) as one 64-bit word."""
+    h, w = p.shape
+    a = p.astype(np.int64)
+    seen = 0
+    for j in range(2, h - 1, 2):
+        mean = int(a[j, 0])
+        for i in range(2, w - 1, 2):
+            cur = int(a[j, i])
+            seen |= 1 << (abs(cur - mean) >> 4)
+            mean = (3 * mean + cur + 2) >> 2
+    if h > 3 and w > 3:
+        j = np.arange(2, h - 1, 2)[:, None]
+        i = np.arange(2, w - 1, 2)[None, :]
+        cur, left, top, tl = a[j, i], a[j, i - 1], a[j - 1, i], a[j - 1, i - 1]
+        grad = np.clip(left + top - tl, 0, 255)
+        for f, d in ((1, np.abs(cur - left) >> 4), (2, np.abs(cur - top) >> 4), (3, np.abs(cur - grad) >> 4)):
+            for v in np.unique(d):
+                seen |= 1 << (16 * f + int(v))
+    return seen
+
+
+@pytest.mark.gpu
+def test_gpu_estimate_bins(cuda):
+    """The raw bins (work buffer word per image) == a numpy statement, on planes
+    whose bins are sparse, fast-path (w % 16 == 0) and byte-path widths."""
+    import torch
+    from webp_amd._lib import call, lib
+    for i, (h, w) in enumerate([(64, 128), (130, 96), (33, 47), (200, 256), (5, 16), (71, 1000)]):
+        y, x = np.mgrid[0:h, 0:w]
+        rng = np.random.default_rng(i)
+        kinds = [((x * 3 + y) % 256), ((x // 9) * 20 + (y // 7) * 5) % 256, rng.integers(0, 40, (h, w)),
+                 (((x * y) >> 4) % 256)]
+        b = np.stack([k.astype(np.uint8) for k in kinds])
+        n = b.shape[0]
+        t = torch.from_numpy(b).to(cuda).contiguous()
+        best = torch.empty(n, dtype=torch.int32, device=cuda)
+        colors = torch.empty(n, dtype=torch.int32, device=cuda)
+        work = torch.empty(lib.wg_alpha_estimate_work_bytes(n), dtype=torch.uint8, device=cuda)
+        call("wg_alpha_estimate_filter", t.data_ptr(), w, h, h * w, n, best.data_ptr(), colors.data_ptr(),
+             work.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        bins = work[:8 * n].cpu().numpy().view(np.uint64)
+        for k in range(n):
+            assert int(bins[k]) == _bins_np(b[k]), (h, w, k, hex(int(bins[k])), hex(_bins_np(b[k])))
+            assert int(best[k]) == O.alpha_estimate_best_filter(b[k])
+            assert int(colors[k]) == O.alpha_num_colors(b[k])
+
+
+@pytest.mark.gpu
+def test_gpu_unfilter_fast_path_bands(cuda):
+    """16-B-aligned widths through the LDS-staged gradient walk and the
+    segmented vertical scan: several chunks and bands, ragged last band."""
+    from webp_amd import alpha as A
+    for f in (2, 3):
+        for i, (h, w) in enumerate([(64 * 5 + 2, 320), (129, 256), (2, 64), (700, 4096 // 8), (18, 16)]):
+            r = np.stack([plane(h, w, 300 + 5 * i + k) for k in range(3)])
+            want = np.stack([O.alpha_unfilter(f, x) for x in r])
+            d = _t(r, cuda)
+            A.alpha_unfilter(f, d, check=True)
+            assert (d.cpu().numpy() == want).all(), (f, h, w)

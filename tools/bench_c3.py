@@ -1,6 +1,6 @@
 """C3 (BASELINE.json configs[2]) and single-frame latencies on one GPU.
 
-  C3: one 4096x4096 lossy decode = reconstruct + loop filter (k_decode_rows)
+  C3: one 4096x4096 lossy decode = reconstruct + loop filter (k_decode_bands)
       + fancy upsample to NRGBA (k_upsample), from seeded synthetic parsed
       macroblocks (SURVEY.md 8(d) recipe, normal filter, half I4);
   C2: one 1920x1080 q75 encode RD pass (k_encode_rows) on each content type;

@@ -1,4 +1,4 @@
-"""Diagnostic: cycles per phase of k_decode_rows (stamped build: make -C webp_amd
+"""Diagnostic: cycles per phase of k_decode_bands (stamped build: make -C webp_amd
 libwebpgpu_stamps.so; WEBPGPU_LIB=webp_amd/libwebpgpu_stamps.so).  BATCH frames of
 SIZE (1080p default, "4096" for the C3 frame)."""
 import ctypes, os, sys

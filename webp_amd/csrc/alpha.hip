@@ -16,10 +16,12 @@
 //                       shift); bands hand their last row down 64 columns at a
 //                       time (plain stores, vmcnt(0) + release fence, then a
 //                       relaxed progress counter)
-//   k_alpha_estimate    estimateBestFilter (:321-385): one thread per sampled row
-//                       (the running mean is serial along the row); the 4 x 16
-//                       "seen" bins are OR-ed into one 64-bit word per image
-//   k_alpha_colors      getNumColors (:302-317): 256-bit OR per image
+//   k_alpha_meanwalk    estimateBestFilter (:321-385), the "none" bin: one lane per
+//                       sampled row (the running mean is serial along the row)
+//   k_alpha_stats       the horizontal / vertical / gradient bins and
+//                       getNumColors (:302-317): one thread per 16 bytes; the
+//                       4 x 16 "seen" bins are OR-ed into one 64-bit word per
+//                       image, the colours into a 256-bit set
 //   premultiply         ApplyAlphaMultiply, MultARGBRow, ApplyAlphaMultiply4444
 //                       (internal/dsp/alpha_proc.go:13-135): one thread per pixel
 //   dispatch / extract  DispatchAlpha / ExtractAlpha (:140-176) with their
@@ -32,28 +34,57 @@ namespace {
 __device__ __forceinline__ int clip255(int v) { return min(max(v, 0), 255); }
 
 // -------------------------------------------------------------- filters
+// one thread per 16 pixels of a row: the 16 bytes, the row above's 16 and the
+// byte left of each (16-B accesses when rows are 16-B aligned)
 __global__ __launch_bounds__(256) void k_alpha_filter(int filter, const uint8_t* in, uint8_t* out, int w, int h,
-                                                      int64_t pitch, int64_t total) {
+                                                      int64_t pitch, int groups, int64_t total, int fast) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
-  const int64_t per = (int64_t)w * h;
-  const int64_t img = i / per, r = i - img * per;
-  const int y = (int)(r / w), x = (int)(r % w);
-  const uint8_t* src = in + img * pitch;
-  const int v = src[r];
-  int pred = 0;
-  if (filter != 0) {
-    if (y == 0) {
-      pred = x > 0 ? src[r - 1] : 0;
-    } else if (filter == 2) {
-      pred = src[r - w];
-    } else if (x == 0) {
-      pred = src[r - w];
-    } else {
-      pred = filter == 1 ? src[r - 1] : clip255(src[r - 1] + src[r - w] - src[r - w - 1]);
+  const int g = (int)(i % groups);
+  const int64_t ry = i / groups;
+  const int y = (int)(ry % h);
+  const int64_t img = ry / h;
+  const int x0 = g * 16;
+  const uint8_t* row = in + img * pitch + (int64_t)y * w;
+  uint8_t* dst = out + img * pitch + (int64_t)y * w;
+  uint8_t cur[16], up[16];
+  const int n = min(16, w - x0);
+  if (fast) {
+    *reinterpret_cast<uint4*>(cur) = *reinterpret_cast<const uint4*>(row + x0);
+    if (y > 0) *reinterpret_cast<uint4*>(up) = *reinterpret_cast<const uint4*>(row - w + x0);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      cur[k] = k < n ? row[x0 + k] : 0;
+      up[k] = (y > 0 && k < n) ? row[x0 + k - w] : 0;
     }
   }
-  out[img * pitch + r] = (uint8_t)(v - pred);
+  const int left0 = x0 > 0 ? row[x0 - 1] : 0;
+  const int upleft0 = (x0 > 0 && y > 0) ? row[x0 - 1 - w] : 0;
+  uint8_t res[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int x = x0 + k;
+    const int v = cur[k];
+    const int left = k > 0 ? cur[k - 1] : left0;
+    int pred = 0;
+    if (filter != 0) {
+      if (y == 0) {
+        pred = x > 0 ? left : 0;
+      } else if (filter == 2 || x == 0) {
+        pred = up[k];
+      } else {
+        const int ul = k > 0 ? up[k - 1] : upleft0;
+        pred = filter == 1 ? left : clip255(left + up[k] - ul);
+      }
+    }
+    res[k] = (uint8_t)(v - pred);
+  }
+  if (fast) {
+    *reinterpret_cast<uint4*>(dst + x0) = *reinterpret_cast<const uint4*>(res);
+  } else {
+    for (int k = 0; k < n; k++) dst[x0 + k] = res[k];
+  }
 }
 
 // inclusive scan (mod 256, carried in int) of v over the 64 lanes
@@ -66,15 +97,18 @@ __device__ __forceinline__ int wave_scan(int v, int lane) {
   return v;
 }
 
-// scan of n bytes at p, stride `step` (in place): one wave
+// scan of n bytes at p, stride `step` (in place): one wave.  Lane k owns a
+// run of ceil(n/64) consecutive elements: its run's sum (independent loads),
+// an exclusive wave scan of the sums, then the run re-walked with the offset.
 __device__ __forceinline__ void scan_line(uint8_t* p, int64_t step, int n, int lane) {
-  int carry = 0;
-  for (int c0 = 0; c0 < n; c0 += 64) {
-    const int i = c0 + lane;
-    const int v = i < n ? p[i * step] : 0;
-    const int s = wave_scan(v, lane) + carry;
-    if (i < n) p[i * step] = (uint8_t)s;
-    carry = __shfl(s, 63, 64);
+  const int len = (n + 63) >> 6;
+  const int i0 = min(lane * len, n), i1 = min(i0 + len, n);
+  int sum = 0;
+  for (int i = i0; i < i1; i++) sum += p[i * step];
+  int acc = wave_scan(sum, lane) - sum;
+  for (int i = i0; i < i1; i++) {
+    acc += p[i * step];
+    p[i * step] = (uint8_t)acc;
   }
 }
 
@@ -88,11 +122,32 @@ __global__ __launch_bounds__(64) void k_alpha_scan_edge(uint8_t* data, int w, in
 }
 
 // horizontal unfilter, rows: one wave per (image, row); column 0 already holds
-// its prefix, x >= 1 add the row's running sum
-__global__ __launch_bounds__(64) void k_alpha_hrows(uint8_t* data, int w, int h, int64_t pitch) {
+// its prefix, x >= 1 add the row's running sum.  Fast path (16-B rows): lane
+// = 16 bytes, an in-lane prefix, then a wave scan of the lane totals.
+__global__ __launch_bounds__(64) void k_alpha_hrows(uint8_t* data, int w, int h, int64_t pitch, int fast) {
   const int lane = threadIdx.x;
   const int img = blockIdx.x / h, y = blockIdx.x % h;
   uint8_t* row = data + img * pitch + (int64_t)y * w;
+  if (fast) {
+    int carry = 0;  // sum of the row up to the current 1 KB block (column 0's prefix included)
+    for (int c0 = 0; c0 < w; c0 += 1024) {
+      const int x0 = c0 + 16 * lane;
+      uint8_t b[16];
+      if (x0 < w) *reinterpret_cast<uint4*>(b) = *reinterpret_cast<const uint4*>(row + x0);
+      int run[16], acc = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        acc += x0 < w ? b[k] : 0;
+        run[k] = acc;
+      }
+      const int excl = wave_scan(acc, lane) - acc + carry;
+#pragma unroll
+      for (int k = 0; k < 16; k++) b[k] = (uint8_t)(run[k] + excl);
+      if (x0 < w) *reinterpret_cast<uint4*>(row + x0) = *reinterpret_cast<const uint4*>(b);
+      carry = __shfl(excl + acc, 63, 64);
+    }
+    return;
+  }
   int carry = row[0];
   for (int c0 = 1; c0 < w; c0 += 64) {
     const int i = c0 + lane;
@@ -117,6 +172,41 @@ __global__ __launch_bounds__(256) void k_alpha_vcols(uint8_t* data, int w, int h
   }
 }
 
+// vertical unfilter below row 0, dword columns (w % 4 == 0, aligned rows):
+// a 1024-thread workgroup owns a strip of 64 dword columns; wave g walks the
+// g-th of 16 row segments.  Pass 1 sums each segment (per-byte adds, mod 256,
+// packed four to a dword), the segment prefixes are combined through LDS, and
+// pass 2 re-walks the segment writing the running sums.
+__device__ __forceinline__ uint32_t padd8(uint32_t a, uint32_t b) {
+  return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ ((a ^ b) & 0x80808080u);
+}
+
+__global__ __launch_bounds__(1024) void k_alpha_vseg(uint8_t* data, int w, int h, int64_t pitch, int strips) {
+  __shared__ uint32_t seg_sum[16][64];
+  const int col = threadIdx.x & 63, seg = threadIdx.x >> 6;
+  const int img = blockIdx.x / strips, strip = blockIdx.x % strips;
+  const int wd = w >> 2;
+  const int q = strip * 64 + col;
+  const int n = h - 1, len = (n + 15) / 16;
+  const int r0 = 1 + seg * len, r1 = min(r0 + len, h);
+  uint32_t* base = reinterpret_cast<uint32_t*>(data + img * pitch) + q;
+  uint32_t sum = 0;
+  if (q < wd) {
+#pragma unroll 8
+    for (int r = r0; r < r1; r++) sum = padd8(sum, base[(int64_t)r * wd]);
+  }
+  seg_sum[seg][col] = sum;
+  __syncthreads();
+  if (q >= wd) return;
+  uint32_t acc = base[0];  // row 0, already unfiltered
+  for (int g = 0; g < seg; g++) acc = padd8(acc, seg_sum[g][col]);
+#pragma unroll 8
+  for (int r = r0; r < r1; r++) {
+    acc = padd8(acc, base[(int64_t)r * wd]);
+    base[(int64_t)r * wd] = acc;
+  }
+}
+
 struct GArgs {
   uint8_t* data;
   int* ctl;       // [0] band dequeue, [1] error
@@ -127,13 +217,54 @@ struct GArgs {
 constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
 
 // gradient unfilter below row 0 (row 0 already scanned).  Rows 1.. are cut
-// into bands of 64; band b holds rows 1 + 64b .. 64 + 64b.
+// into bands of 64; band b holds rows 1 + 64b .. 64 + 64b, one wave each.
+// Lane k owns row 1 + 64b + k and walks it one pixel per step, lane k at
+// x = s - k (a diagonal), so the row above (lane k-1's newest and previous
+// outputs) comes by a lane shift.  The band's pixels are staged through LDS
+// in 64-column chunks, a two-chunk ring per lane (row stride 132 B): at step
+// 64m the wave stores chunk m-2 back (every lane is past it) and loads chunk
+// m with 16-B global accesses, so the per-step work is LDS-only.  The band
+// above hands its last row down as before: lane `last_lane` also stores each
+// output byte straight to global and publishes progress every 64 columns
+// (vmcnt(0), agent release, relaxed counter); the band below reads it with
+// agent-scope dword loads into up_buf.
+constexpr int GB_STRIDE = 132;
+
+__device__ __forceinline__ void gb_chunk_io(uint8_t* ring_row, uint8_t* row, int c0, int w, bool fast, bool store) {
+  uint8_t* slot = ring_row + (c0 & 127);
+  if (fast && c0 + 64 <= w) {
+    uint4* g = reinterpret_cast<uint4*>(row + c0);
+    uint32_t* l = reinterpret_cast<uint32_t*>(slot);
+    if (store) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) g[q] = make_uint4(l[4 * q], l[4 * q + 1], l[4 * q + 2], l[4 * q + 3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint4 v = g[q];
+        l[4 * q] = v.x, l[4 * q + 1] = v.y, l[4 * q + 2] = v.z, l[4 * q + 3] = v.w;
+      }
+    }
+    return;
+  }
+  const int n = min(64, w - c0);
+  for (int i = 0; i < n; i++) {
+    if (store)
+      row[c0 + i] = slot[i];
+    else
+      slot[i] = row[c0 + i];
+  }
+}
+
 __global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
   __shared__ uint8_t up_buf[65];  // the band above's last row, columns c0-1 .. c0+63
+  __shared__ __attribute__((aligned(16))) uint8_t ring[64 * GB_STRIDE];
   __shared__ int sh_band;
   const int lane = threadIdx.x;
   const int w = a.w;
   const int total = a.bands * a.n_img;
+  const bool fast = ((w & 15) == 0) && ((a.pitch & 15) == 0) && ((reinterpret_cast<uintptr_t>(a.data) & 15) == 0);
+  uint8_t* my_ring = ring + lane * GB_STRIDE;
   for (;;) {
     if (lane == 0) sh_band = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -144,15 +275,21 @@ __global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
     const int y = 1 + band * 64 + lane;
     const bool live = y < a.h;
     uint8_t* d = a.data + img * a.pitch;
+    uint8_t* my_row = d + (int64_t)y * w;
     const int* prog_above = a.progress + img * a.bands + band - 1;
     int* prog_mine = a.progress + img * a.bands + band;
     const int last_lane = min(63, a.h - 2 - band * 64);
+    const int chunks = (w + 63) >> 6;
     int o1 = 0, o2 = 0;  // this lane's outputs at x-1, x-2 (o2: the value before o1)
     int first = 0;       // row above's value at x = 0 for lane 0 is read with the rest
     const int steps = w + last_lane;
     for (int s = 0; s < steps; s++) {
       const int x = s - lane;
-      if ((s & 63) == 0 && s < w) {  // next 64 columns of the row above this band
+      if ((s & 63) == 0 && s < w) {  // chunk m = s / 64 starts for lane 0
+        const int c0 = s;
+        if (live && c0 >= 128) gb_chunk_io(my_ring, my_row, c0 - 128, w, fast, true);  // chunk m-2 is done
+        if (live) gb_chunk_io(my_ring, my_row, c0, w, fast, false);
+        // next 64 columns of the row above this band
         if (band > 0) {
           const int need = min(s + 64, w);
           if (lane == 0) {
@@ -192,11 +329,12 @@ __global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
         // x == 0: left = top_left = top (alpha.go:177-181)
         const int left = x == 0 ? top : o1;
         const int tl = x == 0 ? top : top_left;
-        const int v = (d[(int64_t)y * w + x] + clip255(left + top - tl)) & 0xff;
+        uint8_t* cell = my_ring + (x & 127);
+        const int v = (*cell + clip255(left + top - tl)) & 0xff;
         o2 = o1;
         o1 = v;
-        uint8_t* dst = d + (int64_t)y * w + x;
-        *dst = (uint8_t)v;
+        *cell = (uint8_t)v;
+        if (lane == last_lane) my_row[x] = (uint8_t)v;  // hand-off copy for the band below
       } else {
         o2 = o1;
         o1 = 0;
@@ -210,52 +348,136 @@ __global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
         if (lane == last_lane) __hip_atomic_store(prog_mine, xl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+    // the last two chunks (or one) have not been stored yet
+    if (live)
+      for (int m = max(0, chunks - 2); m < chunks; m++) gb_chunk_io(my_ring, my_row, m * 64, w, fast, true);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // the ring is reused by the next band this wave dequeues
   }
 }
 
 // -------------------------------------------------------------- estimate
-__global__ __launch_bounds__(64) void k_alpha_estimate(const uint8_t* data, int w, int h, int64_t pitch, int n_img,
-                                                       unsigned long long* bins) {
-  const int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int rows = (h - 2) / 2;  // j = 2, 4, .. < h - 1
-  if (rows <= 0 || t >= (int64_t)rows * n_img) return;
-  const int img = (int)(t / rows), j = 2 + 2 * (int)(t % rows);
-  if (j >= h - 1) return;
-  const uint8_t* p = data + img * pitch + (int64_t)j * w;
+// estimateBestFilter's bins split by dependence: the "none" bin follows a
+// running mean along each sampled row (serial per row: one lane per row,
+// k_alpha_meanwalk); the horizontal / vertical / gradient bins and the colour
+// set are per pixel (k_alpha_stats: one thread per 16 bytes of a row, a 2-D
+// grid so a block never straddles images).  Bins are 16 bits per filter in one
+// 64-bit word per image; every |diff| >> 4 is < 16, so each sets a bit.
+__global__ __launch_bounds__(256) void k_alpha_stats(const uint8_t* data, int w, int h, int64_t pitch, int groups,
+                                                     int fast, unsigned long long* bins, uint32_t* sets) {
+  __shared__ uint32_t set[8];
+  __shared__ unsigned long long bin;
+  if (threadIdx.x < 8) set[threadIdx.x] = 0;
+  if (threadIdx.x == 0) bin = 0;
+  __syncthreads();
+  const int img = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   unsigned long long seen = 0;
-  int mean = p[0];
-  for (int i = 2; i < w - 1; i += 2) {
-    const int cur = p[i];
-    const int d0 = abs(cur - mean) >> 4, d1 = abs(cur - p[i - 1]) >> 4, d2 = abs(cur - p[i - w]) >> 4;
-    const int d3 = abs(cur - clip255(p[i - 1] + p[i - w] - p[i - w - 1])) >> 4;
-    if (d0 < 16) seen |= 1ull << d0;
-    if (d1 < 16) seen |= 1ull << (16 + d1);
-    if (d2 < 16) seen |= 1ull << (32 + d2);
-    if (d3 < 16) seen |= 1ull << (48 + d3);
-    mean = (3 * mean + cur + 2) >> 2;
+  if (i < (int64_t)groups * h) {
+    const int y = (int)(i / groups), x0 = (int)(i % groups) * 16;
+    const uint8_t* row = data + img * pitch + (int64_t)y * w;
+    const int n = min(16, w - x0);
+    uint8_t cur[16];
+    if (fast) {
+      *reinterpret_cast<uint4*>(cur) = *reinterpret_cast<const uint4*>(row + x0);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++) cur[k] = k < n ? row[x0 + k] : 0;
+    }
+    uint32_t local[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (k < n) {
+#pragma unroll
+        for (int b = 0; b < 8; b++)
+          if ((cur[k] >> 5) == b) local[b] |= 1u << (cur[k] & 31);
+      }
+#pragma unroll
+    for (int b = 0; b < 8; b++)
+      if (local[b]) atomicOr(&set[b], local[b]);
+    // sampled positions: rows j = 2, 4, .. < h-1; columns i = 2, 4, .. < w-1
+    if (y >= 2 && (y & 1) == 0 && y < h - 1) {
+      uint8_t up[16];
+      if (fast) {
+        *reinterpret_cast<uint4*>(up) = *reinterpret_cast<const uint4*>(row - w + x0);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) up[k] = k < n ? row[x0 + k - w] : 0;
+      }
+      // x0 is a multiple of 16, so the sampled columns are the even k; their left
+      // neighbours (odd k) are inside the group
+#pragma unroll
+      for (int k = 0; k < 16; k += 2) {
+        const int x = x0 + k;
+        if (x >= 2 && x < w - 1) {
+          const int c = cur[k], l = cur[k - 1 < 0 ? 0 : k - 1], t = up[k], tl = up[k - 1 < 0 ? 0 : k - 1];
+          const int lft = k > 0 ? l : row[x - 1], tlf = k > 0 ? tl : row[x - 1 - w];
+          const int g = clip255(lft + t - tlf);
+          seen |= 1ull << (16 + (abs(c - lft) >> 4));
+          seen |= 1ull << (32 + (abs(c - t) >> 4));
+          seen |= 1ull << (48 + (abs(c - g) >> 4));
+        }
+      }
+    }
   }
-  if (seen) atomicOr(&bins[img], seen);
+  // OR over the wave, then the block
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) seen |= __shfl_xor(seen, o, 64);
+  if ((threadIdx.x & 63) == 0 && seen) atomicOr(&bin, seen);
+  __syncthreads();
+  if (threadIdx.x < 8 && set[threadIdx.x]) atomicOr(&sets[img * 8 + threadIdx.x], set[threadIdx.x]);
+  if (threadIdx.x == 0 && bin) atomicOr(&bins[img], bin);
 }
 
-__global__ __launch_bounds__(256) void k_alpha_colors(const uint8_t* data, int w, int h, int64_t pitch,
-                                                      uint32_t* sets, int64_t total) {
-  __shared__ uint32_t set[8];
-  if (threadIdx.x < 8) set[threadIdx.x] = 0;
-  __syncthreads();
-  const int64_t per = (int64_t)w * h;
-  const int64_t i0 = (int64_t)blockIdx.x * 256;
-  const int64_t i = i0 + threadIdx.x;
-  const int64_t img0 = i0 / per;  // blocks may straddle two images: track the first, flush others directly
-  if (i < total) {
-    const int64_t img = i / per;
-    const int v = data[img * pitch + (i - img * per)];
-    if (img == img0)
-      atomicOr(&set[v >> 5], 1u << (v & 31));
-    else
-      atomicOr(&sets[img * 8 + (v >> 5)], 1u << (v & 31));
+// the "none" bin: lane = sampled row j = 2 + 2t, the running mean walked over
+// its even columns (estimateBestFilter :343-375), rows read 64 B at a time
+__global__ __launch_bounds__(64) void k_alpha_meanwalk(const uint8_t* data, int w, int h, int64_t pitch, int rows,
+                                                       int fast, unsigned long long* bins) {
+  const int img = blockIdx.y;
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  unsigned long long seen = 0;
+  if (t < rows) {
+    const uint8_t* p = data + img * pitch + (int64_t)(2 + 2 * t) * w;
+    int mean = p[0];
+    const int end = w - 1;  // i < w - 1
+    if (fast) {
+      // 64-byte blocks; i even in [2, end)
+      const uint4* q = reinterpret_cast<const uint4*>(p);
+      const int blocks = (end + 63) >> 6;
+      uint4 nxt[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) nxt[k] = (k < (w >> 4)) ? q[k] : make_uint4(0, 0, 0, 0);
+      for (int b = 0; b < blocks; b++) {
+        uint4 cb[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) cb[k] = nxt[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int qi = 4 * (b + 1) + k;
+          nxt[k] = qi < (w >> 4) ? q[qi] : make_uint4(0, 0, 0, 0);
+        }
+        const uint32_t* wd = reinterpret_cast<const uint32_t*>(cb);
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+          const int i = 64 * b + 2 * k;
+          const int cur = (wd[k >> 1] >> (16 * (k & 1))) & 0xff;
+          if (i >= 2 && i < end) {
+            seen |= 1ull << (abs(cur - mean) >> 4);
+            mean = (3 * mean + cur + 2) >> 2;
+          }
+        }
+      }
+    } else {
+      for (int i = 2; i < end; i += 2) {
+        const int cur = p[i];
+        seen |= 1ull << (abs(cur - mean) >> 4);
+        mean = (3 * mean + cur + 2) >> 2;
+      }
+    }
   }
-  __syncthreads();
-  if (threadIdx.x < 8 && set[threadIdx.x]) atomicOr(&sets[img0 * 8 + threadIdx.x], set[threadIdx.x]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) seen |= __shfl_xor(seen, o, 64);
+  if (threadIdx.x == 0 && seen) atomicOr(&bins[img], seen);
 }
 
 __global__ void k_alpha_finalize(const unsigned long long* bins, const uint32_t* sets, int n_img, int32_t* best,
@@ -406,9 +628,11 @@ extern "C" int wg_alpha_filter(int32_t filter, const uint8_t* in, uint8_t* out, 
                                int64_t pitch, int32_t n_images, void* stream) {
   WG_REQUIRE(in && out && width > 0 && height > 0 && n_images > 0 && filter >= 0 && filter <= 3);
   WG_REQUIRE(pitch >= (int64_t)width * height);
-  const int64_t total = (int64_t)width * height * n_images;
+  const int groups = (width + 15) / 16;
+  const int64_t total = (int64_t)groups * height * n_images;
+  const int fast = (width & 15) == 0 && (pitch & 15) == 0 && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
   hipLaunchKernelGGL(k_alpha_filter, dim3(grid_of(total, 256)), dim3(256), 0, wg::as_stream(stream), (int)filter, in, out,
-                     (int)width, (int)height, pitch, total);
+                     (int)width, (int)height, pitch, groups, total, fast);
   return wg::check_launch("k_alpha_filter");
 }
 
@@ -428,13 +652,20 @@ extern "C" int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, i
     hipLaunchKernelGGL(k_alpha_scan_edge, dim3(n_images), dim3(64), 0, s, data, (int)width, (int)height, pitch, 0);
     int rc = wg::check_launch("k_alpha_scan_edge");
     if (rc != WG_OK) return rc;
+    const int fast = (width & 15) == 0 && (pitch & 15) == 0 && (reinterpret_cast<uintptr_t>(data) & 15) == 0;
     hipLaunchKernelGGL(k_alpha_hrows, dim3((unsigned)((int64_t)height * n_images)), dim3(64), 0, s, data, (int)width,
-                       (int)height, pitch);
+                       (int)height, pitch, fast);
     return wg::check_launch("k_alpha_hrows");
   }
   hipLaunchKernelGGL(k_alpha_scan_edge, dim3(n_images), dim3(64), 0, s, data, (int)width, (int)height, pitch, 1);
   int rc = wg::check_launch("k_alpha_scan_edge");
   if (rc != WG_OK || height == 1) return rc;
+  if (filter == 2 && (width & 3) == 0 && (pitch & 3) == 0 && (reinterpret_cast<uintptr_t>(data) & 3) == 0) {
+    const int strips = (width / 4 + 63) / 64;
+    hipLaunchKernelGGL(k_alpha_vseg, dim3((unsigned)(strips * n_images)), dim3(1024), 0, s, data, (int)width,
+                       (int)height, pitch, strips);
+    return wg::check_launch("k_alpha_vseg");
+  }
   if (filter == 2) {
     const int64_t total = (int64_t)width * n_images;
     hipLaunchKernelGGL(k_alpha_vcols, dim3(grid_of(total, 256)), dim3(256), 0, s, data, (int)width, (int)height, pitch,
@@ -491,16 +722,17 @@ extern "C" int wg_alpha_estimate_filter(const uint8_t* data, int32_t width, int3
   if (hipMemsetAsync(work, 0, wg_alpha_estimate_work_bytes(n_images), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(alpha estimate)");
   const int rows = (height - 2) / 2;
+  const int fast = (width & 15) == 0 && (pitch & 15) == 0 && (reinterpret_cast<uintptr_t>(data) & 15) == 0;
   if (rows > 0) {
-    hipLaunchKernelGGL(k_alpha_estimate, dim3(grid_of((int64_t)rows * n_images, 64)), dim3(64), 0, s, data, (int)width,
-                       (int)height, pitch, (int)n_images, bins);
-    const int rc = wg::check_launch("k_alpha_estimate");
+    hipLaunchKernelGGL(k_alpha_meanwalk, dim3(grid_of(rows, 64), n_images), dim3(64), 0, s, data, (int)width,
+                       (int)height, pitch, rows, fast, bins);
+    const int rc = wg::check_launch("k_alpha_meanwalk");
     if (rc != WG_OK) return rc;
   }
-  const int64_t total = (int64_t)width * height * n_images;
-  hipLaunchKernelGGL(k_alpha_colors, dim3(grid_of(total, 256)), dim3(256), 0, s, data, (int)width, (int)height, pitch,
-                     sets, total);
-  int rc = wg::check_launch("k_alpha_colors");
+  const int groups = (width + 15) / 16;
+  hipLaunchKernelGGL(k_alpha_stats, dim3(grid_of((int64_t)groups * height, 256), n_images), dim3(256), 0, s, data,
+                     (int)width, (int)height, pitch, groups, fast, bins, sets);
+  int rc = wg::check_launch("k_alpha_stats");
   if (rc != WG_OK) return rc;
   hipLaunchKernelGGL(k_alpha_finalize, dim3(grid_of(n_images, 64)), dim3(64), 0, s, bins, sets, (int)n_images,
                      best_filter, num_colors);

@@ -108,11 +108,18 @@ __device__ unsigned long long g_phase[16];
 #define STAMP_FLUSH() (void)st_unused_
 #endif
 
+// wave-level LDS ordering: this wave's LDS accesses retire before what follows
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // Loop filter of one MB on the LDS tiles (doFilter, decode_frame.go:293-342):
 // lanes 0-15 luma line 0-15, lanes 16-31 chroma line 0-7 of U / V.  A line is
 // 20 (luma) / 12 (chroma) pixels: 4 of the left / upper neighbour, then the
 // MB.  Each lane filters all edges of its line in registers (rf_line); the
-// row pass (H edges) completes before the column pass (V edges).
+// row pass (H edges) completes before the column pass (V edges).  One wave:
+// the passes are ordered with wave-level LDS syncs.
 template <bool COMPLEX>
 __device__ __forceinline__ void filter_mb(uint8_t* fy, uint8_t* fu, uint8_t* fv, int lane, bool chroma, bool left,
                                           bool top, bool inner, int limit, int ilevel, int hev_t) {
@@ -138,7 +145,7 @@ __device__ __forceinline__ void filter_mb(uint8_t* fy, uint8_t* fu, uint8_t* fv,
       *reinterpret_cast<uint32_t*>(rowp + 16) = pack4(v[16], v[17], v[18], v[19]);
     }
   }
-  __syncthreads();
+  lds_sync();
   if (active) {
     uint8_t* col = luma ? fy + FY_X0 + lane : (pl ? fv : fu) + FC_X0 + j;
     const int st = luma ? FY_STRIDE : FC_STRIDE;
@@ -153,7 +160,7 @@ __device__ __forceinline__ void filter_mb(uint8_t* fy, uint8_t* fu, uint8_t* fv,
       for (int k = 12; k < 20; k++) col[k * st] = (uint8_t)v[k];
     }
   }
-  __syncthreads();
+  lds_sync();
 }
 
 // threadIdx.x through an opaque move, re-read at every phase of the MB loop:
@@ -168,281 +175,391 @@ __device__ __forceinline__ int opaque_lane() {
 
 constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of the 100 MHz s_memrealtime clock per wait
 
-__global__ __launch_bounds__(64) void k_decode_rows(DecArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t wb[WB_SIZE];
+// Rows per workgroup (one wave each) and the depth of the intra-band LDS rings.
+constexpr int DW = 4;
+constexpr int RING = 8;
+constexpr int BOT_BYTES = 128;  // final rows 12..15 of an MB: Y 4 x 16, U 4 x 8, V 4 x 8
+
+// bounded spin on a progress word (LDS or agent-scope global) by lane 0
+template <bool GLOBAL>
+__device__ __forceinline__ int wait_progress(const int* p, int need, int* err_flag, int give_up) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t it = 0;; it++) {
+    int v;
+    if (GLOBAL) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (v >= need) return v;
+    // never hang the GPU: after SPIN_TICKS (or once any wait has timed out)
+    // flag the error and carry on with whatever is in memory
+    if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+                            __hip_atomic_load(err_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+      __hip_atomic_fetch_or(err_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return give_up;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Band schedule: a workgroup of DW waves dequeues a band of DW consecutive
+// macroblock rows of one image (ordered counter over (band, image)); wave r
+// walks row DW*band + r.  Wave 0 depends on the previous band's last row
+// through global memory exactly as a lone row would (sc1 hand-off, progress
+// counter); waves r > 0 depend on wave r-1 through LDS: a RING-deep ring per
+// wave of the unfiltered top context (32 B) and the final bottom rows 12..15
+// (128 B) of each finished MB, and an LDS progress word.  The bottom rows of
+// an MB are final once the MB to its right has run its left-edge filter, so,
+// as across bands, the consumer waits for MB x+1 of the row above.  Writes
+// to the frame never overlap between the waves of a band: a producer whose
+// consumer is in the band leaves its rows 13..15 (Y) / 5..7 (U, V) to the
+// consumer, which stores them after its top-edge filter (changed or not).
+// Across bands the original protocol stands (the producer stores everything
+// and drains before publishing; the consumer stores what it modified).
+__global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t wb_all[DW][WB_SIZE];
   // prefetch landing zone: coefficients (48 x 16 B) then the wg_mb_info (2 x 16 B)
-  __shared__ __attribute__((aligned(16))) int4 stage[50];
-  int16_t* const cof = reinterpret_cast<int16_t*>(stage);
+  __shared__ __attribute__((aligned(16))) int4 stage_all[DW][50];
   // filter tiles Y | U | V, then slack that chroma lanes of filter_mb read
   // (never write) when they run the 20-pixel luma code path
-  __shared__ __attribute__((aligned(16))) uint8_t ftiles[20 * FY_STRIDE + 2 * 12 * FC_STRIDE + 8 * FC_STRIDE];
-  uint8_t* const fy = ftiles;
-  uint8_t* const fu = ftiles + 20 * FY_STRIDE;
-  uint8_t* const fv = fu + 12 * FC_STRIDE;
+  constexpr int FT_BYTES = 20 * FY_STRIDE + 2 * 12 * FC_STRIDE + 8 * FC_STRIDE;
+  __shared__ __attribute__((aligned(16))) uint8_t ftiles_all[DW][FT_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t top_ring[DW][RING][TOP_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t bot_ring[DW][RING][BOT_BYTES];
+  __shared__ int prog_lds[DW];
   __shared__ int sh_word;
 
-  int lane = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  uint8_t* const wb = wb_all[wave];
+  int16_t* const cof = reinterpret_cast<int16_t*>(stage_all[wave]);
+  int4* const stage = stage_all[wave];
+  uint8_t* const fy = ftiles_all[wave];
+  uint8_t* const fu = fy + 20 * FY_STRIDE;
+  uint8_t* const fv = fu + 12 * FC_STRIDE;
   const int mbw = a.mbw, mbh = a.mbh;
-  const int total_rows = a.n_img * mbh;
+  const int bands = (mbh + DW - 1) / DW;
+  const int total = a.n_img * bands;
   const int ys = 16 * mbw, uvs = 8 * mbw;
   const bool luma_only = a.filter_type == 1;
   STAMP_DECL;
 
   for (;;) {
-    if (lane == 0) sh_word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) sh_word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) prog_lds[wave] = 0;
     __syncthreads();
-    const int row = __builtin_amdgcn_readfirstlane(sh_word);
+    const int idx = __builtin_amdgcn_readfirstlane(sh_word);
     __syncthreads();
-    if (row >= total_rows) break;
-    const int mby = row / a.n_img, img = row % a.n_img;
-    uint8_t* top = a.top + (int64_t)img * mbw * TOP_BYTES;
-    int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
-    int* prog_mine = a.progress + (int64_t)img * mbh + mby;
-    uint8_t* Yp = a.Y + (int64_t)img * ys * 16 * mbh;
-    uint8_t* Up = a.U + (int64_t)img * uvs * 8 * mbh;
-    uint8_t* Vp = a.V + (int64_t)img * uvs * 8 * mbh;
+    if (idx >= total) break;
+    const int band = idx / a.n_img, img = idx % a.n_img;
+    const int mby = band * DW + wave;
+    const int last_wave = min(DW, mbh - band * DW) - 1;  // the band's last row
+    if (wave <= last_wave) {
+      const bool from_lds = wave > 0;           // the row above is in this band
+      const bool to_lds = wave < last_wave;      // the row below is in this band
+      uint8_t* top = a.top + (int64_t)img * mbw * TOP_BYTES;
+      int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
+      int* prog_mine = a.progress + (int64_t)img * mbh + mby;
+      uint8_t* Yp = a.Y + (int64_t)img * ys * 16 * mbh;
+      uint8_t* Up = a.U + (int64_t)img * uvs * 8 * mbh;
+      uint8_t* Vp = a.V + (int64_t)img * uvs * 8 * mbh;
 
-    // row start: left border 129, top-left 129 (127 on the first row) -- decode_frame.go:93-110
-    if (lane < 16) wb[LY - 1 + lane * WG_BPS] = 129;
-    else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = 129;
-    else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = 129;
-    else if (lane < 35) wb[(lane == 32 ? LY : lane == 33 ? LU : LV) - WG_BPS - 1] = mby > 0 ? 129 : 127;
-    int seen = 0;  // progress of the row above observed so far
-    // Register prefetch of the next macroblock's coefficients + info (lanes
-    // 0-47 / 48-49): issued once the current MB's hand-off loads are consumed,
-    // so it overlaps the MB's compute (loads retire in order: issuing it
-    // earlier would make every wait on a hand-off load wait for it too).
-    const int64_t row_mb0 = ((int64_t)img * mbh + mby) * mbw;
-    int4 pf = make_int4(0, 0, 0, 0);
-    if (lane < 48) pf = reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384)[lane];
-    else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + row_mb0)[lane - 48];
+      // row start: left border 129, top-left 129 (127 on the first row) -- decode_frame.go:93-110
+      if (lane < 16) wb[LY - 1 + lane * WG_BPS] = 129;
+      else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = 129;
+      else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = 129;
+      else if (lane < 35) wb[(lane == 32 ? LY : lane == 33 ? LU : LV) - WG_BPS - 1] = mby > 0 ? 129 : 127;
+      int seen = 0;  // progress of the row above observed so far
+      // Register prefetch of the next macroblock's coefficients + info (lanes
+      // 0-47 / 48-49): issued once the current MB's hand-off loads are consumed,
+      // so it overlaps the MB's compute (loads retire in order: issuing it
+      // earlier would make every wait on a hand-off load wait for it too).
+      const int64_t row_mb0 = ((int64_t)img * mbh + mby) * mbw;
+      int4 pf = make_int4(0, 0, 0, 0);
+      if (lane < 48) pf = reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384)[lane];
+      else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + row_mb0)[lane - 48];
 
-    for (int mbx = 0; mbx < mbw; mbx++) {
-      const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
-      STAMP(0);
-      // ---- dependency on the row above ----
-      if (mby > 0) {
-        const int need = min(mbx + 2, mbw);
-        if (seen < need) {
-          int v = 0;
-          if (lane == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (uint32_t it = 0;; it++) {
-              v = __hip_atomic_load(prog_above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if (v >= need) break;
-              // never hang the GPU: after SPIN_TICKS (or once any row has timed out)
-              // flag the error and carry on with whatever is in memory
-              if ((it & 63) == 63 &&
-                  (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
-                   __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
-                __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                v = mbw;
-                break;
+      for (int mbx = 0; mbx < mbw; mbx++) {
+        const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
+        const int slot = mbx & (RING - 1);
+        STAMP(0);
+        // ---- dependency on the row above (and ring space in the row below) ----
+        if (mby > 0) {
+          const int need = min(mbx + 2, mbw);
+          if (seen < need) {
+            int v = 0;
+            if (lane == 0)
+              v = from_lds ? wait_progress<false>(&prog_lds[wave - 1], need, &a.ctl[1], mbw)
+                           : wait_progress<true>(prog_above, need, &a.ctl[1], mbw);
+            seen = __shfl(v, 0, 64);
+          }
+        }
+        if (to_lds && mbx >= RING - 1) {  // ring slot `slot` must have been read by the row below
+          if (lane == 0) wait_progress<false>(&prog_lds[wave + 1], mbx - RING + 2, &a.ctl[1], mbw);
+          lds_sync();
+        }
+        STAMP(1);
+        lane = opaque_lane() & 63;
+        // ---- loads: macroblock info (scalar), coefficients -> LDS, top context, filter rows above ----
+        if (lane < 50) stage[lane] = pf;
+        // rotate the filter tile: the left MB's final columns 12..15 become columns -4..-1
+        if (mbx > 0) {
+          if (lane < 16) {
+            uint8_t* r = fy + (lane + 4) * FY_STRIDE + FY_X0;
+            *reinterpret_cast<uint32_t*>(r - 4) = lds32(r + 12);
+          } else if (lane < 32) {
+            const int j = (lane - 16) & 7;
+            uint8_t* r = ((lane < 24) ? fu : fv) + (j + 4) * FC_STRIDE + FC_X0;
+            *reinterpret_cast<uint32_t*>(r - 4) = lds32(r + 4);
+          }
+        }
+        if (mby > 0 && from_lds) {
+          const uint8_t* tc = top_ring[wave - 1][slot];
+          const uint8_t* bt = bot_ring[wave - 1][slot];
+          if (lane >= 48 && lane < 52) {  // unfiltered top context Y16 U8 V8
+            const int k = lane - 48;
+            uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
+            *reinterpret_cast<uint64_t*>(dst) = lds64(tc + 8 * k);
+          } else if (lane >= 52 && lane < 60) {  // final rows 12..15 of the MB above (Y)
+            const int k = lane - 52, rr = k >> 1, half = k & 1;
+            *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = lds64(bt + 16 * rr + 8 * half);
+          } else if (lane >= 60) {  // U rows 4..7
+            const int rr = lane - 60;
+            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) = lds64(bt + 64 + 8 * rr);
+          } else if (lane >= 44) {  // V rows (lanes 44..47)
+            const int rr = lane - 44;
+            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = lds64(bt + 96 + 8 * rr);
+          }
+          if (lane == 0) {  // top-right: next MB's top context, or replicate top[15] at the right edge
+            uint32_t tr;
+            if (mbx < mbw - 1) tr = lds32(top_ring[wave - 1][(mbx + 1) & (RING - 1)]);
+            else tr = 0x01010101u * (uint32_t)tc[15];
+            *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
+          }
+        } else if (mby > 0) {
+          const uint8_t* tc = top + mbx * TOP_BYTES;
+          if (lane >= 48 && lane < 52) {  // unfiltered top context Y16 U8 V8
+            const uint64_t w = ld_sc1_64(tc + 8 * (lane - 48));
+            const int k = lane - 48;
+            uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
+            *reinterpret_cast<uint64_t*>(dst) = w;
+          } else if (lane >= 52 && lane < 60) {  // filtered frame rows 16y-4..16y-1 (Y)
+            const int k = lane - 52, rr = k >> 1, half = k & 1;
+            const uint64_t w = ld_sc1_64(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half);
+            *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = w;
+          } else if (lane >= 60) {  // U rows 8y-4..8y-1
+            const int rr = lane - 60;
+            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) =
+                ld_sc1_64(Up + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
+          } else if (lane >= 44) {  // V rows (lanes 44..47)
+            const int rr = lane - 44;
+            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) =
+                ld_sc1_64(Vp + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
+          }
+          if (lane == 0) {  // top-right: next MB's top context, or replicate top[15] at the right edge
+            uint32_t tr;
+            if (mbx < mbw - 1) tr = (uint32_t)ld_sc1_64(tc + TOP_BYTES);
+            else tr = 0x01010101u * (uint32_t)(ld_sc1_64(tc + 8) >> 56);
+            *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
+          }
+        } else {  // first row: everything above is 127 (decode_frame.go:104-108)
+          if (lane < 21) wb[LY - WG_BPS + lane - 1] = 127;
+          else if (lane < 30) wb[LU - WG_BPS + lane - 22] = 127;
+          else if (lane < 39) wb[LV - WG_BPS + lane - 31] = 127;
+        }
+        lds_sync();
+        if (mbx + 1 < mbw) {  // prefetch the next MB (see above)
+          if (lane < 48) pf = reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384)[lane];
+          else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + mbi + 1)[lane - 48];
+        }
+        const uint32_t* iw = reinterpret_cast<const uint32_t*>(stage + 48);  // wg_mb_info words
+        const uint32_t nz_y = __builtin_amdgcn_readfirstlane(iw[0]), nz_uv = __builtin_amdgcn_readfirstlane(iw[1]);
+        const uint32_t im0 = __builtin_amdgcn_readfirstlane(iw[2]);
+        const uint32_t w6 = __builtin_amdgcn_readfirstlane(iw[6]), w7 = __builtin_amdgcn_readfirstlane(iw[7]);
+        const int is_i4 = w6 & 0xff, uv_mode = (w6 >> 8) & 0xff;
+        const int f_limit = w7 & 0xff, ilevel = (w7 >> 8) & 0xff, f_inner = (w7 >> 16) & 0xff, hev_t = w7 >> 24;
+        const uint8_t* imodes = reinterpret_cast<const uint8_t*>(stage + 48) + 8;
+        if (is_i4 && lane < 12) {  // replicate top-right down to rows 3, 7, 11 (:155-160)
+          const int r = 4 * (lane / 4 + 1) - 1, i = lane & 3;
+          wb[LY + r * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
+        }
+        lds_sync();
+
+        STAMP(2);
+        lane = opaque_lane() & 63;
+        // ---- luma prediction + residual ----
+        {
+          const int blk = lane >> 2, r = lane & 3, bx = blk & 3, by = blk >> 2;
+          const int off = LY + (4 * by + r) * WG_BPS + 4 * bx;
+          const int code = (nz_y >> (30 - 2 * blk)) & 3;
+          int res[4];
+          dec_residual_row(cof + blk * 16, code, r, res);
+          if (!is_i4) {
+            const int mode = check_mode(mbx, mby, im0 & 0xff);
+            const int dc = predsq_dc(mode, wb + LY, 16);
+            const uint32_t pred = predsq_row4(mode, wb + LY, 4 * bx, 4 * by + r, dc);
+            *reinterpret_cast<uint32_t*>(wb + off) =
+                pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
+                      clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+          } else {
+            const int my_step = bx + 2 * by;  // in-MB dependency wavefront
+            const int mode = imodes[blk];
+            for (int s = 0; s < 10; s++) {
+              if (s == my_step) {
+                int X, T[8], L[4];
+                pred4_ctx(wb, LY + 4 * by * WG_BPS + 4 * bx, X, T, L);
+                const uint32_t pred = pred4_row(mode, r, X, T, L);
+                *reinterpret_cast<uint32_t*>(wb + off) =
+                    pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
+                          clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
               }
-              __builtin_amdgcn_s_sleep(2);
+              lds_sync();
             }
           }
-          seen = __shfl(v, 0, 64);
         }
-      }
-      STAMP(1);
-      lane = opaque_lane();
-      // ---- loads: macroblock info (scalar), coefficients -> LDS, top context, filter rows above ----
-      if (lane < 50) stage[lane] = pf;
-      // rotate the filter tile: the left MB's final columns 12..15 become columns -4..-1
-      if (mbx > 0) {
-        if (lane < 16) {
-          uint8_t* r = fy + (lane + 4) * FY_STRIDE + FY_X0;
-          *reinterpret_cast<uint32_t*>(r - 4) = lds32(r + 12);
-        } else if (lane < 32) {
-          const int j = (lane - 16) & 7;
-          uint8_t* r = ((lane < 24) ? fu : fv) + (j + 4) * FC_STRIDE + FC_X0;
-          *reinterpret_cast<uint32_t*>(r - 4) = lds32(r + 4);
-        }
-      }
-      if (mby > 0) {
-        const uint8_t* tc = top + mbx * TOP_BYTES;
-        if (lane >= 48 && lane < 52) {  // unfiltered top context Y16 U8 V8
-          const uint64_t w = ld_sc1_64(tc + 8 * (lane - 48));
-          const int k = lane - 48;
-          uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
-          *reinterpret_cast<uint64_t*>(dst) = w;
-        } else if (lane >= 52 && lane < 60) {  // filtered frame rows 16y-4..16y-1 (Y)
-          const int k = lane - 52, rr = k >> 1, half = k & 1;
-          const uint64_t w = ld_sc1_64(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half);
-          *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = w;
-        } else if (lane >= 60) {  // U rows 8y-4..8y-1
-          const int rr = lane - 60;
-          *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) =
-              ld_sc1_64(Up + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
-        } else if (lane >= 44) {  // V rows (lanes 44..47)
-          const int rr = lane - 44;
-          *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) =
-              ld_sc1_64(Vp + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
-        }
-        if (lane == 0) {  // top-right: next MB's top context, or replicate top[15] at the right edge
-          uint32_t tr;
-          if (mbx < mbw - 1) tr = (uint32_t)ld_sc1_64(tc + TOP_BYTES);
-          else tr = 0x01010101u * (uint32_t)(ld_sc1_64(tc + 8) >> 56);
-          *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
-        }
-      } else {  // first row: everything above is 127 (decode_frame.go:104-108)
-        if (lane < 21) wb[LY - WG_BPS + lane - 1] = 127;
-        else if (lane < 30) wb[LU - WG_BPS + lane - 22] = 127;
-        else if (lane < 39) wb[LV - WG_BPS + lane - 31] = 127;
-      }
-      __syncthreads();
-      if (mbx + 1 < mbw) {  // prefetch the next MB (see above)
-        if (lane < 48) pf = reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384)[lane];
-        else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + mbi + 1)[lane - 48];
-      }
-      const uint32_t* iw = reinterpret_cast<const uint32_t*>(stage + 48);  // wg_mb_info words
-      const uint32_t nz_y = __builtin_amdgcn_readfirstlane(iw[0]), nz_uv = __builtin_amdgcn_readfirstlane(iw[1]);
-      const uint32_t im0 = __builtin_amdgcn_readfirstlane(iw[2]);
-      const uint32_t w6 = __builtin_amdgcn_readfirstlane(iw[6]), w7 = __builtin_amdgcn_readfirstlane(iw[7]);
-      const int is_i4 = w6 & 0xff, uv_mode = (w6 >> 8) & 0xff;
-      const int f_limit = w7 & 0xff, ilevel = (w7 >> 8) & 0xff, f_inner = (w7 >> 16) & 0xff, hev_t = w7 >> 24;
-      const uint8_t* imodes = reinterpret_cast<const uint8_t*>(stage + 48) + 8;
-      if (is_i4 && lane < 12) {  // replicate top-right down to rows 3, 7, 11 (:155-160)
-        const int r = 4 * (lane / 4 + 1) - 1, i = lane & 3;
-        wb[LY + r * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
-      }
-      __syncthreads();
-
-      STAMP(2);
-      lane = opaque_lane();
-      // ---- luma prediction + residual ----
-      {
-        const int blk = lane >> 2, r = lane & 3, bx = blk & 3, by = blk >> 2;
-        const int off = LY + (4 * by + r) * WG_BPS + 4 * bx;
-        const int code = (nz_y >> (30 - 2 * blk)) & 3;
-        int res[4];
-        dec_residual_row(cof + blk * 16, code, r, res);
-        if (!is_i4) {
-          const int mode = check_mode(mbx, mby, im0 & 0xff);
-          const int dc = predsq_dc(mode, wb + LY, 16);
-          const uint32_t pred = predsq_row4(mode, wb + LY, 4 * bx, 4 * by + r, dc);
-          *reinterpret_cast<uint32_t*>(wb + off) =
+        STAMP(3);
+        lane = opaque_lane() & 63;
+        // ---- chroma prediction + residual (doUVTransform :47-68) ----
+        if (lane < 32) {
+          const int pl = lane >> 4, cblk = (lane >> 2) & 3, r = lane & 3;
+          const int cbx = cblk & 1, cby = cblk >> 1;
+          const int base = pl ? LV : LU;
+          const int mode = check_mode(mbx, mby, uv_mode);
+          const int dc = predsq_dc(mode, wb + base, 8);
+          const uint32_t pred = predsq_row4(mode, wb + base, 4 * cbx, 4 * cby + r, dc);
+          const uint32_t bits = nz_uv >> (8 * pl);
+          const int16_t* bco = cof + (16 + 4 * pl + cblk) * 16;
+          int res[4] = {0, 0, 0, 0};
+          if (bits & 0xff) {
+            if (bits & 0xaa) dec_residual_row(bco, 3, r, res);
+            else if (bco[0] != 0) dec_residual_row(bco, 1, r, res);
+          }
+          *reinterpret_cast<uint32_t*>(wb + base + (4 * cby + r) * WG_BPS + 4 * cbx) =
               pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
                     clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
-        } else {
-          const int my_step = bx + 2 * by;  // in-MB dependency wavefront
-          const int mode = imodes[blk];
-          for (int s = 0; s < 10; s++) {
-            if (s == my_step) {
-              int X, T[8], L[4];
-              pred4_ctx(wb, LY + 4 * by * WG_BPS + 4 * bx, X, T, L);
-              const uint32_t pred = pred4_row(mode, r, X, T, L);
-              *reinterpret_cast<uint32_t*>(wb + off) =
-                  pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
-                        clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
-            }
-            __syncthreads();
-          }
         }
-      }
-      STAMP(3);
-      lane = opaque_lane();
-      // ---- chroma prediction + residual (doUVTransform :47-68) ----
-      if (lane < 32) {
-        const int pl = lane >> 4, cblk = (lane >> 2) & 3, r = lane & 3;
-        const int cbx = cblk & 1, cby = cblk >> 1;
-        const int base = pl ? LV : LU;
-        const int mode = check_mode(mbx, mby, uv_mode);
-        const int dc = predsq_dc(mode, wb + base, 8);
-        const uint32_t pred = predsq_row4(mode, wb + base, 4 * cbx, 4 * cby + r, dc);
-        const uint32_t bits = nz_uv >> (8 * pl);
-        const int16_t* bco = cof + (16 + 4 * pl + cblk) * 16;
-        int res[4] = {0, 0, 0, 0};
-        if (bits & 0xff) {
-          if (bits & 0xaa) dec_residual_row(bco, 3, r, res);
-          else if (bco[0] != 0) dec_residual_row(bco, 1, r, res);
+        lds_sync();
+
+        STAMP(4);
+        lane = opaque_lane() & 63;
+        // ---- unfiltered top context for the row below (:190-194) + MB into the filter tiles ----
+        if (mby < mbh - 1 && lane >= 32 && lane < 36) {
+          const int k = lane - 32;
+          const uint8_t* src =
+              k < 2 ? wb + LY + 15 * WG_BPS + 8 * k : (k == 2 ? wb + LU + 7 * WG_BPS : wb + LV + 7 * WG_BPS);
+          if (to_lds) *reinterpret_cast<uint64_t*>(top_ring[wave][slot] + 8 * k) = lds64(src);
+          else st_sc1_64(top + mbx * TOP_BYTES + 8 * k, lds64(src));
         }
-        *reinterpret_cast<uint32_t*>(wb + base + (4 * cby + r) * WG_BPS + 4 * cbx) =
-            pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
-                  clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
-      }
-      __syncthreads();
+        if (lane < 16) {
+          *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) =
+              *reinterpret_cast<const uint4*>(wb + LY + lane * WG_BPS);
+        } else if (lane < 32) {
+          const int pl = lane >= 24, j = (lane - 16) & 7;
+          *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0) =
+              lds64(wb + (pl ? LV : LU) + j * WG_BPS);
+        }
+        lds_sync();
 
-      STAMP(4);
-      lane = opaque_lane();
-      // ---- unfiltered top context for the row below (:190-194) + MB into the filter tiles ----
-      if (mby < mbh - 1 && lane >= 32 && lane < 36) {
-        const int k = lane - 32;
-        const uint8_t* src =
-            k < 2 ? wb + LY + 15 * WG_BPS + 8 * k : (k == 2 ? wb + LU + 7 * WG_BPS : wb + LV + 7 * WG_BPS);
-        st_sc1_64(top + mbx * TOP_BYTES + 8 * k, lds64(src));
-      }
-      if (lane < 16) {
-        *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) =
-            *reinterpret_cast<const uint4*>(wb + LY + lane * WG_BPS);
-      } else if (lane < 32) {
-        const int pl = lane >= 24, j = (lane - 16) & 7;
-        *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0) =
-            lds64(wb + (pl ? LV : LU) + j * WG_BPS);
-      }
-      __syncthreads();
+        STAMP(5);
+        lane = opaque_lane() & 63;
+        // ---- loop filter (doFilter :293-342): H edges (left MB edge, inner x=4,8,12), then V edges ----
+        const bool do_filter = a.filter_type > 0 && f_limit > 0;
+        const bool inner = f_inner != 0;
+        if (do_filter) {
+          if (a.filter_type == 2) filter_mb<true>(fy, fu, fv, lane, true, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
+          else filter_mb<false>(fy, fu, fv, lane, false, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
+        }
 
-      STAMP(5);
-      lane = opaque_lane();
-      // ---- loop filter (doFilter :293-342): H edges (left MB edge, inner x=4,8,12), then V edges ----
-      const bool do_filter = a.filter_type > 0 && f_limit > 0;
-      const bool inner = f_inner != 0;
-      if (do_filter) {
-        if (a.filter_type == 2) filter_mb<true>(fy, fu, fv, lane, true, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
-        else filter_mb<false>(fy, fu, fv, lane, false, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
-      }
-
-      STAMP(6);
-      lane = opaque_lane();
-      // ---- stores (all sc1: the row below reads them) ----
-      if (lane < 32) {  // Y rows, 2 x 8 B
-        const int j = lane >> 1, half = lane & 1;
-        st_sc1_64(Yp + (int64_t)(16 * mby + j) * ys + 16 * mbx + 8 * half,
-                  lds64(fy + (j + 4) * FY_STRIDE + FY_X0 + 8 * half));
-      } else if (lane < 48) {  // U, V rows
-        const int pl = lane >= 40, j = (lane - 32) & 7;
-        st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx,
-                  lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0));
-      }
-      if (do_filter) {
-        if (mbx > 0) {  // the 3 columns of the left MB modified by our left-edge filter
+        STAMP(6);
+        lane = opaque_lane() & 63;
+        // ---- stores (sc1 where another workgroup reads them) ----
+        // Y rows 13..15 / U, V rows 5..7 are left to the row below when it is in this band
+        if (lane < 32) {  // Y rows, 2 x 8 B
+          const int j = lane >> 1, half = lane & 1;
+          if (!to_lds || j < 13)
+            st_sc1_64(Yp + (int64_t)(16 * mby + j) * ys + 16 * mbx + 8 * half,
+                      lds64(fy + (j + 4) * FY_STRIDE + FY_X0 + 8 * half));
+        } else if (lane < 48) {  // U, V rows
+          const int pl = lane >= 40, j = (lane - 32) & 7;
+          if (!to_lds || j < 5)
+            st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx,
+                      lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0));
+        }
+        if (do_filter && mbx > 0) {  // the 3 columns of the left MB modified by our left-edge filter
           if (lane >= 48) {
-            st_sc1_32(Yp + (int64_t)(16 * mby + lane - 48) * ys + 16 * mbx - 4,
-                      lds32(fy + (lane - 48 + 4) * FY_STRIDE + FY_X0 - 4));
+            if (!to_lds || lane - 48 < 13)
+              st_sc1_32(Yp + (int64_t)(16 * mby + lane - 48) * ys + 16 * mbx - 4,
+                        lds32(fy + (lane - 48 + 4) * FY_STRIDE + FY_X0 - 4));
           } else if (!luma_only && lane < 16) {
             const int pl = lane >= 8, j = lane & 7;
-            st_sc1_32((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx - 4,
-                      lds32((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 - 4));
+            if (!to_lds || j < 5)
+              st_sc1_32((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx - 4,
+                        lds32((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 - 4));
           }
         }
-        if (mby > 0) {  // the 3 rows of the MB above modified by our top-edge filter
+        if (mby > 0 && (from_lds || do_filter)) {
+          // the 3 rows of the MB above modified by our top-edge filter; always,
+          // when the row above (in this band) left them to us
           if (lane >= 16 && lane < 22) {
             const int k = lane - 16, rr = 1 + (k >> 1), half = k & 1;
             st_sc1_64(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half,
                       lds64(fy + rr * FY_STRIDE + FY_X0 + 8 * half));
-          } else if (!luma_only && lane >= 22 && lane < 28) {
+          } else if ((from_lds || !luma_only) && lane >= 22 && lane < 28) {
             const int k = lane - 22, pl = k >= 3, rr = 1 + (k % 3);
             st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx,
                       lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0));
           }
         }
+        if (to_lds) {
+          // final rows 12..15 of this MB for the row below, and the left MB's
+          // columns 12..15 of those rows as our left-edge filter left them
+          uint8_t* bt = bot_ring[wave][slot];
+          if (lane < 8) {
+            const int rr = lane >> 1, half = lane & 1;
+            *reinterpret_cast<uint64_t*>(bt + 16 * rr + 8 * half) = lds64(fy + (16 + rr) * FY_STRIDE + FY_X0 + 8 * half);
+          } else if (lane < 16) {
+            const int k = lane - 8, pl = k >= 4, rr = k & 3;
+            *reinterpret_cast<uint64_t*>(bt + 64 + 32 * pl + 8 * rr) =
+                lds64((pl ? fv : fu) + (8 + rr) * FC_STRIDE + FC_X0);
+          } else if (mbx > 0 && do_filter && lane < 28) {
+            uint8_t* bl = bot_ring[wave][(mbx - 1) & (RING - 1)];
+            const int k = lane - 16;
+            if (k < 4) {
+              *reinterpret_cast<uint32_t*>(bl + 16 * k + 12) = lds32(fy + (16 + k) * FY_STRIDE + FY_X0 - 4);
+            } else if (!luma_only) {
+              const int pl = k >= 8, rr = k & 3;
+              *reinterpret_cast<uint32_t*>(bl + 64 + 32 * pl + 8 * rr + 4) =
+                  lds32((pl ? fv : fu) + (8 + rr) * FC_STRIDE + FC_X0 - 4);
+            }
+          }
+        }
+        // ---- rotate the reconstruction context for the next MB (:118-126) ----
+        if (lane < 16) wb[LY - 1 + lane * WG_BPS] = wb[LY + 15 + lane * WG_BPS];
+        else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = wb[LU + 7 + (lane - 16) * WG_BPS];
+        else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = wb[LV + 7 + (lane - 24) * WG_BPS];
+        else if (lane == 32) wb[LY - WG_BPS - 1] = wb[LY - WG_BPS + 15];
+        else if (lane == 33) wb[LU - WG_BPS - 1] = wb[LU - WG_BPS + 7];
+        else if (lane == 34) wb[LV - WG_BPS - 1] = wb[LV - WG_BPS + 7];
+        lds_sync();
+        STAMP(7);
+        lane = opaque_lane() & 63;
+        // ---- publish ----
+        if (to_lds) {
+          // the rings are written (lds_sync above); the frame stores of a band's
+          // rows never overlap, so no drain is needed before the LDS flag
+          if (lane == 0) __hip_atomic_store(&prog_lds[wave], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          // every store of this MB is complete before the flag
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (from_lds && lane == 0) {
+          // our progress is also what the row above's ring waits on
+          __hip_atomic_store(&prog_lds[wave], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        STAMP(8);
       }
-      // ---- rotate the reconstruction context for the next MB (:118-126) ----
-      if (lane < 16) wb[LY - 1 + lane * WG_BPS] = wb[LY + 15 + lane * WG_BPS];
-      else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = wb[LU + 7 + (lane - 16) * WG_BPS];
-      else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = wb[LV + 7 + (lane - 24) * WG_BPS];
-      else if (lane == 32) wb[LY - WG_BPS - 1] = wb[LY - WG_BPS + 15];
-      else if (lane == 33) wb[LU - WG_BPS - 1] = wb[LU - WG_BPS + 7];
-      else if (lane == 34) wb[LV - WG_BPS - 1] = wb[LV - WG_BPS + 7];
-      __syncthreads();
-      STAMP(7);
-      lane = opaque_lane();
-      // ---- publish: every store of this MB is complete before the flag ----
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      STAMP(8);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // the band's LDS rings are reused by the next band
   }
   STAMP_FLUSH();
 }
@@ -492,7 +609,7 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0 ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_rows, 64, 0) != hipSuccess || per_cu <= 0)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_bands, 64 * DW, 0) != hipSuccess || per_cu <= 0)
       return wg::check_launch("decode occupancy query");
     g_num_cus = cus;
     g_rows_per_cu = per_cu;
@@ -500,10 +617,10 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   }
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(decode ctl)");
-  const int rows = n_images * mbh;
-  const int grid = rows < g_rows_per_cu * g_num_cus ? rows : g_rows_per_cu * g_num_cus;
-  hipLaunchKernelGGL(k_decode_rows, dim3((unsigned)grid), dim3(64), 0, s, a);
-  return wg::check_launch("k_decode_rows");
+  const int bands = n_images * ((mbh + DW - 1) / DW);
+  const int grid = bands < g_rows_per_cu * g_num_cus ? bands : g_rows_per_cu * g_num_cus;
+  hipLaunchKernelGGL(k_decode_bands, dim3((unsigned)grid), dim3(64 * DW), 0, s, a);
+  return wg::check_launch("k_decode_bands");
 }
 
 extern "C" int wg_decode_status(const void* work, int32_t mbw, int32_t n_images, void* stream) {
