@@ -101,7 +101,8 @@ def test_decode_bitstreams(cuda, name):
 
 @pytest.mark.parametrize("w,h,kind,alpha", [(1, 1, "noise", False), (17, 33, "noise", True), (96, 80, "grad", False),
                                             (53, 37, "blobs", True), (200, 3, "noise", True),
-                                            (1920, 1080, "grad", False), (640, 480, "blobs", True)])
+                                            (1920, 1080, "grad", False), (640, 480, "blobs", True),
+                                            (2050, 19, "noise", False), (1028, 16, "noise", True)])
 def test_import(cuda, w, h, kind, alpha):
     gen = {"noise": lambda: synth.noise_rgba(w, h, seed=w + h, alpha=alpha),
            "grad": lambda: synth.gradient_rgba(w, h), "blobs": lambda: synth.blobs_rgba(w, h, alpha=alpha)}[kind]
@@ -154,6 +155,23 @@ def test_analysis_alphas(cuda, w, h, src):
 def test_build_nrgba(cuda, w, h, alpha):
     rng = np.random.default_rng(w * 1000 + h)
     ys, cs = w + 5, (w + 1) // 2 + 3  # strides wider than the image
+    Y = rng.integers(0, 256, (2, h, ys), dtype=np.uint8)
+    U = rng.integers(0, 256, (2, (h + 1) // 2, cs), dtype=np.uint8)
+    V = rng.integers(0, 256, (2, (h + 1) // 2, cs), dtype=np.uint8)
+    A = rng.integers(0, 256, (2, h, w), dtype=np.uint8) if alpha else None
+    out = host(frames.build_nrgba(dev(Y), dev(U), dev(V), w, h, alpha=dev(A) if alpha else None))
+    for i in range(2):
+        exp = O.build_nrgba(Y[i], U[i], V[i], w, h, alpha=A[i] if alpha else None)
+        assert (out[i] == exp).all()
+
+
+@pytest.mark.parametrize("w,h", [(16, 2), (4096, 3), (4100, 6), (8192 + 36, 5), (1936, 17)])
+@pytest.mark.parametrize("alpha", [False, True])
+def test_build_nrgba_aligned(cuda, w, h, alpha):
+    """Aligned strides (the kernel's 16-byte luma / 8-byte chroma / 16-byte
+    output paths), several 4096-column blocks per line pair."""
+    rng = np.random.default_rng(w * 7 + h)
+    ys, cs = (w + 15) // 16 * 16, ((w + 1) // 2 + 7) // 8 * 8
     Y = rng.integers(0, 256, (2, h, ys), dtype=np.uint8)
     U = rng.integers(0, 256, (2, (h + 1) // 2, cs), dtype=np.uint8)
     V = rng.integers(0, 256, (2, (h + 1) // 2, cs), dtype=np.uint8)

@@ -51,6 +51,8 @@ def main():
     out = torch.empty((B, H, W, 4), dtype=torch.uint8, device=dev)
     t = timeit(lambda: frames.build_nrgba(Y, U, V, W, H, out=out))
     print(f"upsample    {t:8.3f} ms  {px / t / 1e3:9.1f} MPix/s  {5.5 * px / t / 1e6:7.1f} GB/s")
+    if os.environ.get("STREAM_ONLY"):
+        return
     decode_cases(Y, U, V, px, dev)
     encode_cases(Y, U, V, px, dev)
 

@@ -2,9 +2,9 @@
 // (replaces VP8Encoder.importImage, internal/lossy/encode.go:671-943,
 // non-dithered direct-pixel path; arithmetic of internal/dsp/yuv.go).
 //
-// Streaming kernel: one thread per 2 rows x 8 columns of the padded frame
-// (four 2x2 chroma quads).  Reads 2x32 B of RGBA, writes 2x8 B of Y and 4 B
-// each of U and V.  Gamma tables (yuv.go:193-215) are built on the host with
+// Streaming kernel: one thread per 2 rows x 4 columns of the padded frame
+// (two 2x2 chroma quads), walking 8 row pairs.  Reads 2x16 B of RGBA, writes
+// 2x4 B of Y and 2 B each of U and V per row pair.  Gamma tables (yuv.go:193-215) are built on the host with
 // float64 pow, passed in the kernel argument block and staged in LDS.
 // Padding replicates the last column / row exactly as the reference's clamp.
 #include <math.h>
@@ -88,66 +88,66 @@ struct ImportArgs {
   const uint8_t* rgba;
   uint8_t *y, *u, *v;
   int64_t rgba_pitch, y_pitch, uv_pitch;
-  int w, h, stride, has_alpha, padw, padh, groups;  // groups = padw / 8
-  int aligned;  // rows start 16-byte aligned -> 2 x 16 B loads per row
+  int w, h, stride, has_alpha, padw, padh;
+  int chunks;    // padw / 4: 4-pixel chunks per row
+  int pairs;     // n_images * padh / 2 row pairs in the batch
+  int rp;        // row pairs walked per block (>= IM_RP; grid.y stays <= 65535)
+  int aligned;   // rows start 16-byte aligned -> one 16 B load per row and chunk
   GammaTabs tabs;
 };
 
-__global__ __launch_bounds__(256) void k_import(const ImportArgs a, int64_t total) {
+constexpr int IM_T = 256;   // threads per block: 256 chunks = 1024 columns of a row pair
+constexpr int IM_RP = 8;    // minimum row pairs walked per block (amortises the table fill)
+
+// Thread = one 4-pixel chunk of a row pair (two 2x2 chroma quads).  Lane i of
+// a wave loads bytes [16i, 16i + 16) of each of the two RGBA rows, so every
+// load instruction is one contiguous 1 KB span, and stores 4 B of Y per row
+// and 2 B each of U and V (contiguous 256 B / 128 B per wave instruction).
+__global__ __launch_bounds__(IM_T) void k_import(const ImportArgs a) {
   __shared__ uint32_t tl[256];
   __shared__ uint32_t tg[34];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) tl[i] = a.tabs.to_lin[i];
+  for (int i = threadIdx.x; i < 256; i += IM_T) tl[i] = a.tabs.to_lin[i];
   if (threadIdx.x < 34) tg[threadIdx.x] = a.tabs.to_gamma[threadIdx.x];
   __syncthreads();
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= total) return;
-  const int g = tid % a.groups;
-  const int64_t rest = tid / a.groups;
-  const int yp = rest % (a.padh / 2);
-  const int img = (int)(rest / (a.padh / 2));
-  const int x0 = 8 * g;
-  const uint8_t* src = a.rgba + img * a.rgba_pitch;
-
-  // gather 2 rows x 8 pixels (clamped to the real image)
-  uint32_t px[2][8];
-  const bool fast = a.aligned && x0 + 8 <= a.w;  // same path for both rows
+  const int cx = blockIdx.x * IM_T + threadIdx.x;
+  if (cx >= a.chunks) return;
+  const int x0 = 4 * cx;
+  const bool fast = a.aligned && x0 + 4 <= a.w;
+  const int hp = a.padh >> 1;
+  const int pair_end = min((int)(blockIdx.y + 1) * a.rp, a.pairs);
+  for (int pr = blockIdx.y * a.rp; pr < pair_end; pr++) {
+    const int img = pr / hp, yp = pr - img * hp;
+    const uint8_t* src = a.rgba + img * a.rgba_pitch;
+    uint32_t px[2][4];
 #pragma unroll
-  for (int r = 0; r < 2; r++) {
-    const int sy = min(2 * yp + r, a.h - 1);
-    const uint8_t* row = src + (int64_t)sy * a.stride;
-    if (fast) {
-      const uint4 q0 = *reinterpret_cast<const uint4*>(row + 4 * x0);
-      const uint4 q1 = *reinterpret_cast<const uint4*>(row + 4 * x0 + 16);
-      px[r][0] = q0.x; px[r][1] = q0.y; px[r][2] = q0.z; px[r][3] = q0.w;
-      px[r][4] = q1.x; px[r][5] = q1.y; px[r][6] = q1.z; px[r][7] = q1.w;
-    } else {
+    for (int r = 0; r < 2; r++) {
+      const uint8_t* row = src + (int64_t)min(2 * yp + r, a.h - 1) * a.stride;
+      if (fast) {
+        const uint4 q = *reinterpret_cast<const uint4*>(row + 4 * x0);
+        px[r][0] = q.x; px[r][1] = q.y; px[r][2] = q.z; px[r][3] = q.w;
+      } else {
 #pragma unroll
-      for (int i = 0; i < 8; i++) px[r][i] = *reinterpret_cast<const uint32_t*>(row + 4 * min(x0 + i, a.w - 1));
+        for (int i = 0; i < 4; i++) px[r][i] = *reinterpret_cast<const uint32_t*>(row + 4 * min(x0 + i, a.w - 1));
+      }
     }
-  }
-  // Y (encode.go:757-793)
+    // Y (encode.go:757-793)
 #pragma unroll
-  for (int r = 0; r < 2; r++) {
-    uint32_t lo = 0, hi = 0;
+    for (int r = 0; r < 2; r++) {
+      uint32_t yw = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const uint32_t p = px[r][i];
-      const uint32_t yv = (uint32_t)rgb_to_y(p & 0xff, (p >> 8) & 0xff, (p >> 16) & 0xff);
-      if (i < 4) lo |= yv << (8 * i);
-      else hi |= yv << (8 * (i - 4));
+      for (int i = 0; i < 4; i++) {
+        const uint32_t p = px[r][i];
+        yw |= (uint32_t)rgb_to_y(p & 0xff, (p >> 8) & 0xff, (p >> 16) & 0xff) << (8 * i);
+      }
+      *reinterpret_cast<uint32_t*>(a.y + img * a.y_pitch + (int64_t)(2 * yp + r) * a.padw + x0) = yw;
     }
-    *reinterpret_cast<uint2*>(a.y + img * a.y_pitch + (int64_t)(2 * yp + r) * a.padw + x0) = make_uint2(lo, hi);
+    // U/V: AccumulateRGBA (yuv.go:486-517) + ConvertRGBA32ToUV (:553-562)
+    const uint32_t uv0 = quad_uv(tl, tg, px[0][0], px[0][1], px[1][0], px[1][1], a.has_alpha);
+    const uint32_t uv1 = quad_uv(tl, tg, px[0][2], px[0][3], px[1][2], px[1][3], a.has_alpha);
+    const int64_t co = img * a.uv_pitch + (int64_t)yp * (a.padw >> 1) + (x0 >> 1);
+    *reinterpret_cast<uint16_t*>(a.u + co) = (uint16_t)((uv0 & 0xff) | ((uv1 & 0xff) << 8));
+    *reinterpret_cast<uint16_t*>(a.v + co) = (uint16_t)((uv0 >> 8) | (uv1 & 0xff00));
   }
-  // U/V: AccumulateRGBA (yuv.go:486-517) + ConvertRGBA32ToUV (:553-562)
-  const uint32_t uv0 = quad_uv(tl, tg, px[0][0], px[0][1], px[1][0], px[1][1], a.has_alpha);
-  const uint32_t uv1 = quad_uv(tl, tg, px[0][2], px[0][3], px[1][2], px[1][3], a.has_alpha);
-  const uint32_t uv2 = quad_uv(tl, tg, px[0][4], px[0][5], px[1][4], px[1][5], a.has_alpha);
-  const uint32_t uv3 = quad_uv(tl, tg, px[0][6], px[0][7], px[1][6], px[1][7], a.has_alpha);
-  const uint32_t uo = (uv0 & 0xff) | ((uv1 & 0xff) << 8) | ((uv2 & 0xff) << 16) | ((uv3 & 0xff) << 24);
-  const uint32_t vo = (uv0 >> 8) | ((uv1 >> 8) << 8) | ((uv2 >> 8) << 16) | ((uv3 >> 8) << 24);
-  const int64_t co = img * a.uv_pitch + (int64_t)yp * (a.padw / 2) + x0 / 2;
-  *reinterpret_cast<uint32_t*>(a.u + co) = uo;
-  *reinterpret_cast<uint32_t*>(a.v + co) = vo;
 }
 
 }  // namespace
@@ -176,10 +176,13 @@ extern "C" int wg_import_rgba(const uint8_t* rgba, int32_t w, int32_t h, int32_t
   a.has_alpha = has_alpha ? 1 : 0;
   a.padw = 16 * mbw;
   a.padh = 16 * mbh;
-  a.groups = a.padw / 8;
+  a.chunks = a.padw / 4;
+  WG_REQUIRE((int64_t)n_images * (a.padh / 2) < (1ll << 31) / 2);
+  a.pairs = n_images * (a.padh / 2);
   a.tabs = host_tabs();
   a.aligned = ((reinterpret_cast<uintptr_t>(rgba) | (uintptr_t)stride | (uintptr_t)rgba_pitch) & 15) == 0;
-  const int64_t total = (int64_t)n_images * (a.padh / 2) * a.groups;
-  hipLaunchKernelGGL(k_import, dim3(wg::blocks_for(total, 256)), dim3(256), 0, wg::as_stream(stream), a, total);
+  a.rp = max(IM_RP, (int)wg::blocks_for(a.pairs, 65535));
+  const dim3 grid(wg::blocks_for(a.chunks, IM_T), wg::blocks_for(a.pairs, a.rp));
+  hipLaunchKernelGGL(k_import, grid, dim3(IM_T), 0, wg::as_stream(stream), a);
   return wg::check_launch("k_import");
 }
