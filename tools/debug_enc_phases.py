@@ -12,7 +12,9 @@ from tools import synth
 B, W, H = int(os.environ.get("BATCH", "64")), 1920, 1080
 MBW, MBH = 120, 68
 names = ["wait", "import+ctx", "i16rd", "i4rd", "uvrd", "final", "recon+export", "-", "i4:prescreen", "i4:select", "i4:candidates", "i4:winner", "c:pred+fdct", "c:trellis", "c:recon+disto", "c:rate"]
-_lib.lib.wg_debug_enc_phases.argtypes = [ctypes.c_void_p, ctypes.c_int]
+STAMPED = hasattr(_lib.lib, "wg_debug_enc_phases")  # only the stamped build (-DWG_STAMPS) exports it
+if STAMPED:
+    _lib.lib.wg_debug_enc_phases.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = (ctypes.c_ulonglong * 16)()
 content = os.environ.get("CONTENT", "blobs")
 gens = {"blobs": lambda: synth.blobs_rgba(W, H, seed=3), "noise": lambda: synth.noise_rgba(W, H, seed=3),
@@ -26,10 +28,14 @@ segs = np.stack([frames.setup_segment(q) for q in (20, 24, 28, 32)])
 seg_ids = torch.from_numpy((np.arange(B * MBW * MBH) % 4).astype(np.uint8)).cuda()
 out, rec = frames.encode_mbs(Yt, Ut, Vt, W, H, seg_ids, segs, O.default_proba())
 torch.cuda.synchronize()
-_lib.lib.wg_debug_enc_phases(ctypes.addressof(buf), 16)
+if STAMPED:
+    _lib.lib.wg_debug_enc_phases(ctypes.addressof(buf), 16)
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record(); frames.encode_mbs(Yt, Ut, Vt, W, H, seg_ids, segs, O.default_proba(), out=out, recon=rec); e1.record()
 torch.cuda.synchronize()
+if not STAMPED:
+    print(f"[{content}] {e0.elapsed_time(e1):.3f} ms")
+    sys.exit(0)
 _lib.lib.wg_debug_enc_phases(ctypes.addressof(buf), 16)
 v = np.frombuffer(buf, dtype=np.uint64)[:16].astype(np.float64) / (MBW * MBH * B)
 print(f"[{content}] {e0.elapsed_time(e1):.3f} ms; cycles per MB: " + ", ".join(f"{n}={x:.0f}" for n, x in zip(names, v)) + f"; total={v[:7].sum():.0f}")

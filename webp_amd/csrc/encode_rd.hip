@@ -334,29 +334,49 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   int best = -1;  // n << 2 | end context
   const int64_t* mine = &rec[0].x[role][0];
   constexpr int STRIDE = sizeof(TRec) / sizeof(int64_t);
+  // Everything position n reads from LDS (its three transitions, its class,
+  // the EOB costs of band n+1) is loaded during position n-1 and pinned by
+  // the asm below, so the wait for it lands one full position after the
+  // load; loading and using within one position put two LDS round trips on
+  // the DP's serial chain.
   int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
-  int cls_next = l0s[FIRST] & 3;
+  // raw loads only: any use right after the load (even "& 3") makes the
+  // compiler wait for it there
+  int cls_raw = l0s[FIRST];
+  uint2 eob_raw = *reinterpret_cast<const uint2*>(t.tok[CTX_TYPE * 8 + kBand[FIRST + 1]].eob);  // eob[0..3]
 #pragma unroll
   for (int n = 0; n < 16; n++) {
     if (n < FIRST) {
       if (!(n & 1)) path[n >> 1] = 0;
       continue;
     }
-    const int64_t c0 = ps0 + x0, c1 = ps1 + x1, c2 = ps2 + x2;
-    const int cls = cls_next;
-    if (n < 15) {  // one position ahead
-      x0 = mine[(n + 1) * STRIDE];
-      x1 = mine[(n + 1) * STRIDE + 1];
-      x2 = mine[(n + 1) * STRIDE + 2];
-      cls_next = l0s[n + 1] & 3;
+    // issue the next position's loads first; the asm then keeps this
+    // position's compute (everything hangs off ps*) from floating above them
+    int64_t nx0 = 0, nx1 = 0, nx2 = 0;
+    int ncls = 0;
+    uint2 neob = make_uint2(0, 0);
+    if (n < 15) {
+      nx0 = mine[(n + 1) * STRIDE];
+      nx1 = mine[(n + 1) * STRIDE + 1];
+      nx2 = mine[(n + 1) * STRIDE + 2];
+      ncls = l0s[n + 1];
+      if (n + 1 < 15) neob = *reinterpret_cast<const uint2*>(t.tok[CTX_TYPE * 8 + kBand[n + 2]].eob);
     }
     asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
+    const int64_t c0 = ps0 + x0, c1 = ps1 + x1, c2 = ps2 + x2;
+    const int cls_n = cls_raw & 3;
+    const uint32_t e1_n = eob_raw.x >> 16, e2_n = eob_raw.y & 0xffff;
+    x0 = nx0;
+    x1 = nx1;
+    x2 = nx2;
+    cls_raw = ncls;
+    eob_raw = neob;
     int64_t m = c1 < c0 ? c1 : c0;
     m = c2 < m ? c2 : m;
     const int64_t kz = quad_bcast<0>(m), ka = quad_bcast<1>(m), kb = quad_bcast<2>(m);
     const int64_t kab = kb < ka ? kb : ka;
-    const int64_t k1 = cls == 0 ? kb : (cls == 1 ? ka : BIG);
-    const int64_t k2 = cls == 0 ? BIG : (cls == 1 ? kb : kab);
+    const int64_t k1 = cls_n == 0 ? kb : (cls_n == 1 ? ka : BIG);
+    const int64_t k2 = cls_n == 0 ? BIG : (cls_n == 1 ? kb : kab);
     const uint32_t pr = ((uint32_t)kz & 15) | (((uint32_t)k1 & 15) << 4) | (((uint32_t)k2 & 15) << 8);
     if (n & 1)
       path[n >> 1] |= pr << 16;
@@ -366,12 +386,11 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
     ps1 = k1 & ~15ll;
     ps2 = k2 & ~15ll;
     // terminal (EOB after this position) from end contexts 1 and 2
-    const TokRow& tr = t.tok[CTX_TYPE * 8 + kBand[n + 1]];
-    const int64_t eob1 = ps1 + (n < 15 ? (int64_t)tr.eob[1] * lam16 : 0);
+    const int64_t eob1 = ps1 + (n < 15 ? (int64_t)e1_n * lam16 : 0);
     const bool w1 = ps1 < VALID && eob1 < best_terminal;
     best_terminal = w1 ? eob1 : best_terminal;
     best = w1 ? (n << 2 | 1) : best;
-    const int64_t eob2 = ps2 + (n < 15 ? (int64_t)tr.eob[2] * lam16 : 0);
+    const int64_t eob2 = ps2 + (n < 15 ? (int64_t)e2_n * lam16 : 0);
     const bool w2 = ps2 < VALID && eob2 < best_terminal;
     best_terminal = w2 ? eob2 : best_terminal;
     best = w2 ? (n << 2 | 2) : best;
