@@ -373,6 +373,12 @@ int wg_sharpyuv_convert(const uint8_t* rgb, int32_t width, int32_t height, int32
                         uint8_t* u, uint8_t* v, int32_t uv_stride, int64_t uv_pitch, void* work, void* stream);
 /* The gamma tables used (gamma.go:48-88), host copies: g2l[1026], l2g[514]. */
 int wg_sharpyuv_tables_host(uint32_t* g2l, uint32_t* l2g);
+/* After wg_sharpyuv_convert on `work` (same stream): the refinement
+ * iterations each image ran, the count the reference's early exit gives
+ * (sharpyuv.go:254-263; 2..4).  Synchronises the stream; WG_EHIP if a
+ * pipeline dependency wait timed out (the output is then invalid). */
+int wg_sharpyuv_iterations(const void* work, int32_t width, int32_t height, int32_t n_images, int32_t* out,
+                           void* stream);
 
 #ifdef __cplusplus
 }

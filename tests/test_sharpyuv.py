@@ -49,12 +49,16 @@ def rgb_cases():
 def test_gpu_matches_oracle(cuda):
     import torch
     from webp_amd import frames
+    seen = set()
     for name, rgb in rgb_cases():
-        Y, U, V = frames.sharpyuv_convert(torch.from_numpy(rgb[None].copy()).cuda())
-        ey, eu, ev, _ = O.sharpyuv_convert(rgb)
+        Y, U, V, its = frames.sharpyuv_convert(torch.from_numpy(rgb[None].copy()).cuda(), iterations=True)
+        ey, eu, ev, eits = O.sharpyuv_convert(rgb)
         torch.cuda.synchronize()
         assert (Y[0].cpu().numpy() == ey).all(), name
         assert (U[0].cpu().numpy() == eu).all() and (V[0].cpu().numpy() == ev).all(), name
+        assert its[0] == eits, name  # the speculative pipeline stops where the reference's early exit does
+        seen.add(int(eits))
+    assert len(seen) >= 2, seen  # the cases reach more than one exit point
 
 
 @pytest.mark.gpu

@@ -86,6 +86,7 @@ SIGNATURES = {
     "wg_sharpyuv_work_bytes": [_i32, _i32, _i32],
     "wg_sharpyuv_convert": [_vp, _i32, _i32, _i32, _i64, _vp, _i32, _vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _vp],
     "wg_sharpyuv_tables_host": [_vp, _vp],
+    "wg_sharpyuv_iterations": [_vp, _i32, _i32, _i32, _vp, _vp],
     "wg_setup_segment": [_i32, _vp, _i32, _i32, _vp],
     "wg_encode_work_bytes": [_i32, _i32, _i32],
     "wg_encode_mbs": [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
