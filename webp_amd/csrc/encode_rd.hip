@@ -1261,35 +1261,88 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           for (int i = 1; i < 16; i++) s.co_buf[lane][i] = co[i];
         }
         lds_sync();
-        // trellis along block diagonals (each block needs its left / top nz):
-        // lane (diagonal slot j, pair pp) prepares positions 2pp, 2pp + 1 of
-        // block j on the diagonal, then the block's lane runs the DP
+        // Trellis of the 16 AC blocks.  A block's DP depends on its left / top
+        // neighbours' nz only through its initial context min(l + t, 2), so
+        // it is run speculatively for every context the block can still get
+        // (1 for block 0, 2 along the MB's top row / left column, 3 inside):
+        // three rounds of up to six blocks (their position records fit the
+        // six trellis slots) and up to 16 DPs, one per lane quad, each
+        // followed by the reference's raster-order resolution of the actual
+        // contexts.  (Walking the 7 block diagonals took 7 prep + DP rounds.)
         const int lam16 = sg.tlambda_i16 * 16;
-        for (int d = 0; d < 7; d++) {
+        int16_t* res_q = reinterpret_cast<int16_t*>(s.yout2);  // [16 tasks][16] levels (yout2 is free for I16 MBs)
+        int* res_nz = reinterpret_cast<int*>(s.yout2 + 512);   // [16]
+        for (int r = 0; r < 3; r++) {
           Shared& s = launder(s_waves[wave]);
           Tables& t = launder(t_lds);
-          const int by_lo = max(0, d - 3), nblk = min(d, 3) - by_lo + 1;
+          const int first = r == 0 ? 0 : (r == 1 ? 6 : 11), m = r == 0 ? 6 : 5;
           bool pnz = false;
-          if (lane < 8 * nblk) {
-            const int j = lane >> 3, n0 = 2 * (lane & 7), pb = (by_lo + j) * 4 + d - (by_lo + j);
+          if (lane < 8 * m) {
+            const int j = lane >> 3, n0 = 2 * (lane & 7), pb = first + j;
+            TRec rr[2];
+            int l0[2];
+#pragma unroll
+            for (int k = 0; k < 2; k++) {  // position 0 (the DC, coded by the WHT) is not part of this trellis
+              const bool used = n0 + k >= 1;
+              pnz |= trellis_prep<0>(t, used ? s.co_buf[pb][zig_of(n0 + k)] : 0, n0 + k, sg.y1, lam16, rr[k], l0[k]) && used;
+            }
 #pragma unroll
             for (int k = 0; k < 2; k++)
-              if (n0 + k >= 1) pnz |= trellis_prep<0>(t, s.co_buf[pb][zig_of(n0 + k)], n0 + k, sg.y1, lam16, s.trec[j][n0 + k], s.l0s[j][n0 + k]);
+              if (n0 + k >= 1) {
+                s.trec[j][n0 + k] = rr[k];
+                s.l0s[j][n0 + k] = l0[k];
+              }
           }
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
-          if (lane < 4 * nblk) {  // one lane quad per block of the diagonal
-            const int j = lane >> 2, qby = by_lo + j, qbx = d - qby, qb = qby * 4 + qbx;
-            const int l = qbx > 0 ? (s.nzy[qb - 1] > 0) : (int)((left_nz >> qby) & 1);
-            const int tp = qby > 0 ? (s.nzy[qb - 4] > 0) : (int)((top_nz >> qbx) & 1);
-            int nzv = 0;
-            if ((pnz_mask >> (8 * j)) & 0xff) {
-              trellis_dp4<1, 0>(t, s.trec[j], s.l0s[j], min(l + tp, 2), lam16, lane & 3, s.coeffs + qb * 16, &nzv);
-            } else if ((lane & 3) == 0) {
-#pragma unroll
-              for (int i = 0; i < 16; i++) s.coeffs[qb * 16 + i] = 0;
+          // quad q runs task q: walk the round's blocks to find its (block, context)
+          {
+            const int q = lane >> 2;
+            int acc = 0, tj = -1, tctx = 0;
+            for (int j = 0; j < m; j++) {
+              const int qb = first + j, qbx = qb & 3, qby = qb >> 2;
+              const int nfix = (qbx == 0) + (qby == 0);
+              const int fixed = (qbx == 0 ? (int)((left_nz >> qby) & 1) : 0) + (qby == 0 ? (int)((top_nz >> qbx) & 1) : 0);
+              const int nopt = 3 - nfix;  // contexts fixed + 0 .. fixed + nopt - 1
+              if (tj < 0 && q < acc + nopt) {
+                tj = j;
+                tctx = fixed + (q - acc);
+              }
+              acc += nopt;
             }
-            if ((lane & 3) == 0) s.nzy[qb] = (uint8_t)nzv;
+            if (tj >= 0) {
+              if ((pnz_mask >> (8 * tj)) & 0xff) {
+                int nzv = 0;
+                trellis_dp4<1, 0>(t, s.trec[tj], s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
+                if ((lane & 3) == 0) res_nz[q] = nzv;
+              } else if ((lane & 3) == 0) {
+#pragma unroll
+                for (int i = 0; i < 16; i++) res_q[q * 16 + i] = 0;
+                res_nz[q] = 0;
+              }
+            }
+          }
+          lds_sync();
+          // the reference's raster order: each block's actual context picks its task
+          if (lane == 0) {
+            int acc = 0;
+            for (int j = 0; j < m; j++) {
+              const int qb = first + j, qbx = qb & 3, qby = qb >> 2;
+              const int nfix = (qbx == 0) + (qby == 0);
+              const int fixed = (qbx == 0 ? (int)((left_nz >> qby) & 1) : 0) + (qby == 0 ? (int)((top_nz >> qbx) & 1) : 0);
+              const int l = qbx > 0 ? (s.nzy[qb - 1] > 0) : (int)((left_nz >> qby) & 1);
+              const int tp = qby > 0 ? (s.nzy[qb - 4] > 0) : (int)((top_nz >> qbx) & 1);
+              const int task = acc + min(l + tp, 2) - fixed;
+              s.nzy[qb] = (uint8_t)res_nz[task];
+              s.modes4[qb] = (uint8_t)task;  // scratch: the task each block takes (modes4 is I4-only)
+              acc += 3 - nfix;
+            }
+          }
+          lds_sync();
+          if (lane < 8 * m) {  // copy the chosen levels, two per lane
+            const int j = lane >> 3, qb = first + j, task = s.modes4[qb];
+            reinterpret_cast<uint32_t*>(s.coeffs + qb * 16)[lane & 7] =
+                reinterpret_cast<const uint32_t*>(res_q + task * 16)[lane & 7];
           }
           lds_sync();
         }
