@@ -586,6 +586,18 @@ __device__ __forceinline__ int check_mode(int mbx, int mby, int mode) {
 __device__ __forceinline__ uint64_t rd_score(int disto, int rate, int lambda) {
   return (uint64_t)(int64_t)rate * (uint64_t)(int64_t)lambda + 256ull * (uint64_t)(int64_t)disto;
 }
+// Sum over an aligned group of 8 / 16 lanes, valid in the group's FIRST lane
+// only, by DPP (quad_perm swaps, then row_ror): the __shfl_xor form went
+// through ds_bpermute, an LDS round trip per level.
+template <int WIDTH>
+__device__ __forceinline__ int group_sum_first(int v) {
+  static_assert(WIDTH == 8 || WIDTH == 16, "group width");
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x12C, 0xf, 0xf, false);  // row_ror:12 (lane i <- i + 4 mod 16)
+  if (WIDTH == 16) v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  return v;
+}
 template <typename T>
 __device__ __forceinline__ T group_sum(T v, int width) {  // sum over aligned groups of `width` lanes
   for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -913,7 +925,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
         recon4(pred16, dq, rec16);
         const int sse = sse16(src16, rec16);
         const int td = sg.tlambda_sd > 0 ? tdisto(src16, rec16) : 0;
-        const int rsum = group_sum(rate, 16), ssum = group_sum(sse, 16), tsum = group_sum(td, 16);
+        const int rsum = group_sum_first<16>(rate), ssum = group_sum_first<16>(sse), tsum = group_sum_first<16>(td);  // used by lane b == 0
         const unsigned long long acmask = __ballot(acnz);
         if (b == 0 && mvalid) {
           const int total_rate = s.mode_rate[m] + rsum;
@@ -1205,7 +1217,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
 #pragma unroll
           for (int i = 1; i < 16; i++) acn += q[i] != 0;
         }
-        const int rsum = group_sum(rate, 8), ssum = group_sum(sse, 8), asum = group_sum(acn, 8);
+        const int rsum = group_sum_first<8>(rate), ssum = group_sum_first<8>(sse), asum = group_sum_first<8>(acn);  // used by lane k == 0
         if (act && k == 0) {
           int total = vp8_mode_fixed_cost_uv[um] + rsum;
           if (um > 0 && asum <= 2) total += 140 * 8;
