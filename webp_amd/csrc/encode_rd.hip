@@ -1129,10 +1129,16 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
             const int nzc = s.cand_nz[sl];
             part = token_cost_pos<3>(t, s.cand_q[sl], n0, nzc, nz_ctx, 0) + token_cost_pos<3>(t, s.cand_q[sl], n0 + 1, nzc, nz_ctx, 0);
           }
-          part += __shfl_xor(part, 1, 64);
-          part += __shfl_xor(part, 2, 64);
-          part += __shfl_xor(part, 4, 64);
-          const int tok_rate = __shfl(part, 32 * half + 8 * qc, 64);
+          // candidate c's rate sits in lane 32 * half + 8c; read the six with
+          // v_readlane (wave-uniform lanes) instead of LDS permutes
+          part = group_sum_first<8>(part);
+          int tok_rate;
+          {
+            const int r00 = __builtin_amdgcn_readlane(part, 0), r01 = __builtin_amdgcn_readlane(part, 8);
+            const int r02 = __builtin_amdgcn_readlane(part, 16), r10 = __builtin_amdgcn_readlane(part, 32);
+            const int r11 = __builtin_amdgcn_readlane(part, 40), r12 = __builtin_amdgcn_readlane(part, 48);
+            tok_rate = half ? pick3(qc, r10, r11, r12) : pick3(qc, r00, r01, r02);
+          }
           uint64_t score = ~0ull;
           int rate = 0;
           if (qact) {
