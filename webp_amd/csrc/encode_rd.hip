@@ -889,7 +889,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
         nz16 = quantize(co, q16, sg.y1, 1);
       }
       // contexts from the neighbours' nz within the same mode
-      const int nz_left = __shfl(nz16, (lane - 1) & 63, 64), nz_top = __shfl(nz16, (lane - 4) & 63, 64);
+      // left / top neighbour within the mode's 16-lane row (only read when bx / by > 0): DPP row shifts
+      const int nz_left = __builtin_amdgcn_update_dpp(0, nz16, 0x111, 0xf, 0xf, false);  // row_shr:1
+      const int nz_top = __builtin_amdgcn_update_dpp(0, nz16, 0x114, 0xf, 0xf, false);   // row_shr:4
       {
         const int l = bx > 0 ? (nz_left > 0) : (int)((left_nz >> by) & 1);
         const int tp = by > 0 ? (nz_top > 0) : (int)((top_nz >> bx) & 1);
@@ -1210,7 +1212,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           fdct(src, pred, co);
           nz = quantize(co, q, sg.uv, 0);
         }
-        const int nzl = __shfl(nz, (lane - 1) & 63, 64), nzt = __shfl(nz, (lane - 2) & 63, 64);
+        // left / top block of the same plane (only read when ubx / uby > 0): DPP row shifts
+        const int nzl = __builtin_amdgcn_update_dpp(0, nz, 0x111, 0xf, 0xf, false);  // row_shr:1
+        const int nzt = __builtin_amdgcn_update_dpp(0, nz, 0x112, 0xf, 0xf, false);  // row_shr:2
         int rate = 0, sse = 0, acn = 0;
         if (act) {
           const int l = ubx > 0 ? (nzl > 0) : (int)((left_nz >> (4 + 2 * pl + uby)) & 1);
