@@ -249,7 +249,6 @@ __global__ __launch_bounds__(ITER_THREADS) void k_sharp_pipe(SharpArgs a) {
       if (i >= uvw) continue;
       // interpolateTwoRows (:322-359) for pixels x = 2i, 2i+1 of rows j, j+1
       int iv[2][2][3];
-      const int64_t y0 = (int64_t)j * w + 2 * i, y1 = y0 + w;
       const uint32_t r0 = ycur[k][0], r1 = ycur[k][1];
       const int by00 = r0 & 0xffff, by01 = r0 >> 16, by10 = r1 & 0xffff, by11 = r1 >> 16;
       for (int ch = 0; ch < 3; ch++) {
