@@ -318,8 +318,10 @@ __global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __syncthreads();
       }
-      // row above at x (lane k-1's newest output) and x-1 (its previous one)
-      int top = __shfl_up(o1, 1, 64), top_left = __shfl_up(o2, 1, 64);
+      // row above at x (lane k-1's newest output) and x-1 (its previous one),
+      // by a whole-wave DPP shift (wave_shr:1) rather than an LDS permute
+      int top = __builtin_amdgcn_update_dpp(0, o1, 0x138, 0xf, 0xf, false);
+      int top_left = __builtin_amdgcn_update_dpp(0, o2, 0x138, 0xf, 0xf, false);
       if (lane == 0 && x < w) {
         const int k = x - (s & ~63);  // x - c0
         top = up_buf[k + 1];
@@ -334,7 +336,7 @@ __global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
         o2 = o1;
         o1 = v;
         *cell = (uint8_t)v;
-        if (lane == last_lane) my_row[x] = (uint8_t)v;  // hand-off copy for the band below
+        if (!fast && lane == last_lane) my_row[x] = (uint8_t)v;  // hand-off copy for the band below
       } else {
         o2 = o1;
         o1 = 0;
@@ -343,9 +345,25 @@ __global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
       // publish the band's last row every 64 columns (and at its end)
       const int xl = s - last_lane;
       if (band + 1 < a.bands && xl >= 0 && ((xl & 63) == 63 || xl == w - 1)) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == last_lane) __hip_atomic_store(prog_mine, xl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (fast) {
+          // the chunk of the last row, from the last lane's ring, as 4-byte
+          // write-through (sc1) stores: no L2 write-back fence per chunk (a
+          // release fence here cost microseconds every 64 steps)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+          const int c0 = xl & ~63, n = xl - c0 + 1;
+          if (4 * lane < n) {
+            const uint32_t word = *reinterpret_cast<const uint32_t*>(ring + last_lane * GB_STRIDE + ((c0 + 4 * lane) & 127));
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(d + (int64_t)(1 + band * 64 + last_lane) * w + c0 + 4 * lane), word,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_store(prog_mine, xl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          if (lane == last_lane) __hip_atomic_store(prog_mine, xl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
     // the last two chunks (or one) have not been stored yet
