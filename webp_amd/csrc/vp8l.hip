@@ -40,26 +40,41 @@ __device__ __forceinline__ uint32_t add_pixels(uint32_t a, uint32_t b) {
 }
 __device__ __forceinline__ uint32_t avg2(uint32_t a, uint32_t b) { return (((a ^ b) & 0xfefefefeu) >> 1) + (a & b); }
 __device__ __forceinline__ int chan(uint32_t v, int s) { return (int)((v >> s) & 0xff); }
+// Select (encode_predictor.go:49-95): sum over channels of |l - tl| minus
+// that of |t - tl|, as two v_sad_u8 (sum of absolute byte differences)
 __device__ __forceinline__ uint32_t select_pred(uint32_t l, uint32_t t, uint32_t tl) {
-  int pa = 0;
-#pragma unroll
-  for (int s = 0; s < 32; s += 8) pa += abs(chan(l, s) - chan(tl, s)) - abs(chan(t, s) - chan(tl, s));
+  const int pa = (int)__builtin_amdgcn_sad_u8(l, tl, 0u) - (int)__builtin_amdgcn_sad_u8(t, tl, 0u);
   return pa <= 0 ? t : l;
 }
-__device__ __forceinline__ uint32_t clamp_add_sub_full(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int s = 0; s < 32; s += 8) r |= (uint32_t)min(max(chan(a, s) + chan(b, s) - chan(c, s), 0), 255) << s;
+// The clamped predictors on two 16-bit lanes at a time (bytes 0, 2 and bytes
+// 1, 3 of the pixel); every intermediate fits int16.
+typedef short v2i16 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2i16 lanes16(uint32_t x) {
+  v2i16 r;
+  r.x = (short)(x & 0xff);
+  r.y = (short)((x >> 16) & 0xff);
   return r;
 }
+__device__ __forceinline__ uint32_t pack16(v2i16 v) { return (uint32_t)(uint16_t)v.x | (uint32_t)(uint16_t)v.y << 16; }
+__device__ __forceinline__ v2i16 clamp255(v2i16 v) {
+  const v2i16 zero = {0, 0}, top = {255, 255};
+  return __builtin_elementwise_min(__builtin_elementwise_max(v, zero), top);
+}
+__device__ __forceinline__ uint32_t clamp_add_sub_full(uint32_t a, uint32_t b, uint32_t c) {
+  const v2i16 lo = clamp255(lanes16(a) + lanes16(b) - lanes16(c));                // bytes 0, 2
+  const v2i16 hi = clamp255(lanes16(a >> 8) + lanes16(b >> 8) - lanes16(c >> 8));  // bytes 1, 3
+  return pack16(lo) | pack16(hi) << 8;
+}
+__device__ __forceinline__ v2i16 half_step(v2i16 va, v2i16 vc) {
+  const v2i16 d = va - vc;
+  // d / 2 truncating toward zero, as Go's '/': add 1 to negative d before the arithmetic shift
+  const v2i16 neg = {(short)(d.x < 0), (short)(d.y < 0)};
+  return clamp255(va + ((d + neg) >> (v2i16){1, 1}));
+}
 __device__ __forceinline__ uint32_t clamp_add_sub_half(uint32_t avg, uint32_t c) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int s = 0; s < 32; s += 8) {
-    const int va = chan(avg, s), vc = chan(c, s);
-    r |= (uint32_t)min(max(va + (va - vc) / 2, 0), 255) << s;  // '/' truncates toward zero, as Go's
-  }
-  return r;
+  const v2i16 lo = half_step(lanes16(avg), lanes16(c));
+  const v2i16 hi = half_step(lanes16(avg >> 8), lanes16(c >> 8));
+  return pack16(lo) | pack16(hi) << 8;
 }
 // predictPixel (encode_predictor.go:148-180); the decoder's switch
 // (decode_transform.go:257-350) computes the same predictors.
