@@ -1045,7 +1045,11 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           if (bvalid && hl < 4 * K) {
             const int c = hl >> 2, sl = half * 3 + c;
             if ((pnz_mask >> (32 * half + 8 * c)) & 0xff) {
+              // the DP is the step's serial chain: let it win issue arbitration
+              // against the SIMD's other wave while it runs
+              __builtin_amdgcn_s_setprio(2);
               trellis_dp4<0, 3>(t, s.trec[sl], s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
+              __builtin_amdgcn_s_setprio(0);
             } else if ((hl & 3) == 0) {
 #pragma unroll
               for (int i = 0; i < 16; i++) s.cand_q[sl][i] = 0;
