@@ -740,6 +740,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
     t.tok[tid] = r;
   }
   __syncthreads();  // the tables are read-only from here; the waves run independently
+  __builtin_amdgcn_s_setprio(1);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
   Shared& s = s_waves[wave];
@@ -956,7 +957,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
       const uint64_t s16 = rd_score(disto16, rate16, sg.lambda_mode);
 
       ESTAMP(3);
-      __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(2);
       // ================= I4 RD (tryI4ModesRDParallel :739-846) =================
       // The 16 blocks run as a wavefront, step st = bx + 2 by: a block's left,
       // top and top-right neighbours (the LD/VL context) all finish in earlier
@@ -1048,9 +1049,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
             if ((pnz_mask >> (32 * half + 8 * c)) & 0xff) {
               // the DP is the step's serial chain: let it win issue arbitration
               // against the SIMD's other wave while it runs
-              __builtin_amdgcn_s_setprio(2);
+              __builtin_amdgcn_s_setprio(3);
               trellis_dp4<0, 3>(t, s.trec[sl], s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
-              __builtin_amdgcn_s_setprio(1);
+              __builtin_amdgcn_s_setprio(2);
             } else if ((hl & 3) == 0) {
 #pragma unroll
               for (int i = 0; i < 16; i++) s.cand_q[sl][i] = 0;
@@ -1198,7 +1199,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
         s4 = early ? ~0ull : rd_score(run_disto, run_rate + 211, sg.lambda_mode);
       }
       const bool is_i4 = s4 < s16;
-      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(1);
 
       ESTAMP(4);
       // ================= UV RD (pickBestUVModeRDParallel :1030-1114) =================
