@@ -147,9 +147,13 @@ int wg_vp8_parse(const uint8_t* data, size_t size, int32_t* dims, wg_mb_info* mb
 /* Encoder macroblock RD loop: Phase A of encodeFrameParallel
  * (internal/lossy/encode_parallel.go:168-1495; encodeRow :252-338), method
  * >= 4 (methods 4-6 run the same Phase A; method 3 returns WG_EINVAL).
+ * Frames with mbh < 4 (height <= 48) return WG_EINVAL: EncodeFrame
+ * (internal/lossy/encode.go:1356) encodes those with the serial encodeFrame.
+ * out / work must be 16-byte aligned, the planes 4-byte aligned.
  * y/u/v: the encoder's padded planes (importImage output: Y stride 16*mbw,
  * U/V 8*mbw), pitches per image.  segments: per-MB segment id (NULL = all 0).
- * segs: 4 x wg_segment (device).  proba: the 4x8x3x11 coefficient
+ * segs: 4 x wg_segment per image (device, 16-byte aligned), segs_pitch bytes
+ * apart (0: the same 4 for every image; wg_segment_analysis writes them).  proba: the 4x8x3x11 coefficient
  * probabilities Phase A prices tokens with (device; ResetProba gives
  * CoeffsProba0).  out: n_images*mbw*mbh wg_mb_enc.  ry/ru/rv receive the
  * reconstruction (exportParallel writes it over the source planes; passing
@@ -178,13 +182,55 @@ typedef struct wg_mb_enc {  /* MBEncInfo, encode.go:241-276 (Phase A outputs) */
 /* setupSegment (encode.go:1085-1181) for quantiser index q and the frame's
  * dq deltas {y1_dc, y2_dc, y2_ac, uv_dc, uv_ac}; host memory. */
 int wg_setup_segment(int32_t q, const int32_t* dq5, int32_t method, int32_t sns_strength, wg_segment* out);
+/* Encoder configuration the analysis reads: the EncodeConfig fields of
+ * internal/lossy/encode.go:30-63 (DefaultConfig(75) :66-86 = quality 75,
+ * method 4, sns 50, filter strength 60, sharpness 0, type 1, 4 segments,
+ * preprocessing 0).  seg_quant[a + 127] is setSegmentParams' quantiser for a
+ * segment alpha a in [-127, 127] (encode_analysis.go:128-142, the one
+ * floating-point step, built on the host by wg_encoder_config). */
+typedef struct wg_enc_config {
+  int32_t quality, method, sns_strength, filter_strength, filter_sharpness, filter_type, segments, preprocessing;
+  uint8_t seg_quant[256];
+} wg_enc_config;
+int wg_encoder_config(int32_t quality, int32_t method, int32_t sns_strength, int32_t filter_strength,
+                      int32_t filter_sharpness, int32_t filter_type, int32_t segments, int32_t preprocessing,
+                      wg_enc_config* out);
+/* Per image, what analysis() and setSegmentProbas leave for Phase A / B and
+ * the segment header (encode_analysis.go:29-73, :852-903). */
+typedef struct wg_frame_segs {
+  int32_t num_segments;   /* after simplifySegments */
+  int32_t base_quant;     /* dqm[0].Quant */
+  int32_t global_uv_alpha;
+  int32_t dq_uv_ac, dq_uv_dc;
+  int32_t filter_level;   /* filterHdr.Level */
+  int32_t update_map;     /* segmentHdr.UpdateMap after setSegmentProbas */
+  int32_t pad;
+  int32_t quant[4], fstrength[4], alpha[4], beta[4];
+  uint8_t seg_proba[4];   /* proba.Segments[0..2] */
+  int32_t pad2[3];
+} wg_frame_segs;          /* 112 bytes */
+/* Segment analysis after computeAlphas, on the device, per image: assignSegments
+ * (encode_analysis.go:737-849, smoothSegmentMap :76-119), setSegmentParams
+ * (:122-195: per-segment quantiser, dq_uv deltas, setupFilterStrength
+ * encode.go:1276, simplifySegments :197), setSegmentProbas' map reset
+ * (:874-903) and setupSegment (encode.go:1084) for all 4 segments.
+ * cfg: HOST pointer.  alphas [n][mbw*mbh], uv_sum [n] as wg_analysis_alphas
+ * writes them.  Outputs seg_ids [n][mbw*mbh], segs (4 wg_segment per image,
+ * segs_pitch bytes apart, 16-byte aligned) for wg_encode_mbs, and info [n]
+ * (may be NULL). */
+int wg_segment_analysis(const wg_enc_config* cfg, const int32_t* alphas, const int32_t* uv_sum, int32_t mbw,
+                        int32_t mbh, int32_t n_images, uint8_t* seg_ids, void* segs, int64_t segs_pitch,
+                        wg_frame_segs* info, void* stream);
 size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images);
 int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t y_pitch, int64_t uv_pitch,
                   int32_t width, int32_t height, int32_t n_images, const uint8_t* segments, const void* segs,
-                  const uint8_t* proba, int32_t method, int32_t quality, void* out, uint8_t* ry, uint8_t* ru,
+                  int64_t segs_pitch, const uint8_t* proba, int32_t method, int32_t quality, void* out, uint8_t* ry, uint8_t* ru,
                   uint8_t* rv, void* work, void* stream);
 /* After wg_encode_mbs on the same stream: WG_OK or WG_EHIP on a row-wait timeout.  Synchronises. */
 int wg_encode_status(const void* work, int32_t mbw, int32_t n_images, void* stream);
+/* VP8FixedCostsI4[top][left][mode] (encode_analysis.go:1498-1520) as
+ * uploaded by wg_encode_mbs; host memory, 1000 uint16. */
+int wg_fixed_costs_i4_host(uint16_t* out);
 
 /* After wg_decode_frames on the same stream: WG_OK, or WG_EHIP if a row
  * dependency wait timed out inside the kernel (output invalid).  Synchronises

@@ -125,6 +125,15 @@ _SIGS = {
     "or_sharpyuv_tables": (None, [ctypes.c_void_p, ctypes.c_void_p]),
     "or_setup_segment": (None, [_i] * 8 + [ctypes.c_void_p]),
     "or_fixed_costs_i4": (None, [ctypes.c_void_p]),
+    "or_quantize_coeffs": (_i, [ctypes.c_void_p] * 3 + [_i]),
+    "or_dequant_coeffs": (None, [ctypes.c_void_p] * 3),
+    "or_rd_score": (ctypes.c_uint64, [_i, _i, _i]),
+    "or_token_cost": (_i, [ctypes.c_void_p, _i, _i, ctypes.c_void_p, _i, _i]),
+    "or_trellis_quantize": (_i, [ctypes.c_void_p] * 3 + [_i, _i, _i, ctypes.c_void_p, _i]),
+    "or_quality_to_compression": (ctypes.c_double, [_i]),
+    "or_quality_to_qindex": (_i, [_i]),
+    "or_segment_quant": (_i, [_i, _i, _i]),
+    "or_segment_analysis": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "or_encode_frame_rd": (None, [ctypes.c_void_p] * 3 + [_i] * 4 + [ctypes.c_void_p] * 3 + [_i, _i, ctypes.c_void_p]),
     "or_sharpyuv_convert": (_i, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i, ctypes.c_void_p, ctypes.c_void_p, _i,
                                  ctypes.c_void_p]),
@@ -469,3 +478,50 @@ def encode_frame_rd(Y, U, V, width, height, segments, segs, proba, method=4, qua
     lib.or_encode_frame_rd(Y.ctypes.data, U.ctypes.data, V.ctypes.data, width, height, mbw, mbh, seg_ids.ctypes.data,
                            segs.ctypes.data, proba.ctypes.data, method, quality, out.ctypes.data)
     return out, Y, U, V
+
+
+# ---------------- segment analysis (analysis() after computeAlphas) ----------------
+
+FRAME_SEGS_DTYPE = np.dtype([("num_segments", "<i4"), ("base_quant", "<i4"), ("global_uv_alpha", "<i4"),
+                             ("dq_uv_ac", "<i4"), ("dq_uv_dc", "<i4"), ("filter_level", "<i4"), ("update_map", "<i4"),
+                             ("pad", "<i4"), ("quant", "<i4", (4,)), ("fstrength", "<i4", (4,)), ("alpha", "<i4", (4,)),
+                             ("beta", "<i4", (4,)), ("seg_proba", "u1", (4,)), ("pad2", "<i4", (3,))])
+assert FRAME_SEGS_DTYPE.itemsize == 112
+
+
+def encoder_config(quality=75, method=4, sns_strength=50, filter_strength=60, filter_sharpness=0, filter_type=1,
+                   segments=4, preprocessing=0):
+    """The EncodeConfig fields the analysis reads; defaults = DefaultConfig(75)
+    (internal/lossy/encode.go:66-86), which webp.Encode's DefaultOptions resolve to."""
+    return np.array([quality, method, sns_strength, filter_strength, filter_sharpness, filter_type, segments,
+                     preprocessing], np.int32)
+
+
+def segment_analysis(alphas, mbw, mbh, uv_sum, cfg):
+    """assignSegments + setSegmentParams + setSegmentProbas for one frame:
+    returns (seg_ids uint8 (mbh*mbw,), FRAME_SEGS record, 4 SEGMENT_DTYPE quantiser records)."""
+    a = np.ascontiguousarray(alphas, np.int32).reshape(-1)
+    assert a.size == mbw * mbh
+    cfg = np.ascontiguousarray(cfg, np.int32)
+    seg_ids = np.zeros(mbw * mbh, np.uint8)
+    info = np.zeros(1, FRAME_SEGS_DTYPE)
+    lib.or_segment_analysis(a.ctypes.data, mbw, mbh, int(uv_sum), cfg.ctypes.data, seg_ids.ctypes.data,
+                            info.ctypes.data)
+    info = info[0]
+    dq = (0, 0, 0, int(info["dq_uv_dc"]), int(info["dq_uv_ac"]))
+    segs = np.stack([setup_segment(int(q), dq, method=int(cfg[1]), sns_strength=int(cfg[2])) for q in info["quant"]])
+    return seg_ids, info, segs
+
+
+def encode_frame(Y, U, V, width, height, cfg=None, proba=None):
+    """The lossy encoder's DSP path after import for one frame, as
+    EncodeFrame runs it: computeAlphas -> analysis() segments -> Phase A.
+    Returns (mb_enc, (RY, RU, RV), seg_ids, info)."""
+    cfg = encoder_config() if cfg is None else cfg
+    mbw, mbh = Y.shape[1] // 16, Y.shape[0] // 16
+    alphas, _, uva, _ = compute_alphas(Y, U, V, width, height)
+    seg_ids, info, segs = segment_analysis(alphas, mbw, mbh, int(uva.sum()), cfg)
+    proba = default_proba() if proba is None else proba
+    enc, ry, ru, rv = encode_frame_rd(Y, U, V, width, height, seg_ids, segs, proba, method=int(cfg[1]),
+                                      quality=int(cfg[0]))
+    return enc, (ry, ru, rv), seg_ids, info

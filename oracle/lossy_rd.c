@@ -934,3 +934,22 @@ void or_encode_frame_rd(uint8_t* yp, uint8_t* up, uint8_t* vp, int width, int he
   free(top_nz);
   free(top_nz_dc);
 }
+
+/* ---------------- exported for the per-function KAT tests (tests/test_rd_kats.py) ---------------- */
+/* QuantizeCoeffs (encode_quant.go:16-75) */
+int or_quantize_coeffs(const int16_t* in, int16_t* out, const or_squant* sq, int first) {
+  return quantize_coeffs(in, out, sq, first);
+}
+/* DequantCoeffs (encode_quant.go:81-101) */
+void or_dequant_coeffs(const int16_t* in, int16_t* out, const or_squant* sq) { dequant_coeffs(in, out, sq); }
+/* RDScore (encode_quant.go:109-111) */
+uint64_t or_rd_score(int disto, int rate, int lambda) { return rd_score(disto, rate, lambda); }
+/* TokenCostForCoeffs (encode_quant.go:170-220) */
+int or_token_cost(const int16_t* coeffs, int nz_count, int type, const uint8_t* proba, int ctx0, int first) {
+  return token_cost(coeffs, nz_count, type, proba, ctx0, first);
+}
+/* TrellisQuantizeBlock (encode_trellis.go:23-301) */
+int or_trellis_quantize(const int16_t* in, int16_t* out, const or_squant* sq, int first, int ctx_type, int init_ctx,
+                        const uint8_t* proba, int lambda) {
+  return trellis_quantize(in, out, sq, first, ctx_type, init_ctx, proba, lambda);
+}

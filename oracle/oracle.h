@@ -225,9 +225,31 @@ typedef struct {          /* MBEncInfo (encode.go:241-276), Phase A outputs */
 void or_setup_segment(int q, int dq_y1_dc, int dq_y2_dc, int dq_y2_ac, int dq_uv_dc, int dq_uv_ac, int method,
                       int sns_strength, or_segment* seg);
 void or_fixed_costs_i4(uint16_t* out /* [10][10][10] */);
+int or_quantize_coeffs(const int16_t* in, int16_t* out, const or_squant* sq, int first);
+void or_dequant_coeffs(const int16_t* in, int16_t* out, const or_squant* sq);
+uint64_t or_rd_score(int disto, int rate, int lambda);
+int or_token_cost(const int16_t* coeffs, int nz_count, int type, const uint8_t* proba, int ctx0, int first);
+int or_trellis_quantize(const int16_t* in, int16_t* out, const or_squant* sq, int first, int ctx_type, int init_ctx,
+                        const uint8_t* proba, int lambda);
 void or_encode_frame_rd(uint8_t* y, uint8_t* u, uint8_t* v, int width, int height, int mbw, int mbh,
                         const uint8_t* segments, const or_segment* segs, const uint8_t* proba, int method,
                         int quality, or_mb_enc* out);
+
+/* ---- segment analysis (segments.c; encode_analysis.go:29-903) ---- */
+typedef struct { /* the EncodeConfig fields the analysis reads (internal/lossy/encode.go:30-63) */
+  int quality, method, sns_strength, filter_strength, filter_sharpness, filter_type, segments, preprocessing;
+} or_enc_config;
+typedef struct { /* what analysis() + setSegmentProbas leave for Phase A/B (= wg_frame_segs) */
+  int32_t num_segments, base_quant, global_uv_alpha, dq_uv_ac, dq_uv_dc, filter_level, update_map, pad;
+  int32_t quant[4], fstrength[4], alpha[4], beta[4];
+  uint8_t seg_proba[4];
+  int32_t pad2[3];
+} or_frame_segs;        /* 112 bytes */
+double or_quality_to_compression(int quality);
+int or_quality_to_qindex(int quality);
+int or_segment_quant(int quality, int sns_strength, int seg_alpha);
+void or_segment_analysis(const int32_t* alphas, int mbw, int mbh, int uv_alpha_sum, const or_enc_config* cfg,
+                         uint8_t* seg_ids, or_frame_segs* info);
 
 /* ---- SharpYUV (sharpyuv.c; sharpyuv/sharpyuv.go, gamma.go) ---- */
 void or_sharpyuv_tables(uint32_t* g2l_out /* 1026 */, uint32_t* l2g_out /* 514 */);

@@ -61,6 +61,8 @@ def main():
     out["ssim_c"], out["ssim_d"] = g, q[:45, :61].copy()
     out["ssim_value2"] = np.array([L.plane_ssim(g, out["ssim_d"])], np.float64)
     np.savez_compressed(os.path.join(HERE, "libwebp_fixtures.npz"), **out)
+    make_c1_fixture(img)
+    make_bench_bitstreams()
     make_decode_fixtures(img)
     make_sharpyuv_fixtures(img)
     print("wrote", os.path.join(HERE, "libwebp_fixtures.npz"), sum(v.nbytes for v in out.values()), "bytes raw")
@@ -116,6 +118,29 @@ def make_sharpyuv_fixtures(img):
         out[name + "_rgb"], out[name + "_y"], out[name + "_u"], out[name + "_v"] = rgb, Y, U, V
     path = os.path.join(HERE, "libsharpyuv_fixtures.npz")
     np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def make_c1_fixture(img):
+    """testdata/test.png (768x576, opaque) as decoded RGBA: the C1 frame, for
+    the full-frame encode parity test (the reference checkout is not on the GPU
+    box).  Data only -- no expected outputs (those come from the oracle)."""
+    path = os.path.join(HERE, "test_png_rgba.npz")
+    np.savez_compressed(path, rgba=img)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def make_bench_bitstreams():
+    """libwebp 1.6.0 q75 (WebPEncodeRGBA defaults) encodes of the bench's three
+    1920x1080 synthetic contents (gradient, noise seed 1, blobs seed 2): the
+    decode side of bench.py parses them with wg_vp8_parse (SURVEY 8(d) C3,
+    "real q75 bitstreams").  Stored as raw bytes in an uncompressed .npz."""
+    w, h = 1920, 1080
+    out = {"grad": L.encode_lossy(synth.gradient_rgba(w, h), 75.0),
+           "noise": L.encode_lossy(synth.noise_rgba(w, h, seed=1), 75.0),
+           "blobs": L.encode_lossy(synth.blobs_rgba(w, h, seed=2), 75.0)}
+    path = os.path.join(HERE, "q75_1080p.npz")
+    np.savez(path, **{k: np.frombuffer(bytes(v), np.uint8) for k, v in out.items()})
     print("wrote", path, os.path.getsize(path), "bytes")
 
 

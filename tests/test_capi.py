@@ -63,3 +63,26 @@ def test_library_is_gfx950_only():
 @pytest.mark.parametrize("mod", ["webp_amd.dsp", "webp_amd.frames"])
 def test_modules_import(mod):
     __import__(mod)
+
+
+def test_encode_refuses_small_frames_and_bad_alignment():
+    """wg_encode_mbs returns WG_EINVAL before any device work for mbh < 4
+    (encode.go:1356 encodes those serially) and for misaligned buffers."""
+    from webp_amd import _lib
+    lib = _lib.lib
+    p = 1 << 20  # never dereferenced: validation fails first
+    args = lambda w, h, out: (p, p, p, 256 * 8 * 8, 64 * 8 * 8, w, h, 1, None, p, 0, p, 4, 75, out, p, p, p, p, None)
+    assert lib.wg_encode_mbs(*args(64, 48, p)) == -1
+    assert b"mbh >= 4" in lib.wg_last_error()
+    assert lib.wg_encode_mbs(*args(64, 64, p + 8)) == -1  # out not 16-byte aligned
+    assert lib.wg_encode_mbs(*(args(64, 64, p)[:3] + (100,) + args(64, 64, p)[4:])) == -1  # y pitch too small
+
+
+def test_segment_analysis_validates_without_gpu():
+    from webp_amd import _lib, frames
+    lib = _lib.lib
+    cfg = frames.encoder_config()
+    p = 1 << 20
+    assert lib.wg_segment_analysis(cfg.ctypes.data, p, p, 0, 4, 1, p, p, 896, None, None) == -1
+    assert lib.wg_segment_analysis(cfg.ctypes.data, p, p, 4, 4, 1, p, p, 100, None, None) == -1  # pitch < 4 segments
+    assert lib.wg_encoder_config(101, 4, 50, 60, 0, 1, 4, 0, cfg.ctypes.data) == -1

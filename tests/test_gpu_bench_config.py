@@ -1,0 +1,73 @@
+"""GPU parity of the exact configuration bench.py times: 64 x 1920x1080 frames
+per batch, three batches in flight on three HIP streams (4,352 encoder rows
+on 2,048 resident wave slots, persistent kernels overlapping), the
+reference's q75 defaults with the device segment analysis, and the libwebp q75
+bitstreams on the decode side.
+
+After four steps (slot 0 reused) every slot's in-kernel wait flags are
+checked, one frame of each content is compared bit-for-bit with the oracle
+(every MBEncInfo field, the reconstruction, the segment map and records, the
+decoded planes and the NRGBA), and every other frame of the batch must equal
+the representative of its content byte for byte."""
+import numpy as np
+import pytest
+import torch
+
+import bench
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("coeffs", "modes", "nz_y", "nz_uv", "non_zero_y", "non_zero_uv", "mb_type", "i16_mode", "uv_mode", "nz_dc",
+          "skip", "segment", "score")
+
+
+@pytest.fixture(scope="module")
+def ran(cuda):
+    rgba, mb, co, parsed = bench.make_inputs(64, 0, cuda)
+    pipe = bench.Pipeline(rgba, mb, co, 64, cuda, slots=3)
+    for _ in range(4):
+        pipe.step()
+    torch.cuda.synchronize()
+    pipe.check_status()
+    return rgba, parsed, pipe
+
+
+def expected(content, rgba_np, parsed):
+    W, H = bench.W, bench.H
+    y, u, v = O.import_rgba(rgba_np, has_alpha=False)
+    enc, recon, ids, info = O.encode_frame(y, u, v, W, H, O.encoder_config(**bench.ENC_CFG))
+    mb, co = parsed[content]
+    dy, du, dv = O.decode_frame(mb, co, 2, bench.MBW, bench.MBH)
+    nrgba = O.build_nrgba(dy, du, dv, W, H)
+    return enc, recon, ids, info, (dy, du, dv), nrgba
+
+
+def test_bench_batch_matches_oracle(ran):
+    from webp_amd import frames
+    rgba, parsed, pipe = ran
+    per = bench.MBW * bench.MBH
+    exp = {}
+    for i, content in enumerate(bench.CONTENTS):
+        exp[i] = expected(content, rgba[i].cpu().numpy(), parsed)
+    for s, sl in enumerate(pipe.slots):
+        got = sl.enc_out.cpu().numpy().view(frames.MB_ENC_DTYPE).reshape(64, per)
+        info = sl.seg_info.cpu().numpy().view(frames.FRAME_SEGS_DTYPE).reshape(64)
+        seg_ids = sl.seg_ids.cpu().numpy()
+        planes = [t.cpu().numpy() for t in (sl.rY, sl.rU, sl.rV, sl.dY, sl.dU, sl.dV, sl.out)]
+        for i in range(3):
+            enc, (ry, ru, rv), ids, inf, (dy, du, dv), nrgba = exp[i]
+            assert (seg_ids[i] == ids).all() and info[i].tobytes() == inf.tobytes(), (s, i)
+            for f in FIELDS:
+                assert (got[i][f] == enc[f]).all(), f"slot {s} frame {i}: field {f}"
+            assert (planes[0][i][:bench.H] == ry[:bench.H]).all() and (planes[1][i] == ru).all() and \
+                (planes[2][i] == rv).all(), (s, i)
+            assert (planes[3][i] == dy).all() and (planes[4][i] == du).all() and (planes[5][i] == dv).all(), (s, i)
+            assert (planes[6][i] == nrgba).all(), (s, i)
+        # the rest of the batch: identical inputs give identical outputs
+        raw = sl.enc_out.cpu().numpy().reshape(64, -1)
+        for i in range(3, 64):
+            r = i % 3
+            assert (raw[i] == raw[r]).all() and (seg_ids[i] == seg_ids[r]).all(), (s, i)
+            for p in planes:
+                assert (p[i] == p[r]).all(), (s, i)

@@ -4,7 +4,14 @@ C ABI vs the C restatement (oracle/lossy_rd.c): every MBEncInfo field
 bit-exact.  Frames cover image edges (non-multiple-of-16 sizes), all four
 segments with different quantisers, fine / coarse quantisers (I4-heavy and
 I16-heavy), SNS on / off, quality < 50 (2 I4 RD candidates), a batch, and
-the 1920x1080 C2 frame."""
+the 1920x1080 C2 frame.  Frames have mbh >= 4: smaller ones take the
+reference's serial encodeFrame (encode.go:1356), which wg_encode_mbs refuses.
+
+test_encode_pipeline_* run the whole device encode path of frames.encode_frames
+(import -> analysis -> segment analysis -> Phase A) against oracle.encode_frame
+on the C1 frame (testdata/test.png) and 1080p frames of each content type."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -46,15 +53,15 @@ def run(imgs, w, h, qs, sns=50, quality=75):
         assert (RY[i][:h, :w] == ry[:h, :w]).all() and (RU[i] == ru).all() and (RV[i] == rv).all()
 
 
-@pytest.mark.parametrize("w,h,kind,qs", [(16, 16, "noise", (20, 30, 40, 50)), (48, 32, "blobs", (10, 20, 30, 40)),
-                                         (37, 29, "noise", (30, 30, 30, 30)), (80, 64, "grad", (60, 70, 80, 90)),
-                                         (100, 20, "blobs", (5, 15, 100, 127))])
+@pytest.mark.parametrize("w,h,kind,qs", [(16, 64, "noise", (20, 30, 40, 50)), (48, 64, "blobs", (10, 20, 30, 40)),
+                                         (37, 61, "noise", (30, 30, 30, 30)), (80, 64, "grad", (60, 70, 80, 90)),
+                                         (100, 64, "blobs", (5, 15, 100, 127))])
 def test_encode_matches_oracle(cuda, w, h, kind, qs):
     run([planes(w, h, kind, seed=w)], w, h, qs)
 
 
 def test_encode_low_quality_and_no_sns(cuda):
-    run([planes(64, 48, "noise", 3)], 64, 48, (25, 35, 45, 55), sns=0, quality=30)
+    run([planes(64, 64, "noise", 3)], 64, 64, (25, 35, 45, 55), sns=0, quality=30)
 
 
 def test_encode_batch(cuda):
@@ -63,3 +70,50 @@ def test_encode_batch(cuda):
 
 def test_encode_1080p(cuda):
     run([planes(1920, 1080, "blobs", 7)], 1920, 1080, (30, 35, 40, 45))
+
+
+def test_small_frames_refused(cuda):
+    """mbh < 4: EncodeFrame uses the serial encodeFrame (encode.go:1356)."""
+    from webp_amd._lib import WebpGpuError
+    with pytest.raises(WebpGpuError, match="mbh >= 4"):
+        run([planes(64, 48, "noise", 3)], 64, 48, (25, 35, 45, 55))
+
+
+def pipeline(rgbas, w, h, **cfg):
+    out, (RY, RU, RV), seg_ids, segs, info = frames.encode_frames(torch.from_numpy(np.stack(rgbas)).cuda(),
+                                                                  frames.encoder_config(**cfg))
+    n = len(rgbas)
+    mbw, mbh = frames.mb_dims(w, h)
+    got = out.cpu().numpy().view(frames.MB_ENC_DTYPE).reshape(n, mbw * mbh)
+    RY, RU, RV, seg_ids = RY.cpu().numpy(), RU.cpu().numpy(), RV.cpu().numpy(), seg_ids.cpu().numpy()
+    info = info.cpu().numpy().view(frames.FRAME_SEGS_DTYPE).reshape(n)
+    for i, rgba in enumerate(rgbas):
+        y, u, v = O.import_rgba(rgba, has_alpha=False)
+        enc, (ry, ru, rv), e_ids, e_info = O.encode_frame(y, u, v, w, h, O.encoder_config(**cfg))
+        assert (seg_ids[i] == e_ids).all() and info[i].tobytes() == e_info.tobytes(), f"image {i}: segments"
+        for f in FIELDS:
+            bad = np.argwhere(np.asarray(got[i][f] != enc[f]).reshape(len(enc), -1).any(axis=1))
+            assert len(bad) == 0, f"image {i} field {f}: MBs {bad[:5].ravel()} (of {len(enc)})"
+        assert (RY[i][:h, :w] == ry[:h, :w]).all() and (RU[i] == ru).all() and (RV[i] == rv).all()
+    return info
+
+
+def test_encode_pipeline_c1_test_png(cuda):
+    """C1: testdata/test.png (768x576), webp.Encode defaults (q75, method 4)."""
+    rgba = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "test_png_rgba.npz"))["rgba"]
+    info = pipeline([rgba], 768, 576)
+    assert info[0]["base_quant"] > 0
+
+
+def test_encode_pipeline_1080p_contents(cuda):
+    """C2 frames of each content at the reference's q75 defaults, one batch."""
+    w, h = 1920, 1080
+    pipeline([synth.gradient_rgba(w, h), synth.noise_rgba(w, h, seed=1), synth.blobs_rgba(w, h, seed=2)], w, h)
+
+
+def test_encode_pipeline_presets(cuda):
+    """Non-default analysis knobs feeding Phase A: smoothing, 2 segments, low quality."""
+    w, h = 320, 240
+    imgs = [synth.blobs_rgba(w, h, seed=5), synth.noise_rgba(w, h, seed=6)]
+    pipeline(imgs, w, h, quality=30, sns_strength=80, filter_strength=35, filter_sharpness=4, preprocessing=1)
+    pipeline(imgs, w, h, quality=90, sns_strength=0, segments=2)

@@ -50,6 +50,24 @@ def test_decode_bitstreams_vs_libwebp(name):
     assert crop_eq(y, DEC[name + "_y"]) and crop_eq(u, DEC[name + "_u"]) and crop_eq(v, DEC[name + "_v"])
 
 
+@pytest.mark.parametrize("content", ["grad", "noise", "blobs"])
+def test_bench_bitstreams_vs_libwebp(content):
+    """The decode side of bench.py: libwebp q75 encodes of the bench's 1080p
+    contents (tests/golden/q75_1080p.npz), parsed by wg_vp8_parse and decoded by
+    the oracle, equal libwebp's WebPDecodeYUV (run live where Pillow's libwebp
+    is present)."""
+    import libwebp_ref as L
+    if not L.available:
+        pytest.skip("Pillow libwebp not present")
+    from webp_amd import frames
+    data = np.load(os.path.join(os.path.dirname(__file__), "golden", "q75_1080p.npz"))[content].tobytes()
+    dims, mb, co = frames.vp8_parse(data)
+    assert (dims["width"], dims["height"], dims["filter_type"]) == (1920, 1080, 2)
+    y, u, v = O.decode_frame(libwebp_skip_rule(mb), co, 2, dims["mbw"], dims["mbh"])
+    ly, lu, lv = L.decode_yuv(data)
+    assert crop_eq(y, ly) and crop_eq(u, lu) and crop_eq(v, lv)
+
+
 def test_parser_rejects_garbage():
     from webp_amd import frames
     from webp_amd._lib import WebpGpuError

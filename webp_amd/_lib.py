@@ -89,8 +89,11 @@ SIGNATURES = {
     "wg_sharpyuv_iterations": [_vp, _i32, _i32, _i32, _vp, _vp],
     "wg_setup_segment": [_i32, _vp, _i32, _i32, _vp],
     "wg_encode_work_bytes": [_i32, _i32, _i32],
-    "wg_encode_mbs": [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
-                      _vp],
+    "wg_encode_mbs": [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _i32, _i32, _vp, _vp, _vp, _vp,
+                      _vp, _vp],
+    "wg_fixed_costs_i4_host": [_vp],
+    "wg_encoder_config": [_i32] * 8 + [_vp],
+    "wg_segment_analysis": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp],
     "wg_encode_status": [_vp, _i32, _i32, _vp],
 }
 _RES = {"wg_last_error": ctypes.c_char_p, "wg_decode_work_bytes": ctypes.c_size_t,

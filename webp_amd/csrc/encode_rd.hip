@@ -23,6 +23,8 @@
 //              (each needs its left / top neighbour's nz), DC and chroma in
 //              parallel, then reconstruction and export
 // All integer; bit-exact with the C restatement (oracle/lossy_rd.c).
+#include <mutex>
+
 #include "vp8_tables.h"
 #include "wg_common.h"
 #include "wg_dsp.h"
@@ -142,13 +144,13 @@ struct Tables {
   // variableLevelCost, encode_quant.go:258-273): the three contexts of one
   // level sit in one 8-byte word so one ds_read_b64 serves a trellis step
   uint64_t vcost[4 * 8][68];
-  Segment seg[4];
   uint16_t fixed_i4[1000];
   int wtr[16];  // trellis distortion weights (kWeightTrellis)
   alignas(16) uint8_t pcode[10][16];  // kPred4Code
 };
 // Per-wave state: each wave of the workgroup encodes its own macroblock row
 struct Shared {
+  Segment seg[4];  // the quantisers of the row's image (per-image segment tables)
   uint8_t yin[YUV], yout[YUV], yout2[YUV];
   alignas(16) int16_t coeffs[400];
   uint8_t modes4[16];
@@ -649,7 +651,8 @@ struct EncArgs {
   uint8_t* ru;
   uint8_t* rv;
   const uint8_t* segments;  // per MB segment id, n_img * mbw * mbh
-  const Segment* segs;      // 4
+  const Segment* segs;      // 4 per image, segs_pitch bytes apart (0: one table for all)
+  int64_t segs_pitch;
   const uint8_t* proba;     // 1056
   MbEnc* out;
   uint8_t* top;   // [n_img][mbw][REC]
@@ -719,8 +722,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
   for (int i = tid; i < 1000; i += NT) t.fixed_i4[i] = c_fixed_i4[i];
   if (tid < 16) t.wtr[tid] = c_wtrellis[tid];
   if (tid < 160) t.pcode[tid >> 4][tid & 15] = kPred4Code[tid >> 4][tid & 15];
-  for (int i = tid; i < (int)(4 * sizeof(Segment) / 4); i += NT)
-    reinterpret_cast<int*>(t.seg)[i] = reinterpret_cast<const int*>(a.segs)[i];
   __syncthreads();
   for (int i = tid; i < 4 * 8 * 68; i += NT) {
     const int tb = i / 68, level = i % 68;
@@ -766,6 +767,10 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
     uint8_t* top = a.top + (int64_t)img * mbw * REC;
     int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
     int* prog_mine = a.progress + (int64_t)img * mbh + mby;
+    {  // this image's four segments (4 x 224 B = 56 x 16 B)
+      const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.segs) + img * a.segs_pitch);
+      if (lane < 56) reinterpret_cast<uint4*>(s.seg)[lane] = src[lane];
+    }
     // left context (encodeRow :257-282)
     if (lane < 16) s.yout[YOFF - 1 + lane * BPS] = 129;
     else if (lane < 24) s.yout[UOFF - 1 + (lane - 16) * BPS] = 129;
@@ -806,7 +811,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
       }
       ESTAMP(1);
       const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
-      const Segment& sg = t.seg[segid];
+      const Segment& sg = s.seg[segid];
       // ---- import (importBlockParallel :433-452) with edge replication ----
       {
         const int x = 16 * mbx, y = 16 * mby;
@@ -1566,9 +1571,44 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
   ESTAMP_FLUSH();
 }
 
-int g_tables_ready_dev = -1;
+// Devices whose constant tables are uploaded: one bit per device, set under
+// the mutex so host threads driving different devices do not race.
+std::mutex g_tables_mu;
+uint64_t g_tables_ready_mask = 0;
+
+// VP8FixedCostsI4[top][left][mode] (computeFixedCostsI4,
+// internal/lossy/encode_analysis.go:1498-1520): the mode tree walked with the
+// VP8 bmode probabilities (i4ModeCost :1511).
+void build_fixed_costs_i4(uint16_t* fixed) {
+  for (int t = 0; t < 10; t++)
+    for (int l = 0; l < 10; l++) {
+      const uint8_t* prob = vp8_bmodes_proba + (t * 10 + l) * 9;
+      for (int m = 0; m < 10; m++) {
+        auto contains = [](int node, int mode, auto&& self) -> bool {
+          if (node <= 0) return -node == mode;
+          return self(vp8_ymodes_intra4[2 * node], mode, self) || self(vp8_ymodes_intra4[2 * node + 1], mode, self);
+        };
+        int cost = 0, bit = contains(vp8_ymodes_intra4[0], m, contains) ? 0 : 1;
+        cost += bit ? vp8_entropy_cost[255 - prob[0]] : vp8_entropy_cost[prob[0]];
+        int i = vp8_ymodes_intra4[bit];
+        while (i > 0) {
+          bit = contains(vp8_ymodes_intra4[2 * i], m, contains) ? 0 : 1;
+          cost += bit ? vp8_entropy_cost[255 - prob[i]] : vp8_entropy_cost[prob[i]];
+          i = vp8_ymodes_intra4[2 * i + bit];
+        }
+        fixed[(t * 10 + l) * 10 + m] = (uint16_t)cost;
+      }
+    }
+}
 
 }  // namespace
+
+/* The VP8FixedCostsI4 table wg_encode_mbs uploads (host copy, 1000 entries). */
+extern "C" int wg_fixed_costs_i4_host(uint16_t* out) {
+  WG_REQUIRE(out);
+  build_fixed_costs_i4(out);
+  return WG_OK;
+}
 
 #ifdef WG_STAMPS
 extern "C" int wg_debug_enc_phases(unsigned long long* host, int n) {
@@ -1585,42 +1625,38 @@ extern "C" size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_image
 
 extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t y_pitch, int64_t uv_pitch,
                              int32_t width, int32_t height, int32_t n_images, const uint8_t* segments,
-                             const void* segs, const uint8_t* proba, int32_t method, int32_t quality, void* out,
+                             const void* segs, int64_t segs_pitch, const uint8_t* proba, int32_t method, int32_t quality, void* out,
                              uint8_t* ry, uint8_t* ru, uint8_t* rv, void* work, void* stream) {
   WG_REQUIRE(y && u && v && segs && proba && out && ry && ru && rv && work);
   WG_REQUIRE(width > 0 && height > 0 && n_images > 0);
   if (method < 4) return wg::invalid("wg_encode_mbs implements method >= 4 (the default); method 3 is not built");
   const int mbw = (width + 15) >> 4, mbh = (height + 15) >> 4;
+  // EncodeFrame (internal/lossy/encode.go:1356) runs the row-parallel Phase A
+  // only for mbH >= 4; smaller frames take the serial encodeFrame (chroma DC
+  // error diffusion, mid-frame proba refresh), which this kernel is not.
+  if (mbh < 4) return wg::invalid("wg_encode_mbs needs mbh >= 4 (height > 48): encode.go:1356 encodes smaller frames serially");
+  WG_REQUIRE(((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(work)) & 15) == 0);
+  WG_REQUIRE(((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(v) |
+               reinterpret_cast<uintptr_t>(ry) | reinterpret_cast<uintptr_t>(ru) | reinterpret_cast<uintptr_t>(rv) |
+               reinterpret_cast<uintptr_t>(segs)) & 3) == 0);
+  WG_REQUIRE((reinterpret_cast<uintptr_t>(segs) & 15) == 0 && (segs_pitch == 0 || segs_pitch >= (int64_t)(4 * sizeof(Segment))) &&
+             (segs_pitch & 15) == 0);
+  WG_REQUIRE(y_pitch >= (int64_t)256 * mbw * mbh && uv_pitch >= (int64_t)64 * mbw * mbh && ((y_pitch | uv_pitch) & 3) == 0);
   hipStream_t s = wg::as_stream(stream);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return wg::check_launch("hipGetDevice");
-  if (g_tables_ready_dev != dev) {  // constant tables: level codes, fixed I4 mode costs, scan orders
-    uint16_t fixed[1000];
-    for (int t = 0; t < 10; t++)
-      for (int l = 0; l < 10; l++) {
-        const uint8_t* prob = vp8_bmodes_proba + (t * 10 + l) * 9;
-        for (int m = 0; m < 10; m++) {
-          // walk the mode tree (i4ModeCost, encode_analysis.go:1505)
-          auto contains = [](int node, int mode, auto&& self) -> bool {
-            if (node <= 0) return -node == mode;
-            return self(vp8_ymodes_intra4[2 * node], mode, self) || self(vp8_ymodes_intra4[2 * node + 1], mode, self);
-          };
-          int cost = 0, bit = contains(vp8_ymodes_intra4[0], m, contains) ? 0 : 1;
-          cost += bit ? vp8_entropy_cost[255 - prob[0]] : vp8_entropy_cost[prob[0]];
-          int i = vp8_ymodes_intra4[bit];
-          while (i > 0) {
-            bit = contains(vp8_ymodes_intra4[2 * i], m, contains) ? 0 : 1;
-            cost += bit ? vp8_entropy_cost[255 - prob[i]] : vp8_entropy_cost[prob[i]];
-            i = vp8_ymodes_intra4[2 * i + bit];
-          }
-          fixed[(t * 10 + l) * 10 + m] = (uint16_t)cost;
-        }
-      }
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_fixed_i4), fixed, sizeof(fixed)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_level_codes), vp8_level_codes, sizeof(vp8_level_codes)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_wtrellis), vp8_weight_trellis, sizeof(vp8_weight_trellis)) != hipSuccess)
-      return wg::check_launch("encode tables");
-    g_tables_ready_dev = dev;
+  WG_REQUIRE(dev >= 0 && dev < 64);
+  {
+    std::lock_guard<std::mutex> lock(g_tables_mu);
+    if (!(g_tables_ready_mask >> dev & 1)) {  // constant tables: level codes, fixed I4 mode costs, scan orders
+      uint16_t fixed[1000];
+      build_fixed_costs_i4(fixed);
+      if (hipMemcpyToSymbol(HIP_SYMBOL(c_fixed_i4), fixed, sizeof(fixed)) != hipSuccess ||
+          hipMemcpyToSymbol(HIP_SYMBOL(c_level_codes), vp8_level_codes, sizeof(vp8_level_codes)) != hipSuccess ||
+          hipMemcpyToSymbol(HIP_SYMBOL(c_wtrellis), vp8_weight_trellis, sizeof(vp8_weight_trellis)) != hipSuccess)
+        return wg::check_launch("encode tables");
+      g_tables_ready_mask |= 1ull << dev;
+    }
   }
   EncArgs a;
   a.y = y;
@@ -1631,6 +1667,7 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   a.rv = rv;
   a.segments = segments;
   a.segs = static_cast<const Segment*>(segs);
+  a.segs_pitch = segs_pitch;
   a.proba = proba;
   a.out = static_cast<MbEnc*>(out);
   a.top = static_cast<uint8_t*>(work);

@@ -187,11 +187,18 @@ def setup_segment(q, dq=(0, 0, 0, 0, 0), method=4, sns_strength=50):
 def encode_mbs(Y, U, V, width, height, segments, segs, proba, method=4, quality=75, recon=None, work=None,
                out=None, check=False):
     """Phase A over n frames: Y (n, 16*mbh, 16*mbw) / U, V planes (CUDA uint8),
-    segments (n, mbh*mbw) uint8, segs (4,) SEGMENT_DTYPE, proba (1056,) uint8.
-    Returns (out uint8 tensor viewed as (n*mbw*mbh, 864) wg_mb_enc bytes, (RY, RU, RV))."""
+    segments (n, mbh*mbw) uint8, segs (4,) SEGMENT_DTYPE shared by all images, or
+    a (n, 4*224) uint8 CUDA tensor of per-image tables (segment_analysis), proba
+    (1056,) uint8.  Returns (out uint8 tensor viewed as (n*mbw*mbh, 864)
+    wg_mb_enc bytes, (RY, RU, RV))."""
     n = Y.shape[0]
     mbw, mbh = mb_dims(width, height)
     dev = Y.device
+    # the kernel addresses rows at stride 16*mbw / 8*mbw (encode_rd.hip)
+    assert Y.is_contiguous() and U.is_contiguous() and V.is_contiguous()
+    assert tuple(Y.shape) == (n, 16 * mbh, 16 * mbw), (tuple(Y.shape), mbw, mbh)
+    assert tuple(U.shape) == (n, 8 * mbh, 8 * mbw) and tuple(V.shape) == (n, 8 * mbh, 8 * mbw)
+    assert segments is None or segments.numel() == n * mbw * mbh
     if recon is None:
         recon = (torch.empty_like(Y), torch.empty_like(U), torch.empty_like(V))
     if out is None:
@@ -200,12 +207,101 @@ def encode_mbs(Y, U, V, width, height, segments, segs, proba, method=4, quality=
         work = torch.empty(lib.wg_encode_work_bytes(mbw, mbh, n), dtype=torch.uint8, device=dev)
     if not torch.is_tensor(segs):
         segs = torch.from_numpy(np.ascontiguousarray(segs, SEGMENT_DTYPE).view(np.uint8).copy()).to(dev)
+    segs_pitch = 0 if segs.numel() == 4 * SEGMENT_DTYPE.itemsize else segs[0].numel()
+    assert segs_pitch == 0 or (segs.shape[0] == n and segs_pitch >= 4 * SEGMENT_DTYPE.itemsize)
     if not torch.is_tensor(proba):
         proba = torch.from_numpy(np.ascontiguousarray(proba, np.uint8)).to(dev)
     seg_ptr = None if segments is None else segments.data_ptr()
     call("wg_encode_mbs", Y.data_ptr(), U.data_ptr(), V.data_ptr(), Y[0].numel(), U[0].numel(), width, height, n,
-         seg_ptr, segs.data_ptr(), proba.data_ptr(), method, quality, out.data_ptr(), recon[0].data_ptr(),
+         seg_ptr, segs.data_ptr(), segs_pitch, proba.data_ptr(), method, quality, out.data_ptr(), recon[0].data_ptr(),
          recon[1].data_ptr(), recon[2].data_ptr(), work.data_ptr(), _stream())
     if check:
         call("wg_encode_status", work.data_ptr(), mbw, n, _stream())
     return out, recon
+
+
+def encode_status(work, mbw, n):
+    """Raises if a row-dependency wait of the last wg_encode_mbs on `work` timed out (synchronises)."""
+    call("wg_encode_status", work.data_ptr(), mbw, n, _stream())
+
+
+def decode_status(work, mbw, n):
+    """Raises if a row-dependency wait of the last wg_decode_frames on `work` timed out (synchronises)."""
+    call("wg_decode_status", work.data_ptr(), mbw, n, _stream())
+
+
+def fixed_costs_i4():
+    """VP8FixedCostsI4 as wg_encode_mbs uploads it: (10, 10, 10) uint16 [top][left][mode]."""
+    out = np.zeros(1000, np.uint16)
+    call("wg_fixed_costs_i4_host", out.ctypes.data)
+    return out.reshape(10, 10, 10)
+
+
+# ---------------- segment analysis (analysis() after computeAlphas) ----------------
+
+ENC_CONFIG_DTYPE = np.dtype([("quality", "<i4"), ("method", "<i4"), ("sns_strength", "<i4"),
+                             ("filter_strength", "<i4"), ("filter_sharpness", "<i4"), ("filter_type", "<i4"),
+                             ("segments", "<i4"), ("preprocessing", "<i4"), ("seg_quant", "u1", (256,))])
+FRAME_SEGS_DTYPE = np.dtype([("num_segments", "<i4"), ("base_quant", "<i4"), ("global_uv_alpha", "<i4"),
+                             ("dq_uv_ac", "<i4"), ("dq_uv_dc", "<i4"), ("filter_level", "<i4"), ("update_map", "<i4"),
+                             ("pad", "<i4"), ("quant", "<i4", (4,)), ("fstrength", "<i4", (4,)), ("alpha", "<i4", (4,)),
+                             ("beta", "<i4", (4,)), ("seg_proba", "u1", (4,)), ("pad2", "<i4", (3,))])  # wg_frame_segs
+assert ENC_CONFIG_DTYPE.itemsize == 288 and FRAME_SEGS_DTYPE.itemsize == 112
+
+
+def encoder_config(quality=75, method=4, sns_strength=50, filter_strength=60, filter_sharpness=0, filter_type=1,
+                   segments=4, preprocessing=0):
+    """wg_enc_config for EncodeConfig (defaults = DefaultConfig(75), internal/lossy/encode.go:66-86)."""
+    cfg = np.zeros(1, ENC_CONFIG_DTYPE)
+    call("wg_encoder_config", quality, method, sns_strength, filter_strength, filter_sharpness, filter_type, segments,
+         preprocessing, cfg.ctypes.data)
+    return cfg
+
+
+def segment_analysis(cfg, alphas, uv_sum, mbw, mbh, out=None, info=True):
+    """assignSegments + setSegmentParams + setSegmentProbas + setupSegment per
+    image on the device: alphas (n, mbh*mbw) int32, uv_sum (n,) int32 ->
+    (seg_ids (n, mbh*mbw) uint8, segs (n, 896) uint8 per-image wg_segment x 4,
+    info (n, 112) uint8 wg_frame_segs bytes or None)."""
+    n = alphas.shape[0]
+    dev = alphas.device
+    assert alphas.dtype == torch.int32 and alphas.numel() == n * mbw * mbh and uv_sum.numel() == n
+    if out is None:
+        seg_ids = torch.empty((n, mbw * mbh), dtype=torch.uint8, device=dev)
+        segs = torch.empty((n, 4 * SEGMENT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        inf = torch.empty((n, FRAME_SEGS_DTYPE.itemsize), dtype=torch.uint8, device=dev) if info else None
+    else:
+        seg_ids, segs, inf = out
+    call("wg_segment_analysis", cfg.ctypes.data, alphas.data_ptr(), uv_sum.data_ptr(), mbw, mbh, n, seg_ids.data_ptr(),
+         segs.data_ptr(), segs[0].numel(), inf.data_ptr() if inf is not None else None, _stream())
+    return seg_ids, segs, inf
+
+
+def encode_frames(rgba, cfg=None, has_alpha=False, proba=None, check=True):
+    """The lossy encoder's DSP path for n same-sized RGBA frames, as
+    NewEncoder + EncodeFrame run it up to Phase A (internal/lossy/encode.go:452,
+    :1324-1366): importImage -> computeAlphas -> analysis() segments ->
+    encodeFrameParallel Phase A.  Everything stays on the device.
+    Returns (mb_enc bytes (n*mbw*mbh, 864), (RY, RU, RV), seg_ids, segs, info)."""
+    n, h, w, _ = rgba.shape
+    mbw, mbh = mb_dims(w, h)
+    cfg = encoder_config() if cfg is None else cfg
+    Y, U, V = import_rgba(rgba, has_alpha=has_alpha)
+    alphas, uv_sum = analysis_alphas(Y, U, V, w, h)
+    seg_ids, segs, info = segment_analysis(cfg, alphas, uv_sum, mbw, mbh)
+    if proba is None:
+        proba = default_proba()
+    out, recon = encode_mbs(Y, U, V, w, h, seg_ids, segs, proba, method=int(cfg["method"][0]),
+                            quality=int(cfg["quality"][0]), check=check)
+    return out, recon, seg_ids, segs, info
+
+
+def default_proba(device="cuda"):
+    """CoeffsProba0 (internal/lossy/proba.go:45): the token probabilities Phase A
+    prices with after ResetProba, from the generated table."""
+    import os
+    import re
+    txt = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "vp8_tables.h")).read()
+    body = txt[txt.index("vp8_coeffs_proba0["):]
+    body = body[body.index("{") + 1:body.index("};")]
+    return torch.tensor([int(x) for x in re.findall(r"\d+", body)], dtype=torch.uint8, device=device)
