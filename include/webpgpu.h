@@ -268,6 +268,19 @@ int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uin
                   int64_t b_pitch, int32_t w, int32_t h, int32_t n_images, double* out, void* work,
                   void* stream);
 
+/* Row-band form for sharding one large plane over GPUs (SSIM
+ * shards by row bands with a 3-row halo).  Tile rows [ty_begin, ty_end) of
+ * 16 pixel rows each; a and b must hold rows 16*ty_begin - 3 .. 16*ty_end + 2
+ * (clipped to the plane) at their full-plane positions.  partial receives
+ * ceil(w/16) * (ty_end - ty_begin) doubles per image (image-major).  The
+ * bands' partials concatenated in tile-row order and passed to
+ * wg_plane_ssim_reduce give exactly wg_plane_ssim's sum. */
+int wg_plane_ssim_rows(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uint8_t* b, int32_t b_stride,
+                       int64_t b_pitch, int32_t w, int32_t h, int32_t ty_begin, int32_t ty_end, int32_t n_images,
+                       double* partial, void* stream);
+/* out[img] = the fixed-order sum of partial[img][0 .. per_image) */
+int wg_plane_ssim_reduce(const double* partial, int64_t per_image, int32_t n_images, double* out, void* stream);
+
 /* ===================================================================== *
  * 3. VP8L (lossless) predictor transform.
  *    ARGB images are uint32 [n_images][image_pitch] (width*height used),
@@ -282,6 +295,15 @@ int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uin
 int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32_t height, int64_t image_pitch,
                            int32_t bits, int32_t quality, int32_t n_images, uint32_t* modes, uint32_t* residuals,
                            void* stream);
+/* Row-band form for sharding one large image over GPUs (the
+ * residual shards by tile rows with a 1-row halo): only tile rows
+ * [ty_begin, ty_end) (2^bits pixel rows each) are selected and their pixel
+ * rows' residuals written, at their full-image positions in modes and
+ * residuals.  argb must hold pixel rows (ty_begin << bits) - 1 ..
+ * min(ty_end << bits, height) - 1. */
+int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, int32_t height, int64_t image_pitch,
+                                int32_t bits, int32_t quality, int32_t ty_begin, int32_t ty_end, int32_t n_images,
+                                uint32_t* modes, uint32_t* residuals, void* stream);
 /* predictorInverseTransform (internal/lossless/decode_transform.go:202-360):
  * out = residuals +mod prediction from reconstructed pixels.  `work` needs
  * wg_vp8l_inverse_work_bytes(height, n_images) bytes. */

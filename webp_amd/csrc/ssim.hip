@@ -21,6 +21,7 @@ struct SsimArgs {
   const uint8_t *a, *b;
   int64_t a_pitch, b_pitch;
   int a_stride, b_stride, w, h, tiles_x, tiles_y;
+  int ty0;  // first tile row; tiles_y tile rows from there
   double* partial;
 };
 
@@ -30,7 +31,7 @@ __global__ __launch_bounds__(256) void k_plane_ssim(const SsimArgs p) {
   const int tiles = p.tiles_x * p.tiles_y;
   const int img = blockIdx.x / tiles;
   const int tile = blockIdx.x % tiles;
-  const int tx0 = (tile % p.tiles_x) * TILE, ty0 = (tile / p.tiles_x) * TILE;
+  const int tx0 = (tile % p.tiles_x) * TILE, ty0 = (tile / p.tiles_x + p.ty0) * TILE;
   const uint8_t* A = p.a + img * p.a_pitch;
   const uint8_t* B = p.b + img * p.b_pitch;
   for (int i = threadIdx.x; i < TS * TS; i += blockDim.x) {
@@ -90,10 +91,11 @@ extern "C" size_t wg_plane_ssim_work_bytes(int32_t w, int32_t h, int32_t n_image
   return sizeof(double) * (size_t)n_images * ((w + TILE - 1) / TILE) * ((h + TILE - 1) / TILE);
 }
 
-extern "C" int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uint8_t* b, int32_t b_stride,
-                             int64_t b_pitch, int32_t w, int32_t h, int32_t n_images, double* out, void* work,
-                             void* stream) {
-  WG_REQUIRE(a && b && out && work && w > 0 && h > 0 && n_images > 0 && a_stride >= w && b_stride >= w);
+extern "C" int wg_plane_ssim_rows(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uint8_t* b,
+                                  int32_t b_stride, int64_t b_pitch, int32_t w, int32_t h, int32_t ty_begin,
+                                  int32_t ty_end, int32_t n_images, double* partial, void* stream) {
+  WG_REQUIRE(a && b && partial && w > 0 && h > 0 && n_images > 0 && a_stride >= w && b_stride >= w);
+  WG_REQUIRE(ty_begin >= 0 && ty_begin < ty_end && ty_end <= (h + TILE - 1) / TILE);
   SsimArgs p;
   p.a = a;
   p.b = b;
@@ -104,13 +106,29 @@ extern "C" int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch
   p.w = w;
   p.h = h;
   p.tiles_x = (w + TILE - 1) / TILE;
-  p.tiles_y = (h + TILE - 1) / TILE;
-  p.partial = static_cast<double*>(work);
-  hipStream_t s = wg::as_stream(stream);
+  p.tiles_y = ty_end - ty_begin;
+  p.ty0 = ty_begin;
+  p.partial = partial;
   const int per = p.tiles_x * p.tiles_y;
-  hipLaunchKernelGGL(k_plane_ssim, dim3((unsigned)(per * n_images)), dim3(256), 0, s, p);
-  int rc = wg::check_launch("k_plane_ssim");
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)n_images), dim3(256), 0, s, p.partial, per, out);
+  hipLaunchKernelGGL(k_plane_ssim, dim3((unsigned)(per * n_images)), dim3(256), 0, wg::as_stream(stream), p);
+  return wg::check_launch("k_plane_ssim");
+}
+
+extern "C" int wg_plane_ssim_reduce(const double* partial, int64_t per_image, int32_t n_images, double* out,
+                                    void* stream) {
+  WG_REQUIRE(partial && out && per_image > 0 && per_image < (1ll << 31) && n_images > 0);
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)n_images), dim3(256), 0, wg::as_stream(stream), partial,
+                     (int)per_image, out);
   return wg::check_launch("k_sum_partials");
+}
+
+extern "C" int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uint8_t* b, int32_t b_stride,
+                             int64_t b_pitch, int32_t w, int32_t h, int32_t n_images, double* out, void* work,
+                             void* stream) {
+  WG_REQUIRE(a && b && out && work && w > 0 && h > 0 && n_images > 0 && a_stride >= w && b_stride >= w);
+  const int tiles_y = (h + TILE - 1) / TILE;
+  double* partial = static_cast<double*>(work);
+  int rc = wg_plane_ssim_rows(a, a_stride, a_pitch, b, b_stride, b_pitch, w, h, 0, tiles_y, n_images, partial, stream);
+  if (rc) return rc;
+  return wg_plane_ssim_reduce(partial, (int64_t)((w + TILE - 1) / TILE) * tiles_y, n_images, out, stream);
 }

@@ -133,6 +133,7 @@ struct SelArgs {
   uint32_t* modes;
   const double* lut;
   int width, height, bits, tiles_x, tiles_y, max_mode;
+  int ty0, band_tiles;  // tile rows [ty0, ty0 + band_tiles / tiles_x) of each image
 };
 
 constexpr int SEL_WAVES = 4;
@@ -145,8 +146,8 @@ __global__ __launch_bounds__(64 * SEL_WAVES) void k_vp8l_select(SelArgs a) {
   __shared__ double chan_cost[SEL_WAVES][4];
   __shared__ double cost[14];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tile = blockIdx.x % (a.tiles_x * a.tiles_y);
-  const int img = blockIdx.x / (a.tiles_x * a.tiles_y);
+  const int tile = blockIdx.x % a.band_tiles + a.ty0 * a.tiles_x;
+  const int img = blockIdx.x / a.band_tiles;
   const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
   const uint32_t* argb = a.argb + img * a.pitch;
   const int ts = 1 << a.bits, w = a.width, h = a.height;
@@ -213,6 +214,7 @@ struct ResArgs {
   uint32_t* out;
   int64_t pitch;
   int width, height, bits, tiles_x, tiles_y;
+  int y0, rows;  // pixel rows [y0, y0 + rows) of each image
 };
 
 // copyImageWithPrediction: one thread per pixel, predictions from original
@@ -221,9 +223,9 @@ struct ResArgs {
 __global__ __launch_bounds__(256) void k_vp8l_residual(ResArgs a, int64_t total) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= total) return;
-  const int64_t per = (int64_t)a.width * a.height;
+  const int64_t per = (int64_t)a.width * a.rows;
   const int img = (int)(gid / per);
-  const int64_t p = gid - img * per;
+  const int64_t p = gid - img * per + (int64_t)a.y0 * a.width;
   const int y = (int)(p / a.width), x = (int)(p - (int64_t)y * a.width);
   const uint32_t* cur = a.argb + img * a.pitch + (int64_t)y * a.width;
   uint32_t pred;
@@ -401,11 +403,13 @@ namespace wg {
 const double* vp8l_slog2_lut_device();  // vp8l_host.cpp
 }
 
-extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32_t height, int64_t image_pitch,
-                                      int32_t bits, int32_t quality, int32_t n_images, uint32_t* modes,
-                                      uint32_t* residuals, void* stream) {
+extern "C" int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, int32_t height, int64_t image_pitch,
+                                           int32_t bits, int32_t quality, int32_t ty_begin, int32_t ty_end,
+                                           int32_t n_images, uint32_t* modes, uint32_t* residuals, void* stream) {
   WG_REQUIRE(argb && modes && residuals && width > 0 && height > 0 && n_images > 0);
   WG_REQUIRE(bits >= 2 && bits <= 9 && image_pitch >= (int64_t)width * height);
+  const int tiles_x = subsample(width, bits), tiles_y = subsample(height, bits);
+  WG_REQUIRE(ty_begin >= 0 && ty_begin < ty_end && ty_end <= tiles_y);
   const double* lut = wg::vp8l_slog2_lut_device();
   if (!lut) return WG_EHIP;
   hipStream_t s = wg::as_stream(stream);
@@ -417,10 +421,12 @@ extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32
   sa.width = width;
   sa.height = height;
   sa.bits = bits;
-  sa.tiles_x = subsample(width, bits);
-  sa.tiles_y = subsample(height, bits);
+  sa.tiles_x = tiles_x;
+  sa.tiles_y = tiles_y;
   sa.max_mode = quality < 25 ? 4 : (quality < 50 ? 8 : 14);
-  const int64_t tiles = (int64_t)sa.tiles_x * sa.tiles_y * n_images;
+  sa.ty0 = ty_begin;
+  sa.band_tiles = tiles_x * (ty_end - ty_begin);
+  const int64_t tiles = (int64_t)sa.band_tiles * n_images;
   WG_REQUIRE(tiles < (1ll << 31));
   hipLaunchKernelGGL(k_vp8l_select, dim3((unsigned)tiles), dim3(64 * SEL_WAVES), 0, s, sa);
   int rc = wg::check_launch("k_vp8l_select");
@@ -433,11 +439,21 @@ extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32
   ra.width = width;
   ra.height = height;
   ra.bits = bits;
-  ra.tiles_x = sa.tiles_x;
-  ra.tiles_y = sa.tiles_y;
-  const int64_t total = (int64_t)width * height * n_images;
+  ra.tiles_x = tiles_x;
+  ra.tiles_y = tiles_y;
+  ra.y0 = ty_begin << bits;
+  ra.rows = min(ty_end << bits, height) - ra.y0;
+  const int64_t total = (int64_t)width * ra.rows * n_images;
   hipLaunchKernelGGL(k_vp8l_residual, dim3(wg::blocks_for(total, 256)), dim3(256), 0, s, ra, total);
   return wg::check_launch("k_vp8l_residual");
+}
+
+extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32_t height, int64_t image_pitch,
+                                      int32_t bits, int32_t quality, int32_t n_images, uint32_t* modes,
+                                      uint32_t* residuals, void* stream) {
+  WG_REQUIRE(width > 0 && height > 0 && bits >= 2 && bits <= 9);
+  return wg_vp8l_residual_image_rows(argb, width, height, image_pitch, bits, quality, 0, subsample(height, bits),
+                                     n_images, modes, residuals, stream);
 }
 
 extern "C" size_t wg_vp8l_inverse_work_bytes(int32_t height, int32_t n_images) {
