@@ -19,8 +19,10 @@ measures each kernel's isolated launch time for the roofline.
 
 Multi-GPU: one process per GPU (torch.distributed.run), frames sharded across
 ranks with no data-path collective in the timed region ("weak" scaling);
-value = all pixels / max rank time.  With --gather, each rank then sends its
-outputs to rank 0 over RCCL (webp_amd/shard.py), timed and reported separately.
+value = all pixels / max rank time.  With N > 1, each rank then sends its last
+batch's outputs (wg_mb_enc records, reconstruction, NRGBA) to rank 0 with
+grouped RCCL send/recv (webp_amd/shard.py), timed and reported separately
+("gather"), outside `value`.
 Rank 0 prints one JSON line.
 """
 import argparse
@@ -98,7 +100,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--slots", type=int, default=3, help="batches in flight (one HIP stream each)")
     p.add_argument("--iso-steps", type=int, default=2, help="untimed one-batch passes for the isolated kernel times")
-    p.add_argument("--gather", action="store_true", help="after timing, gather outputs to rank 0 over RCCL (timed apart)")
+    p.add_argument("--no-gather", action="store_true",
+                   help="with N > 1, skip the gather of the last batch's outputs to rank 0 (timed apart from value)")
     return p.parse_args()
 
 
@@ -364,7 +367,7 @@ def main():
     pipe.check_status()  # raises if any timed launch hit an in-kernel wait timeout
     iso = isolated_stage_ms(rgba, mb, co, args.batch, device, args.iso_steps)
     gather = None
-    if args.gather and world > 1:
+    if world > 1 and not args.no_gather:
         from webp_amd import shard
         sl = pipe.slots[(pipe.k - 1) % len(pipe.slots)]
         gather = shard.timed_gather_to_root([sl.enc_out, sl.rY, sl.rU, sl.rV, sl.out], world, rank, device)

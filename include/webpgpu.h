@@ -238,12 +238,31 @@ int wg_fixed_costs_i4_host(uint16_t* out);
 int wg_decode_status(const void* work, int32_t mbw, int32_t n_images, void* stream);
 
 /* RGBA -> YUV420 import: replaces VP8Encoder.importImage
- * (internal/lossy/encode.go:671-943, non-dithered path).  rgba: w x h, row
+ * (internal/lossy/encode.go:671-943, non-dithered path; dithered below).  rgba: w x h, row
  * pitch `stride`, image pitch rgba_pitch.  Outputs padded planes (Y stride
  * 16*mbw, U/V stride 8*mbw) with per-image pitches y_pitch / uv_pitch. */
 int wg_import_rgba(const uint8_t* rgba, int32_t w, int32_t h, int32_t stride, int64_t rgba_pitch,
                    int32_t has_alpha, uint8_t* y, uint8_t* u, uint8_t* v, int64_t y_pitch, int64_t uv_pitch,
                    int32_t n_images, void* stream);
+
+/* Dithered import (webp.Encode Preprocessing bit 1): importImage's dithered
+ * path (internal/lossy/encode.go:690-695, :793-809, :903-940:
+ * RGBToYRounding with RandomBits(16) over every padded pixel, then
+ * ConvertRGBA32ToUVDithered with RandomBits(18) for U and V,
+ * internal/dsp/yuv.go:568-576).  The VP8Random stream (random.go) is the same
+ * for every image of a padded size, so it is built once into `plan`
+ * (wg_dither_plan_bytes device bytes, 16-byte aligned; wg_dither_plan builds
+ * it on the host, copies it and synchronises `stream`).  amp: the generator's
+ * amplitude, wg_dither_amp(quality, preprocessing) for webp.Encode's options
+ * (encode.go (root):517-521, InitRandom random.go:39). */
+int32_t wg_dither_amp(float quality, int32_t preprocessing);
+size_t wg_dither_plan_bytes(int32_t w, int32_t h);
+int wg_dither_plan(int32_t w, int32_t h, void* plan, void* stream);
+/* the same plan in host memory (no device work; tests) */
+int wg_dither_plan_host(int32_t w, int32_t h, void* plan_host);
+int wg_import_rgba_dithered(const uint8_t* rgba, int32_t w, int32_t h, int32_t stride, int64_t rgba_pitch,
+                            int32_t has_alpha, int32_t amp, const void* plan, uint8_t* y, uint8_t* u, uint8_t* v,
+                            int64_t y_pitch, int64_t uv_pitch, int32_t n_images, void* stream);
 
 /* Encoder analysis: replaces computeAlphas (internal/lossy/encode_analysis.go:245-307).
  * Outputs per MB: alphas (mixed), lum/uv parts (may be NULL); uv_sum[img] is

@@ -92,6 +92,8 @@ _SIGS = {
     "or_plane_ssim": (ctypes.c_double, [_u8p, _i, _u8p, _i, _i, _i]),
     "or_sse_plane": (ctypes.c_uint64, [_u8p, _i, _u8p, _i, _i, _i]),
     "or_import_rgba": (None, [_u8p, _i, _i, _i, _i, _u8p, _u8p, _u8p]),
+    "or_dithering_strength": (ctypes.c_float, [ctypes.c_float]),
+    "or_import_rgba_dithered": (None, [_u8p, _i, _i, _i, _i, ctypes.c_float, _u8p, _u8p, _u8p]),
     "or_compute_alphas": (_i, [_u8p, _u8p, _u8p, _i, _i, _i32p, _i32p, _i32p]),
     "or_decode_reconstruct": (None, [ctypes.c_void_p, _i16p, _i, _i, _u8p, _u8p, _u8p]),
     "or_decode_filter": (None, [ctypes.c_void_p, _i, _i, _i, _u8p, _u8p, _u8p]),
@@ -176,6 +178,21 @@ def import_rgba(rgba, has_alpha=True):
     U = np.zeros((mbh * 8, mbw * 8), np.uint8)
     V = np.zeros((mbh * 8, mbw * 8), np.uint8)
     lib.or_import_rgba(u8(rgba), w, h, w * 4, int(has_alpha), u8(Y), u8(U), u8(V))
+    return Y, U, V
+
+
+def import_rgba_dithered(rgba, has_alpha=True, dithering=None, quality=75.0):
+    """importImage with dithering (Preprocessing bit 1): dithering defaults to
+    webp.Encode's strength for `quality`."""
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    h, w, _ = rgba.shape
+    if dithering is None:
+        dithering = lib.or_dithering_strength(float(quality))
+    mbw, mbh = plane_dims(w, h)
+    Y = np.zeros((mbh * 16, mbw * 16), np.uint8)
+    U = np.zeros((mbh * 8, mbw * 8), np.uint8)
+    V = np.zeros((mbh * 8, mbw * 8), np.uint8)
+    lib.or_import_rgba_dithered(u8(rgba), w, h, w * 4, int(has_alpha), float(dithering), u8(Y), u8(U), u8(V))
     return Y, U, V
 
 

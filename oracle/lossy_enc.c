@@ -213,3 +213,61 @@ int or_compute_alphas(const uint8_t* y, const uint8_t* u, const uint8_t* v, int 
     }
   return total > 0 ? (int)(uv_sum / total) : 0;
 }
+
+/* ---------------- dithered import (Preprocessing bit 1) ---------------- */
+/* webp.Encode's dithering amplitude, encode.go (root):517-521, float32:
+ * x = quality / 100; dithering = 1 + (0.5 - 1) * x^2 * x^2 */
+float or_dithering_strength(float quality) {
+  const float x = quality / 100.0f;
+  const float x2 = x * x;
+  return 1.0f + (0.5f - 1.0f) * x2 * x2;
+}
+
+/* importImage's dithered path (internal/lossy/encode.go:690-695, :793-809,
+ * :903-940): one VP8Random stream per image (InitRandom), Y first over every
+ * padded pixel in raster order (RGBToYRounding with RandomBits(16)), then per
+ * row pair ConvertRGBA32ToUVDithered (RandomBits(18) for U, then V, per chroma
+ * pixel; yuv.go:568-576). */
+void or_import_rgba_dithered(const uint8_t* rgba, int w, int h, int stride, int has_alpha, float dithering, uint8_t* Y,
+                             uint8_t* U, uint8_t* V) {
+  const int mbw = (w + 15) >> 4, mbh = (h + 15) >> 4;
+  const int padw = mbw * 16, padh = mbh * 16;
+  const int ys = padw, uvs = mbw * 8, uvw = (padw + 1) >> 1;
+  or_random rg;
+  or_random_init(&rg, dithering);
+  for (int y = 0; y < padh; y++) {
+    const int sy = y < h ? y : h - 1;
+    const uint8_t* row = rgba + (size_t)sy * stride;
+    for (int x = 0; x < padw; x++) {
+      const int sx = x < w ? x : w - 1;
+      const int rnd = or_random_bits2(&rg, 16, rg.amp);
+      Y[(size_t)y * ys + x] =
+          (uint8_t)((16839 * row[4 * sx] + 33059 * row[4 * sx + 1] + 6420 * row[4 * sx + 2] + rnd + (16 << 16)) >> 16);
+    }
+  }
+  uint8_t* pr = (uint8_t*)malloc((size_t)padw * 2 * 4);
+  uint8_t *pg = pr + 2 * padw, *pb = pg + 2 * padw, *pa = pb + 2 * padw;
+  uint16_t* tmp = (uint16_t*)malloc((size_t)uvw * 4 * sizeof(uint16_t));
+  for (int yp = 0; yp < padh / 2; yp++) {
+    for (int r = 0; r < 2; r++) {
+      int sy = yp * 2 + r;
+      if (sy >= h) sy = h - 1;
+      const uint8_t* row = rgba + (size_t)sy * stride;
+      for (int x = 0; x < padw; x++) {
+        const int sx = x < w ? x : w - 1;
+        pr[r * padw + x] = row[4 * sx];
+        pg[r * padw + x] = row[4 * sx + 1];
+        pb[r * padw + x] = row[4 * sx + 2];
+        pa[r * padw + x] = has_alpha ? row[4 * sx + 3] : 0xff;
+      }
+    }
+    or_accumulate_rgba(pr, pg, pb, pa, padw, tmp, padw);
+    for (int i = 0; i < uvw; i++) {
+      const int r = tmp[4 * i], g = tmp[4 * i + 1], b = tmp[4 * i + 2];
+      U[(size_t)yp * uvs + i] = (uint8_t)or_rgb_to_u(r, g, b, or_random_bits2(&rg, 18, rg.amp));
+      V[(size_t)yp * uvs + i] = (uint8_t)or_rgb_to_v(r, g, b, or_random_bits2(&rg, 18, rg.amp));
+    }
+  }
+  free(pr);
+  free(tmp);
+}

@@ -80,6 +80,9 @@ void or_convert_rgba32_to_uv(const uint16_t* rgb, uint8_t* u, uint8_t* v, int wi
 typedef struct { int index1, index2; uint32_t tab[55]; int amp; } or_random;
 void or_random_init(or_random* rg, float dithering);            /* :39 */
 int or_random_bits2(or_random* rg, int num_bits, int amp);      /* :54 */
+float or_dithering_strength(float quality);                      /* encode.go (root):517-521 */
+void or_import_rgba_dithered(const uint8_t* rgba, int w, int h, int stride, int has_alpha, float dithering,
+                             uint8_t* Y, uint8_t* U, uint8_t* V); /* internal/lossy/encode.go:690-940 */
 
 /* ---- upsampling (internal/dsp/upsample.go, webp.go) ---- */
 void or_upsample_line_pair_nrgba(const uint8_t* top_y, const uint8_t* bot_y,

@@ -50,6 +50,11 @@ SIGNATURES = {
     "wg_vp8_parse": [_vp, ctypes.c_size_t, _vp, _vp, _vp, _i64],
     "wg_decode_status": [_vp, _i32, _i32, _vp],
     "wg_import_rgba": [_vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
+    "wg_dither_amp": [ctypes.c_float, _i32],
+    "wg_dither_plan_bytes": [_i32, _i32],
+    "wg_dither_plan": [_i32, _i32, _vp, _vp],
+    "wg_dither_plan_host": [_i32, _i32, _vp],
+    "wg_import_rgba_dithered": [_vp, _i32, _i32, _i32, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "wg_analysis_alphas": [_vp, _vp, _vp, _i32, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp],
     "wg_upsample_nrgba": [_vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp],
     "wg_plane_ssim_work_bytes": [_i32, _i32, _i32],
@@ -103,7 +108,8 @@ _RES = {"wg_last_error": ctypes.c_char_p, "wg_decode_work_bytes": ctypes.c_size_
         "wg_plane_ssim_work_bytes": ctypes.c_size_t, "wg_vp8l_inverse_work_bytes": ctypes.c_size_t,
         "wg_sharpyuv_work_bytes": ctypes.c_size_t, "wg_encode_work_bytes": ctypes.c_size_t,
         "wg_alpha_unfilter_work_bytes": ctypes.c_size_t, "wg_alpha_estimate_work_bytes": ctypes.c_size_t,
-        "wg_rescaler_plan_bytes": ctypes.c_size_t}
+        "wg_rescaler_plan_bytes": ctypes.c_size_t, "wg_dither_plan_bytes": ctypes.c_size_t,
+        "wg_dither_amp": ctypes.c_int32}
 
 for _name, _args in SIGNATURES.items():
     _f = getattr(lib, _name)

@@ -75,6 +75,42 @@ def import_rgba(rgba, has_alpha=True, out=None):
     return Y, U, V
 
 
+_DITHER_PLANS = {}
+
+
+def dither_plan(w, h, device="cuda"):
+    """The per-size VP8Random draws of importImage's dithered path, built once
+    per (padded size, device) and kept resident."""
+    key = (mb_dims(w, h), str(device))
+    if key not in _DITHER_PLANS:
+        plan = torch.empty(lib.wg_dither_plan_bytes(w, h), dtype=torch.uint8, device=device)
+        call("wg_dither_plan", w, h, plan.data_ptr(), _stream())
+        _DITHER_PLANS[key] = plan
+    return _DITHER_PLANS[key]
+
+
+def dither_amp(quality=75.0, preprocessing=2):
+    """InitRandom's amplitude for webp.Encode's dithering at this quality (0 without preprocessing bit 1)."""
+    return int(lib.wg_dither_amp(float(quality), int(preprocessing)))
+
+
+def import_rgba_dithered(rgba, amp, has_alpha=True, out=None):
+    """importImage with dithering: (n, h, w, 4) uint8 RGBA -> padded (Y, U, V)."""
+    assert rgba.is_cuda and rgba.dtype == torch.uint8 and rgba.dim() == 4 and rgba.is_contiguous()
+    n, h, w, _ = rgba.shape
+    mbw, mbh = mb_dims(w, h)
+    if out is None:
+        Y = torch.empty((n, 16 * mbh, 16 * mbw), dtype=torch.uint8, device=rgba.device)
+        U = torch.empty((n, 8 * mbh, 8 * mbw), dtype=torch.uint8, device=rgba.device)
+        V = torch.empty_like(U)
+    else:
+        Y, U, V = out
+    plan = dither_plan(w, h, rgba.device)
+    call("wg_import_rgba_dithered", rgba.data_ptr(), w, h, 4 * w, 4 * w * h, int(bool(has_alpha)), int(amp),
+         plan.data_ptr(), Y.data_ptr(), U.data_ptr(), V.data_ptr(), Y[0].numel(), U[0].numel(), n, _stream())
+    return Y, U, V
+
+
 def analysis_alphas(Y, U, V, w, h, parts=False, out=None):
     """computeAlphas: per-MB mixed alpha (n, mbh*mbw) int32 and the UV alpha average per image."""
     n = Y.shape[0]
