@@ -458,6 +458,18 @@ size_t wg_sharpyuv_work_bytes(int32_t width, int32_t height, int32_t n_images);
 int wg_sharpyuv_convert(const uint8_t* rgb, int32_t width, int32_t height, int32_t rgb_stride, int64_t rgb_pitch,
                         const int32_t* matrix_host, int32_t n_images, uint8_t* y, int32_t y_stride, int64_t y_pitch,
                         uint8_t* u, uint8_t* v, int32_t uv_stride, int64_t uv_pitch, void* work, void* stream);
+/* sharpyuv.Convert with Options{Matrix, TransferType, SharpEnabled}
+ * (sharpyuv.go:17-64): transfer is the H.273 code (gamma.go:11-28; 13 = sRGB,
+ * the default, as in wg_sharpyuv_convert); sharp_enabled = 0 runs
+ * convertStandard (:68-115, 2x2 average, no work buffer needed). */
+int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t height, int32_t rgb_stride, int64_t rgb_pitch,
+                           const int32_t* matrix_host, int32_t transfer, int32_t sharp_enabled, int32_t n_images,
+                           uint8_t* y, int32_t y_stride, int64_t y_pitch, uint8_t* u, uint8_t* v, int32_t uv_stride,
+                           int64_t uv_pitch, void* work, void* stream);
+/* GammaToLinear over the 1024 10-bit codes (g2l) and the LinearToGamma table
+ * (l2g, *n entries; l2g may be NULL to query n) the kernels use for a
+ * transfer function other than sRGB (gamma.go:360-446); host memory. */
+int wg_sharpyuv_transfer_tables_host(int32_t tf, uint32_t* g2l, uint16_t* l2g, int32_t* n);
 /* The gamma tables used (gamma.go:48-88), host copies: g2l[1026], l2g[514]. */
 int wg_sharpyuv_tables_host(uint32_t* g2l, uint32_t* l2g);
 /* After wg_sharpyuv_convert on `work` (same stream): the refinement

@@ -125,6 +125,13 @@ _SIGS = {
     "or_pack_rgb": (None, [ctypes.c_void_p] * 3 + [ctypes.c_size_t, _i, ctypes.c_void_p]),
     "or_rescale_plane": (_i, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i, _i, _i]),
     "or_sharpyuv_tables": (None, [ctypes.c_void_p, ctypes.c_void_p]),
+    "or_sharpyuv_convert_tf": (_i, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i, ctypes.c_void_p, ctypes.c_void_p,
+                                    _i, ctypes.c_void_p, _i]),
+    "or_sharpyuv_convert_standard": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, _i, ctypes.c_void_p,
+                                            ctypes.c_void_p, _i, ctypes.c_void_p]),
+    "or_sharpyuv_gamma_to_linear": (ctypes.c_uint32, [ctypes.c_uint16, _i, _i]),
+    "or_sharpyuv_linear_to_gamma": (ctypes.c_uint16, [ctypes.c_uint32, _i, _i]),
+    "or_sharpyuv_tf_long_double": (None, [_i]),
     "or_setup_segment": (None, [_i] * 8 + [ctypes.c_void_p]),
     "or_fixed_costs_i4": (None, [ctypes.c_void_p]),
     "or_quantize_coeffs": (_i, [ctypes.c_void_p] * 3 + [_i]),
@@ -433,8 +440,13 @@ WEBP_MATRIX = np.array([16839, 33059, 6420, 16 << 16, -9719, -19081, 28800, 128 
                         28800, -24116, -4684, 128 << 16], np.int32)  # sharpyuv/csp.go:66-70
 
 
-def sharpyuv_convert(rgb, matrix=WEBP_MATRIX):
-    """convertSharp: rgb (h, w, 3) uint8 -> (Y (h, w), U, V ((h+1)//2, (w+1)//2), iterations)."""
+TRANSFER_FUNCS = (1, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18)  # sharpyuv/gamma.go:11-28
+
+
+def sharpyuv_convert(rgb, matrix=WEBP_MATRIX, transfer=13, sharp=True):
+    """sharpyuv.Convert: rgb (h, w, 3) uint8 -> (Y (h, w), U, V ((h+1)//2, (w+1)//2),
+    iterations).  sharp=False is convertStandard (iterations 0); transfer is
+    the H.273 code (13 = sRGB, the default)."""
     rgb = np.ascontiguousarray(rgb, np.uint8)
     h, w, _ = rgb.shape
     cw, ch = (w + 1) // 2, (h + 1) // 2
@@ -442,9 +454,21 @@ def sharpyuv_convert(rgb, matrix=WEBP_MATRIX):
     U = np.zeros((ch, cw), np.uint8)
     V = np.zeros((ch, cw), np.uint8)
     m = np.ascontiguousarray(matrix, np.int32)
-    it = lib.or_sharpyuv_convert(rgb.ctypes.data, w, h, 3 * w, Y.ctypes.data, w, U.ctypes.data, V.ctypes.data, cw,
-                                 m.ctypes.data)
+    if not sharp:
+        lib.or_sharpyuv_convert_standard(rgb.ctypes.data, w, h, 3 * w, Y.ctypes.data, w, U.ctypes.data, V.ctypes.data,
+                                         cw, m.ctypes.data)
+        return Y, U, V, 0
+    it = lib.or_sharpyuv_convert_tf(rgb.ctypes.data, w, h, 3 * w, Y.ctypes.data, w, U.ctypes.data, V.ctypes.data, cw,
+                                    m.ctypes.data, int(transfer))
     return Y, U, V, it
+
+
+def sharpyuv_transfer_tables(transfer, bit_depth=10):
+    """GammaToLinear over [0, 2^bd) and LinearToGamma over [0, max + 1] (gamma.go:360-446)."""
+    g2l = np.array([lib.or_sharpyuv_gamma_to_linear(v, bit_depth, transfer) for v in range(1 << bit_depth)], np.uint32)
+    n = int(g2l.max()) + 1
+    l2g = np.array([lib.or_sharpyuv_linear_to_gamma(v, bit_depth, transfer) for v in range(n)], np.uint16)
+    return g2l, l2g
 
 
 def sharpyuv_tables():

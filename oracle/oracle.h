@@ -258,6 +258,13 @@ void or_segment_analysis(const int32_t* alphas, int mbw, int mbh, int uv_alpha_s
 void or_sharpyuv_tables(uint32_t* g2l_out /* 1026 */, uint32_t* l2g_out /* 514 */);
 int or_sharpyuv_convert(const uint8_t* rgb, int width, int height, int rgb_stride, uint8_t* y, int y_stride,
                         uint8_t* u, uint8_t* v, int uv_stride, const int32_t* matrix /* 12 */);
+int or_sharpyuv_convert_tf(const uint8_t* rgb, int width, int height, int rgb_stride, uint8_t* y, int y_stride,
+                           uint8_t* u, uint8_t* v, int uv_stride, const int32_t* matrix, int tf);
+void or_sharpyuv_convert_standard(const uint8_t* rgb, int width, int height, int rgb_stride, uint8_t* y, int y_stride,
+                                  uint8_t* u, uint8_t* v, int uv_stride, const int32_t* matrix);
+uint32_t or_sharpyuv_gamma_to_linear(uint16_t v, int bit_depth, int tf);
+void or_sharpyuv_tf_long_double(int on);
+uint16_t or_sharpyuv_linear_to_gamma(uint32_t v, int bit_depth, int tf);
 
 #ifdef __cplusplus
 }

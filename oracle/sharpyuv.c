@@ -85,12 +85,147 @@ static uint16_t from_linear(uint32_t value, int bit_depth) {
   return (uint16_t)fp_interp((int)value, l2g, G2L_VALUE_BITS - L2G_BITS, bit_depth - G2L_VALUE_BITS);
 }
 
+/* ---- the other transfer functions, gamma.go:125-446 (float32 arithmetic like
+ * the Go code: every float32 operation rounds; powf/log10f/exp/log go through
+ * float64 libm and round back, like Go's float32(math.Pow(float64(.), .))) ---- */
+static int g_long_double = 0; /* tests: evaluate pow/log10/exp/log in long double to probe rounding margins */
+void or_sharpyuv_tf_long_double(int on) { g_long_double = on; }
+static float powf_go(float b, float e) {
+  return g_long_double ? (float)(double)powl((long double)b, (long double)e) : (float)pow((double)b, (double)e);
+}
+static float log10f_go(float x) { return g_long_double ? (float)(double)log10l((long double)x) : (float)log10((double)x); }
+static float clampf_go(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+static float minf_go(float a, float b) { return a < b ? a : b; }
+static float maxf_go(float a, float b) { return a > b ? a : b; }
+static float roundf_go(float x) { /* :159-164 */
+  return x < 0 ? (float)ceil((double)(x - 0.5f)) : (float)floor((double)(x + 0.5f));
+}
+/* Constant expressions are exact in Go and rounded once to float32; the
+ * literals below are those products / quotients written out (e.g.
+ * 4.5*0.018053968510807 = 0.0812428582986315). */
+static float to_linear_tf(float g, int tf) {
+  switch (tf) {
+    case 1: case 6: case 14: case 15: /* toLinear709 :167-176 */
+      if (g < 0) return 0;
+      if (g < 0.0812428582986315f) return g / 4.5f;
+      if (g < 1) return powf_go((g + 0.09929682680944f) / 1.09929682680944f, (float)(1.0 / 0.45));
+      return 1;
+    case 4: return powf_go(clampf_go(g, 0, 1), 2.2f);                  /* :190 */
+    case 5: return powf_go(clampf_go(g, 0, 1), 2.8f);                  /* :199 */
+    case 7:                                                          /* :208-217 */
+      if (g < 0) return 0;
+      if (g < 0.09128634211778f) return g / 4.0f;
+      if (g < 1) return powf_go((g + 0.111572195921731f) / 1.111572195921731f, (float)(1.0 / 0.45));
+      return 1;
+    case 9: /* :231-237 */
+      if (g <= 0) return 0.005f;
+      return powf_go(10.0f, 2.0f * (minf_go(g, 1.0f) - 1.0f));
+    case 10: /* :247-253 */
+      if (g <= 0) return 0.00158113883f;
+      return powf_go(10.0f, 2.5f * (minf_go(g, 1.0f) - 1.0f));
+    case 11: /* :263-270 */
+      if (g <= -0.0812428582986315f) return powf_go((-g + 0.09929682680944f) / -1.09929682680944f, (float)(1.0 / 0.45));
+      if (g < 0.0812428582986315f) return g / 4.5f;
+      return powf_go((g + 0.09929682680944f) / 1.09929682680944f, (float)(1.0 / 0.45));
+    case 12: /* :282-293 */
+      if (g < -0.25f) return -0.25f;
+      if (g < 0) return powf_go((g - 0.02482420670236f) / -0.27482420670236f, (float)(1.0 / 0.45)) / -4.0f;
+      if (g < 0.0812428582986315f) return g / 4.5f;
+      if (g < 1) return powf_go((g + 0.09929682680944f) / 1.09929682680944f, (float)(1.0 / 0.45));
+      return 1;
+    case 16: /* PQ :309-317 */
+      if (g > 0) {
+        const float pg = powf_go(g, (float)(32.0 / 2523.0));
+        const float num = maxf_go(pg - 0.8359375f, 0.0f);
+        const float den = maxf_go(18.8515625f - 18.6875f * pg, 1.401298464324817e-45f);
+        return powf_go(num / den, (float)(4096.0 / 653.0));
+      }
+      return 0;
+    case 17: return powf_go(maxf_go(g, 0), 2.6f) / 0.91655527974030934f; /* :330 */
+    case 18: /* HLG :339-346 */
+      if (g < 0) return 0;
+      if (g <= 0.5f) return powf_go((g * g) * (float)(1.0 / 3.0), 1.2f);
+      {
+        const double e = g_long_double ? (double)expl((long double)((g - 0.55991073f) / 0.17883277f))
+                                       : exp((double)((g - 0.55991073f) / 0.17883277f));
+        return powf_go(((float)e + 0.28466892f) / 12.0f, 1.2f);
+      }
+    default: return 0;
+  }
+}
+static float from_linear_tf(float l, int tf) {
+  switch (tf) {
+    case 1: case 6: case 14: case 15: /* fromLinear709 :178-187 */
+      if (l < 0) return 0;
+      if (l < 0.018053968510807f) return l * 4.5f;
+      if (l < 1) return 1.09929682680944f * powf_go(l, 0.45f) - 0.09929682680944f;
+      return 1;
+    case 4: return powf_go(clampf_go(l, 0, 1), (float)(1.0 / 2.2)); /* :194 */
+    case 5: return powf_go(clampf_go(l, 0, 1), (float)(1.0 / 2.8)); /* :203 */
+    case 7:                                                        /* :219-228 */
+      if (l < 0) return 0;
+      if (l < 0.022821585529445f) return l * 4.0f;
+      if (l < 1) return 1.111572195921731f * powf_go(l, 0.45f) - 0.111572195921731f;
+      return 1;
+    case 9: /* :239-244 */
+      if (l < 0.01f) return 0;
+      return 1.0f + log10f_go(minf_go(l, 1.0f)) / 2.0f;
+    case 10: /* :255-260 */
+      if (l < 0.00316227766f) return 0;
+      return 1.0f + log10f_go(minf_go(l, 1.0f)) / 2.5f;
+    case 11: /* :272-279 */
+      if (l <= -0.018053968510807f) return -1.09929682680944f * powf_go(-l, 0.45f) + 0.09929682680944f;
+      if (l < 0.018053968510807f) return l * 4.5f;
+      return 1.09929682680944f * powf_go(l, 0.45f) - 0.09929682680944f;
+    case 12: /* :295-306 */
+      if (l < -0.25f) return -0.25f;
+      if (l < 0) return -0.27482420670236f * powf_go(-4.0f * l, 0.45f) + 0.02482420670236f;
+      if (l < 0.018053968510807f) return l * 4.5f;
+      if (l < 1) return 1.09929682680944f * powf_go(l, 0.45f) - 0.09929682680944f;
+      return 1;
+    case 16: /* PQ :319-327 */
+      if (l > 0) {
+        const float pl = powf_go(l, (float)(653.0 / 4096.0));
+        const float num = 0.8359375f + 18.8515625f * pl;
+        const float den = 1.0f + 18.6875f * pl;
+        return powf_go(num / den, (float)(2523.0 / 32.0));
+      }
+      return 0;
+    case 17: return powf_go(0.91655527974030934f * maxf_go(l, 0), (float)(1.0 / 2.6)); /* :334 */
+    case 18: /* HLG :348-356 */
+      l = powf_go(l, (float)(1.0 / 1.2));
+      if (l < 0) return 0;
+      if (l <= (float)(1.0 / 12.0)) return (float)sqrt((double)(3.0f * l));
+      return 0.17883277f * (float)(g_long_double ? (double)logl((long double)(12.0f * l - 0.28466892f))
+                                                 : log((double)(12.0f * l - 0.28466892f))) + 0.55991073f;
+    default: return 0;
+  }
+}
+/* GammaToLinear / LinearToGamma (gamma.go:360-446) */
+uint32_t or_sharpyuv_gamma_to_linear(uint16_t v, int bit_depth, int tf) {
+  init_tables();
+  if (tf == 13) return to_linear(v, bit_depth);
+  if (tf == 8) return v;
+  const float vf = (float)v / (float)((1 << bit_depth) - 1);
+  return (uint32_t)(int64_t)roundf_go(to_linear_tf(vf, tf) * 65535.0f);
+}
+uint16_t or_sharpyuv_linear_to_gamma(uint32_t v, int bit_depth, int tf) {
+  init_tables();
+  if (tf == 13) return from_linear(v, bit_depth);
+  if (tf == 8) return (uint16_t)v;
+  const float vf = (float)v / 65535.0f;
+  return (uint16_t)(int64_t)roundf_go(from_linear_tf(vf, tf) * (float)((1 << bit_depth) - 1));
+}
+static int g_tf = 13; /* transfer of the conversion in progress (the oracle is single-threaded per call) */
+static uint32_t to_lin(uint16_t v, int bd) { return g_tf == 13 ? to_linear(v, bd) : or_sharpyuv_gamma_to_linear(v, bd, g_tf); }
+static uint16_t from_lin(uint32_t v, int bd) { return g_tf == 13 ? from_linear(v, bd) : or_sharpyuv_linear_to_gamma(v, bd, g_tf); }
+
 static int rgb_to_gray(int64_t r, int64_t g, int64_t b) {
   return (int)((13933 * r + 46871 * g + 4732 * b + YUV_HALF) >> YUV_FIX);
 }
 static uint32_t scale_down(uint16_t a, uint16_t b, uint16_t c, uint16_t d, int bd) {
-  const uint32_t la = to_linear(a, bd), lb = to_linear(b, bd), lc = to_linear(c, bd), ld = to_linear(d, bd);
-  return from_linear((la + lb + lc + ld + 2) >> 2, bd);
+  const uint32_t la = to_lin(a, bd), lb = to_lin(b, bd), lc = to_lin(c, bd), ld = to_lin(d, bd);
+  return from_lin((la + lb + lc + ld + 2) >> 2, bd);
 }
 static uint16_t clip_bd(int y, int bd) {
   const int mx = (1 << bd) - 1;
@@ -116,8 +251,8 @@ static void store_gray(const uint16_t* src, uint16_t* y, int w) {
 }
 static void update_w(const uint16_t* src, uint16_t* dst, int w, int bd) {
   for (int i = 0; i < w; i++) {
-    const uint32_t r = to_linear(src[i], bd), g = to_linear(src[i + w], bd), b = to_linear(src[i + 2 * w], bd);
-    dst[i] = from_linear((uint32_t)rgb_to_gray(r, g, b), bd);
+    const uint32_t r = to_lin(src[i], bd), g = to_lin(src[i + w], bd), b = to_lin(src[i + 2 * w], bd);
+    dst[i] = from_lin((uint32_t)rgb_to_gray(r, g, b), bd);
   }
 }
 static void update_chroma(const uint16_t* s1, const uint16_t* s2, int16_t* dst, int uvw, int bd) {
@@ -202,10 +337,52 @@ static void convert_wrgb_to_yuv(const uint16_t* best_y, const int16_t* best_uv, 
     }
 }
 
-/* convertSharp (sharpyuv.go:170-269).  Returns the number of iterations run. */
+/* convertStandard (sharpyuv.go:68-115) */
+static int32_t rgb_to_yuv_component(int32_t r, int32_t g, int32_t b, const int32_t* c) {
+  const int64_t luma = (int64_t)c[0] * r + (int64_t)c[1] * g + (int64_t)c[2] * b + (int64_t)c[3] + YUV_HALF;
+  return (int32_t)(luma >> YUV_FIX);
+}
+void or_sharpyuv_convert_standard(const uint8_t* rgb, int width, int height, int rgb_stride, uint8_t* y, int y_stride,
+                                  uint8_t* u, uint8_t* v, int uv_stride, const int32_t* m) {
+  for (int j = 0; j < height; j++)
+    for (int i = 0; i < width; i++) {
+      const uint8_t* p = rgb + (size_t)j * rgb_stride + 3 * i;
+      y[(size_t)j * y_stride + i] = clip_u8(rgb_to_yuv_component(p[0], p[1], p[2], m));
+    }
+  const int uvw = (width + 1) >> 1, uvh = (height + 1) >> 1;
+  for (int j = 0; j < uvh; j++)
+    for (int i = 0; i < uvw; i++) {
+      int32_t sr = 0, sg = 0, sb = 0, n = 0;
+      for (int dy = 0; dy < 2; dy++) {
+        const int yy = 2 * j + dy;
+        if (yy >= height) continue;
+        for (int dx = 0; dx < 2; dx++) {
+          const int xx = 2 * i + dx;
+          if (xx >= width) continue;
+          const uint8_t* p = rgb + (size_t)yy * rgb_stride + 3 * xx;
+          sr += p[0];
+          sg += p[1];
+          sb += p[2];
+          n++;
+        }
+      }
+      const int32_t ar = (sr + n / 2) / n, ag = (sg + n / 2) / n, ab = (sb + n / 2) / n;
+      u[(size_t)j * uv_stride + i] = clip_u8(rgb_to_yuv_component(ar, ag, ab, m + 4));
+      v[(size_t)j * uv_stride + i] = clip_u8(rgb_to_yuv_component(ar, ag, ab, m + 8));
+    }
+}
+
 int or_sharpyuv_convert(const uint8_t* rgb, int width, int height, int rgb_stride, uint8_t* y, int y_stride,
                         uint8_t* u, uint8_t* v, int uv_stride, const int32_t* matrix) {
+  return or_sharpyuv_convert_tf(rgb, width, height, rgb_stride, y, y_stride, u, v, uv_stride, matrix, 13);
+}
+
+/* convertSharp (sharpyuv.go:170-269) with transfer function tf (H.273 code,
+ * gamma.go:11-28).  Returns the number of iterations run. */
+int or_sharpyuv_convert_tf(const uint8_t* rgb, int width, int height, int rgb_stride, uint8_t* y, int y_stride,
+                           uint8_t* u, uint8_t* v, int uv_stride, const int32_t* matrix, int tf) {
   init_tables();
+  g_tf = tf;
   const int w = (width + 1) & ~1, h = (height + 1) & ~1;
   const int uvw = w >> 1, uvh = h >> 1, sfix = 2, bd = 8 + sfix;
   uint16_t* tmp1 = malloc(sizeof(uint16_t) * 3 * w);

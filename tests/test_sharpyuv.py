@@ -86,3 +86,82 @@ def test_gpu_wide(cuda, w, h):
     Y, U, V = frames.sharpyuv_convert(torch.from_numpy(rgb[None].copy()).cuda())
     ey, eu, ev, _ = O.sharpyuv_convert(rgb)
     assert (Y[0].cpu().numpy() == ey).all() and (U[0].cpu().numpy() == eu).all() and (V[0].cpu().numpy() == ev).all()
+
+
+# ---- the other transfer functions and convertStandard (sharpyuv.go:68-115, gamma.go:125-446) ----
+
+NON_SRGB = [tf for tf in O.TRANSFER_FUNCS if tf != 13]
+
+
+def product_transfer_tables(tf):
+    from webp_amd import _lib
+    g2l = np.zeros(1024, np.uint32)
+    n = np.zeros(1, np.int32)
+    _lib.call("wg_sharpyuv_transfer_tables_host", tf, g2l.ctypes.data, None, n.ctypes.data)
+    l2g = np.zeros(int(n[0]), np.uint16)
+    _lib.call("wg_sharpyuv_transfer_tables_host", tf, g2l.ctypes.data, l2g.ctypes.data, n.ctypes.data)
+    return g2l, l2g
+
+
+@pytest.mark.parametrize("tf", NON_SRGB)
+def test_transfer_tables_product_equals_oracle(tf):
+    """The kernels' GammaToLinear / LinearToGamma tables (host-built, product)
+    equal the restatement's per-value functions over their whole domains."""
+    g, l = product_transfer_tables(tf)
+    eg, el = O.sharpyuv_transfer_tables(tf)
+    assert (g == eg).all() and len(l) == len(el) and (l == el).all()
+
+
+def test_transfer_tables_are_robust_to_the_math_library():
+    """Evaluating pow / log10 / exp / log in long double instead of double
+    gives the same tables for every transfer function: no entry sits close
+    enough to a float32 or final rounding boundary for Go's math package and
+    libm to disagree."""
+    for tf in NON_SRGB:
+        g, l = O.sharpyuv_transfer_tables(tf)
+        O.lib.or_sharpyuv_tf_long_double(1)
+        try:
+            g2, l2 = O.sharpyuv_transfer_tables(tf)
+        finally:
+            O.lib.or_sharpyuv_tf_long_double(0)
+        assert (g == g2).all() and (l == l2).all(), tf
+
+
+def test_transfer_known_values():
+    """Spot values from gamma.go's formulas: linear is the identity at
+    bitDepth 10; every curve maps 0 -> 0 (log curves: to their floors) and
+    full scale -> 65535 / 1023."""
+    g, l = O.sharpyuv_transfer_tables(8)
+    assert (g == np.arange(1024)).all() and (l == np.arange(1024)).all()
+    for tf in (1, 4, 5, 6, 7, 11, 12, 14, 15, 16):
+        g, l = O.sharpyuv_transfer_tables(tf)
+        assert g[0] == 0 and g[1023] == 65535 and l[0] == 0 and l[65535] == 1023, tf
+    g, _ = O.sharpyuv_transfer_tables(9)
+    assert g[0] == round(0.005 * 65535)  # log100: midInterval at 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tf", NON_SRGB)
+def test_gpu_transfer_functions(cuda, tf):
+    import torch
+    from webp_amd import frames
+    imgs = [np.ascontiguousarray(synth.blobs_rgba(67, 41, seed=tf)[..., :3]),
+            np.ascontiguousarray(synth.noise_rgba(67, 41, seed=tf)[..., :3])]
+    Y, U, V, its = frames.sharpyuv_convert(torch.from_numpy(np.stack(imgs)).cuda(), transfer=tf, iterations=True)
+    for i, rgb in enumerate(imgs):
+        ey, eu, ev, eits = O.sharpyuv_convert(rgb, transfer=tf)
+        assert (Y[i].cpu().numpy() == ey).all() and (U[i].cpu().numpy() == eu).all() and \
+            (V[i].cpu().numpy() == ev).all(), (tf, i)
+        assert its[i] == eits
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h", [(1, 1), (2, 2), (3, 5), (67, 41), (1920, 1080)])
+def test_gpu_convert_standard(cuda, w, h):
+    """convertStandard (SharpEnabled = false): per-pixel matrix Y, 2x2 average U/V."""
+    import torch
+    from webp_amd import frames
+    rgb = np.ascontiguousarray(synth.noise_rgba(w, h, seed=w * h)[..., :3])
+    Y, U, V = frames.sharpyuv_convert(torch.from_numpy(rgb[None].copy()).cuda(), sharp=False)
+    ey, eu, ev, _ = O.sharpyuv_convert(rgb, sharp=False)
+    assert (Y[0].cpu().numpy() == ey).all() and (U[0].cpu().numpy() == eu).all() and (V[0].cpu().numpy() == ev).all()

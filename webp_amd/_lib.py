@@ -94,6 +94,9 @@ SIGNATURES = {
     "wg_sharpyuv_work_bytes": [_i32, _i32, _i32],
     "wg_sharpyuv_convert": [_vp, _i32, _i32, _i32, _i64, _vp, _i32, _vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _vp],
     "wg_sharpyuv_tables_host": [_vp, _vp],
+    "wg_sharpyuv_convert_ex": [_vp, _i32, _i32, _i32, _i64, _vp, _i32, _i32, _i32, _vp, _i32, _i64, _vp, _vp, _i32,
+                               _i64, _vp, _vp],
+    "wg_sharpyuv_transfer_tables_host": [_i32, _vp, _vp, _vp],
     "wg_sharpyuv_iterations": [_vp, _i32, _i32, _i32, _vp, _vp],
     "wg_setup_segment": [_i32, _vp, _i32, _i32, _vp],
     "wg_encode_work_bytes": [_i32, _i32, _i32],

@@ -1,5 +1,6 @@
 // sharpyuv.hip -- SharpYUV RGB -> YUV420 on gfx950,
-// sRGB transfer, any conversion matrix (sharpyuv/sharpyuv.go:170-432).
+// any transfer function and conversion matrix (sharpyuv/sharpyuv.go:39-432),
+// and convertStandard (:68-115) when sharpening is off (k_sharp_standard).
 //
 //   k_sharp_init   import + gray Y, target W, target / initial chroma
 //                  residuals (convertSharp phase 1, :196-222): one thread per
@@ -24,7 +25,10 @@
 //
 // All arithmetic is integer (the reference's int / int64 / int16 with wrap);
 // the gamma tables are built on the host (sharpyuv_host.cpp) like
-// initGammaTables (gamma.go:48-88) and staged in LDS.
+// initGammaTables (gamma.go:48-88) and staged in LDS.  For the transfer
+// functions other than sRGB (LUT = true) GammaToLinear is the same 1024-entry
+// LDS table and LinearToGamma a direct uint16 table in global memory (up to
+// 72k entries, L2-resident), gamma.go:360-446.
 #include <algorithm>
 
 #include "wg_common.h"
@@ -45,6 +49,12 @@ __device__ __forceinline__ int from_linear(const uint32_t* l2g, uint32_t v) {
   const uint32_t pos = v >> 7, x = v & 127u;
   const uint32_t v0 = l2g[pos] >> 6, v1 = l2g[pos + 1] >> 6;
   return (int)(v0 + (((v1 - v0) * x + 64u) >> 7));
+}
+// LinearToGamma: the sRGB interpolation, or the direct table of another transfer
+template <bool LUT>
+__device__ __forceinline__ int from_lin(const uint32_t* l2g, const uint16_t* lut, int n, uint32_t v) {
+  if (LUT) return lut[min(v, (uint32_t)(n - 1))];
+  return from_linear(l2g, v);
 }
 __device__ __forceinline__ int gray(int64_t r, int64_t g, int64_t b) {
   return (int)((13933 * r + 46871 * g + 4732 * b + 32768) >> 16);
@@ -67,6 +77,8 @@ struct SharpArgs {
   int16_t* target_uv;
   int64_t img_y, state_y, img_uv, state_uv;  // elements
   const SharpTabs* tabs;
+  const uint16_t* lut;  // LinearToGamma of a non-sRGB transfer (LUT kernels)
+  int lut_n;
   uint64_t* sums;  // [n_img][4]
   int* prog;       // [n_img][4] row pairs finished per iteration
   int* iters;      // [n_img] iterations the reference runs (-1: a dependency wait timed out)
@@ -80,6 +92,7 @@ __device__ __forceinline__ void load_tabs(SharpTabs& dst, const SharpTabs* src) 
 }
 
 // phase 1: thread = one UV position (i, jUV) of one image
+template <bool LUT>
 __global__ __launch_bounds__(256) void k_sharp_init(SharpArgs a, int n_img) {
   __shared__ SharpTabs t;
   load_tabs(t, a.tabs);
@@ -111,11 +124,11 @@ __global__ __launch_bounds__(256) void k_sharp_init(SharpArgs a, int n_img) {
       const int64_t o = (int64_t)(j + r) * a.w + 2 * i + k;
       by[o] = (uint16_t)gray(c[r][k][0], c[r][k][1], c[r][k][2]);  // storeGray
       for (int ch = 0; ch < 3; ch++) lin[r][k][ch] = to_linear(t.g2l, c[r][k][ch]);
-      ty[o] = (uint16_t)from_linear(t.l2g, (uint32_t)gray(lin[r][k][0], lin[r][k][1], lin[r][k][2]));  // updateW
+      ty[o] = (uint16_t)from_lin<LUT>(t.l2g, a.lut, a.lut_n, (uint32_t)gray(lin[r][k][0], lin[r][k][1], lin[r][k][2]));  // updateW
     }
   int rgbv[3];  // updateChroma (:303-315): scaleDown in linear light
   for (int ch = 0; ch < 3; ch++)
-    rgbv[ch] = from_linear(t.l2g, (lin[0][0][ch] + lin[0][1][ch] + lin[1][0][ch] + lin[1][1][ch] + 2) >> 2);
+    rgbv[ch] = from_lin<LUT>(t.l2g, a.lut, a.lut_n, (lin[0][0][ch] + lin[0][1][ch] + lin[1][0][ch] + lin[1][1][ch] + 2) >> 2);
   const int gv = gray(rgbv[0], rgbv[1], rgbv[2]);
   int16_t* tuv = a.target_uv + img * a.img_uv + (int64_t)ju * a.uv_rs;
   int16_t* buv = a.best_uv + img * a.img_uv + (int64_t)ju * a.uv_rs;
@@ -146,7 +159,7 @@ __device__ __forceinline__ void st_sc1(void* p, uint32_t v) {
 // under the round-robin placement: a speed matter only) and iteration k's
 // block precedes iteration k+1's.  Thread t owns UV columns t + k*1024,
 // k < MAX_COLS: 2 covers widths up to 4096, 8 up to 16384.
-template <int MAX_COLS>
+template <int MAX_COLS, bool LUT>
 __global__ __launch_bounds__(ITER_THREADS) void k_sharp_pipe(SharpArgs a) {
   __shared__ SharpTabs t;
   extern __shared__ int16_t rows[];  // prev / cur / next UV rows: 3 rows of uv_rs
@@ -282,7 +295,7 @@ __global__ __launch_bounds__(ITER_THREADS) void k_sharp_pipe(SharpArgs a) {
       for (int r = 0; r < 2; r++)
         for (int c = 0; c < 2; c++) {
           for (int ch = 0; ch < 3; ch++) lin[r][c][ch] = to_linear(t.g2l, iv[r][c][ch]);
-          yv[r][c] = from_linear(t.l2g, (uint32_t)gray(lin[r][c][0], lin[r][c][1], lin[r][c][2]));
+          yv[r][c] = from_lin<LUT>(t.l2g, a.lut, a.lut_n, (uint32_t)gray(lin[r][c][0], lin[r][c][1], lin[r][c][2]));
         }
       const int byv[2][2] = {{by00, by01}, {by10, by11}};
       int ny[2][2];
@@ -297,7 +310,7 @@ __global__ __launch_bounds__(ITER_THREADS) void k_sharp_pipe(SharpArgs a) {
       // updateChroma -> bestRGBUV, sharpYUVUpdateRGB (:383-388)
       int rgbv[3];
       for (int ch = 0; ch < 3; ch++)
-        rgbv[ch] = from_linear(t.l2g, (lin[0][0][ch] + lin[0][1][ch] + lin[1][0][ch] + lin[1][1][ch] + 2) >> 2);
+        rgbv[ch] = from_lin<LUT>(t.l2g, a.lut, a.lut_n, (lin[0][0][ch] + lin[0][1][ch] + lin[1][0][ch] + lin[1][1][ch] + 2) >> 2);
       const int gv = gray(rgbv[0], rgbv[1], rgbv[2]);
       for (int ch = 0; ch < 3; ch++) {
         const int16_t src = (int16_t)(rgbv[ch] - gv);
@@ -418,10 +431,54 @@ __global__ __launch_bounds__(256) void k_sharp_final(FinalArgs a, int n_img) {
   }
 }
 
+// convertStandard (:68-115): thread = one U/V sample; it also writes the up
+// to four Y pixels of its 2x2 block (rgbToYUVComponent, clipU8)
+struct StdArgs {
+  const uint8_t* rgb;
+  uint8_t *y, *u, *v;
+  int64_t rgb_pitch, y_pitch, uv_pitch;
+  int rgb_stride, y_stride, uv_stride, width, height, uvw, uvh;
+  int m[12];
+};
+__device__ __forceinline__ int yuv_comp(int r, int g, int b, const int* c) {
+  const int64_t l = (int64_t)c[0] * r + (int64_t)c[1] * g + (int64_t)c[2] * b + (int64_t)c[3] + (1 << 15);
+  return min(max((int)(int32_t)(l >> 16), 0), 255);
+}
+__global__ __launch_bounds__(256) void k_sharp_standard(StdArgs a, int n_img) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = (int64_t)a.uvw * a.uvh;
+  if (gid >= per * n_img) return;
+  const int img = (int)(gid / per);
+  const int64_t p = gid - img * per;
+  const int j = (int)(p / a.uvw), i = (int)(p - (int64_t)j * a.uvw);
+  const uint8_t* rgb = a.rgb + img * a.rgb_pitch;
+  int sr = 0, sg = 0, sb = 0, n = 0;
+  for (int dy = 0; dy < 2; dy++) {
+    const int yy = 2 * j + dy;
+    if (yy >= a.height) continue;
+    for (int dx = 0; dx < 2; dx++) {
+      const int xx = 2 * i + dx;
+      if (xx >= a.width) continue;
+      const uint8_t* px = rgb + (int64_t)yy * a.rgb_stride + 3 * xx;
+      sr += px[0];
+      sg += px[1];
+      sb += px[2];
+      n++;
+      a.y[img * a.y_pitch + (int64_t)yy * a.y_stride + xx] = (uint8_t)yuv_comp(px[0], px[1], px[2], a.m);
+    }
+  }
+  const int ar = (sr + n / 2) / n, ag = (sg + n / 2) / n, ab = (sb + n / 2) / n;
+  const int64_t o = img * a.uv_pitch + (int64_t)j * a.uv_stride + i;
+  a.u[o] = (uint8_t)yuv_comp(ar, ag, ab, a.m + 4);
+  a.v[o] = (uint8_t)yuv_comp(ar, ag, ab, a.m + 8);
+}
+
 }  // namespace
 
 namespace wg {
-const void* sharpyuv_tables_device();  // sharpyuv_host.cpp: g2l[1026] then l2g[514] (uint32)
+// sharpyuv_host.cpp: g2l[1026] then l2g[514] (uint32), then for tf != sRGB
+// the direct LinearToGamma table (uint16, *lut_n entries)
+const void* sharpyuv_tables_device(int tf, int* lut_n);
 }
 
 namespace {
@@ -448,19 +505,45 @@ extern "C" size_t wg_sharpyuv_work_bytes(int32_t width, int32_t height, int32_t 
   return n_images * L.bytes_img + (size_t)n_images * (4 * 8 + 4 * 4 + 4) + 16;
 }
 
-extern "C" int wg_sharpyuv_convert(const uint8_t* rgb, int32_t width, int32_t height, int32_t rgb_stride,
-                                   int64_t rgb_pitch, const int32_t* matrix_host, int32_t n_images, uint8_t* y,
-                                   int32_t y_stride, int64_t y_pitch, uint8_t* u, uint8_t* v, int32_t uv_stride,
-                                   int64_t uv_pitch, void* work, void* stream) {
-  WG_REQUIRE(rgb && matrix_host && y && u && v && work && width > 0 && height > 0 && n_images > 0);
+extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t height, int32_t rgb_stride,
+                                      int64_t rgb_pitch, const int32_t* matrix_host, int32_t transfer,
+                                      int32_t sharp_enabled, int32_t n_images, uint8_t* y, int32_t y_stride,
+                                      int64_t y_pitch, uint8_t* u, uint8_t* v, int32_t uv_stride, int64_t uv_pitch,
+                                      void* work, void* stream) {
+  WG_REQUIRE(rgb && matrix_host && y && u && v && width > 0 && height > 0 && n_images > 0);
   WG_REQUIRE(rgb_stride >= 3 * width && y_stride >= width && uv_stride >= (width + 1) / 2);
-  WG_REQUIRE((reinterpret_cast<uintptr_t>(work) & 15) == 0);
+  hipStream_t s = wg::as_stream(stream);
+  if (!sharp_enabled) {  // convertStandard (sharpyuv.go:68-115)
+    StdArgs sa;
+    sa.rgb = rgb;
+    sa.y = y;
+    sa.u = u;
+    sa.v = v;
+    sa.rgb_pitch = rgb_pitch;
+    sa.y_pitch = y_pitch;
+    sa.uv_pitch = uv_pitch;
+    sa.rgb_stride = rgb_stride;
+    sa.y_stride = y_stride;
+    sa.uv_stride = uv_stride;
+    sa.width = width;
+    sa.height = height;
+    sa.uvw = (width + 1) >> 1;
+    sa.uvh = (height + 1) >> 1;
+    for (int k = 0; k < 12; k++) sa.m[k] = matrix_host[k];
+    const int64_t cells = (int64_t)sa.uvw * sa.uvh * n_images;
+    hipLaunchKernelGGL(k_sharp_standard, dim3(wg::blocks_for(cells, 256)), dim3(256), 0, s, sa, n_images);
+    return wg::check_launch("k_sharp_standard");
+  }
+  WG_REQUIRE(work && (reinterpret_cast<uintptr_t>(work) & 15) == 0);
+  // H.273 codes the reference implements (gamma.go:11-28); others give 0 there too
+  WG_REQUIRE(transfer >= 0 && transfer <= 18);
   const int w = (width + 1) & ~1, h = (height + 1) & ~1;
   const int uvw = w / 2, uvh = h / 2;
   WG_REQUIRE(uvw <= 8 * ITER_THREADS);
-  const void* tabs = wg::sharpyuv_tables_device();
+  int lut_n = 0;
+  const void* tabs = wg::sharpyuv_tables_device(transfer, &lut_n);
   if (!tabs) return WG_EHIP;
-  hipStream_t s = wg::as_stream(stream);
+  const bool lut = transfer != 13;
   const SharpLayout L = sharp_layout(width, height);
   uint8_t* base = static_cast<uint8_t*>(work);
   SharpArgs a;
@@ -485,6 +568,8 @@ extern "C" int wg_sharpyuv_convert(const uint8_t* rgb, int32_t width, int32_t he
   a.state_y = (int64_t)L.y_elems;
   a.state_uv = (int64_t)L.uv_elems;
   a.tabs = static_cast<const SharpTabs*>(tabs);
+  a.lut = reinterpret_cast<const uint16_t*>(static_cast<const uint8_t*>(tabs) + sizeof(SharpTabs));
+  a.lut_n = lut_n;
   uint8_t* tail = base + n_images * L.bytes_img;
   a.sums = reinterpret_cast<uint64_t*>(tail);
   a.prog = reinterpret_cast<int*>(tail + (size_t)n_images * 32);
@@ -493,7 +578,10 @@ extern "C" int wg_sharpyuv_convert(const uint8_t* rgb, int32_t width, int32_t he
   if (hipMemsetAsync(tail, 0, (size_t)n_images * (32 + 16 + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(sharpyuv)");
   const int64_t cells = (int64_t)uvw * uvh * n_images;
-  hipLaunchKernelGGL(k_sharp_init, dim3(wg::blocks_for(cells, 256)), dim3(256), 0, s, a, n_images);
+  if (lut)
+    hipLaunchKernelGGL(k_sharp_init<true>, dim3(wg::blocks_for(cells, 256)), dim3(256), 0, s, a, n_images);
+  else
+    hipLaunchKernelGGL(k_sharp_init<false>, dim3(wg::blocks_for(cells, 256)), dim3(256), 0, s, a, n_images);
   int rc = wg::check_launch("k_sharp_init");
   if (rc != WG_OK) return rc;
   // the pipeline's waits need every image's four workgroups resident at
@@ -502,8 +590,8 @@ extern "C" int wg_sharpyuv_convert(const uint8_t* rgb, int32_t width, int32_t he
   const bool wide = uvw > 2 * ITER_THREADS;
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide ? k_sharp_pipe<8> : k_sharp_pipe<2>, ITER_THREADS,
-                                                   lds_rows) != hipSuccess || per_cu <= 0)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide ? k_sharp_pipe<8, false> : k_sharp_pipe<2, false>,
+                                                   ITER_THREADS, lds_rows) != hipSuccess || per_cu <= 0)
     return wg::check_launch("sharpyuv occupancy");
   const int chunk = std::max(8, (per_cu * cus / 32) * 8);  // images per launch (groups of eight = 32 blocks)
   for (int i0 = 0; i0 < n_images; i0 += chunk) {
@@ -517,10 +605,14 @@ extern "C" int wg_sharpyuv_convert(const uint8_t* rgb, int32_t width, int32_t he
     c.prog += 4 * i0;
     c.iters += i0;
     const unsigned grid = (unsigned)((c.n_img + 7) / 8 * 32);
-    if (wide)
-      hipLaunchKernelGGL(k_sharp_pipe<8>, dim3(grid), dim3(ITER_THREADS), lds_rows, s, c);
+    if (wide && lut)
+      hipLaunchKernelGGL((k_sharp_pipe<8, true>), dim3(grid), dim3(ITER_THREADS), lds_rows, s, c);
+    else if (wide)
+      hipLaunchKernelGGL((k_sharp_pipe<8, false>), dim3(grid), dim3(ITER_THREADS), lds_rows, s, c);
+    else if (lut)
+      hipLaunchKernelGGL((k_sharp_pipe<2, true>), dim3(grid), dim3(ITER_THREADS), lds_rows, s, c);
     else
-      hipLaunchKernelGGL(k_sharp_pipe<2>, dim3(grid), dim3(ITER_THREADS), lds_rows, s, c);
+      hipLaunchKernelGGL((k_sharp_pipe<2, false>), dim3(grid), dim3(ITER_THREADS), lds_rows, s, c);
     rc = wg::check_launch("k_sharp_pipe");
     if (rc != WG_OK) return rc;
   }
@@ -550,6 +642,14 @@ extern "C" int wg_sharpyuv_convert(const uint8_t* rgb, int32_t width, int32_t he
   const int64_t px = (int64_t)width * height * n_images;
   hipLaunchKernelGGL(k_sharp_final, dim3(wg::blocks_for(px, 256)), dim3(256), 0, s, f, n_images);
   return wg::check_launch("k_sharp_final");
+}
+
+extern "C" int wg_sharpyuv_convert(const uint8_t* rgb, int32_t width, int32_t height, int32_t rgb_stride,
+                                   int64_t rgb_pitch, const int32_t* matrix_host, int32_t n_images, uint8_t* y,
+                                   int32_t y_stride, int64_t y_pitch, uint8_t* u, uint8_t* v, int32_t uv_stride,
+                                   int64_t uv_pitch, void* work, void* stream) {
+  return wg_sharpyuv_convert_ex(rgb, width, height, rgb_stride, rgb_pitch, matrix_host, 13, 1, n_images, y, y_stride,
+                                y_pitch, u, v, uv_stride, uv_pitch, work, stream);
 }
 
 // Iterations each image ran (the reference's count, 2..4), or -1 where a

@@ -171,10 +171,11 @@ WEBP_MATRIX = np.array([16839, 33059, 6420, 16 << 16, -9719, -19081, 28800, 128 
                         28800, -24116, -4684, 128 << 16], np.int32)  # sharpyuv/csp.go:66-70
 
 
-def sharpyuv_convert(rgb, matrix=WEBP_MATRIX, out=None, work=None, iterations=False):
-    """sharpyuv.Convert (SharpEnabled, sRGB): (n, h, w, 3) uint8 RGB -> Y (n, h, w),
-    U, V (n, (h+1)//2, (w+1)//2).  iterations=True also returns the refinement
-    iterations each image ran (numpy int32; synchronises the stream)."""
+def sharpyuv_convert(rgb, matrix=WEBP_MATRIX, out=None, work=None, iterations=False, transfer=13, sharp=True):
+    """sharpyuv.Convert: (n, h, w, 3) uint8 RGB -> Y (n, h, w), U, V (n, (h+1)//2,
+    (w+1)//2).  transfer: H.273 code (13 = sRGB, the default); sharp=False is
+    convertStandard.  iterations=True also returns the refinement iterations
+    each image ran (numpy int32; synchronises the stream)."""
     assert rgb.is_cuda and rgb.dtype == torch.uint8 and rgb.dim() == 4 and rgb.is_contiguous()
     n, h, w, _ = rgb.shape
     cw, ch = (w + 1) // 2, (h + 1) // 2
@@ -187,8 +188,8 @@ def sharpyuv_convert(rgb, matrix=WEBP_MATRIX, out=None, work=None, iterations=Fa
     if work is None:
         work = torch.empty(lib.wg_sharpyuv_work_bytes(w, h, n), dtype=torch.uint8, device=rgb.device)
     m = np.ascontiguousarray(matrix, np.int32)
-    call("wg_sharpyuv_convert", rgb.data_ptr(), w, h, 3 * w, 3 * w * h, m.ctypes.data, n, Y.data_ptr(), w, h * w,
-         U.data_ptr(), V.data_ptr(), cw, cw * ch, work.data_ptr(), _stream())
+    call("wg_sharpyuv_convert_ex", rgb.data_ptr(), w, h, 3 * w, 3 * w * h, m.ctypes.data, int(transfer), int(bool(sharp)),
+         n, Y.data_ptr(), w, h * w, U.data_ptr(), V.data_ptr(), cw, cw * ch, work.data_ptr(), _stream())
     if iterations:
         its = np.zeros(n, np.int32)
         call("wg_sharpyuv_iterations", work.data_ptr(), w, h, n, its.ctypes.data, _stream())
