@@ -24,8 +24,9 @@ planes = [O.import_rgba(gens[k](), has_alpha=False) for k in kinds]
 Yt = torch.from_numpy(np.stack([planes[i % len(planes)][0] for i in range(B)])).cuda()
 Ut = torch.from_numpy(np.stack([planes[i % len(planes)][1] for i in range(B)])).cuda()
 Vt = torch.from_numpy(np.stack([planes[i % len(planes)][2] for i in range(B)])).cuda()
-segs = np.stack([frames.setup_segment(q) for q in (20, 24, 28, 32)])
-seg_ids = torch.from_numpy((np.arange(B * MBW * MBH) % 4).astype(np.uint8)).cuda()
+# the reference's q75 defaults: alphas -> segment analysis on the device (as bench.py)
+alphas, uv_sum = frames.analysis_alphas(Yt, Ut, Vt, W, H)
+seg_ids, segs, _ = frames.segment_analysis(frames.encoder_config(), alphas, uv_sum, MBW, MBH)
 out, rec = frames.encode_mbs(Yt, Ut, Vt, W, H, seg_ids, segs, O.default_proba())
 torch.cuda.synchronize()
 if STAMPED:

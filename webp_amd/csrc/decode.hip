@@ -470,42 +470,54 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
 
         STAMP(6);
         lane = opaque_lane() & 63;
-        // ---- stores (sc1 where another workgroup reads them) ----
-        // Y rows 13..15 / U, V rows 5..7 are left to the row below when it is in this band
+        // ---- stores ----
+        // Only what another workgroup reads while this launch runs is written
+        // through (sc1): the bottom rows 12..15 (Y) / 4..7 (U, V) of a band's
+        // last row, which the next band's first row loads as its filter
+        // context.  Every other frame byte is read by nobody before the launch
+        // ends and goes out as a plain (write-back) store, so L2 merges a row's
+        // 16-B pieces into whole lines.  Y rows 13..15 / U, V rows 5..7 are
+        // left to the row below when it is in this band.
         if (lane < 32) {  // Y rows, 2 x 8 B
           const int j = lane >> 1, half = lane & 1;
-          if (!to_lds || j < 13)
-            st_sc1_64(Yp + (int64_t)(16 * mby + j) * ys + 16 * mbx + 8 * half,
-                      lds64(fy + (j + 4) * FY_STRIDE + FY_X0 + 8 * half));
+          uint8_t* dst = Yp + (int64_t)(16 * mby + j) * ys + 16 * mbx + 8 * half;
+          const uint64_t w = lds64(fy + (j + 4) * FY_STRIDE + FY_X0 + 8 * half);
+          if (!to_lds && j >= 12) st_sc1_64(dst, w);
+          else if (!to_lds || j < 13) *reinterpret_cast<uint64_t*>(dst) = w;
         } else if (lane < 48) {  // U, V rows
           const int pl = lane >= 40, j = (lane - 32) & 7;
-          if (!to_lds || j < 5)
-            st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx,
-                      lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0));
+          uint8_t* dst = (pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx;
+          const uint64_t w = lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0);
+          if (!to_lds && j >= 4) st_sc1_64(dst, w);
+          else if (!to_lds || j < 5) *reinterpret_cast<uint64_t*>(dst) = w;
         }
         if (do_filter && mbx > 0) {  // the 3 columns of the left MB modified by our left-edge filter
           if (lane >= 48) {
-            if (!to_lds || lane - 48 < 13)
-              st_sc1_32(Yp + (int64_t)(16 * mby + lane - 48) * ys + 16 * mbx - 4,
-                        lds32(fy + (lane - 48 + 4) * FY_STRIDE + FY_X0 - 4));
+            const int j = lane - 48;
+            uint8_t* dst = Yp + (int64_t)(16 * mby + j) * ys + 16 * mbx - 4;
+            const uint32_t w = lds32(fy + (j + 4) * FY_STRIDE + FY_X0 - 4);
+            if (!to_lds && j >= 12) st_sc1_32(dst, w);
+            else if (!to_lds || j < 13) *reinterpret_cast<uint32_t*>(dst) = w;
           } else if (!luma_only && lane < 16) {
             const int pl = lane >= 8, j = lane & 7;
-            if (!to_lds || j < 5)
-              st_sc1_32((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx - 4,
-                        lds32((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 - 4));
+            uint8_t* dst = (pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx - 4;
+            const uint32_t w = lds32((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 - 4);
+            if (!to_lds && j >= 4) st_sc1_32(dst, w);
+            else if (!to_lds || j < 5) *reinterpret_cast<uint32_t*>(dst) = w;
           }
         }
         if (mby > 0 && (from_lds || do_filter)) {
           // the 3 rows of the MB above modified by our top-edge filter; always,
-          // when the row above (in this band) left them to us
+          // when the row above (in this band) left them to us.  Nobody reads
+          // them again in this launch: plain stores.
           if (lane >= 16 && lane < 22) {
             const int k = lane - 16, rr = 1 + (k >> 1), half = k & 1;
-            st_sc1_64(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half,
-                      lds64(fy + rr * FY_STRIDE + FY_X0 + 8 * half));
+            *reinterpret_cast<uint64_t*>(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half) =
+                lds64(fy + rr * FY_STRIDE + FY_X0 + 8 * half);
           } else if ((from_lds || !luma_only) && lane >= 22 && lane < 28) {
             const int k = lane - 22, pl = k >= 3, rr = 1 + (k % 3);
-            st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx,
-                      lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0));
+            *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx) =
+                lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0);
           }
         }
         if (to_lds) {

@@ -38,7 +38,7 @@ constexpr int YOFF = BPS * 1 + 8;
 constexpr int UOFF = YOFF + BPS * 16 + BPS;
 constexpr int VOFF = UOFF + 16;
 constexpr int YUV = BPS * 17 + BPS * 9;
-constexpr int REC = 48;  // per MB column hand-off record
+constexpr int REC = 64;  // per MB column hand-off record (48 B used), one 64-B memory granule
 
 struct SQuant {  // SegmentQuant (encode.go:311-323); layout = wg_squant
   int32_t quant, iquant, bias, zthresh;
@@ -153,6 +153,8 @@ struct Shared {
   Segment seg[4];  // the quantisers of the row's image (per-image segment tables)
   uint8_t yin[YUV], yout[YUV], yout2[YUV];
   alignas(16) int16_t coeffs[400];
+  uint8_t mbtail[64];  // wg_mb_enc bytes 800..863, staged so the record leaves in one 16-B-per-lane store
+  alignas(16) uint32_t handoff[12];  // the 48-B hand-off record, staged for three 16-B write-through stores
   uint8_t modes4[16];
   uint8_t nzy[16], nzuv[8];
   int dcin[4][16];
@@ -641,6 +643,12 @@ __device__ __forceinline__ uint32_t ld_sc1_32(const uint8_t* p) {
 }
 __device__ __forceinline__ void st_sc1_32(uint8_t* p, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one 16-B write-through (sc1) store: a hand-off record leaves as whole
+// 16-B pieces of one 64-B granule instead of eleven 4-B partial writes
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_sc1_128(uint8_t* p, u32x4_t v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
 
 struct EncArgs {
@@ -1457,38 +1465,54 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
 
       // ================= outputs, export, contexts (exportParallel :1412-1495) =================
       MbEnc* o = a.out + mbi;
-      {
-        uint4* dst = reinterpret_cast<uint4*>(o->coeffs);
-        const uint4* srcv = reinterpret_cast<const uint4*>(s.coeffs);
-        if (lane < 50) dst[lane] = srcv[lane];
+      {  // the record's tail (bytes 800..863) staged next to the levels in LDS
+        MbEnc* so = reinterpret_cast<MbEnc*>(s.coeffs);
         if (lane < 16) {
-          o->modes[lane] = is_i4 ? s.modes4[lane] : 0;
-          o->nz_y[lane] = s.nzy[lane];
+          so->modes[lane] = is_i4 ? s.modes4[lane] : 0;
+          so->nz_y[lane] = s.nzy[lane];
         } else if (lane < 24) {
-          o->nz_uv[lane - 16] = s.nzuv[lane - 16];
+          so->nz_uv[lane - 16] = s.nzuv[lane - 16];
         } else if (lane == 24) {
-          o->non_zero_y = nzy_mask;
-          o->non_zero_uv = nzuv_mask;
-          o->mb_type = is_i4 ? 1 : 0;
-          o->i16_mode = is_i4 ? 0 : (uint8_t)best16;
-          o->uv_mode = (uint8_t)best_uv;
-          o->nz_dc = (uint8_t)nz_dc;
-          o->skip = (nzy_mask == 0 && nzuv_mask == 0) ? 1 : 0;
-          o->segment = (uint8_t)segid;
-          o->pad0 = o->pad1 = 0;
-          o->score = is_i4 ? s4 : s16;
+          so->non_zero_y = nzy_mask;
+          so->non_zero_uv = nzuv_mask;
+          so->mb_type = is_i4 ? 1 : 0;
+          so->i16_mode = is_i4 ? 0 : (uint8_t)best16;
+          so->uv_mode = (uint8_t)best_uv;
+          so->nz_dc = (uint8_t)nz_dc;
+          so->skip = (nzy_mask == 0 && nzuv_mask == 0) ? 1 : 0;
+          so->segment = (uint8_t)segid;
+          so->pad0 = so->pad1 = 0;
+          so->score = is_i4 ? s4 : s16;
         }
+        lds_sync();
+        // the whole 864-B record: 54 lanes x 16 B, one store instruction
+        uint4* dst = reinterpret_cast<uint4*>(o);
+        const uint4* srcv = reinterpret_cast<const uint4*>(s.coeffs);
+#ifndef WG_EXP_NO_MBENC
+        if (lane < 54) dst[lane] = srcv[lane];
+#endif
       }
       {
         const int x = 16 * mbx, y = 16 * mby;
         const int wy = min(a.width - x, 16), hy = min(a.height - y, 16);
-        if (lane < hy)
-          for (int c = 0; c < wy; c++) RY[(int64_t)(y + lane) * ys + x + c] = s.yout[YOFF + lane * BPS + c];
-        if (lane >= 16 && lane < 32) {
+#ifndef WG_EXP_NO_RECON
+        if (lane < hy) {
+          const uint8_t* srow = s.yout + YOFF + lane * BPS;  // 8-B aligned in LDS
+          uint8_t* drow = RY + (int64_t)(y + lane) * ys + x;
+          if (wy == 16) {  // one 16-B store per row
+            const uint2 lo = *reinterpret_cast<const uint2*>(srow), hi = *reinterpret_cast<const uint2*>(srow + 8);
+            *reinterpret_cast<uint4*>(drow) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          } else {
+            for (int c = 0; c < wy; c++) drow[c] = srow[c];
+          }
+        }
+        if (lane >= 16 && lane < 32) {  // U / V rows: one 8-B store each
           const int k = lane - 16, pl = k >> 3, j = k & 7;
           uint8_t* P = pl ? RV : RU;
-          for (int c = 0; c < 8; c++) P[(int64_t)(8 * mby + j) * uvs + 8 * mbx + c] = s.yout[(pl ? VOFF : UOFF) + j * BPS + c];
+          *reinterpret_cast<uint2*>(P + (int64_t)(8 * mby + j) * uvs + 8 * mbx) =
+              *reinterpret_cast<const uint2*>(s.yout + (pl ? VOFF : UOFF) + j * BPS);
         }
+#endif
       }
       // new top-left: the row above's bottom-right of this column (before we overwrite it)
       tl_y = s.yout[YOFF - BPS + 15];
@@ -1542,18 +1566,26 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
         left_modes = 0;
       }
       left_nz = out_l;
-      // hand-off record for the row below (sc1 stores), then publish
+      // hand-off record for the row below, then publish: staged in LDS and
+      // written as three 16-B write-through stores
       if (mby < mbh - 1) {
-        uint8_t* rec = top + mbx * REC;
         if (lane < 8) {
           const int so = lane < 4 ? YOFF + 15 * BPS + 4 * lane : (lane < 6 ? UOFF + 7 * BPS + 4 * (lane - 4) : VOFF + 7 * BPS + 4 * (lane - 6));
-          st_sc1_32(rec + 4 * lane, *reinterpret_cast<const uint32_t*>(s.yout + so));
+          s.handoff[lane] = *reinterpret_cast<const uint32_t*>(s.yout + so);
         } else if (lane == 8) {
-          st_sc1_32(rec + 32, out_t);
+          s.handoff[8] = out_t;
         } else if (lane == 9) {
-          st_sc1_32(rec + 36, new_top_modes);
+          s.handoff[9] = new_top_modes;
         } else if (lane == 10) {
-          st_sc1_32(rec + 40, (uint32_t)new_top_dc);
+          s.handoff[10] = (uint32_t)new_top_dc;
+        } else if (lane == 11) {
+          s.handoff[11] = 0;
+        }
+        lds_sync();
+        if (lane < 3) {
+          const uint4 w = reinterpret_cast<const uint4*>(s.handoff)[lane];
+          u32x4_t v = {w.x, w.y, w.z, w.w};
+          st_sc1_128(top + mbx * REC + 16 * lane, v);
         }
       }
       // rotate the left context: column 15 / 7 becomes column -1
