@@ -583,7 +583,7 @@ int g_rows_per_cu = 0;  // resident workgroups per CU (occupancy)
 
 #ifdef WG_STAMPS
 extern "C" int wg_debug_phases(unsigned long long* host, int n) {
-  hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n);
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n);
   unsigned long long z[16] = {0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) == hipSuccess ? 0 : -2;
 }

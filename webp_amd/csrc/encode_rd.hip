@@ -89,11 +89,13 @@ __device__ __forceinline__ int band_of(int n) { return (int)((pack_band() >> (3 
 // One trellis position, prepared by a lane of its own (trellis_prep) and
 // consumed by the lane quad running the DP (trellis_dp4).
 struct alignas(8) TRec {
-  // x[role][pc]: the transition from predecessor context pc, as a key
-  // (score x16 + order idx) to add to that predecessor's state:
-  //   role 0  level 0 (end context 0): zero-token cost * lam16 + idx pc
-  //   role 1  level L0: (nz token + level cost) * lam16 + distortion + idx 2pc
-  //   role 2  level L0 + 1: likewise, idx 2pc + 1
+  // x[row][pc]: the transition from predecessor context pc, as a key
+  // (score x16 + order idx) to add to that predecessor's state, with the
+  // rows routed by the end context they reach:
+  //   R0  level 0 (end context 0): zero-token cost * lam16 + idx pc
+  //   R1  level 1 or L0 >= 2: (nz token + level cost) * lam16 + distortion,
+  //       idx 2pc for level L0, 2pc + 1 for level L0 + 1 (= 1 when L0 = 0)
+  //   R2  level L0 + 1 >= 2 (idx 2pc + 1), all BIG when L0 = 0
   // + BIG when that level is not a candidate
   int64_t x[3][3];
 };
@@ -288,11 +290,17 @@ __device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, c
   const int64_t A1 = (int64_t)t.lfixed[min(L0 + 1, 2047)] * lam16 + (int64_t)w4096 * (e1 * e1 - c0 * c0) + (has1 ? 0 : BIG);
   const TokRow& tr = t.tok[CTX_TYPE * 8 + band];
   const uint64_t v0 = t.vcost[CTX_TYPE * 8 + band][min(L0, 67)], v1 = t.vcost[CTX_TYPE * 8 + band][min(L0 + 1, 67)];
+  // rows by end context: L0 = 0 sends level 1 (= L0 + 1) to context 1 and
+  // nothing to context 2; otherwise L0 -> R1, L0 + 1 -> R2 (trellis_dp4
+  // merges R1 into context 2 when L0 >= 2)
+  const bool z = L0 == 0;
 #pragma unroll
   for (int pc = 0; pc < 3; pc++) {
+    const int64_t r1 = (int64_t)(tr.nz[pc] + vc_of(v0, pc)) * lam16 + A0 + 2 * pc;
+    const int64_t r2 = (int64_t)(tr.nz[pc] + vc_of(v1, pc)) * lam16 + A1 + 2 * pc + 1;
     out.x[0][pc] = (int64_t)tr.zero[pc] * lam16 + pc;
-    out.x[1][pc] = (int64_t)(tr.nz[pc] + vc_of(v0, pc)) * lam16 + A0 + 2 * pc;
-    out.x[2][pc] = (int64_t)(tr.nz[pc] + vc_of(v1, pc)) * lam16 + A1 + 2 * pc + 1;
+    out.x[1][pc] = z ? r2 : r1;
+    out.x[2][pc] = z ? BIG : r2;
   }
   l0s = L0 << 3 | (co_z < 0 ? 4 : 0) | min(L0, 2);
   return L0raw > 0;
@@ -317,111 +325,109 @@ __device__ __forceinline__ int quad_bcast32(int v) {
   return __builtin_amdgcn_mov_dpp(v, J | J << 2 | J << 4 | J << 6, 0xf, 0xf, false);
 }
 
-// The trellis DP on a quad of lanes.  Lane r (0..2) of the quad owns one
-// transition role (level 0 / L0 / L0 + 1, see TRec): it adds its row of the
-// position record to the three predecessor states and takes the min; the
-// three minima are exchanged by DPP broadcasts and routed to the end
-// contexts (min(level, 2)) in every lane, so all lanes carry the same
-// states.  Lane 3 shadows lane 2.  Keys and order are those of the
-// sequential DP; the quad's lane 0 walks the path back and writes the
-// levels (raster) to q and the zigzag nz count to *nz.
+// The trellis DP on a quad of lanes.  trellis_prep routes the transitions
+// by the end context they reach (TRec rows R0 / R1 / R2), so lane k of the
+// quad (e = min(k, 2); lane 3 shadows lane 2) takes the minimum of the three
+// predecessor states plus its row: keys are score x16 + the candidate's index
+// in the reference's update order, so the first strict minimum of
+// encode_trellis.go:215-245 is a plain min and the keys of one end context
+// never tie.  The three minima reach every lane by DPP broadcasts; where L0 >= 2
+// both non-zero levels end in context 2, which then takes min(R1, R2) and
+// context 1 is empty.
+//
+// Instead of a path table walked back from the best terminal, every state
+// carries its own history: 2 bits per position (0 = level 0, 1 = L0,
+// 2 = L0 + 1), copied from the winning predecessor.  The best terminal
+// (EOB after position n from context 1 or 2, :257-270) keeps the history it
+// ended, and the levels then follow position by position with no serial
+// chain: the quad's lane r writes positions 4r..4r+3 (raster) to q, and lane
+// 0 writes the zigzag nz count to *nz.
 template <int FIRST, int CTX_TYPE>
 __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int* l0s, int init_ctx, int lam16,
                                             int k, int16_t* q, int* nz) {
   constexpr int64_t BIG = 1ll << 59, VALID = 1ll << 58;
   init_ctx = min(init_ctx, 2);
-  const int role = min(k, 2);
+  const int e = min(k, 2);
+  const int psh = e == 0 ? 0 : 1;  // index -> predecessor context shift; also the level-code offset
   int64_t ps0 = init_ctx == 0 ? 0 : BIG, ps1 = init_ctx == 1 ? 0 : BIG, ps2 = init_ctx == 2 ? 0 : BIG;
-  uint32_t path[8];
+  uint32_t h0 = 0, h1 = 0, h2 = 0;  // the states' histories
   const TokRow& t_init = t.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
+  // lanes 0, 1 follow the terminals of context 1 (lane 0's copy is unused), lanes 2, 3 context 2
+  const int tctx = e == 2 ? 2 : 1;
   int64_t best_terminal = (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16;
-  int best = -1;  // n << 2 | end context
-  const int64_t* mine = &rec[0].x[role][0];
-  constexpr int STRIDE = sizeof(TRec) / sizeof(int64_t);
-  // Everything position n reads from LDS (its three transitions, its class,
-  // the EOB costs of band n+1) is loaded during position n-1 and pinned by
-  // the asm below, so the wait for it lands one full position after the
-  // load; loading and using within one position put two LDS round trips on
-  // the DP's serial chain.
+  int best_n = -1;
+  uint32_t best_h = 0;
+  const int64_t* mine = &rec[0].x[e][0];
+  const uint16_t* eobp = &t.tok[CTX_TYPE * 8].eob[0] + tctx;
+  constexpr int STRIDE = sizeof(TRec) / sizeof(int64_t), TSTR = sizeof(TokRow) / 2;
+  // Position n's row, class and EOB cost are loaded during position n - 1
+  // and pinned by the asm below, so no LDS round trip sits on the chain.
   int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
-  // raw loads only: any use right after the load (even "& 3") makes the
-  // compiler wait for it there
   int cls_raw = l0s[FIRST];
-  uint2 eob_raw = *reinterpret_cast<const uint2*>(t.tok[CTX_TYPE * 8 + kBand[FIRST + 1]].eob);  // eob[0..3]
+  uint32_t eob_raw = FIRST < 15 ? eobp[kBand[FIRST + 1] * TSTR] : 0;
 #pragma unroll
-  for (int n = 0; n < 16; n++) {
-    if (n < FIRST) {
-      if (!(n & 1)) path[n >> 1] = 0;
-      continue;
-    }
-    // issue the next position's loads first; the asm then keeps this
-    // position's compute (everything hangs off ps*) from floating above them
+  for (int n = FIRST; n < 16; n++) {
     int64_t nx0 = 0, nx1 = 0, nx2 = 0;
     int ncls = 0;
-    uint2 neob = make_uint2(0, 0);
+    uint32_t neob = 0;
     if (n < 15) {
       nx0 = mine[(n + 1) * STRIDE];
       nx1 = mine[(n + 1) * STRIDE + 1];
       nx2 = mine[(n + 1) * STRIDE + 2];
       ncls = l0s[n + 1];
-      if (n + 1 < 15) neob = *reinterpret_cast<const uint2*>(t.tok[CTX_TYPE * 8 + kBand[n + 2]].eob);
+      if (n + 1 < 15) neob = eobp[kBand[n + 2] * TSTR];
     }
     asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
     const int64_t c0 = ps0 + x0, c1 = ps1 + x1, c2 = ps2 + x2;
-    const int cls_n = cls_raw & 3;
-    const uint32_t e1_n = eob_raw.x >> 16, e2_n = eob_raw.y & 0xffff;
+    const bool two = (cls_raw & 2) != 0;  // class 2: L0 >= 2
+    const uint32_t eob_n = eob_raw;
     x0 = nx0;
     x1 = nx1;
     x2 = nx2;
     cls_raw = ncls;
     eob_raw = neob;
-    int64_t m = c1 < c0 ? c1 : c0;
-    m = c2 < m ? c2 : m;
-    const int64_t kz = quad_bcast<0>(m), ka = quad_bcast<1>(m), kb = quad_bcast<2>(m);
-    const int64_t kab = kb < ka ? kb : ka;
-    const int64_t k1 = cls_n == 0 ? kb : (cls_n == 1 ? ka : BIG);
-    const int64_t k2 = cls_n == 0 ? BIG : (cls_n == 1 ? kb : kab);
-    const uint32_t pr = ((uint32_t)kz & 15) | (((uint32_t)k1 & 15) << 4) | (((uint32_t)k2 & 15) << 8);
-    if (n & 1)
-      path[n >> 1] |= pr << 16;
-    else
-      path[n >> 1] = pr;
-    ps0 = kz & ~15ll;
-    ps1 = k1 & ~15ll;
-    ps2 = k2 & ~15ll;
-    // terminal (EOB after this position) from end contexts 1 and 2
-    const int64_t eob1 = ps1 + (n < 15 ? (int64_t)e1_n * lam16 : 0);
-    const bool w1 = ps1 < VALID && eob1 < best_terminal;
-    best_terminal = w1 ? eob1 : best_terminal;
-    best = w1 ? (n << 2 | 1) : best;
-    const int64_t eob2 = ps2 + (n < 15 ? (int64_t)e2_n * lam16 : 0);
-    const bool w2 = ps2 < VALID && eob2 < best_terminal;
-    best_terminal = w2 ? eob2 : best_terminal;
-    best = w2 ? (n << 2 | 2) : best;
+    const int64_t m01 = c1 < c0 ? c1 : c0;
+    const int64_t m = c2 < m01 ? c2 : m01;
+    const uint32_t idx = (uint32_t)m & 15, pc = idx >> psh;
+    const uint32_t code = (idx & (uint32_t)psh) + (uint32_t)psh;  // R0: 0; R1 / R2: 1 (L0) or 2 (L0 + 1)
+    const uint32_t hm = (pc == 0 ? h0 : (pc == 1 ? h1 : h2)) | code << (2 * n);
+    const int64_t M0 = quad_bcast<0>(m), M1 = quad_bcast<1>(m), M2 = quad_bcast<2>(m);
+    const uint32_t H0 = quad_bcast32<0>(hm), H1 = quad_bcast32<1>(hm), H2 = quad_bcast32<2>(hm);
+    const bool lt = M1 < M2;
+    ps0 = M0 & ~15ll;
+    ps1 = two ? BIG : (M1 & ~15ll);
+    ps2 = (two && lt ? M1 : M2) & ~15ll;
+    h0 = H0;
+    h1 = H1;
+    h2 = two && lt ? H1 : H2;
+    // terminal (EOB after this position) of context tctx
+    const int64_t tps = tctx == 2 ? ps2 : ps1;
+    const int64_t eobs = tps + (n < 15 ? (int64_t)eob_n * lam16 : 0);
+    const bool w = tps < VALID && eobs < best_terminal;
+    best_terminal = w ? eobs : best_terminal;
+    best_n = w ? n : best_n;
+    best_h = w ? (tctx == 2 ? h2 : h1) : best_h;
   }
-  if (k != 0) return;
-  const int best_n = best >> 2;  // -1 when no terminal beat the all-zero block
-  int ctx = best & 3, last = 0;
-  int16_t lv_out[16];
+  // the first strict minimum over (position, context 1 then 2), in every lane
+  const int64_t bt1 = quad_bcast<1>(best_terminal), bt2 = quad_bcast<2>(best_terminal);
+  const int bn1 = quad_bcast32<1>(best_n), bn2 = quad_bcast32<2>(best_n);
+  const uint32_t bh1 = quad_bcast32<1>(best_h), bh2 = quad_bcast32<2>(best_h);
+  const bool second = bt2 < bt1 || (bt2 == bt1 && bn2 < bn1);
+  const uint32_t hist = second ? bh2 : bh1;  // 0 when no terminal beat the all-zero block
+  // lane r: positions 4r .. 4r + 3
+  const int r = k;
 #pragma unroll
-  for (int n = 15; n >= 0; n--) {
-    const int zig = kZig[n];
-    if (n < FIRST) {
-      lv_out[zig] = 0;
-      continue;
-    }
-    const bool act = n <= best_n;
-    const int idx = (int)(((path[n >> 1] >> (16 * (n & 1))) >> (4 * ctx)) & 15);
+  for (int j = 0; j < 4; j++) {
+    const int n = 4 * r + j;
+    const int code = (int)((hist >> (2 * n)) & 3);
     const int ls = l0s[n];
-    const int mag = ctx == 0 ? 0 : (ls >> 3) + (idx & 1);
-    const int lv = act ? ((ls & 4) ? -mag : mag) : 0;
-    lv_out[zig] = (int16_t)lv;
-    last = (lv != 0 && last == 0) ? n + 1 : last;
-    ctx = act ? (ctx == 0 ? idx : idx >> 1) : ctx;
+    const int mag = code == 0 ? 0 : (ls >> 3) + code - 1;
+    q[zig_of(n)] = (int16_t)((ls & 4) ? -mag : mag);
   }
-#pragma unroll
-  for (int i = 0; i < 16; i++) q[i] = lv_out[i];
-  *nz = best < 0 ? 0 : last;
+  if (k == 0) {
+    const uint32_t nzb = (hist | hist >> 1) & 0x55555555u;
+    *nz = nzb == 0 ? 0 : ((31 - __builtin_clz(nzb)) >> 1) + 1;
+  }
 }
 
 // TokenCostForCoeffs's term for position n alone (lane-parallel form of
