@@ -23,7 +23,6 @@
 //              (each needs its left / top neighbour's nz), DC and chroma in
 //              parallel, then reconstruction and export
 // All integer; bit-exact with the C restatement (oracle/lossy_rd.c).
-#include <cstdlib>
 #include <mutex>
 
 #include "vp8_tables.h"
@@ -87,8 +86,24 @@ constexpr uint64_t pack_band() {
 __device__ __forceinline__ int zig_of(int n) { return (int)((pack_zig() >> (4 * n)) & 15); }
 __device__ __forceinline__ int band_of(int n) { return (int)((pack_band() >> (3 * n)) & 7); }
 
+// One trellis position, prepared by a lane of its own (trellis_prep) and
+// consumed by the lane quad running the DP (trellis_dp4).
+struct alignas(8) TRec {
+  // x[row][pc]: the transition from predecessor context pc, as a key
+  // (score x16 + order idx) to add to that predecessor's state, with the
+  // rows routed by the end context they reach:
+  //   R0  level 0 (end context 0): zero-token cost * lam16 + idx pc
+  //   R1  level 1 or L0 >= 2: (nz token + level cost) * lam16 + distortion,
+  //       idx 2pc for level L0, 2pc + 1 for level L0 + 1 (= 1 when L0 = 0)
+  //   R2  level L0 + 1 >= 2 (idx 2pc + 1), all BIG when L0 = 0
+  // + BIG when that level is not a candidate
+  int64_t x[3][3];
+};
+static_assert(sizeof(TRec) == 72, "TRec layout");
+
 __constant__ uint16_t c_level_codes[134];
 __constant__ uint16_t c_fixed_i4[1000];
+__constant__ int32_t c_wtrellis[16];
 
 // ------------------------------------------------------------------ LDS state
 // token costs of one (type, band) row, per context 0..2: `zero` = not-EOB +
@@ -132,6 +147,7 @@ struct Tables {
   // level sit in one 8-byte word so one ds_read_b64 serves a trellis step
   uint64_t vcost[4 * 8][68];
   uint16_t fixed_i4[1000];
+  int wtr[16];  // trellis distortion weights (kWeightTrellis)
   alignas(16) uint8_t pcode[10][16];  // kPred4Code
 };
 // Per-wave state: each wave of the workgroup encodes its own macroblock row
@@ -148,6 +164,8 @@ struct Shared {
   int mode_rate[4], mode_disto[4];
   int blk_rate[16], blk_disto[16], blk_hdr[16];
   int co_buf[16][16];      // transform coefficients handed to the trellis prep lanes
+  TRec trec[6][16];        // trellis position records: I4 (half, candidate) / final I16 (diagonal slot)
+  int l0s[6][16];          // per position: L0 << 3 | negative << 2 | min(L0, 2)
   int16_t cand_q[6][16];   // I4 candidates' levels for the lane-parallel token cost
   int cand_nz[6], cand_rate[6];
   alignas(16) uint8_t pv[2][64];  // per half-wave: the I4 block's prediction value table
@@ -234,6 +252,60 @@ __device__ __forceinline__ int token_cost(const Tables& t, const int16_t q[16], 
   return cost;
 }
 
+// TrellisQuantizeBlock (encode_trellis.go:23-301), split across lanes.
+//
+// Scores are kept x16 so the low 4 bits of a 64-bit key can carry the
+// candidate's position in the reference's update order; "first strict
+// minimum in order" then is a plain min over keys.  Candidates per position
+// and end context: level 0 from predecessor pc (key idx = pc, end ctx 0),
+// level L0 (idx 2pc) and L0 + 1 (idx 2pc + 1), whose end context is
+// min(level, 2).  Invalid states carry scores >= 2^58 (valid ones stay below
+// 2^51), so they never win against a valid candidate.  The path keeps the
+// winning idx per end context (4 bits each, 16 bits per position); levels
+// are re-derived from the position records when walking back.
+//
+// ---- TrellisQuantizeBlock split across lanes ----------------------------
+// Everything a trellis position needs that does not depend on the DP state
+// (level candidates, distortion deltas, token + level costs per predecessor
+// context) is computed by one lane per position into a TRec; the lane that
+// runs the serial DP then does only the 3 x 3 transitions per position.
+// Returns whether the position has a non-zero level under the neutral bias
+// (the reference's all-zero pre-scan).
+template <int CTX_TYPE>
+__device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, const SQuant& sq, int lam16, TRec& out,
+                                             int& l0s) {
+  constexpr int64_t BIG = 1ll << 59;
+  const int zig = zig_of(n), band = band_of(n + 1);
+  const int c0 = max(abs(co_z) + sq.sharpen[zig], 0);
+  const int quant = n == 0 ? sq.dc_quant : sq.quant;
+  const int iquant = n == 0 ? sq.dc_iquant : sq.iquant;
+  const int L0raw = (c0 * iquant) >> 17;
+  const int L0 = min(L0raw, 2047);
+  const int thresh = min((int)(((uint32_t)c0 * (uint32_t)iquant + 65536u) >> 17), 2047);
+  const bool has0 = L0 > 0 && L0 <= thresh;
+  const bool has1 = L0 + 1 <= 2047 && L0 + 1 <= thresh;
+  const int w4096 = t.wtr[zig] * 4096;
+  const int e0 = c0 - L0 * quant, e1 = c0 - (L0 + 1) * quant;
+  const int64_t A0 = (int64_t)t.lfixed[L0] * lam16 + (int64_t)w4096 * (e0 * e0 - c0 * c0) + (has0 ? 0 : BIG);
+  const int64_t A1 = (int64_t)t.lfixed[min(L0 + 1, 2047)] * lam16 + (int64_t)w4096 * (e1 * e1 - c0 * c0) + (has1 ? 0 : BIG);
+  const TokRow& tr = t.tok[CTX_TYPE * 8 + band];
+  const uint64_t v0 = t.vcost[CTX_TYPE * 8 + band][min(L0, 67)], v1 = t.vcost[CTX_TYPE * 8 + band][min(L0 + 1, 67)];
+  // rows by end context: L0 = 0 sends level 1 (= L0 + 1) to context 1 and
+  // nothing to context 2; otherwise L0 -> R1, L0 + 1 -> R2 (trellis_dp4
+  // merges R1 into context 2 when L0 >= 2)
+  const bool z = L0 == 0;
+#pragma unroll
+  for (int pc = 0; pc < 3; pc++) {
+    const int64_t r1 = (int64_t)(tr.nz[pc] + vc_of(v0, pc)) * lam16 + A0 + 2 * pc;
+    const int64_t r2 = (int64_t)(tr.nz[pc] + vc_of(v1, pc)) * lam16 + A1 + 2 * pc + 1;
+    out.x[0][pc] = (int64_t)tr.zero[pc] * lam16 + pc;
+    out.x[1][pc] = z ? r2 : r1;
+    out.x[2][pc] = z ? BIG : r2;
+  }
+  l0s = L0 << 3 | (co_z < 0 ? 4 : 0) | min(L0, 2);
+  return L0raw > 0;
+}
+
 // 64-bit value of lane j of this lane's quad (DPP quad_perm broadcast)
 template <int J>
 __device__ __forceinline__ int64_t quad_bcast(int64_t v) {
@@ -253,160 +325,71 @@ __device__ __forceinline__ int quad_bcast32(int v) {
   return __builtin_amdgcn_mov_dpp(v, J | J << 2 | J << 4 | J << 6, 0xf, 0xf, false);
 }
 
-// 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate), as inline asm
-// so the compiler cannot widen them back once it loses the operands' range
-__device__ __forceinline__ uint32_t umul24(uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ uint32_t umad24(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t r;
-  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-__device__ __forceinline__ int smul24(int a, int b) {
-  int r;
-  asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-
-// The trellis DP on a quad of lanes (TrellisQuantizeBlock,
-// encode_trellis.go:23-301).  Lane k of the quad owns END context
-// e = min(k, 2) (lane 3 shadows lane 2).  Per position it builds its own
-// transitions -- the keys score x16 + the candidate's index in the
-// reference's update order, so the first strict minimum of :215-245 is a
-// plain min and the keys of one end context never tie:
-//   e = 0  level 0 from each predecessor pc: zero-token cost, index pc
-//   e = 1  level 1: L0 when L0 = 1 (index 2pc), L0 + 1 when L0 = 0 (2pc + 1)
-//   e = 2  level L0 + 1 >= 2 (index 2pc + 1)
-// and where L0 >= 2 the level-L0 transitions (lane 1's, index 2pc) also end
-// in context 2, which then takes the min of lanes 1 and 2 while context 1 is
-// empty.  A key is (token + level cost) * lam16 + 256 * 16 * weight *
-// (err^2 - c0^2) (+ BIG when the level is not a candidate); with lvl = 0 the
-// same formula gives lane 0's zero-token keys (level-0 costs and distortion
-// delta are 0).  The per-position work (level candidates, costs) runs one
-// position ahead of the DP step and its table reads two ahead, so no LDS
-// round trip sits on the serial chain; the minima reach every lane by DPP
-// broadcasts.
+// The trellis DP on a quad of lanes.  trellis_prep routes the transitions
+// by the end context they reach (TRec rows R0 / R1 / R2), so lane k of the
+// quad (e = min(k, 2); lane 3 shadows lane 2) takes the minimum of the three
+// predecessor states plus its row: keys are score x16 + the candidate's index
+// in the reference's update order, so the first strict minimum of
+// encode_trellis.go:215-245 is a plain min and the keys of one end context
+// never tie.  The three minima reach every lane by DPP broadcasts; where L0 >= 2
+// both non-zero levels end in context 2, which then takes min(R1, R2) and
+// context 1 is empty.
 //
-// Every state carries its history (2 bits a position: 0 = level 0, 1 = L0,
-// 2 = L0 + 1) instead of a path table: the best terminal (EOB after position
-// n from context 1 or 2, :257-270) keeps the history it ended, and the
-// levels then follow with no serial walk-back: lane r of the quad writes
-// positions 4r .. 4r + 3 (raster) to q, lane 0 the zigzag nz count to *nz.
-// co: the block's coefficients (raster, LDS).
-constexpr int kWTrellis[16] = {30, 27, 19, 11, 27, 24, 17, 10, 19, 17, 12, 8, 11, 10, 8, 6};  // = vp8_weight_trellis
-
+// Instead of a path table walked back from the best terminal, every state
+// carries its own history: 2 bits per position (0 = level 0, 1 = L0,
+// 2 = L0 + 1), copied from the winning predecessor.  The best terminal
+// (EOB after position n from context 1 or 2, :257-270) keeps the history it
+// ended, and the levels then follow position by position with no serial
+// chain: the quad's lane r writes positions 4r..4r+3 (raster) to q, and lane
+// 0 writes the zigzag nz count to *nz.
 template <int FIRST, int CTX_TYPE>
-__device__ __forceinline__ void trellis_dp4(const Tables& t, const int* co, const SQuant& sq, int init_ctx, int lam16,
+__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int* l0s, int init_ctx, int lam16,
                                             int k, int16_t* q, int* nz) {
   constexpr int64_t BIG = 1ll << 59, VALID = 1ll << 58;
   init_ctx = min(init_ctx, 2);
   const int e = min(k, 2);
-  const int psh = e == 0 ? 0 : 1;  // index -> predecessor shift; also the level-code offset
-  const int2 qa = *reinterpret_cast<const int2*>(&sq.quant);     // quant, iquant
-  const int2 qd = *reinterpret_cast<const int2*>(&sq.dc_quant);  // dc_quant, dc_iquant
-  // this lane's token-cost half of a TokRow: zero[] (e = 0) or nz[]
-  const uint16_t* tokp = (e == 0 ? &t.tok[CTX_TYPE * 8].zero[0] : &t.tok[CTX_TYPE * 8].nz[0]);
-  const uint16_t* eobp = &t.tok[CTX_TYPE * 8].eob[0] + (e == 2 ? 2 : 1);
-  constexpr int TSTR = sizeof(TokRow) / 2;
-  const uint64_t* vcb = &t.vcost[CTX_TYPE * 8][0];
-  constexpr int VSTR = 68;
-
-  // ---- position preparation, branch-free over the lane's end context:
-  //   lvl = 0 (e = 0), max(L0, 1) (e = 1), L0 + 1 (e = 2)
-  //   candidate iff lvl <= thresh (and L0 > 0 for e = 2)
-  //   index offset lvl - L0 for e = 1, 2
-  const uint32_t lmask = e == 0 ? 0u : ~0u;
-  const int la = e == 2 ? 1 : 0, lb = e == 1 ? 1 : 0;
-  const bool e2 = e == 2;
-  const uint32_t mul = 1 + psh;  // index = mul * pc + offset
-  struct Lv {
-    int c0, lvl, iadd;
-    bool valid, two;
-  };
-  auto stage1 = [&](int n, int a, int sh) {
-    Lv r;
-    const int quantiq = n == 0 ? qd.y : qa.y;
-    r.c0 = max(abs(a) + sh, 0);
-    const uint32_t prod = umul24((uint32_t)r.c0, (uint32_t)quantiq);  // < 2^31 (c0 < 2^16, iquant <= 2^15)
-    const int L0 = min((int)(prod >> 17), 2047);
-    const int th = min((int)((prod + 65536u) >> 17), 2047);
-    r.lvl = (int)((uint32_t)max(L0 + la, lb) & lmask);
-    r.valid = r.lvl <= th && !(e2 && L0 == 0);
-    r.iadd = (int)((uint32_t)(r.lvl - L0) & lmask);
-    r.two = L0 >= 2;
-    return r;
-  };
-  // stage 2: the three keys (its table reads are issued with stage 1)
-  auto stage2 = [&](int n, const Lv& r, uint2 tk, uint64_t vw, int lf, int64_t x[3]) {
-    const int quant = n == 0 ? qd.x : qa.x;
-    const int err = r.c0 - smul24(r.lvl, quant);
-    const int d = smul24(err, err) - smul24(r.c0, r.c0);
-    int64_t A = (int64_t)d * (kWTrellis[kZig[n]] * 4096) + (int64_t)(int)umul24((uint32_t)lf, (uint32_t)lam16);
-    A += r.valid ? 0 : BIG;
-    const uint32_t tk16[3] = {tk.x & 0xffff, tk.x >> 16, tk.y & 0xffff};
-#pragma unroll
-    for (int pc = 0; pc < 3; pc++) {
-      const uint32_t rate = tk16[pc] + (uint32_t)vc_of(vw, pc);
-      x[pc] = A + (int64_t)umad24(rate, (uint32_t)lam16, mul * pc + (uint32_t)r.iadd);
-    }
-  };
-
+  const int psh = e == 0 ? 0 : 1;  // index -> predecessor context shift; also the level-code offset
   int64_t ps0 = init_ctx == 0 ? 0 : BIG, ps1 = init_ctx == 1 ? 0 : BIG, ps2 = init_ctx == 2 ? 0 : BIG;
   uint32_t h0 = 0, h1 = 0, h2 = 0;  // the states' histories
   const TokRow& t_init = t.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
+  // lanes 0, 1 follow the terminals of context 1 (lane 0's copy is unused), lanes 2, 3 context 2
+  const int tctx = e == 2 ? 2 : 1;
   int64_t best_terminal = (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16;
   int best_n = -1;
   uint32_t best_h = 0;
-  const int tctx = e == 2 ? 2 : 1;  // lanes 0, 1 follow context 1's terminals (lane 0's copy unused), 2, 3 context 2
-
-  // pipeline: position n's stage 1 result + table reads (cur_*), position
-  // n + 1's coefficient (nxt_a, nxt_sh)
-  Lv cur = stage1(FIRST, co[kZig[FIRST]], sq.sharpen[kZig[FIRST]]);
-  uint2 cur_tk = *reinterpret_cast<const uint2*>(tokp + kBand[FIRST + 1] * TSTR);
-  uint64_t cur_vw = vcb[kBand[FIRST + 1] * VSTR + min(cur.lvl, 67)];
-  int cur_lf = t.lfixed[min(cur.lvl, 2047)];
-  uint32_t cur_eob = FIRST < 15 ? eobp[kBand[FIRST + 1] * TSTR] : 0;
-  int nxt_a = co[kZig[FIRST + 1]], nxt_sh = sq.sharpen[kZig[FIRST + 1]];
+  const int64_t* mine = &rec[0].x[e][0];
+  const uint16_t* eobp = &t.tok[CTX_TYPE * 8].eob[0] + tctx;
+  constexpr int STRIDE = sizeof(TRec) / sizeof(int64_t), TSTR = sizeof(TokRow) / 2;
+  // Position n's row, class and EOB cost are loaded during position n - 1
+  // and pinned by the asm below, so no LDS round trip sits on the chain.
+  int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
+  int cls_raw = l0s[FIRST];
+  uint32_t eob_raw = FIRST < 15 ? eobp[kBand[FIRST + 1] * TSTR] : 0;
 #pragma unroll
   for (int n = FIRST; n < 16; n++) {
-    // stage 1 of position n + 1 and its table reads; the coefficient of n + 2
-    Lv nx = cur;
-    uint2 nx_tk = make_uint2(0, 0);
-    uint64_t nx_vw = 0;
-    int nx_lf = 0, n2_a = 0, n2_sh = 0;
-    uint32_t nx_eob = 0;
+    int64_t nx0 = 0, nx1 = 0, nx2 = 0;
+    int ncls = 0;
+    uint32_t neob = 0;
     if (n < 15) {
-      nx = stage1(n + 1, nxt_a, nxt_sh);
-      nx_tk = *reinterpret_cast<const uint2*>(tokp + kBand[n + 2] * TSTR);
-      nx_vw = vcb[kBand[n + 2] * VSTR + min(nx.lvl, 67)];
-      nx_lf = t.lfixed[min(nx.lvl, 2047)];
-      if (n + 1 < 15) nx_eob = eobp[kBand[n + 2] * TSTR];
-      if (n < 14) {
-        n2_a = co[kZig[n + 2]];
-        n2_sh = sq.sharpen[kZig[n + 2]];
-      }
+      nx0 = mine[(n + 1) * STRIDE];
+      nx1 = mine[(n + 1) * STRIDE + 1];
+      nx2 = mine[(n + 1) * STRIDE + 2];
+      ncls = l0s[n + 1];
+      if (n + 1 < 15) neob = eobp[kBand[n + 2] * TSTR];
     }
     asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
-    int64_t x[3];
-    stage2(n, cur, cur_tk, cur_vw, cur_lf, x);
-    const bool two = cur.two;
-    const uint32_t eob_n = cur_eob;
-    cur = nx;
-    cur_tk = nx_tk;
-    cur_vw = nx_vw;
-    cur_lf = nx_lf;
-    cur_eob = nx_eob;
-    nxt_a = n2_a;
-    nxt_sh = n2_sh;
-    // the DP step
-    const int64_t c0 = ps0 + x[0], c1 = ps1 + x[1], c2 = ps2 + x[2];
+    const int64_t c0 = ps0 + x0, c1 = ps1 + x1, c2 = ps2 + x2;
+    const bool two = (cls_raw & 2) != 0;  // class 2: L0 >= 2
+    const uint32_t eob_n = eob_raw;
+    x0 = nx0;
+    x1 = nx1;
+    x2 = nx2;
+    cls_raw = ncls;
+    eob_raw = neob;
     const int64_t m01 = c1 < c0 ? c1 : c0;
     const int64_t m = c2 < m01 ? c2 : m01;
     const uint32_t idx = (uint32_t)m & 15, pc = idx >> psh;
-    const uint32_t code = (idx & (uint32_t)psh) + (uint32_t)psh;  // e = 0: 0; else 1 (L0) or 2 (L0 + 1)
+    const uint32_t code = (idx & (uint32_t)psh) + (uint32_t)psh;  // R0: 0; R1 / R2: 1 (L0) or 2 (L0 + 1)
     const uint32_t hm = (pc == 0 ? h0 : (pc == 1 ? h1 : h2)) | code << (2 * n);
     const int64_t M0 = quad_bcast<0>(m), M1 = quad_bcast<1>(m), M2 = quad_bcast<2>(m);
     const uint32_t H0 = quad_bcast32<0>(hm), H1 = quad_bcast32<1>(hm), H2 = quad_bcast32<2>(hm);
@@ -431,37 +414,20 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const int* co, cons
   const uint32_t bh1 = quad_bcast32<1>(best_h), bh2 = quad_bcast32<2>(best_h);
   const bool second = bt2 < bt1 || (bt2 == bt1 && bn2 < bn1);
   const uint32_t hist = second ? bh2 : bh1;  // 0 when no terminal beat the all-zero block
-  // lane k: positions 4k .. 4k + 3 (level = L0 + code - 1, sign of the coefficient)
+  // lane r: positions 4r .. 4r + 3
+  const int r = k;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    const int n = 4 * k + j, zig = zig_of(n);
+    const int n = 4 * r + j;
     const int code = (int)((hist >> (2 * n)) & 3);
-    const int a = co[zig];
-    const int c0 = max(abs(a) + sq.sharpen[zig], 0);
-    const int quantiq = n == 0 ? qd.y : qa.y;
-    const int L0 = min((c0 * quantiq) >> 17, 2047);
-    const int mag = code == 0 ? 0 : L0 + code - 1;
-    q[zig] = (int16_t)(a < 0 ? -mag : mag);
+    const int ls = l0s[n];
+    const int mag = code == 0 ? 0 : (ls >> 3) + code - 1;
+    q[zig_of(n)] = (int16_t)((ls & 4) ? -mag : mag);
   }
   if (k == 0) {
     const uint32_t nzb = (hist | hist >> 1) & 0x55555555u;
     *nz = nzb == 0 ? 0 : ((31 - __builtin_clz(nzb)) >> 1) + 1;
   }
-}
-
-// The reference's all-zero pre-scan (encode_trellis.go:36-95): whether any
-// position of the block quantises to a non-zero level with the neutral bias.
-// co: the 16 coefficients in registers (raster).
-template <int FIRST>
-__device__ __forceinline__ bool trellis_nonzero(const int co[16], const SQuant& sq) {
-  const int2 qa = *reinterpret_cast<const int2*>(&sq.quant);
-  const int2 qd = *reinterpret_cast<const int2*>(&sq.dc_quant);
-  int mx = 0;  // max over n >= 1 (all use the AC iquant)
-#pragma unroll
-  for (int n = 1; n < 16; n++) mx = max(mx, abs(co[kZig[n]]) + sq.sharpen[kZig[n]]);
-  bool nzr = ((mx * qa.y) >> 17) > 0;
-  if (FIRST == 0) nzr |= ((max(abs(co[0]) + sq.sharpen[0], 0) * qd.y) >> 17) > 0;
-  return nzr;
 }
 
 // TokenCostForCoeffs's term for position n alone (lane-parallel form of
@@ -768,6 +734,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
   for (int i = tid; i < 256; i += NT) t.ecost[i] = vp8_entropy_cost[i];
   for (int i = tid; i < 2048; i += NT) t.lfixed[i] = vp8_level_fixed_costs[i];
   for (int i = tid; i < 1000; i += NT) t.fixed_i4[i] = c_fixed_i4[i];
+  if (tid < 16) t.wtr[tid] = c_wtrellis[tid];
   if (tid < 160) t.pcode[tid >> 4][tid & 15] = kPred4Code[tid >> 4][tid & 15];
   __syncthreads();
   for (int i = tid; i < 4 * 8 * 68; i += NT) {
@@ -1074,7 +1041,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           const int slot = half * 3 + min(hl, 2);  // candidate slot in the trellis / level buffers
           SSTAMP(1);
           // candidates: prediction + transform (lane hl = candidate hl)
-          bool pnz = false;  // the reference's all-zero pre-scan of the candidate
           if (cand) {
             CSTAMP(-1);
             int pred[16], co[16];
@@ -1082,20 +1048,28 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
             fdct(src, pred, co);
 #pragma unroll
             for (int i = 0; i < 16; i++) s.co_buf[slot][i] = co[i];
-            pnz = trellis_nonzero<0>(co, sg.y1);
             CSTAMP(0);
           }
-          const uint64_t pnz_mask = __ballot(pnz);  // bit 32 * half + candidate
           lds_sync();
+          // trellis positions: lane (candidate c, pair pp) prepares positions 2pp, 2pp + 1
           const int lam16 = sg.tlambda_i4 * 16;
+          bool pnz = false;
+          if (bvalid && hl < 8 * K) {
+            const int c = hl >> 3, n0 = 2 * (hl & 7), sl = half * 3 + c;
+#pragma unroll
+            for (int j = 0; j < 2; j++)
+              pnz |= trellis_prep<3>(t, s.co_buf[sl][zig_of(n0 + j)], n0 + j, sg.y1, lam16, s.trec[sl][n0 + j], s.l0s[sl][n0 + j]);
+          }
+          const uint64_t pnz_mask = __ballot(pnz);
+          lds_sync();
           // the trellis DP: one lane quad per candidate (lane 4c + k owns end context k)
           if (bvalid && hl < 4 * K) {
             const int c = hl >> 2, sl = half * 3 + c;
-            if ((pnz_mask >> (32 * half + c)) & 1) {
+            if ((pnz_mask >> (32 * half + 8 * c)) & 0xff) {
               // the DP is the step's serial chain: let it win issue arbitration
               // against the SIMD's other wave while it runs
               __builtin_amdgcn_s_setprio(3);
-              trellis_dp4<0, 3>(t, s.co_buf[sl], sg.y1, nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
+              trellis_dp4<0, 3>(t, s.trec[sl], s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
               __builtin_amdgcn_s_setprio(2);
             } else if ((hl & 3) == 0) {
 #pragma unroll
@@ -1324,7 +1298,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
       uint32_t nzy_mask = 0, nzuv_mask = 0;
       int nz_dc = 0;
       if (!is_i4) {
-        bool bnz = false;  // the block's all-zero pre-scan (AC positions)
         if (lane < 16) {
           const int off = YOFF + 4 * by * BPS + 4 * bx;
           int src[16], pred[16], co[16];
@@ -1334,15 +1307,14 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           s.dcin[0][lane] = co[0];
 #pragma unroll
           for (int i = 1; i < 16; i++) s.co_buf[lane][i] = co[i];
-          bnz = trellis_nonzero<1>(co, sg.y1);
         }
-        const uint32_t pnz_blocks = (uint32_t)__ballot(bnz);  // bit = block
         lds_sync();
         // Trellis of the 16 AC blocks.  A block's DP depends on its left / top
         // neighbours' nz only through its initial context min(l + t, 2), so
         // it is run speculatively for every context the block can still get
         // (1 for block 0, 2 along the MB's top row / left column, 3 inside):
-        // three rounds of up to six blocks and up to 16 DPs, one per lane quad, each
+        // three rounds of up to six blocks (their position records fit the
+        // six trellis slots) and up to 16 DPs, one per lane quad, each
         // followed by the reference's raster-order resolution of the actual
         // contexts.  (Walking the 7 block diagonals took 7 prep + DP rounds.)
         const int lam16 = sg.tlambda_i16 * 16;
@@ -1352,6 +1324,25 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           Shared& s = launder(s_waves[wave]);
           Tables& t = launder(t_lds);
           const int first = r == 0 ? 0 : (r == 1 ? 6 : 11), m = r == 0 ? 6 : 5;
+          bool pnz = false;
+          if (lane < 8 * m) {
+            const int j = lane >> 3, n0 = 2 * (lane & 7), pb = first + j;
+            TRec rr[2];
+            int l0[2];
+#pragma unroll
+            for (int k = 0; k < 2; k++) {  // position 0 (the DC, coded by the WHT) is not part of this trellis
+              const bool used = n0 + k >= 1;
+              pnz |= trellis_prep<0>(t, used ? s.co_buf[pb][zig_of(n0 + k)] : 0, n0 + k, sg.y1, lam16, rr[k], l0[k]) && used;
+            }
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+              if (n0 + k >= 1) {
+                s.trec[j][n0 + k] = rr[k];
+                s.l0s[j][n0 + k] = l0[k];
+              }
+          }
+          const uint64_t pnz_mask = __ballot(pnz);
+          lds_sync();
           // quad q runs task q: walk the round's blocks to find its (block, context)
           {
             const int q = lane >> 2;
@@ -1368,9 +1359,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
               acc += nopt;
             }
             if (tj >= 0) {
-              if ((pnz_blocks >> (first + tj)) & 1) {
+              if ((pnz_mask >> (8 * tj)) & 0xff) {
                 int nzv = 0;
-                trellis_dp4<1, 0>(t, s.co_buf[first + tj], sg.y1, tctx, lam16, lane & 3, res_q + q * 16, &nzv);
+                trellis_dp4<1, 0>(t, s.trec[tj], s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
                 if ((lane & 3) == 0) res_nz[q] = nzv;
               } else if ((lane & 3) == 0) {
 #pragma unroll
@@ -1699,10 +1690,9 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
       uint16_t fixed[1000];
       build_fixed_costs_i4(fixed);
       if (hipMemcpyToSymbol(HIP_SYMBOL(c_fixed_i4), fixed, sizeof(fixed)) != hipSuccess ||
-          hipMemcpyToSymbol(HIP_SYMBOL(c_level_codes), vp8_level_codes, sizeof(vp8_level_codes)) != hipSuccess)
+          hipMemcpyToSymbol(HIP_SYMBOL(c_level_codes), vp8_level_codes, sizeof(vp8_level_codes)) != hipSuccess ||
+          hipMemcpyToSymbol(HIP_SYMBOL(c_wtrellis), vp8_weight_trellis, sizeof(vp8_weight_trellis)) != hipSuccess)
         return wg::check_launch("encode tables");
-      for (int i = 0; i < 16; i++)  // the DP's compile-time copy of kWeightTrellis
-        if (kWTrellis[i] != vp8_weight_trellis[i]) return wg::invalid("kWTrellis differs from vp8_weight_trellis");
       g_tables_ready_mask |= 1ull << dev;
     }
   }
@@ -1732,15 +1722,13 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(encode ctl)");
   int cus = 0, per_cu = 0;
-  // diagnostic: WEBPGPU_ENC_LDS_PAD=<bytes> of dynamic LDS per workgroup (lowers occupancy)
-  static const size_t pad = [] { const char* e = getenv("WEBPGPU_ENC_LDS_PAD"); return e ? (size_t)atol(e) : (size_t)0; }();
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows, 64 * WAVES, pad) != hipSuccess || per_cu <= 0)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows, 64 * WAVES, 0) != hipSuccess || per_cu <= 0)
     return wg::check_launch("encode occupancy query");
   const int rows = n_images * mbh;
   const int wgs = (rows + WAVES - 1) / WAVES;  // each wave dequeues rows on its own
   const int grid = wgs < per_cu * cus ? wgs : per_cu * cus;
-  hipLaunchKernelGGL(k_encode_rows, dim3((unsigned)grid), dim3(64 * WAVES), pad, s, a);
+  hipLaunchKernelGGL(k_encode_rows, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
   return wg::check_launch("k_encode_rows");
 }
 
