@@ -208,6 +208,19 @@ __device__ __forceinline__ int quantize(const int co[16], int16_t q[16], const S
   return max_zz + 1;
 }
 
+// 16 levels packed two per VGPR (int16 arrays otherwise take one VGPR each)
+struct Q16 {
+  uint32_t w[8];
+  __device__ __forceinline__ int get(int i) const { return (int)(int16_t)(w[i >> 1] >> (16 * (i & 1))); }
+};
+__device__ __forceinline__ int quantize(const int co[16], Q16& q, const SQuant& sq, int first) {
+  int16_t t[16];
+  const int nz = quantize(co, t, sq, first);
+#pragma unroll
+  for (int i = 0; i < 8; i++) q.w[i] = (uint32_t)(uint16_t)t[2 * i] | (uint32_t)(uint16_t)t[2 * i + 1] << 16;
+  return nz;
+}
+
 __device__ __forceinline__ int variable_level_cost(const Tables& t, int level, const uint8_t* p) {
   const int idx = min(level - 1, 66);
   int pattern = c_level_codes[2 * idx], bits = c_level_codes[2 * idx + 1], cost = 0;
@@ -234,14 +247,17 @@ __device__ __forceinline__ int tok_costs(const TokRow& tr, int ctx, bool zero, i
 // TokenCostForCoeffs (encode_quant.go:154-223), branch-free: the context of
 // every position follows from the levels alone (min(|q|, 2) of the previous
 // one), so all table reads are independent and issue back to back.
-__device__ __forceinline__ int token_cost(const Tables& t, const int16_t q[16], int nz_count, int type, int ctx0, int first) {
+__device__ __forceinline__ int lvl_at(const int16_t* q, int i) { return q[i]; }
+__device__ __forceinline__ int lvl_at(const Q16& q, int i) { return q.get(i); }
+template <typename QT>
+__device__ __forceinline__ int token_cost(const Tables& t, const QT& q, int nz_count, int type, int ctx0, int first) {
   int cost = 0, ctx = ctx0;
   const int eob_at = max(nz_count, first);
 #pragma unroll
   for (int n = 0; n < 16; n++) {
     if (n < first) continue;
     const TokRow& tr = t.tok[type * 8 + kBand[n]];
-    const int v = abs((int)q[kZig[n]]);
+    const int v = abs(lvl_at(q, kZig[n]));
     const uint64_t vw = t.vcost[type * 8 + kBand[n]][min(v, 67)];
     int eob;
     const int base = tok_costs(tr, ctx, v == 0, &eob);
@@ -479,11 +495,12 @@ __device__ __forceinline__ void select_i4_modes(int sse, int m, uint32_t eligibl
 }
 
 // residual + reconstruction of one 4x4 block: rec = clip(pred + IDCT(dq))
-__device__ __forceinline__ void dequant(const int16_t q[16], int dq[16], const SQuant& sq) {
+template <typename QT>
+__device__ __forceinline__ void dequant(const QT& q, int dq[16], const SQuant& sq) {
   const int2 qq = make_int2(sq.quant, sq.dc_quant);
-  dq[0] = (int16_t)(q[0] * qq.y);
+  dq[0] = (int16_t)(lvl_at(q, 0) * qq.y);
 #pragma unroll
-  for (int i = 1; i < 16; i++) dq[i] = (int16_t)(q[i] * qq.x);
+  for (int i = 1; i < 16; i++) dq[i] = (int16_t)(lvl_at(q, i) * qq.x);
 }
 __device__ __forceinline__ void recon4(const int pred[16], const int dq[16], int rec[16]) {
 #pragma unroll
@@ -543,6 +560,97 @@ __device__ __forceinline__ void unpack_rows(uint32_t w, int* d) {
 __device__ __forceinline__ void load4x4(const uint8_t* p, int v[16]) {  // p 4-byte aligned (all block origins are)
 #pragma unroll
   for (int r = 0; r < 4; r++) unpack_rows(*reinterpret_cast<const uint32_t*>(p + r * BPS), v + 4 * r);
+}
+// A 4x4 pixel block as four packed row words (4 VGPRs instead of 16):
+// blocks stay packed across the RD phases and are unpacked a row at a time.
+struct P4 {
+  uint32_t r[4];
+};
+__device__ __forceinline__ P4 ld4(const uint8_t* p) {  // p 4-byte aligned
+  P4 b;
+#pragma unroll
+  for (int r = 0; r < 4; r++) b.r[r] = *reinterpret_cast<const uint32_t*>(p + r * BPS);
+  return b;
+}
+__device__ __forceinline__ void st4(uint8_t* p, const P4& b) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) *reinterpret_cast<uint32_t*>(p + r * BPS) = b.r[r];
+}
+// sum of squared byte differences: a.a + b.b - 2 a.b with v_dot4_u32_u8
+__device__ __forceinline__ int sse_p(const P4& a, const P4& b) {
+  uint32_t aa = 0, bb = 0, ab = 0;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    aa = __builtin_amdgcn_udot4(a.r[r], a.r[r], aa, false);
+    bb = __builtin_amdgcn_udot4(b.r[r], b.r[r], bb, false);
+    ab = __builtin_amdgcn_udot4(a.r[r], b.r[r], ab, false);
+  }
+  return (int)(aa + bb - 2 * ab);
+}
+// FTransform of (src - pred), rows unpacked one at a time
+__device__ __forceinline__ void fdct_p(const P4& s, const P4& p, int co[16]) {
+  int tmp[16];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int d0 = byte_of(s.r[r], 0) - byte_of(p.r[r], 0), d1 = byte_of(s.r[r], 1) - byte_of(p.r[r], 1);
+    const int d2 = byte_of(s.r[r], 2) - byte_of(p.r[r], 2), d3 = byte_of(s.r[r], 3) - byte_of(p.r[r], 3);
+    const int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
+    tmp[4 * r + 0] = (a0 + a1) * 8;
+    tmp[4 * r + 1] = (a2 * 2217 + a3 * 5352 + 1812) >> 9;
+    tmp[4 * r + 2] = (a0 - a1) * 8;
+    tmp[4 * r + 3] = (a3 * 2217 - a2 * 5352 + 937) >> 9;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const int a0 = tmp[c] + tmp[12 + c], a1 = tmp[4 + c] + tmp[8 + c];
+    const int a2 = tmp[4 + c] - tmp[8 + c], a3 = tmp[c] - tmp[12 + c];
+    co[c] = (int16_t)((a0 + a1 + 7) >> 4);
+    co[4 + c] = (int16_t)(((a2 * 2217 + a3 * 5352 + 12000) >> 16) + (a3 != 0));
+    co[8 + c] = (int16_t)((a0 - a1 + 7) >> 4);
+    co[12 + c] = (int16_t)((a3 * 2217 - a2 * 5352 + 51000) >> 16);
+  }
+}
+// rec = clip(pred + IDCT(dq)), a row at a time
+__device__ __forceinline__ P4 recon_p(const P4& pred, const int dq[16]) {
+  P4 o;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    int res[4];
+    idct_row(dq, r, res);
+    o.r[r] = pack4(clip8(byte_of(pred.r[r], 0) + res[0]), clip8(byte_of(pred.r[r], 1) + res[1]),
+                   clip8(byte_of(pred.r[r], 2) + res[2]), clip8(byte_of(pred.r[r], 3) + res[3]));
+  }
+  return o;
+}
+// tTransform (ssim.go:266-304) of a packed block
+__device__ __forceinline__ int ttrans_p(const P4& b) {
+  const int kw[16] = {38, 32, 20, 9, 32, 28, 17, 7, 20, 17, 10, 4, 9, 7, 4, 2};
+  int tmp[16];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int r0 = byte_of(b.r[i], 0), r1 = byte_of(b.r[i], 1), r2 = byte_of(b.r[i], 2), r3 = byte_of(b.r[i], 3);
+    const int a0 = r0 + r2, a1 = r1 + r3, a2 = r1 - r3, a3 = r0 - r2;
+    tmp[4 * i] = a0 + a1;
+    tmp[4 * i + 1] = a3 + a2;
+    tmp[4 * i + 2] = a3 - a2;
+    tmp[4 * i + 3] = a0 - a1;
+  }
+  int sum = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int a0 = tmp[i] + tmp[8 + i], a1 = tmp[4 + i] + tmp[12 + i];
+    const int a2 = tmp[4 + i] - tmp[12 + i], a3 = tmp[i] - tmp[8 + i];
+    sum += kw[i] * abs(a0 + a1) + kw[4 + i] * abs(a3 + a2) + kw[8 + i] * abs(a3 - a2) + kw[12 + i] * abs(a0 - a1);
+  }
+  return sum;
+}
+__device__ __forceinline__ int tdisto_p(const P4& a, const P4& b) { return abs(ttrans_p(b) - ttrans_p(a)) >> 5; }
+__device__ __forceinline__ P4 predsq_p(int mode, const uint8_t* base, int size, int px, int py) {
+  const int dc = predsq_dc(mode, base, size);
+  P4 o;
+#pragma unroll
+  for (int r = 0; r < 4; r++) o.r[r] = predsq_row4(mode, base, px, py + r, dc);
+  return o;
 }
 // 16x16 / 8x8 square prediction of the 4x4 block at (px, py) of `base`
 __device__ __forceinline__ void predsq_block(int mode, const uint8_t* base, int size, int px, int py, int pred[16]) {
@@ -724,7 +832,10 @@ __device__ unsigned long long g_enc_phase[16];
 #define ESTAMP_FLUSH() (void)st_unused_
 #endif
 
-__global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
+#ifndef WG_ENC_OCC
+#define WG_ENC_OCC 2  // waves per SIMD (VGPR budget 512 / occupancy)
+#endif
+__global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs a) {
   __shared__ Tables t_lds;
   __shared__ Shared s_waves[WAVES];
   Tables& t = t_lds;
@@ -895,15 +1006,15 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
       }
       const int m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
       const bool mvalid = !((m == 2 && mby == 0) || (m == 3 && mbx == 0) || (m == 1 && (mbx == 0 || mby == 0)));
-      int src16[16], pred16[16], rec16[16];
-      int16_t q16[16];
+      P4 src16, pred16;
+      Q16 q16;
       int nz16 = 0;
       {
         const int off = YOFF + 4 * by * BPS + 4 * bx;
-        load4x4(s.yin + off, src16);
-        predsq_block(check_mode(mbx, mby, m), s.yout + YOFF, 16, 4 * bx, 4 * by, pred16);
+        src16 = ld4(s.yin + off);
+        pred16 = predsq_p(check_mode(mbx, mby, m), s.yout + YOFF, 16, 4 * bx, 4 * by);
         int co[16];
-        fdct(src16, pred16, co);
+        fdct_p(src16, pred16, co);
         s.dcin[m][b] = co[0];
         co[0] = 0;
         nz16 = quantize(co, q16, sg.y1, 1);
@@ -919,7 +1030,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
         int rate = mvalid ? token_cost(t, q16, nz16, 0, ctx, 1) : 0;
         bool acnz = false;
 #pragma unroll
-        for (int i = 1; i < 16; i++) acnz |= q16[i] != 0;
+        for (int i = 1; i < 16; i++) acnz |= q16.get(i) != 0;
         lds_sync();
         // one lane per mode: WHT path
         if (b == 0 && mvalid) {
@@ -944,9 +1055,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
         int dq[16];
         dequant(q16, dq, sg.y1);
         dq[0] = s.dcout[m][b];
-        recon4(pred16, dq, rec16);
-        const int sse = sse16(src16, rec16);
-        const int td = sg.tlambda_sd > 0 ? tdisto(src16, rec16) : 0;
+        const P4 rec16 = recon_p(pred16, dq);
+        const int sse = sse_p(src16, rec16);
+        const int td = sg.tlambda_sd > 0 ? tdisto_p(src16, rec16) : 0;
         const int rsum = group_sum_first<16>(rate), ssum = group_sum_first<16>(sse), tsum = group_sum_first<16>(td);  // used by lane b == 0
         const unsigned long long acmask = __ballot(acnz);
         if (b == 0 && mvalid) {
@@ -1228,14 +1339,14 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
         const bool act = lane < 32;
         const bool uvalid = act && !((um == 2 && mby == 0) || (um == 3 && mbx == 0) || (um == 1 && (mbx == 0 || mby == 0)));
         const int base = pl ? VOFF : UOFF;
-        int src[16], pred[16];
-        int16_t q[16];
+        P4 src, pred;
+        Q16 q;
         int nz = 0;
         if (act) {
-          load4x4(s.yin + base + 4 * uby * BPS + 4 * ubx, src);
-          predsq_block(check_mode(mbx, mby, um), s.yout + base, 8, 4 * ubx, 4 * uby, pred);
+          src = ld4(s.yin + base + 4 * uby * BPS + 4 * ubx);
+          pred = predsq_p(check_mode(mbx, mby, um), s.yout + base, 8, 4 * ubx, 4 * uby);
           int co[16];
-          fdct(src, pred, co);
+          fdct_p(src, pred, co);
           nz = quantize(co, q, sg.uv, 0);
         }
         // left / top block of the same plane (only read when ubx / uby > 0): DPP row shifts
@@ -1246,12 +1357,11 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_encode_rows(EncArgs a) {
           const int l = ubx > 0 ? (nzl > 0) : (int)((left_nz >> (4 + 2 * pl + uby)) & 1);
           const int tp = uby > 0 ? (nzt > 0) : (int)((top_nz >> (4 + 2 * pl + ubx)) & 1);
           rate = uvalid ? token_cost(t, q, nz, 2, min(l + tp, 2), 0) : 0;
-          int dq[16], rec[16];
+          int dq[16];
           dequant(q, dq, sg.uv);
-          recon4(pred, dq, rec);
-          sse = sse16(src, rec);
+          sse = sse_p(src, recon_p(pred, dq));
 #pragma unroll
-          for (int i = 1; i < 16; i++) acn += q[i] != 0;
+          for (int i = 1; i < 16; i++) acn += q.get(i) != 0;
         }
         const int rsum = group_sum_first<8>(rate), ssum = group_sum_first<8>(sse), asum = group_sum_first<8>(acn);  // used by lane k == 0
         if (act && k == 0) {
