@@ -42,8 +42,12 @@ constexpr int LV = 19 * WG_BPS + 0;   // V origin: row 19, col 0
 constexpr int WB_SIZE = 27 * WG_BPS;
 
 // Filter tiles: rows -4..15 (Y) / -4..7 (U,V) of the MB, columns -4..15 / -4..7.
-constexpr int FY_STRIDE = 32, FY_X0 = 16;  // Y col c at byte FY_X0 + c
-constexpr int FC_STRIDE = 16, FC_X0 = 8;
+// Filter tiles: Y col c at byte FY_X0 + c, U / V col c at FC_X0 + c.  The
+// columns left of the MB hold the MBs to its left (two for Y, four for U / V),
+// so the frame rows leave in 32-B pieces -- whole 32-B sectors of an L2 line --
+// once those MBs are final.
+constexpr int FY_STRIDE = 48, FY_X0 = 32;
+constexpr int FC_STRIDE = 40, FC_X0 = 32;
 
 constexpr int TOP_BYTES = 32;  // per MB column: unfiltered Y16 U8 V8 of the MB above
 
@@ -64,6 +68,18 @@ __device__ __forceinline__ void st_sc1_64(uint8_t* p, uint64_t v) {
 }
 __device__ __forceinline__ void st_sc1_32(uint8_t* p, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Coefficients are read exactly once: non-temporal loads, so the stream
+// (2 B / coefficient, the kernel's largest input) does not push the frame's
+// partly written output lines out of L2 before their other pieces arrive.
+__device__ __forceinline__ int4 ld_stream(const int4* p) {
+#ifdef WG_DEC_NO_NT
+  return *p;
+#else
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const v4i v = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
+  return make_int4(v.x, v.y, v.z, v.w);
+#endif
 }
 __device__ __forceinline__ uint64_t lds64(const uint8_t* p) { return *reinterpret_cast<const uint64_t*>(p); }
 __device__ __forceinline__ uint32_t lds32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
@@ -274,7 +290,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
       // earlier would make every wait on a hand-off load wait for it too).
       const int64_t row_mb0 = ((int64_t)img * mbh + mby) * mbw;
       int4 pf = make_int4(0, 0, 0, 0);
-      if (lane < 48) pf = reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384)[lane];
+      if (lane < 48) pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384) + lane);
       else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + row_mb0)[lane - 48];
 
       for (int mbx = 0; mbx < mbw; mbx++) {
@@ -300,15 +316,29 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
         lane = opaque_lane() & 63;
         // ---- loads: macroblock info (scalar), coefficients -> LDS, top context, filter rows above ----
         if (lane < 50) stage[lane] = pf;
-        // rotate the filter tile: the left MB's final columns 12..15 become columns -4..-1
-        if (mbx > 0) {
-          if (lane < 16) {
-            uint8_t* r = fy + (lane + 4) * FY_STRIDE + FY_X0;
-            *reinterpret_cast<uint32_t*>(r - 4) = lds32(r + 12);
-          } else if (lane < 32) {
-            const int j = (lane - 16) & 7;
-            uint8_t* r = ((lane < 24) ? fu : fv) + (j + 4) * FC_STRIDE + FC_X0;
-            *reinterpret_cast<uint32_t*>(r - 4) = lds32(r + 4);
+        // rotate the filter tiles: the MBs to the left move one MB further left
+        // (our left-edge filter then finishes the left MB's columns 13..15)
+        if (mbx > 0) {  // shift every tile row left by one MB (all loads before all stores)
+          uint4 y0 = make_uint4(0, 0, 0, 0);
+          uint64_t c[2] = {0, 0};
+          if (lane < 40) y0 = *reinterpret_cast<const uint4*>(fy + (lane >> 1) * FY_STRIDE + FY_X0 - 16 + 16 * (lane & 1));
+#pragma unroll
+          for (int h = 0; h < 2; h++) {  // U, V: 24 rows x 4 words
+            const int i = lane + 64 * h;
+            if (i < 96) {
+              const int row = i >> 2, pl = row >= 12;
+              c[h] = lds64((pl ? fv : fu) + (row - 12 * pl) * FC_STRIDE + FC_X0 - 24 + 8 * (i & 3));
+            }
+          }
+          lds_sync();
+          if (lane < 40) *reinterpret_cast<uint4*>(fy + (lane >> 1) * FY_STRIDE + FY_X0 - 32 + 16 * (lane & 1)) = y0;
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const int i = lane + 64 * h;
+            if (i < 96) {
+              const int row = i >> 2, pl = row >= 12;
+              *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (row - 12 * pl) * FC_STRIDE + FC_X0 - 32 + 8 * (i & 3)) = c[h];
+            }
           }
         }
         if (mby > 0 && from_lds) {
@@ -367,7 +397,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
         }
         lds_sync();
         if (mbx + 1 < mbw) {  // prefetch the next MB (see above)
-          if (lane < 48) pf = reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384)[lane];
+          if (lane < 48) pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384) + lane);
           else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + mbi + 1)[lane - 48];
         }
         const uint32_t* iw = reinterpret_cast<const uint32_t*>(stage + 48);  // wg_mb_info words
@@ -471,53 +501,97 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
         STAMP(6);
         lane = opaque_lane() & 63;
         // ---- stores ----
-        // Only what another workgroup reads while this launch runs is written
-        // through (sc1): the bottom rows 12..15 (Y) / 4..7 (U, V) of a band's
-        // last row, which the next band's first row loads as its filter
-        // context.  Every other frame byte is read by nobody before the launch
-        // ends and goes out as a plain (write-back) store, so L2 merges a row's
-        // 16-B pieces into whole lines.  Y rows 13..15 / U, V rows 5..7 are
-        // left to the row below when it is in this band.
-        if (lane < 32) {  // Y rows, 2 x 8 B
-          const int j = lane >> 1, half = lane & 1;
-          uint8_t* dst = Yp + (int64_t)(16 * mby + j) * ys + 16 * mbx + 8 * half;
-          const uint64_t w = lds64(fy + (j + 4) * FY_STRIDE + FY_X0 + 8 * half);
-          if (!to_lds && j >= 12) st_sc1_64(dst, w);
-          else if (!to_lds || j < 13) *reinterpret_cast<uint64_t*>(dst) = w;
-        } else if (lane < 48) {  // U, V rows
-          const int pl = lane >= 40, j = (lane - 32) & 7;
-          uint8_t* dst = (pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx;
-          const uint64_t w = lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0);
-          if (!to_lds && j >= 4) st_sc1_64(dst, w);
-          else if (!to_lds || j < 5) *reinterpret_cast<uint64_t*>(dst) = w;
-        }
-        if (do_filter && mbx > 0) {  // the 3 columns of the left MB modified by our left-edge filter
-          if (lane >= 48) {
-            const int j = lane - 48;
-            uint8_t* dst = Yp + (int64_t)(16 * mby + j) * ys + 16 * mbx - 4;
-            const uint32_t w = lds32(fy + (j + 4) * FY_STRIDE + FY_X0 - 4);
-            if (!to_lds && j >= 12) st_sc1_32(dst, w);
-            else if (!to_lds || j < 13) *reinterpret_cast<uint32_t*>(dst) = w;
-          } else if (!luma_only && lane < 16) {
-            const int pl = lane >= 8, j = lane & 7;
-            uint8_t* dst = (pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * mbx - 4;
-            const uint32_t w = lds32((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 - 4);
-            if (!to_lds && j >= 4) st_sc1_32(dst, w);
-            else if (!to_lds || j < 5) *reinterpret_cast<uint32_t*>(dst) = w;
+        // An MB's pixels are final once the MB to its right has run its
+        // left-edge filter, except rows 13..15 (Y) / 5..7 (U, V), which the
+        // row below finishes with its top-edge filter.  Rows leave in 32-B
+        // pieces (two Y MBs, four U / V MBs) once every MB of the piece is
+        // final, and the rest at the row's end: every frame byte is written
+        // once (but rows 13..15 / 5..7 of a band's last row, see below), and
+        // as whole 32-B sectors.  Only what another workgroup reads while
+        // this launch runs is written through (sc1), per MB: rows 12..15 /
+        // 4..7 of a band's last row, which the next band's first row loads as
+        // its filter context (and rewrites after its top-edge filter).  Rows
+        // 13..15 / 5..7 are left to the row below when it is in this band,
+        // which stores them in 32-B pieces too.
+        {
+          const bool last = mbx == mbw - 1;
+          // Y: MBs [y0, y1] leave now (tile column of MB m: 16 (m - mbx)).
+          // Pieces go out at even mbx for the two MBs before it; at the row's
+          // end everything not yet stored (up to 3 MBs) does.
+          int y0 = -1, y1 = -1;
+          if (last) {
+            y0 = mbx > 0 ? (mbx - 1) & ~1 : 0;
+            y1 = mbx;
+          } else if (mbx >= 2 && (mbx & 1) == 0) {
+            y0 = mbx - 2;
+            y1 = mbx - 1;
           }
-        }
-        if (mby > 0 && (from_lds || do_filter)) {
-          // the 3 rows of the MB above modified by our top-edge filter; always,
-          // when the row above (in this band) left them to us.  Nobody reads
-          // them again in this launch: plain stores.
-          if (lane >= 16 && lane < 22) {
-            const int k = lane - 16, rr = 1 + (k >> 1), half = k & 1;
-            *reinterpret_cast<uint64_t*>(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half) =
-                lds64(fy + rr * FY_STRIDE + FY_X0 + 8 * half);
-          } else if ((from_lds || !luma_only) && lane >= 22 && lane < 28) {
-            const int k = lane - 22, pl = k >= 3, rr = 1 + (k % 3);
-            *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx) =
-                lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0);
+          int c0 = -1, c1 = -1;  // U, V: likewise, 4-MB pieces (up to 5 MBs at the end)
+          if (last) {
+            c0 = mbx > 0 ? (mbx - 1) & ~3 : 0;
+            c1 = mbx;
+          } else if (mbx >= 4 && (mbx & 3) == 0) {
+            c0 = mbx - 4;
+            c1 = mbx - 1;
+          }
+          const int ylim = to_lds ? 13 : 12, clim = to_lds ? 5 : 4;  // rows below these: batched
+          if (lane < 48) {  // Y: row lane & 15, MB y0 + (lane >> 4)
+            const int j = lane & 15, x = y0 + (lane >> 4);
+            if (y0 >= 0 && j < ylim && x <= y1) {
+              const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
+              *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby + j) * ys + 16 * x) = w;
+            }
+          }
+#pragma unroll
+          for (int h = 0; h < 2; h++) {  // U, V: row (i & 15), MB c0 + (i >> 4)
+            const int i = lane + 64 * h, pl = (i >> 3) & 1, j = i & 7, x = c0 + (i >> 4);
+            if (c0 >= 0 && i < 80 && j < clim && x <= c1)
+              *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x) =
+                  lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx));
+          }
+          if (!to_lds) {  // a band's last row: rows 12..15 / 4..7 of the left MB (and of this one at the row's end)
+            const int which = lane >> 5, k = lane & 31, x = mbx - 1 + which;
+            if (which == 0 ? mbx > 0 : last) {
+              if (k < 4) {
+                const int j = 12 + k;
+                const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
+                uint8_t* dst = Yp + (int64_t)(16 * mby + j) * ys + 16 * x;
+                st_sc1_64(dst, (uint64_t)w.y << 32 | w.x);
+                st_sc1_64(dst + 8, (uint64_t)w.w << 32 | w.z);
+              } else if (k < 12) {
+                const int pl = k >= 8, j = 4 + (k & 3);
+                st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x,
+                          lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
+              }
+            }
+          }
+          if (mby > 0) {
+            // rows 13..15 / 5..7 of the MBs above, final after our top-edge
+            // filter (tile rows 1..3): 32-B pieces of the MBs above up to this
+            // one, whether or not the filter ran on each (a piece spans MBs;
+            // an unfiltered row rewrites the bytes it was loaded with).
+            // Nobody reads them again in this launch: plain stores.
+            int t0 = -1, t1 = -1;
+            if ((mbx & 1) == 1 || last) {
+              t0 = mbx & ~1;
+              t1 = mbx;
+            }
+            int u0 = -1, u1 = -1;
+            if ((mbx & 3) == 3 || last) {
+              u0 = mbx & ~3;
+              u1 = mbx;
+            }
+            if (lane < 6) {
+              const int rr = 1 + (lane >> 1), part = lane & 1, x = t0 + part;
+              if (t0 >= 0 && x <= t1)
+                *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * x) =
+                    *reinterpret_cast<const uint4*>(fy + rr * FY_STRIDE + FY_X0 + 16 * (x - mbx));
+            } else if ((from_lds || !luma_only) && lane >= 8 && lane < 32) {
+              const int k = lane - 8, pl = k >= 12, rr = 1 + (k % 12) / 4, q = k & 3, x = u0 + q;
+              if (u0 >= 0 && x <= u1)
+                *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * x) =
+                    lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0 + 8 * (x - mbx));
+            }
           }
         }
         if (to_lds) {
