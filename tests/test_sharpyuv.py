@@ -77,9 +77,11 @@ def test_gpu_fixtures_and_batch(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,h", [(1920, 1080), (4096, 256), (4100, 40)])
+@pytest.mark.parametrize("w,h", [(1920, 1080), (4096, 256), (4100, 40), (600, 200), (530, 131)])
 def test_gpu_wide(cuda, w, h):
-    """1080p, the C5 width (4096), and a width past 4096 (the 8-column path)."""
+    """1080p, the C5 width (4096), a width past 4096, and widths whose last
+    column band (k_sharp_band, 256 UV columns + a 32-column halo) is partial,
+    over heights with several halo resynchronisations."""
     import torch
     from webp_amd import frames
     rgb = np.ascontiguousarray(synth.blobs_rgba(w, h, seed=w)[..., :3])

@@ -5,22 +5,22 @@
 //   k_sharp_init   import + gray Y, target W, target / initial chroma
 //                  residuals (convertSharp phase 1, :196-222): one thread per
 //                  2x2 block, fully parallel
-//   k_sharp_pipe   the iterative refinement (:224-264).  Each iteration sweeps
+//   k_sharp_band   the iterative refinement (:224-264).  Each iteration sweeps
 //                  the row pairs in order and updates the chroma residuals in
 //                  place, so row pair j reads row pair j-1's values from the
 //                  SAME iteration (Gauss-Seidel): a sweep is sequential by
 //                  construction.  But iteration k+1 at row pair j needs only
 //                  iteration k's rows up to j+1, so the four iterations run
-//                  as a pipeline: one workgroup per (image, iteration), each
-//                  reading state k and writing state k+1 (five states per
-//                  image, out of place), iteration k+1 trailing k by three
-//                  row pairs behind a progress counter (published one step
-//                  late, when every wave has drained its stores).  The early exit
-//                  (:254-263) needs each iteration's global |dY| sum; all
-//                  four iterations run speculatively and k_sharp_final picks
-//                  the state the reference would stop at.  Inside a
-//                  workgroup the whole width runs in parallel, the updated
-//                  row kept in LDS as the next row's "prev".
+//                  as a pipeline, each reading state k and writing state k+1
+//                  (five states per image, out of place), iteration k+1
+//                  trailing k by three row pairs behind progress counters
+//                  (published one step late, when every wave has drained its
+//                  stores); and an iteration's columns split into bands of
+//                  BAND that recompute a HALO on each side and meet their
+//                  neighbours once every HALO row pairs (see the kernel).
+//                  The early exit (:254-263) needs each iteration's global
+//                  |dY| sum; all four iterations run speculatively and
+//                  k_sharp_final picks the state the reference would stop at.
 //   k_sharp_final  W/RGB -> YUV with the matrix (:390-432), per pixel
 //
 // All arithmetic is integer (the reference's int / int64 / int16 with wrap);
@@ -139,7 +139,6 @@ __global__ __launch_bounds__(256) void k_sharp_init(SharpArgs a, int n_img) {
   }
 }
 
-constexpr int ITER_THREADS = 1024;
 constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 
 // Hand-off loads / stores between the iteration workgroups: agent-scope
@@ -153,134 +152,187 @@ __device__ __forceinline__ uint32_t ld_sc1(const void* p) {
 __device__ __forceinline__ void st_sc1(void* p, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ uint16_t ld_sc1_16(const void* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint16_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_16(void* p, uint16_t v) {
+  __hip_atomic_store(reinterpret_cast<uint16_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-// phase 2: workgroup = (image, iteration).  Blocks are grouped 32 to eight
-// images so that an image's four iterations have equal blockIdx % 8 (one XCD
-// under the round-robin placement: a speed matter only) and iteration k's
-// block precedes iteration k+1's.  Thread t owns UV columns t + k*1024,
-// k < MAX_COLS: 2 covers widths up to 4096, 8 up to 16384.
-template <int MAX_COLS, bool LUT>
-__global__ __launch_bounds__(ITER_THREADS) void k_sharp_pipe(SharpArgs a) {
+// phase 2: workgroup = (image, iteration, column band).  A refinement
+// iteration is a Gauss-Seidel sweep over the row pairs: row pair j reads the
+// chroma row j-1 updated by the SAME iteration (prev), so a sweep is
+// sequential in j; but the update of UV column i reads prev only at columns
+// i-1..i+1, so a band of columns can run ahead of its neighbours by
+// recomputing a halo: with HALO extra columns on each side (computed but not
+// stored), the band's own columns stay exact for HALO row pairs after prev
+// was last taken from the neighbours, and every HALO row pairs the band
+// reloads its halo's prev row from the neighbour bands' output.  So one
+// image's iteration spreads over ceil(uvw / BAND) workgroups that meet once
+// every HALO row pairs.  Iteration k+1 trails iteration k (its input state)
+// by three row pairs behind per-band progress counters, as before; each
+// workgroup (thread = UV column) keeps its prev / cur / next chroma rows in
+// LDS.  Blocks are ordered (image, iteration, band), so every wait is on a
+// block dispatched earlier or on a neighbour of the same iteration, and a
+// launch holds only as many images as are resident at once.
+constexpr int BAND = 256, HALO = 32, BAND_T = BAND + 2 * HALO;  // threads per workgroup = columns incl. halo
+constexpr int PUB = 8;  // progress is published every PUB row pairs
+static_assert(HALO % PUB == 0, "resynchronisation rows must be published rows");
+constexpr int SLOTS = BAND_T + 2;                                // LDS row entries per channel (+1 each side)
+
+template <bool LUT>
+__global__ __launch_bounds__(BAND_T) void k_sharp_band(SharpArgs a, int nb) {
   __shared__ SharpTabs t;
-  extern __shared__ int16_t rows[];  // prev / cur / next UV rows: 3 rows of uv_rs
-  __shared__ unsigned long long part[ITER_THREADS / 64];
+  __shared__ int16_t rows[3][3][SLOTS];  // [prev / cur / next][channel][column - c_lo]
+  __shared__ unsigned long long part[(BAND_T + 63) / 64];
   __shared__ int timed_out;
-  const int b = blockIdx.x, it = (b & 31) >> 3, img = (b >> 5) * 8 + (b & 7);
+  const int blk = blockIdx.x, band = blk % nb, it = (blk / nb) & 3, img = blk / (4 * nb);
   if (img >= a.n_img) return;  // uniform over the block
   load_tabs(t, a.tabs);
   const int tid = threadIdx.x;
   const int uvw = a.uvw, uvh = a.uvh, w = a.w, rs = a.uv_rs;
+  const int c_lo = band * BAND - HALO - 1;       // column of LDS slot 0
+  const int c = c_lo + 1 + tid;                  // this thread's UV column
+  const bool act = c >= 0 && c < uvw;
+  const bool interior = act && c >= band * BAND && c < (band + 1) * BAND;
   const uint16_t* in_y = a.best_y + img * a.img_y + it * a.state_y;
   uint16_t* out_y = const_cast<uint16_t*>(in_y) + a.state_y;
   const int16_t* in_uv = a.best_uv + img * a.img_uv + it * a.state_uv;
   int16_t* out_uv = const_cast<int16_t*>(in_uv) + a.state_uv;
   const uint16_t* ty = a.target_y + img * a.img_y;
   const int16_t* tuv = a.target_uv + img * a.img_uv;
-  int* prog_in = a.prog + img * 4 + it - 1;  // iteration it-1 (it > 0)
-  int* prog_out = a.prog + img * 4 + it;
-  int16_t* lds_row[3] = {rows, rows + rs, rows + 2 * rs};  // rotating prev / cur / next
-  const int words = (3 * uvw + 1) >> 1;  // u32 words of a UV row (the padding absorbs the odd one)
-  int seen = it == 0 ? uvh : 0;
+  int* prog_img = a.prog + (int64_t)img * 4 * nb;  // [iteration][band]: row pairs finished
+  int* prog_out = prog_img + it * nb + band;
   if (tid == 0) timed_out = 0;
 
-  // thread 0: wait until iteration it-1 has finished `need` row pairs
-  auto wait_rows = [&](int need) {
-    if (tid == 0 && seen < need) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      for (uint32_t k = 0;; k++) {
-        seen = (int)ld_sc1(prog_in);
-        if (seen >= need) break;
-        if ((k & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
-          timed_out = 1;
-          seen = uvh;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+  // thread 0: wait until band bb of iteration ii has finished `need` row
+  // pairs; returns the progress it saw (uvh for a band that does not exist)
+  auto wait_for = [&](int ii, int bb, int need) -> int {
+    if (bb < 0 || bb >= nb) return uvh;
+    const int* p = prog_img + ii * nb + bb;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t k = 0;; k++) {
+      const int v = (int)ld_sc1(p);
+      if (v >= need) return v;
+      if ((k & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+        timed_out = 1;
+        return uvh;
       }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  int seen_in = it == 0 ? uvh : 0;  // input state rows known ready (iteration it-1, bands band-1..band+1)
+  auto wait_input = [&](int need) {
+    if (tid == 0 && seen_in < need && !timed_out) {
+      int s = uvh;
+      for (int d = -1; d <= 1; d++) s = min(s, wait_for(it - 1, band + d, need));
+      seen_in = s;
+    }
+  };
+  // LDS slot s (column c_lo + s) of a chroma row of a state, for s = tid + 1 and
+  // the two edge slots 0 and SLOTS - 1 (loaded by threads 0 and 1)
+  auto load_row = [&](int16_t (*dst)[SLOTS], const int16_t* src_row) {
+    for (int s2 = tid; s2 < SLOTS; s2 += BAND_T) {
+      const int cc = c_lo + s2;
+      if (cc >= 0 && cc < uvw)
+        for (int ch = 0; ch < 3; ch++) dst[ch][s2] = (int16_t)ld_sc1_16(src_row + ch * uvw + cc);
     }
   };
 
   uint64_t my_sum = 0;
   int pi = 0, ci = 1, ni = 2;
-  // rows 0 and 1 of the input state: prev(row 0) = cur(row 0) = row 0
-  wait_rows(min(2, uvh));
+  const int sl = tid + 1;                                   // this column's LDS slot
+  const int pe = tid == 0 ? 0 : SLOTS - 1, ce = c_lo + pe;  // threads 0 / 1 also fetch the edge slots
+  // Input rows run two row pairs ahead of their use, so the load latency of
+  // the previous iteration's output never sits on a step: the luma pair and
+  // targets of row pair jp, and UV row `row` of the input state.
+  struct In {
+    uint32_t y[2], ty[2];
+    int16_t tuv[3];
+  };
+  auto load_in = [&](int jp) {
+    In r = {{0, 0}, {0, 0}, {0, 0, 0}};
+    if (act && jp < uvh) {
+      const int64_t yo = (int64_t)(2 * jp) * w + 2 * c;
+      r.y[0] = ld_sc1(in_y + yo);
+      r.y[1] = ld_sc1(in_y + yo + w);
+      r.ty[0] = *reinterpret_cast<const uint32_t*>(ty + yo);
+      r.ty[1] = *reinterpret_cast<const uint32_t*>(ty + yo + w);
+      for (int ch = 0; ch < 3; ch++) r.tuv[ch] = tuv[(int64_t)jp * rs + ch * uvw + c];
+    }
+    return r;
+  };
+  struct Pf {
+    int16_t v[3], e[3];  // slot sl; edge slot pe (threads 0 / 1)
+  };
+  auto load_pf = [&](int row) {
+    Pf r = {{0, 0, 0}, {0, 0, 0}};
+    if (row < uvh) {
+      const int16_t* src = in_uv + (int64_t)row * rs;
+      if (act)
+        for (int ch = 0; ch < 3; ch++) r.v[ch] = (int16_t)ld_sc1_16(src + ch * uvw + c);
+      if (tid < 2 && ce >= 0 && ce < uvw)
+        for (int ch = 0; ch < 3; ch++) r.e[ch] = (int16_t)ld_sc1_16(src + ch * uvw + ce);
+    }
+    return r;
+  };
+  // rows 0 and 1 of the input state: prev(row 0) = cur(row 0) = row 0; row 2
+  // and luma pairs 0, 1 in registers
+  wait_input(min(3, uvh));
   __syncthreads();
-  for (int i = tid; i < words; i += ITER_THREADS) {
-    const uint32_t v0 = ld_sc1(in_uv + 2 * i);
-    reinterpret_cast<uint32_t*>(lds_row[ci])[i] = v0;
-    reinterpret_cast<uint32_t*>(lds_row[pi])[i] = v0;
-    reinterpret_cast<uint32_t*>(lds_row[ni])[i] = uvh > 1 ? ld_sc1(in_uv + rs + 2 * i) : v0;
-  }
-  // luma pair 0 of the input state; later pairs are loaded one step ahead
-  // (and the targets: target luma pair, target chroma of the row)
-  uint32_t ycur[MAX_COLS][2], tycur[MAX_COLS][2];
-  int16_t tuvcur[MAX_COLS][3];
-#pragma unroll
-  for (int k = 0; k < MAX_COLS; k++) {
-    const int i = tid + k * ITER_THREADS;
-    ycur[k][0] = i < uvw ? ld_sc1(in_y + 2 * i) : 0u;
-    ycur[k][1] = i < uvw ? ld_sc1(in_y + w + 2 * i) : 0u;
-    tycur[k][0] = i < uvw ? *reinterpret_cast<const uint32_t*>(ty + 2 * i) : 0u;
-    tycur[k][1] = i < uvw ? *reinterpret_cast<const uint32_t*>(ty + w + 2 * i) : 0u;
-    for (int ch = 0; ch < 3; ch++) tuvcur[k][ch] = i < uvw ? tuv[ch * uvw + i] : 0;
-  }
+  load_row(rows[ci], in_uv);
+  load_row(rows[pi], in_uv);
+  load_row(rows[ni], uvh > 1 ? in_uv + rs : in_uv);
+  Pf pf_a = load_pf(2);
+  In in_cur = load_in(0), in_nxt = load_in(1);
   for (int ju = 0; ju < uvh; ju++) {
-    wait_rows(min(ju + 3, uvh));  // Y pair ju + 1 and UV row ju + 2 of the input state
+    wait_input(min(ju + 4, uvh));  // UV row ju + 3 and luma pair ju + 2 of the input state
+    const bool resync = ju > 0 && ju % HALO == 0;
+    if (resync && tid == 0 && !timed_out) {  // the neighbours' row ju - 1 of this iteration
+      wait_for(it, band - 1, ju);
+      wait_for(it, band + 1, ju);
+    }
     __syncthreads();
-    const int16_t* P = lds_row[pi];
-    const int16_t* C = lds_row[ci];
-    const int16_t* N = lds_row[ni];
+    if (resync && (sl < HALO + 1 || sl >= SLOTS - HALO - 1) && c < uvw && c >= 0)  // halo slots of prev
+      for (int ch = 0; ch < 3; ch++) rows[pi][ch][sl] = (int16_t)ld_sc1_16(out_uv + (int64_t)(ju - 1) * rs + ch * uvw + c);
+    if (resync && tid < 2) {  // slots 0 and SLOTS - 1
+      const int s2 = tid == 0 ? 0 : SLOTS - 1, cc = c_lo + s2;
+      if (cc >= 0 && cc < uvw)
+        for (int ch = 0; ch < 3; ch++) rows[pi][ch][s2] = (int16_t)ld_sc1_16(out_uv + (int64_t)(ju - 1) * rs + ch * uvw + cc);
+    }
+    if (resync) __syncthreads();
     const int j = 2 * ju;
-    // prefetch the row after next (the next step's "next") into registers
-    const bool have_nn = ju + 2 < uvh;
-    uint32_t pf[(MAX_COLS * ITER_THREADS * 3 / 2 + ITER_THREADS - 1) / ITER_THREADS];
-    constexpr int PFN = sizeof(pf) / sizeof(pf[0]);
-#pragma unroll
-    for (int k = 0; k < PFN; k++) {
-      const int i = tid + k * ITER_THREADS;
-      pf[k] = (have_nn && i < words) ? ld_sc1(in_uv + (int64_t)(ju + 2) * rs + 2 * i) : 0u;
-    }
-    uint32_t ynext[MAX_COLS][2], tynext[MAX_COLS][2];  // luma pair ju + 1, its targets
-    int16_t tuvnext[MAX_COLS][3];
-    const bool have_ny = ju + 1 < uvh;
-#pragma unroll
-    for (int k = 0; k < MAX_COLS; k++) {
-      const int i = tid + k * ITER_THREADS;
-      const bool ok = have_ny && i < uvw;
-      const int64_t yn = (int64_t)(j + 2) * w + 2 * i;
-      ynext[k][0] = ok ? ld_sc1(in_y + yn) : 0u;
-      ynext[k][1] = ok ? ld_sc1(in_y + yn + w) : 0u;
-      tynext[k][0] = ok ? *reinterpret_cast<const uint32_t*>(ty + yn) : 0u;
-      tynext[k][1] = ok ? *reinterpret_cast<const uint32_t*>(ty + yn + w) : 0u;
-      for (int ch = 0; ch < 3; ch++) tuvnext[k][ch] = ok ? tuv[(int64_t)(ju + 1) * rs + ch * uvw + i] : 0;
-    }
-    int16_t upd[MAX_COLS][3];  // the updated row: written to LDS only after every thread read P/C/N
-    uint32_t ynew[MAX_COLS][2];  // the updated luma pair: stored after the barriers, off the wait below
-#pragma unroll
-    for (int k = 0; k < MAX_COLS; k++) {
-      const int i = tid + k * ITER_THREADS;
-      if (i >= uvw) continue;
-      // interpolateTwoRows (:322-359) for pixels x = 2i, 2i+1 of rows j, j+1
+    const Pf pf_b = load_pf(ju + 3);
+    const In in_2 = load_in(ju + 2);
+    const uint32_t* ycur = in_cur.y;
+    const uint32_t* tycur = in_cur.ty;
+    const int16_t* tuvcur = in_cur.tuv;
+    int16_t upd[3] = {0, 0, 0};
+    uint32_t ynew[2] = {0, 0};
+    if (act) {
+      const int16_t (*P)[SLOTS] = rows[pi];
+      const int16_t (*C)[SLOTS] = rows[ci];
+      const int16_t (*N)[SLOTS] = rows[ni];
+      // interpolateTwoRows (:322-359) for pixels x = 2c, 2c+1 of rows j, j+1
       int iv[2][2][3];
-      const uint32_t r0 = ycur[k][0], r1 = ycur[k][1];
+      const uint32_t r0 = ycur[0], r1 = ycur[1];
       const int by00 = r0 & 0xffff, by01 = r0 >> 16, by10 = r1 & 0xffff, by11 = r1 >> 16;
       for (int ch = 0; ch < 3; ch++) {
-        const int o = ch * uvw;
-        const int a1 = C[o + i], b1 = P[o + i], n1 = N[o + i];
-        int e0, e1, f0, f1;  // x = 2i: row j / j+1
-        if (i == 0) {
+        const int a1 = C[ch][sl], b1 = P[ch][sl], n1 = N[ch][sl];
+        int e0, e1, f0, f1;  // x = 2c: row j / j+1
+        if (c == 0) {
           e0 = ((a1 * 3 + b1 + 2) >> 2);  // filter2(cur[0], prev[0])
           f0 = ((a1 * 3 + n1 + 2) >> 2);
-        } else {  // v1 of i-1: (a1*9 + a0*3 + b1*3 + b0 + 8) >> 4
-          const int a0 = C[o + i - 1], b0 = P[o + i - 1], n0 = N[o + i - 1];
+        } else {
+          const int a0 = C[ch][sl - 1], b0 = P[ch][sl - 1], n0 = N[ch][sl - 1];
           e0 = (a1 * 9 + a0 * 3 + b1 * 3 + b0 + 8) >> 4;
           f0 = (a1 * 9 + a0 * 3 + n1 * 3 + n0 + 8) >> 4;
         }
-        if (i == uvw - 1) {  // x = w-1: filter2(cur[uvw-1], prev[uvw-1])
+        if (c == uvw - 1) {  // x = w-1: filter2(cur[uvw-1], prev[uvw-1])
           e1 = ((a1 * 3 + b1 + 2) >> 2);
           f1 = ((a1 * 3 + n1 + 2) >> 2);
-        } else {  // v0 of i: (a0*9 + a1*3 + b0*3 + b1 + 8) >> 4 with a0 = cur[i]
-          const int a2 = C[o + i + 1], b2 = P[o + i + 1], n2 = N[o + i + 1];
+        } else {
+          const int a2 = C[ch][sl + 1], b2 = P[ch][sl + 1], n2 = N[ch][sl + 1];
           e1 = (a1 * 9 + a2 * 3 + b1 * 3 + b2 + 8) >> 4;
           f1 = (a1 * 9 + a2 * 3 + n1 * 3 + n2 + 8) >> 4;
         }
@@ -293,89 +345,75 @@ __global__ __launch_bounds__(ITER_THREADS) void k_sharp_pipe(SharpArgs a) {
       uint32_t lin[2][2][3];
       int yv[2][2];
       for (int r = 0; r < 2; r++)
-        for (int c = 0; c < 2; c++) {
-          for (int ch = 0; ch < 3; ch++) lin[r][c][ch] = to_linear(t.g2l, iv[r][c][ch]);
-          yv[r][c] = from_lin<LUT>(t.l2g, a.lut, a.lut_n, (uint32_t)gray(lin[r][c][0], lin[r][c][1], lin[r][c][2]));
+        for (int cc = 0; cc < 2; cc++) {
+          for (int ch = 0; ch < 3; ch++) lin[r][cc][ch] = to_linear(t.g2l, iv[r][cc][ch]);
+          yv[r][cc] = from_lin<LUT>(t.l2g, a.lut, a.lut_n, (uint32_t)gray(lin[r][cc][0], lin[r][cc][1], lin[r][cc][2]));
         }
       const int byv[2][2] = {{by00, by01}, {by10, by11}};
       int ny[2][2];
       for (int r = 0; r < 2; r++)
-        for (int c = 0; c < 2; c++) {
-          const int d = (int)((tycur[k][r] >> (16 * c)) & 0xffff) - yv[r][c];
-          ny[r][c] = clip_bd(byv[r][c] + d);
-          my_sum += (uint64_t)(d < 0 ? -d : d);
+        for (int cc = 0; cc < 2; cc++) {
+          const int d = (int)((tycur[r] >> (16 * cc)) & 0xffff) - yv[r][cc];
+          ny[r][cc] = clip_bd(byv[r][cc] + d);
+          if (interior) my_sum += (uint64_t)(d < 0 ? -d : d);
         }
-      ynew[k][0] = (uint32_t)ny[0][0] | (uint32_t)ny[0][1] << 16;
-      ynew[k][1] = (uint32_t)ny[1][0] | (uint32_t)ny[1][1] << 16;
+      ynew[0] = (uint32_t)ny[0][0] | (uint32_t)ny[0][1] << 16;
+      ynew[1] = (uint32_t)ny[1][0] | (uint32_t)ny[1][1] << 16;
       // updateChroma -> bestRGBUV, sharpYUVUpdateRGB (:383-388)
       int rgbv[3];
       for (int ch = 0; ch < 3; ch++)
         rgbv[ch] = from_lin<LUT>(t.l2g, a.lut, a.lut_n, (lin[0][0][ch] + lin[0][1][ch] + lin[1][0][ch] + lin[1][1][ch] + 2) >> 2);
       const int gv = gray(rgbv[0], rgbv[1], rgbv[2]);
       for (int ch = 0; ch < 3; ch++) {
-        const int16_t src = (int16_t)(rgbv[ch] - gv);
-        const int16_t d = (int16_t)(tuvcur[k][ch] - src);
-        upd[k][ch] = (int16_t)(C[ch * uvw + i] + d);
+        const int16_t srcv = (int16_t)(rgbv[ch] - gv);
+        const int16_t d = (int16_t)(tuvcur[ch] - srcv);
+        upd[ch] = (int16_t)(C[ch][sl] + d);
       }
     }
-    // drain this wave's stores of row pair ju-1 (issued at the end of the
-    // last step) and the prefetches (issued before the compute): the wait
-    // overlaps the compute
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every read of P/C/N for this step is done
-    // row pairs < ju are out: every wave drained its stores of them
-    if (tid == 0 && ju > 0) st_sc1(prog_out, (uint32_t)ju);
-#pragma unroll
-    for (int k = 0; k < MAX_COLS; k++) {
-      ycur[k][0] = ynext[k][0];
-      ycur[k][1] = ynext[k][1];
-      tycur[k][0] = tynext[k][0];
-      tycur[k][1] = tynext[k][1];
-      for (int ch = 0; ch < 3; ch++) tuvcur[k][ch] = tuvnext[k][ch];
-    }
     // rotate: prev <- updated cur (into the old prev slot), cur <- next,
-    // next <- prefetched row (or, on the last row pair, a copy of cur)
+    // next <- row ju + 2 (loaded a step ago; on the last row pair, a copy of cur)
+    const bool have_nn = ju + 2 < uvh;
     const int npi = pi, nci = ni, nni = ci;
-#pragma unroll
-    for (int k = 0; k < MAX_COLS; k++) {
-      const int i = tid + k * ITER_THREADS;
-      if (i < uvw)
-        for (int ch = 0; ch < 3; ch++) lds_row[npi][ch * uvw + i] = upd[k][ch];
+    if (act)
+      for (int ch = 0; ch < 3; ch++) rows[npi][ch][sl] = upd[ch];
+    for (int ch = 0; ch < 3; ch++) {
+      rows[nni][ch][sl] = have_nn ? pf_a.v[ch] : rows[nci][ch][sl];
+      if (tid < 2) rows[nni][ch][pe] = have_nn ? pf_a.e[ch] : rows[nci][ch][pe];
     }
-#pragma unroll
-    for (int k = 0; k < PFN; k++) {
-      const int i = tid + k * ITER_THREADS;
-      if (i < words)
-        reinterpret_cast<uint32_t*>(lds_row[nni])[i] = have_nn ? pf[k] : reinterpret_cast<const uint32_t*>(lds_row[nci])[i];
-    }
+    pf_a = pf_b;
+    in_cur = in_nxt;
+    in_nxt = in_2;
     pi = npi;
     ci = nci;
     ni = nni;
     __syncthreads();
-    // publish the updated UV row ju (write-through) and drain this wave's stores
-    for (int i = tid; i < words; i += ITER_THREADS)
-      st_sc1(out_uv + (int64_t)ju * rs + 2 * i, reinterpret_cast<const uint32_t*>(lds_row[pi])[i]);
-#pragma unroll
-    for (int k = 0; k < MAX_COLS; k++) {
-      const int i = tid + k * ITER_THREADS;
-      if (i < uvw) {
-        st_sc1(out_y + (int64_t)j * w + 2 * i, ynew[k][0]);
-        st_sc1(out_y + (int64_t)(j + 1) * w + 2 * i, ynew[k][1]);
-      }
+    // publish this band's own columns of the updated UV row ju and luma pair (write-through)
+    if (interior) {
+      for (int ch = 0; ch < 3; ch++) st_sc1_16(out_uv + (int64_t)ju * rs + ch * uvw + c, (uint16_t)upd[ch]);
+      st_sc1(out_y + (int64_t)j * w + 2 * c, ynew[0]);
+      st_sc1(out_y + (int64_t)(j + 1) * w + 2 * c, ynew[1]);
+    }
+    if ((ju + 1) % PUB == 0 || ju + 1 == uvh) {
+      // publish row pairs <= ju once every wave drained its stores of them.
+      // Every PUB row pairs only: a drain also waits for the loads in flight
+      // (vmcnt counts both), so per row pair it would put a memory round
+      // trip on every step.  HALO is a multiple of PUB, so the neighbours'
+      // resynchronisation on row ju (at the next step) finds it published.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) st_sc1(prog_out, (uint32_t)(ju + 1));
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) st_sc1(prog_out, (uint32_t)uvh);
-  // the iteration's |dY| sum (:254-263); k_sharp_final applies the exit rule
+  // the band's share of the iteration's |dY| sum (:254-263); k_sharp_final applies the exit rule
   unsigned long long sm = my_sum;
   for (int off = 32; off > 0; off >>= 1) sm += __shfl_down(sm, off, 64);
   if ((tid & 63) == 0) part[tid >> 6] = sm;
   __syncthreads();
   if (tid == 0) {
     uint64_t sum = 0;
-    for (int k = 0; k < ITER_THREADS / 64; k++) sum += part[k];
-    a.sums[img * 4 + it] = sum;
+    for (int k = 0; k < (BAND_T + 63) / 64; k++) sum += part[k];
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.sums + img * 4 + it), (unsigned long long)sum);
     if (timed_out) a.iters[img] = -1;
   }
 }
@@ -497,12 +535,17 @@ SharpLayout sharp_layout(int width, int height) {
   L.bytes_img = 2 * (L.img_y + L.img_uv);
   return L;
 }
+// column bands of one refinement iteration (k_sharp_band)
+int sharp_bands(int width) {
+  const int uvw = ((width + 1) & ~1) / 2;
+  return (uvw + BAND - 1) / BAND;
+}
 }  // namespace
 
 extern "C" size_t wg_sharpyuv_work_bytes(int32_t width, int32_t height, int32_t n_images) {
   if (width <= 0 || height <= 0 || n_images <= 0) return 0;
   const SharpLayout L = sharp_layout(width, height);
-  return n_images * L.bytes_img + (size_t)n_images * (4 * 8 + 4 * 4 + 4) + 16;
+  return n_images * L.bytes_img + (size_t)n_images * (4 * 8 + 4 + 4 * 4 * sharp_bands(width)) + 16;
 }
 
 extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t height, int32_t rgb_stride,
@@ -539,7 +582,7 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
   WG_REQUIRE(transfer >= 0 && transfer <= 18);
   const int w = (width + 1) & ~1, h = (height + 1) & ~1;
   const int uvw = w / 2, uvh = h / 2;
-  WG_REQUIRE(uvw <= 8 * ITER_THREADS);
+  const int nb = sharp_bands(width);
   int lut_n = 0;
   const void* tabs = wg::sharpyuv_tables_device(transfer, &lut_n);
   if (!tabs) return WG_EHIP;
@@ -570,12 +613,13 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
   a.tabs = static_cast<const SharpTabs*>(tabs);
   a.lut = reinterpret_cast<const uint16_t*>(static_cast<const uint8_t*>(tabs) + sizeof(SharpTabs));
   a.lut_n = lut_n;
+  // tail: sums [n][4] u64 | iters [n] | prog [n][4][bands]
   uint8_t* tail = base + n_images * L.bytes_img;
   a.sums = reinterpret_cast<uint64_t*>(tail);
-  a.prog = reinterpret_cast<int*>(tail + (size_t)n_images * 32);
-  a.iters = a.prog + 4 * n_images;
+  a.iters = reinterpret_cast<int*>(tail + (size_t)n_images * 32);
+  a.prog = a.iters + n_images;
   a.n_img = n_images;
-  if (hipMemsetAsync(tail, 0, (size_t)n_images * (32 + 16 + 4), s) != hipSuccess)
+  if (hipMemsetAsync(tail, 0, (size_t)n_images * (32 + 4 + 16 * nb), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(sharpyuv)");
   const int64_t cells = (int64_t)uvw * uvh * n_images;
   if (lut)
@@ -584,16 +628,14 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
     hipLaunchKernelGGL(k_sharp_init<false>, dim3(wg::blocks_for(cells, 256)), dim3(256), 0, s, a, n_images);
   int rc = wg::check_launch("k_sharp_init");
   if (rc != WG_OK) return rc;
-  // the pipeline's waits need every image's four workgroups resident at
-  // once: launch at most as many images as the device holds
-  const size_t lds_rows = sizeof(int16_t) * 3 * (size_t)L.uv_rs;
-  const bool wide = uvw > 2 * ITER_THREADS;
+  // every wait is on a block of the same launch: launch at most as many
+  // images as the device holds at once (4 iterations x nb bands each)
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide ? k_sharp_pipe<8, false> : k_sharp_pipe<2, false>,
-                                                   ITER_THREADS, lds_rows) != hipSuccess || per_cu <= 0)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sharp_band<false>, BAND_T, 0) != hipSuccess || per_cu <= 0)
     return wg::check_launch("sharpyuv occupancy");
-  const int chunk = std::max(8, (per_cu * cus / 32) * 8);  // images per launch (groups of eight = 32 blocks)
+  const int chunk = std::max(1, per_cu * cus / (4 * nb));  // images per launch
+  if (4 * nb > per_cu * cus) return wg::invalid("sharpyuv: image too wide for one device's resident workgroups");
   for (int i0 = 0; i0 < n_images; i0 += chunk) {
     SharpArgs c = a;
     c.n_img = std::min(chunk, n_images - i0);
@@ -602,18 +644,14 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
     c.best_uv += i0 * a.img_uv;
     c.target_uv += i0 * a.img_uv;
     c.sums += 4 * i0;
-    c.prog += 4 * i0;
+    c.prog += 4 * nb * i0;
     c.iters += i0;
-    const unsigned grid = (unsigned)((c.n_img + 7) / 8 * 32);
-    if (wide && lut)
-      hipLaunchKernelGGL((k_sharp_pipe<8, true>), dim3(grid), dim3(ITER_THREADS), lds_rows, s, c);
-    else if (wide)
-      hipLaunchKernelGGL((k_sharp_pipe<8, false>), dim3(grid), dim3(ITER_THREADS), lds_rows, s, c);
-    else if (lut)
-      hipLaunchKernelGGL((k_sharp_pipe<2, true>), dim3(grid), dim3(ITER_THREADS), lds_rows, s, c);
+    const unsigned grid = (unsigned)(c.n_img * 4 * nb);
+    if (lut)
+      hipLaunchKernelGGL(k_sharp_band<true>, dim3(grid), dim3(BAND_T), 0, s, c, nb);
     else
-      hipLaunchKernelGGL((k_sharp_pipe<2, false>), dim3(grid), dim3(ITER_THREADS), lds_rows, s, c);
-    rc = wg::check_launch("k_sharp_pipe");
+      hipLaunchKernelGGL(k_sharp_band<false>, dim3(grid), dim3(BAND_T), 0, s, c, nb);
+    rc = wg::check_launch("k_sharp_band");
     if (rc != WG_OK) return rc;
   }
   FinalArgs f;
@@ -660,7 +698,7 @@ extern "C" int wg_sharpyuv_iterations(const void* work, int32_t width, int32_t h
   const SharpLayout L = sharp_layout(width, height);
   const uint8_t* tail = static_cast<const uint8_t*>(work) + n_images * L.bytes_img;
   hipStream_t s = wg::as_stream(stream);
-  if (hipMemcpyAsync(out, tail + (size_t)n_images * 48, sizeof(int32_t) * n_images, hipMemcpyDeviceToHost, s) !=
+  if (hipMemcpyAsync(out, tail + (size_t)n_images * 32, sizeof(int32_t) * n_images, hipMemcpyDeviceToHost, s) !=
           hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return wg::check_launch("wg_sharpyuv_iterations");
