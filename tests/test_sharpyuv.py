@@ -80,7 +80,7 @@ def test_gpu_fixtures_and_batch(cuda):
 @pytest.mark.parametrize("w,h", [(1920, 1080), (4096, 256), (4100, 40), (600, 200), (530, 131)])
 def test_gpu_wide(cuda, w, h):
     """1080p, the C5 width (4096), a width past 4096, and widths whose last
-    column band (k_sharp_band, 256 UV columns + a 32-column halo) is partial,
+    column band (k_sharp_band, 128 UV columns + a 32-column halo) is partial,
     over heights with several halo resynchronisations."""
     import torch
     from webp_amd import frames

@@ -175,7 +175,7 @@ __device__ __forceinline__ void st_sc1_16(void* p, uint16_t v) {
 // LDS.  Blocks are ordered (image, iteration, band), so every wait is on a
 // block dispatched earlier or on a neighbour of the same iteration, and a
 // launch holds only as many images as are resident at once.
-constexpr int BAND = 256, HALO = 32, BAND_T = BAND + 2 * HALO;  // threads per workgroup = columns incl. halo
+constexpr int BAND = 128, HALO = 32, BAND_T = BAND + 2 * HALO;  // threads per workgroup = columns incl. halo
 constexpr int PUB = 8;  // progress is published every PUB row pairs
 static_assert(HALO % PUB == 0, "resynchronisation rows must be published rows");
 constexpr int SLOTS = BAND_T + 2;                                // LDS row entries per channel (+1 each side)
