@@ -141,10 +141,13 @@ struct Tables {
   uint16_t ecost[256];
   uint16_t lfixed[2048];
   TokRow tok[4 * 8];
-  // probability-dependent part of the level cost for every (type, band),
-  // level 1..67 and context (levels past 67 share entry 67;
-  // variableLevelCost, encode_quant.go:258-273): the three contexts of one
-  // level sit in one 8-byte word so one ds_read_b64 serves a trellis step
+  // token cost of a level for every (type, band), level 0..67 and context,
+  // but the level's fixed cost (lfixed): level 0 = not-EOB + zero token,
+  // level >= 1 = not-EOB + non-zero token + variableLevelCost (levels past
+  // 67 share entry 67; encode_quant.go:170-220, 258-273).  The three
+  // contexts of one level sit in one 8-byte word: one ds_read_b64 per
+  // position, and a position's cost is vcost[.][min(v, 67)] + lfixed[v]
+  // (lfixed[0] = 0) with no select on v == 0
   uint64_t vcost[4 * 8][68];
   uint16_t fixed_i4[1000];
   int wtr[16];  // trellis distortion weights (kWeightTrellis)
@@ -232,18 +235,6 @@ __device__ __forceinline__ int variable_level_cost(const Tables& t, int level, c
   return cost;
 }
 
-// One row of token costs for context ctx, read as two wide LDS loads:
-// returns the zero-token cost (v == 0) or the non-zero prefix, and the EOB
-// cost in *eob.
-__device__ __forceinline__ int tok_costs(const TokRow& tr, int ctx, bool zero, int* eob) {
-  const uint4 zn = *reinterpret_cast<const uint4*>(tr.zero);  // zero[0..3], nz[0..3]
-  const uint2 ew = *reinterpret_cast<const uint2*>(tr.eob);
-  const int sh = 16 * ctx;
-  const uint64_t zw = (uint64_t)zn.y << 32 | zn.x, nw = (uint64_t)zn.w << 32 | zn.z, e64 = (uint64_t)ew.y << 32 | ew.x;
-  *eob = (int)((e64 >> sh) & 0xffff);
-  return (int)(((zero ? zw : nw) >> sh) & 0xffff);
-}
-
 // TokenCostForCoeffs (encode_quant.go:154-223), branch-free: the context of
 // every position follows from the levels alone (min(|q|, 2) of the previous
 // one), so all table reads are independent and issue back to back.
@@ -251,20 +242,19 @@ __device__ __forceinline__ int lvl_at(const int16_t* q, int i) { return q[i]; }
 __device__ __forceinline__ int lvl_at(const Q16& q, int i) { return q.get(i); }
 template <typename QT>
 __device__ __forceinline__ int token_cost(const Tables& t, const QT& q, int nz_count, int type, int ctx0, int first) {
-  int cost = 0, ctx = ctx0;
+  int cost = 0, ctx = ctx0, ctx_eob = ctx0;
   const int eob_at = max(nz_count, first);
 #pragma unroll
   for (int n = 0; n < 16; n++) {
     if (n < first) continue;
-    const TokRow& tr = t.tok[type * 8 + kBand[n]];
     const int v = abs(lvl_at(q, kZig[n]));
-    const uint64_t vw = t.vcost[type * 8 + kBand[n]][min(v, 67)];
-    int eob;
-    const int base = tok_costs(tr, ctx, v == 0, &eob);
-    const int tokc = v == 0 ? base : base + t.lfixed[min(v, 2047)] + vc_of(vw, ctx);
-    cost += n < nz_count ? tokc : (n == eob_at ? eob : 0);
+    const int tokc = vc_of(t.vcost[type * 8 + kBand[n]][min(v, 67)], ctx) + t.lfixed[min(v, 2047)];
+    cost += n < nz_count ? tokc : 0;
+    ctx_eob = n == eob_at ? ctx : ctx_eob;
     ctx = min(v, 2);
   }
+  // EOB at position eob_at (none after position 15)
+  if (eob_at < 16) cost += t.tok[type * 8 + band_of(eob_at)].eob[ctx_eob];
   return cost;
 }
 
@@ -304,7 +294,7 @@ __device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, c
   const int e0 = c0 - L0 * quant, e1 = c0 - (L0 + 1) * quant;
   const int64_t A0 = (int64_t)t.lfixed[L0] * lam16 + (int64_t)w4096 * (e0 * e0 - c0 * c0) + (has0 ? 0 : BIG);
   const int64_t A1 = (int64_t)t.lfixed[min(L0 + 1, 2047)] * lam16 + (int64_t)w4096 * (e1 * e1 - c0 * c0) + (has1 ? 0 : BIG);
-  const TokRow& tr = t.tok[CTX_TYPE * 8 + band];
+  const uint64_t vz = t.vcost[CTX_TYPE * 8 + band][0];
   const uint64_t v0 = t.vcost[CTX_TYPE * 8 + band][min(L0, 67)], v1 = t.vcost[CTX_TYPE * 8 + band][min(L0 + 1, 67)];
   // rows by end context: L0 = 0 sends level 1 (= L0 + 1) to context 1 and
   // nothing to context 2; otherwise L0 -> R1, L0 + 1 -> R2 (trellis_dp4
@@ -312,9 +302,9 @@ __device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, c
   const bool z = L0 == 0;
 #pragma unroll
   for (int pc = 0; pc < 3; pc++) {
-    const int64_t r1 = (int64_t)(tr.nz[pc] + vc_of(v0, pc)) * lam16 + A0 + 2 * pc;
-    const int64_t r2 = (int64_t)(tr.nz[pc] + vc_of(v1, pc)) * lam16 + A1 + 2 * pc + 1;
-    out.x[0][pc] = (int64_t)tr.zero[pc] * lam16 + pc;
+    const int64_t r1 = (int64_t)vc_of(v0, pc) * lam16 + A0 + 2 * pc;
+    const int64_t r2 = (int64_t)vc_of(v1, pc) * lam16 + A1 + 2 * pc + 1;
+    out.x[0][pc] = (int64_t)vc_of(vz, pc) * lam16 + pc;
     out.x[1][pc] = z ? r2 : r1;
     out.x[2][pc] = z ? BIG : r2;
   }
@@ -452,14 +442,10 @@ template <int TYPE>
 __device__ __forceinline__ int token_cost_pos(const Tables& t, const int16_t* q, int n, int nz_count, int ctx0, int first) {
   if (n < first) return 0;
   const int band = band_of(n);
-  const TokRow& tr = t.tok[TYPE * 8 + band];
   const int v = abs((int)q[zig_of(n)]);
   const int ctx = n == first ? ctx0 : min(abs((int)q[zig_of(max(n - 1, 0))]), 2);
-  const uint64_t vw = t.vcost[TYPE * 8 + band][min(v, 67)];
-  int eob;
-  const int base = tok_costs(tr, ctx, v == 0, &eob);
-  const int tokc = v == 0 ? base : base + t.lfixed[min(v, 2047)] + vc_of(vw, ctx);
-  return n < nz_count ? tokc : (n == max(nz_count, first) ? eob : 0);
+  if (n < nz_count) return vc_of(t.vcost[TYPE * 8 + band][min(v, 67)], ctx) + t.lfixed[min(v, 2047)];
+  return n == max(nz_count, first) ? t.tok[TYPE * 8 + band].eob[ctx] : 0;
 }
 
 // min over the 16 lanes of a DPP row, result in every lane of the row
@@ -851,8 +837,15 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
   for (int i = tid; i < 4 * 8 * 68; i += NT) {
     const int tb = i / 68, level = i % 68;
     uint64_t w = 0;
-    for (int c = 0; c < 3; c++)
-      if (level > 0) w |= (uint64_t)variable_level_cost(t, level, t.proba + (tb * 3 + c) * 11) << (16 * c);
+    for (int c = 0; c < 3; c++) {
+      const uint8_t* p = t.proba + (tb * 3 + c) * 11;
+      // the whole token cost of a level at this (type, band, context) but
+      // its fixed part: zero token for level 0, else the non-zero prefix +
+      // variableLevelCost (encode_quant.go:170-220, 258-273)
+      const int cost = level == 0 ? ecost(t, 255 - p[0]) + ecost(t, p[1])
+                                  : ecost(t, 255 - p[0]) + ecost(t, 255 - p[1]) + variable_level_cost(t, level, p);
+      w |= (uint64_t)cost << (16 * c);
+    }
     t.vcost[tb][level] = w;
   }
   if (tid < 4 * 8) {
