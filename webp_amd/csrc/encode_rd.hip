@@ -162,8 +162,6 @@ struct Shared {
   alignas(16) uint32_t handoff[12];  // the 48-B hand-off record, staged for three 16-B write-through stores
   uint8_t modes4[16];
   uint8_t nzy[16], nzuv[8];
-  int dcin[4][16];
-  int dcout[4][16];
   int mode_rate[4], mode_disto[4];
   int blk_rate[16], blk_disto[16], blk_hdr[16];
   int co_buf[16][16];      // transform coefficients handed to the trellis prep lanes
@@ -446,6 +444,99 @@ __device__ __forceinline__ int token_cost_pos(const Tables& t, const int16_t* q,
   const int ctx = n == first ? ctx0 : min(abs((int)q[zig_of(max(n - 1, 0))]), 2);
   if (n < nz_count) return vc_of(t.vcost[TYPE * 8 + band][min(v, 67)], ctx) + t.lfixed[min(v, 2047)];
   return n == max(nz_count, first) ? t.tok[TYPE * 8 + band].eob[ctx] : 0;
+}
+
+template <int WIDTH>
+__device__ __forceinline__ int group_sum_first(int v);
+// ---- the I16 DC path (Walsh-Hadamard, quantise, cost, dequantise, inverse)
+// lane-parallel over a 16-lane DPP row: lane b holds coefficient b (raster)
+// of one 4x4 DC block.  Every WHT pass is four butterflies whose outputs are
+// +-sums of four inputs; kWhtSign[p] gives the signs (bit k: input k
+// negative) of output pattern p for the row and column passes of both
+// transforms (transforms.go:500-531 forward, :232-252 inverse).
+constexpr uint32_t kWhtSign[4] = {0x0, 0xC, 0x6, 0xA};
+__device__ __forceinline__ int sum4_signed(const int v[4], uint32_t m) {
+  return (m & 1 ? -v[0] : v[0]) + (m & 2 ? -v[1] : v[1]) + (m & 4 ? -v[2] : v[2]) + (m & 8 ? -v[3] : v[3]);
+}
+// the lane's quad (lanes 4r..4r+3 of the row): q[m] = value of lane 4r + m
+__device__ __forceinline__ void quad4(int v, int q[4]) {
+  q[0] = quad_bcast32<0>(v);
+  q[1] = quad_bcast32<1>(v);
+  q[2] = quad_bcast32<2>(v);
+  q[3] = quad_bcast32<3>(v);
+}
+// the lane's column (lanes c, 4 + c, 8 + c, 12 + c), rotated: v4[d] = value of
+// lane (b + 4d) & 15, i.e. of row (r + d) & 3
+__device__ __forceinline__ void col4(int v, int v4[4]) {
+  v4[0] = v;
+  v4[1] = __builtin_amdgcn_update_dpp(0, v, 0x12C, 0xf, 0xf, false);  // row_ror:12: lane b <- b + 4
+  v4[2] = __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  v4[3] = __builtin_amdgcn_update_dpp(0, v, 0x124, 0xf, 0xf, false);  // row_ror:4:  lane b <- b + 12
+}
+// sign mask of absolute inputs re-indexed for col4's rotation by `own`
+__device__ __forceinline__ uint32_t rot_sign(uint32_t m, int own) { return ((m | m << 4) >> own) & 15; }
+// FTransformWHT output b of the row's 16 DC inputs (int16 like the reference)
+__device__ __forceinline__ int fwht_lane(int in, int b) {
+  const int r = b >> 2, c = b & 3;
+  int q[4], v4[4];
+  quad4(in, q);
+  col4(sum4_signed(q, kWhtSign[c]), v4);  // row pass: tmp[4r + c]
+  return (int16_t)(sum4_signed(v4, rot_sign(kWhtSign[r], r)) >> 1);
+}
+// TransformWHT (inverse) output b of the row's 16 dequantised inputs
+__device__ __forceinline__ int iwht_lane(int in, int b) {
+  const int k = b >> 2, i = b & 3;
+  int v4[4], q[4];
+  col4(in, v4);
+  quad4(sum4_signed(v4, rot_sign(kWhtSign[k], k)), q);  // column pass: tmp[4k + i]
+  return (int16_t)((sum4_signed(q, kWhtSign[i]) + 3) >> 3);
+}
+// QuantizeCoeffs of coefficient b alone (encode_quant.go:16-75)
+__device__ __forceinline__ int quantize_one(int v, int b, const SQuant& sq) {
+  const int4 h = b == 0 ? *reinterpret_cast<const int4*>(&sq.dc_quant) : *reinterpret_cast<const int4*>(&sq.quant);
+  const int sign = v < 0 ? -1 : 1;
+  const int a = max(abs(v) + sq.sharpen[b], 0);
+  const int c = min((int)(((uint32_t)a * (uint32_t)h.y + (uint32_t)h.z) >> 17), 2047);
+  return sign * c;
+}
+// max over the 16 lanes of a DPP row, in every lane of the row
+__device__ __forceinline__ int row_max(int v) {
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false));  // row_mirror
+  return v;
+}
+constexpr uint64_t pack_rzig() {
+  uint64_t v = 0;
+  for (int i = 0; i < 16; i++) v |= (uint64_t)kRZig[i] << (4 * i);
+  return v;
+}
+__device__ __forceinline__ int rzig_of(int n) { return (int)((pack_rzig() >> (4 * n)) & 15); }
+// The Y2 (DC) block of an I16 macroblock, lane-parallel (pickBestI16ModeRD
+// :640-660 and encodeResiduals's DC part): lane b of a 16-lane row passes
+// its 4x4 block's DC coefficient and gets back the block's reconstructed DC
+// (the inverse WHT of the dequantised levels).  *q = level b; *nz = the
+// block's zigzag nz count and *cost = its TokenCostForCoeffs (type 1) --
+// *nz in every lane of the row, *cost in the row's first lane.
+__device__ __forceinline__ int dc_block_lane(const Tables& t, int dc_in, int lane, const SQuant& y2, int ctx0, int* q,
+                                             int* nz, int* cost) {
+  const int b = lane & 15, base = lane & ~15;
+  const int lv = quantize_one(fwht_lane(dc_in, b), b, y2);
+  const int nzc = row_max(lv != 0 ? rzig_of(b) + 1 : 0);
+  // lane b = zigzag position b of the token cost
+  const int v = abs(__shfl(lv, base + zig_of(b), 64));
+  const int prev = abs(__shfl(lv, base + zig_of(max(b - 1, 0)), 64));
+  const int ctx = b == 0 ? ctx0 : min(prev, 2);
+  const int band = band_of(b);
+  int tc = 0;
+  if (b < nzc) tc = vc_of(t.vcost[8 + band][min(v, 67)], ctx) + t.lfixed[min(v, 2047)];
+  else if (b == nzc) tc = t.tok[8 + band].eob[ctx];
+  *q = lv;
+  *nz = nzc;
+  *cost = group_sum_first<16>(tc);
+  const int2 qq = make_int2(y2.quant, y2.dc_quant);
+  return iwht_lane((int16_t)(lv * (b == 0 ? qq.y : qq.x)), b);
 }
 
 // min over the 16 lanes of a DPP row, result in every lane of the row
@@ -1001,14 +1092,14 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
       const bool mvalid = !((m == 2 && mby == 0) || (m == 3 && mbx == 0) || (m == 1 && (mbx == 0 || mby == 0)));
       P4 src16, pred16;
       Q16 q16;
-      int nz16 = 0;
+      int nz16 = 0, dc_in = 0;
       {
         const int off = YOFF + 4 * by * BPS + 4 * bx;
         src16 = ld4(s.yin + off);
         pred16 = predsq_p(check_mode(mbx, mby, m), s.yout + YOFF, 16, 4 * bx, 4 * by);
         int co[16];
         fdct_p(src16, pred16, co);
-        s.dcin[m][b] = co[0];
+        dc_in = co[0];
         co[0] = 0;
         nz16 = quantize(co, q16, sg.y1, 1);
       }
@@ -1024,37 +1115,19 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
         bool acnz = false;
 #pragma unroll
         for (int i = 1; i < 16; i++) acnz |= q16.get(i) != 0;
-        lds_sync();
-        // one lane per mode: WHT path
-        if (b == 0 && mvalid) {
-          int dcv[16], qdc_i[16];
-          int16_t wht[16], qdc[16];
-#pragma unroll
-          for (int i = 0; i < 16; i++) dcv[i] = s.dcin[m][i];
-          fwht(dcv, wht);
-#pragma unroll
-          for (int i = 0; i < 16; i++) qdc_i[i] = wht[i];
-          const int nzdc = quantize(qdc_i, qdc, sg.y2, 0);
-          const int dc_ctx = min(top_nz_dc + left_nz_dc, 2);
-          s.mode_rate[m] = vp8_mode_fixed_cost16[m] + token_cost(t, qdc, nzdc, 1, dc_ctx, 0);
-          int dq[16];
-          dequant(qdc, dq, sg.y2);
-          int16_t whto[16];
-          iwht(dq, whto);
-#pragma unroll
-          for (int i = 0; i < 16; i++) s.dcout[m][i] = whto[i];
-        }
-        lds_sync();
+        // the mode's DC block (WHT path), lane-parallel over its 16 lanes
+        int dcq = 0, dcnz = 0, dccost = 0;
+        const int dcrec = dc_block_lane(t, dc_in, lane, sg.y2, min(top_nz_dc + left_nz_dc, 2), &dcq, &dcnz, &dccost);
         int dq[16];
         dequant(q16, dq, sg.y1);
-        dq[0] = s.dcout[m][b];
+        dq[0] = dcrec;
         const P4 rec16 = recon_p(pred16, dq);
         const int sse = sse_p(src16, rec16);
         const int td = sg.tlambda_sd > 0 ? tdisto_p(src16, rec16) : 0;
         const int rsum = group_sum_first<16>(rate), ssum = group_sum_first<16>(sse), tsum = group_sum_first<16>(td);  // used by lane b == 0
         const unsigned long long acmask = __ballot(acnz);
         if (b == 0 && mvalid) {
-          const int total_rate = s.mode_rate[m] + rsum;
+          const int total_rate = vp8_mode_fixed_cost16[m] + dccost + rsum;
           int disto = ssum;
           if (sg.tlambda_sd > 0) disto += (sg.tlambda_sd * tsum + 128) >> 8;
           if (src_flat && ((acmask >> (16 * m)) & 0xffffull) == 0) disto *= 2;
@@ -1399,18 +1472,23 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
       ESTAMP(5);
       // ================= final residuals (encodeResidualsParallel :1166-1356) =================
       uint32_t nzy_mask = 0, nzuv_mask = 0;
-      int nz_dc = 0;
+      int nz_dc = 0, dc_rec = 0;  // dc_rec: lane b's reconstructed DC (I16)
       if (!is_i4) {
+        int dc_nz = 0;
         if (lane < 16) {
           const int off = YOFF + 4 * by * BPS + 4 * bx;
           int src[16], pred[16], co[16];
           load4x4(s.yin + off, src);
           load4x4(s.yout + off, pred);
           fdct(src, pred, co);
-          s.dcin[0][lane] = co[0];
 #pragma unroll
           for (int i = 1; i < 16; i++) s.co_buf[lane][i] = co[i];
+          // the Y2 block, lane-parallel over lanes 0..15
+          int dcq = 0, dccost = 0;
+          dc_rec = dc_block_lane(t, co[0], lane, sg.y2, 0, &dcq, &dc_nz, &dccost);
+          s.coeffs[384 + lane] = (int16_t)dcq;
         }
+        nz_dc = __builtin_amdgcn_readfirstlane(dc_nz);
         lds_sync();
         // Trellis of the 16 AC blocks.  A block's DP depends on its left / top
         // neighbours' nz only through its initial context min(l + t, 2), so
@@ -1497,21 +1575,6 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
           }
           lds_sync();
         }
-        if (lane == 0) {
-          int dcv[16], qi[16];
-          int16_t wht[16], qdc[16];
-#pragma unroll
-          for (int i = 0; i < 16; i++) dcv[i] = s.dcin[0][i];
-          fwht(dcv, wht);
-#pragma unroll
-          for (int i = 0; i < 16; i++) qi[i] = wht[i];
-          const int nzdc = quantize(qi, qdc, sg.y2, 0);
-#pragma unroll
-          for (int i = 0; i < 16; i++) s.coeffs[384 + i] = qdc[i];
-          s.word = nzdc;
-        }
-        lds_sync();
-        nz_dc = s.word;
       }
       for (int i = 0; i < 16; i++) nzy_mask |= (s.nzy[i] > 0 ? 1u : 0u) << i;
       if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
@@ -1534,17 +1597,6 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
       ESTAMP(6);
       // ================= reconstruction (reconstructMBParallel :1358-1410) =================
       if (!is_i4) {
-        if (lane == 0) {
-          int dq[16];
-          int16_t qdc[16], whto[16];
-#pragma unroll
-          for (int i = 0; i < 16; i++) qdc[i] = s.coeffs[384 + i];
-          dequant(qdc, dq, sg.y2);
-          iwht(dq, whto);
-#pragma unroll
-          for (int i = 0; i < 16; i++) s.dcout[0][i] = whto[i];
-        }
-        lds_sync();
         if (lane < 16) {
           const int off = YOFF + 4 * by * BPS + 4 * bx;
           int16_t q[16];
@@ -1552,7 +1604,7 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
 #pragma unroll
           for (int i = 0; i < 16; i++) q[i] = s.coeffs[lane * 16 + i];
           dequant(q, dq, sg.y1);
-          dq[0] = s.dcout[0][lane];
+          dq[0] = dc_rec;
           load4x4(s.yout + off, pred);
           recon4(pred, dq, rec);
           store4x4(s.yout + off, rec);
