@@ -163,11 +163,10 @@ struct Shared {
   uint8_t modes4[16];
   uint8_t nzy[16], nzuv[8];
   int mode_rate[4], mode_disto[4];
-  int blk_rate[16], blk_disto[16], blk_hdr[16];
   int co_buf[16][16];      // transform coefficients handed to the trellis prep lanes
   TRec trec[6][16];        // trellis position records: I4 (half, candidate) / final I16 (diagonal slot)
   int l0s[6][16];          // per position: L0 << 3 | negative << 2 | min(L0, 2)
-  int16_t cand_q[6][16];   // I4 candidates' levels for the lane-parallel token cost
+  alignas(16) int16_t cand_q[6][16];  // I4 candidates' levels for the lane-parallel token cost
   int cand_nz[6], cand_rate[6];
   alignas(16) uint8_t pv[2][64];  // per half-wave: the I4 block's prediction value table
   int word;
@@ -539,6 +538,13 @@ __device__ __forceinline__ int dc_block_lane(const Tables& t, int dc_in, int lan
   return iwht_lane((int16_t)(lv * (b == 0 ? qq.y : qq.x)), b);
 }
 
+// lane L of each 16-lane DPP row, broadcast to the row (row_newbcast, gfx90a+)
+template <int L>
+__device__ __forceinline__ uint64_t row_bcast64(uint64_t v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x150 + L, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x150 + L, 0xf, 0xf, false);
+  return (uint64_t)(uint32_t)hi << 32 | (uint32_t)lo;
+}
 // min over the 16 lanes of a DPP row, result in every lane of the row
 __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
@@ -1344,52 +1350,54 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
             tok_rate = half ? pick3(qc, r10, r11, r12) : pick3(qc, r00, r01, r02);
           }
           uint64_t score = ~0ull;
-          int rate = 0;
+          int rate = 0, hdr = 0;
           if (qact) {
+            hdr = t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];
             rate = (qmode > 0 && cnt <= 3) ? 140 : 0;
-            rate += tok_rate;
-            rate += t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];
+            rate += tok_rate + hdr;
             score = rd_score(disto, rate, sg.lambda_i4);
             CSTAMP(3);
           }
           SSTAMP(2);
-          // first minimum over this half's candidates (strict '<' in candidate order)
+          // first minimum over this half's candidates (strict '<' in candidate
+          // order): candidate c's score sits in lane 32 * half + 4c, i.e. lane
+          // 4c of the half's first DPP row, broadcast to the row
           int win = 0;
-          uint64_t wsc = __shfl(score, half * 32, 64);
-#pragma unroll
-          for (int i = 1; i < 3; i++) {
-            const uint64_t sc = __shfl(score, half * 32 + 4 * i, 64);
-            if (i < K && sc < wsc) {
-              wsc = sc;
-              win = i;
+          {
+            const uint64_t sc0 = row_bcast64<0>(score), sc1 = row_bcast64<4>(score), sc2 = row_bcast64<8>(score);
+            uint64_t wsc = sc0;
+            if (1 < K && sc1 < wsc) {
+              wsc = sc1;
+              win = 1;
             }
+            if (2 < K && sc2 < wsc) win = 2;
           }
           if (qact && qc == win) {  // the winning quad: row qr of the reconstruction, 4 levels each
             *reinterpret_cast<uint32_t*>(s.yout2 + off + qr * BPS) = rec_row;
-#pragma unroll
-            for (int k = 0; k < 4; k++) s.coeffs[blk * 16 + 4 * qr + k] = qv[4 * qr + k];
+            // levels 4qr..4qr+3 straight from the candidate's LDS row (a
+            // lane-varying index into qv[] would be a 16-way select)
+            *reinterpret_cast<uint2*>(s.coeffs + blk * 16 + 4 * qr) = *reinterpret_cast<const uint2*>(&s.cand_q[qsl][4 * qr]);
             if (qr == 0) {
               s.modes4[blk] = (uint8_t)qmode;
               s.nzy[blk] = (uint8_t)qnz;
-              s.blk_rate[blk] = rate;
-              s.blk_disto[blk] = disto;
-              s.blk_hdr[blk] = t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];
             }
           }
-          lds_sync();
           {
-            const int b0 = st <= 3 ? st : 4 * ((st - 2) >> 1) + (st & 1) + 2;  // half 0's block
-            run_rate += s.blk_rate[b0];
-            run_disto += s.blk_disto[b0];
-            run_header += s.blk_hdr[b0];
-            if (st >= 2 && st <= 7) {  // half 1's block: (st & 1, by of half 0 + 1)
-              const int b1 = b0 + 4 - 2;
-              run_rate += s.blk_rate[b1];
-              run_disto += s.blk_disto[b1];
-              run_header += s.blk_hdr[b1];
+            // the winners' rate, distortion and header bits, read from their
+            // lanes (the half's winner index is uniform over the half)
+            const int w0 = 4 * __builtin_amdgcn_readfirstlane(win);
+            run_rate += __builtin_amdgcn_readlane(rate, w0);
+            run_disto += __builtin_amdgcn_readlane(disto, w0);
+            run_header += __builtin_amdgcn_readlane(hdr, w0);
+            if (st >= 2 && st <= 7) {  // half 1 holds a block
+              const int w1 = 32 + 4 * __builtin_amdgcn_readlane(win, 32);
+              run_rate += __builtin_amdgcn_readlane(rate, w1);
+              run_disto += __builtin_amdgcn_readlane(disto, w1);
+              run_header += __builtin_amdgcn_readlane(hdr, w1);
             }
             early = rd_score(run_disto, run_rate + 211, sg.lambda_mode) >= s16 || run_header > 15000;
           }
+          lds_sync();
           SSTAMP(3);
         }
         s4 = early ? ~0ull : rd_score(run_disto, run_rate + 211, sg.lambda_mode);
