@@ -748,30 +748,32 @@ __device__ __forceinline__ void pred4_block(int mode, const uint8_t* buf, int of
   for (int r = 0; r < 4; r++) unpack_rows(pred4_row(mode, r, X, T, L), pred + 4 * r);
 }
 // Build the block's value table V (see kPred4Code) from the context around
-// buf + off: lane i (< 32 of the caller's half-wave) fills its entries in
-// two LDS passes.  The caller syncs after each pass (`pass` 0 then 1).
-__device__ __forceinline__ void pred4_values(const uint8_t* buf, int off, int i, uint8_t* v, int pass) {
+// buf + off in one pass of the caller's half-wave (lane i < 32): lanes 0..14
+// load the edge E[i] and take their neighbours' by DPP row shifts for the
+// pair / triple averages, lane 15 the DC, lanes 16..31 the TM values.  The
+// caller syncs once after it.
+__device__ __forceinline__ void pred4_values(const uint8_t* buf, int off, int i, uint8_t* v) {
   const uint8_t* d = buf + off;
-  if (pass == 0) {
-    if (i < 15) {  // E: L L K J I X A..H H
-      const int src = i <= 1 ? -1 + 3 * BPS : (i <= 4 ? -1 + (4 - i) * BPS : (i == 5 ? -1 - BPS : -BPS + min(i - 6, 7)));
-      v[i] = d[src];
-    } else if (i == 15) {
-      int sum = 4;
+  int e = 0;
+  if (i < 15) {  // E: L L K J I X A..H H
+    const int src = i <= 1 ? -1 + 3 * BPS : (i <= 4 ? -1 + (4 - i) * BPS : (i == 5 ? -1 - BPS : -BPS + min(i - 6, 7)));
+    e = d[src];
+  }
+  // E[i + 1] and E[i - 1] (lanes 0..15 are one DPP row of the half-wave)
+  const int en = __builtin_amdgcn_update_dpp(0, e, 0x101, 0xf, 0xf, false);  // row_shl:1: lane i <- i + 1
+  const int ep = __builtin_amdgcn_update_dpp(0, e, 0x111, 0xf, 0xf, false);  // row_shr:1: lane i <- i - 1
+  if (i < 15) {
+    v[i] = (uint8_t)e;
+    if (i < 14) v[16 + i] = (uint8_t)avg2(e, en);
+    if (i >= 1 && i <= 13) v[32 + i] = (uint8_t)avg3(ep, e, en);
+  } else if (i == 15) {
+    int sum = 4;
 #pragma unroll
-      for (int k = 0; k < 4; k++) sum += d[k - BPS] + d[-1 + k * BPS];
-      v[47] = (uint8_t)(sum >> 3);
-    } else {  // TM of pixel p = i - 16
-      const int p = i - 16, x = p & 3, y = p >> 2;
-      v[48 + p] = (uint8_t)clip8(d[-1 + y * BPS] + d[x - BPS] - d[-1 - BPS]);
-    }
-  } else {
-    if (i < 14) {
-      v[16 + i] = (uint8_t)avg2(v[i], v[i + 1]);
-    } else if (i >= 16 && i < 29) {
-      const int c = i - 15;  // 1..13
-      v[32 + c] = (uint8_t)avg3(v[c - 1], v[c], v[c + 1]);
-    }
+    for (int k = 0; k < 4; k++) sum += d[k - BPS] + d[-1 + k * BPS];
+    v[47] = (uint8_t)(sum >> 3);
+  } else {  // TM of pixel p = i - 16
+    const int p = i - 16, x = p & 3, y = p >> 2;
+    v[48 + p] = (uint8_t)clip8(d[-1 + y * BPS] + d[x - BPS] - d[-1 - BPS]);
   }
 }
 __device__ __forceinline__ void pred4_lut(const uint8_t* code, const uint8_t* v, int pred[16]) {
@@ -1201,9 +1203,7 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
           load4x4(s.yin + off, src);
           SSTAMP(-1);
           // pre-screen all eligible modes by prediction SSE (lanes 0-9 of each half)
-          pred4_values(s.yout2, off, hl, s.pv[half], 0);
-          lds_sync();
-          pred4_values(s.yout2, off, hl, s.pv[half], 1);
+          pred4_values(s.yout2, off, hl, s.pv[half]);
           lds_sync();
           int sse_lane = 0;
           if (bvalid && hl < 10) {
