@@ -1004,10 +1004,16 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
       const int lane = opaque_lane();
       const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
       ESTAMP(0);
-      // ---- wait for the row above (MB x+1 done) ----
-      if (mby > 0) {
-        const int need = min(mbx + 2, mbw);
-        if (seen < need) {
+      // ---- wait for the row above ----
+      // The reference starts MB x of row y once row y-1 has finished MB x+1
+      // (encode_parallel.go:286-295); only the I4 blocks on the right edge
+      // (3, 7, 11, 15) read MB x+1 of the row above (its first 4 bottom
+      // pixels, the top-right context), and the first of them runs at I4
+      // step 3.  So the MB starts once MB x of the row above is done, and
+      // waits for MB x+1 only there (wait_above(mbx + 2)): the outputs are
+      // the reference's, the rows just trail each other by less.
+      auto wait_above = [&](int need) {
+        if (mby > 0 && seen < need) {
           int v = 0;
           if (lane == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -1025,7 +1031,8 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
           }
           seen = __shfl(v, 0, 64);
         }
-      }
+      };
+      wait_above(mbx + 1);
       ESTAMP(1);
       const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
       const Segment& sg = s.seg[segid];
@@ -1055,10 +1062,7 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
             const uint32_t w = ld_sc1_32(rec + 4 * lane);
             const int o = lane < 4 ? YOFF - BPS + 4 * lane : (lane < 6 ? UOFF - BPS + 4 * (lane - 4) : VOFF - BPS + 4 * (lane - 6));
             *reinterpret_cast<uint32_t*>(s.yout + o) = w;
-          } else if (lane == 8) {  // top-right
-            const uint32_t tr = mbx < mbw - 1 ? ld_sc1_32(rec + REC) : 0x01010101u * (ld_sc1_32(rec + 12) >> 24);
-            *reinterpret_cast<uint32_t*>(s.yout + YOFF - BPS + 16) = tr;
-          }
+          }  // (the top-right: at I4 step 3)
           top_nz = ld_sc1_32(rec + 32);
           top_modes = ld_sc1_32(rec + 36);
           top_nz_dc = (int)ld_sc1_32(rec + 40);
@@ -1070,11 +1074,6 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
         if (lane == 37) s.yout[YOFF - BPS - 1] = (mbx > 0 && mby > 0) ? tl_y : (mby > 0 ? 129 : 127);
         if (lane == 38) s.yout[UOFF - BPS - 1] = (mbx > 0 && mby > 0) ? tl_u : (mby > 0 ? 129 : 127);
         if (lane == 39) s.yout[VOFF - BPS - 1] = (mbx > 0 && mby > 0) ? tl_v : (mby > 0 ? 129 : 127);
-      }
-      lds_sync();
-      if (lane < 12) {  // replicate the top-right into rows 3, 7, 11
-        const int r = 4 * (lane / 4 + 1) - 1, i = lane & 3;
-        s.yout[YOFF - BPS + 16 + (r + 1) * BPS + i] = s.yout[YOFF - BPS + 16 + i];
       }
       lds_sync();
       // scalar copies of the neighbour context
@@ -1187,6 +1186,26 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
           Shared& s = launder(s_waves[wave]);
           Tables& t = launder(t_lds);
           const int lane = opaque_lane();
+          if (st == 3) {
+            // the top-right context of block 3 (MB x+1 of the row above, or
+            // its last top pixel repeated at the right edge; 127 on the first
+            // row from the context fill) and its copies beside rows 3, 7, 11
+            // for blocks 7, 11, 15 (fillPredContextParallel :455-562)
+            if (mby > 0) {
+              if (mbx < mbw - 1) wait_above(mbx + 2);
+              if (lane == 0) {
+                const uint32_t tr = mbx < mbw - 1 ? ld_sc1_32(top + (mbx + 1) * REC)
+                                                  : 0x01010101u * s.yout2[YOFF - BPS + 15];
+                *reinterpret_cast<uint32_t*>(s.yout2 + YOFF - BPS + 16) = tr;
+              }
+              lds_sync();
+            }
+            if (lane < 12) {
+              const int r = 4 * (lane / 4 + 1) - 1, i = lane & 3;
+              s.yout2[YOFF - BPS + 16 + (r + 1) * BPS + i] = s.yout2[YOFF - BPS + 16 + i];
+            }
+            lds_sync();
+          }
           const int half = lane >> 5, hl = lane & 31;
           const int wy = (st <= 3 ? 0 : (st - 2) >> 1) + half, wx = st - 2 * wy;
           const bool bvalid = wy <= 3 && wx >= 0 && wx <= 3;
