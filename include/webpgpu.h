@@ -145,8 +145,11 @@ int wg_vp8_parse(const uint8_t* data, size_t size, int32_t* dims, wg_mb_info* mb
                  int64_t max_mbs);
 
 /* Encoder macroblock RD loop: Phase A of encodeFrameParallel
- * (internal/lossy/encode_parallel.go:168-1495; encodeRow :252-338), method
- * >= 4 (methods 4-6 run the same Phase A; method 3 returns WG_EINVAL).
+ * (internal/lossy/encode_parallel.go:168-1495; encodeRow :252-338), methods
+ * 3-6: methods 4-6 run the same Phase A (trellis quantisation in the I4 RD
+ * and the final I16 residuals, :793, :1202), method 3 quantises plainly
+ * there (pickBestI4ModeRDParallel :842-929).  Methods 0-2 return WG_EINVAL
+ * (encode.go:1356 encodes them with the serial encodeFrame).
  * Frames with mbh < 4 (height <= 48) return WG_EINVAL: EncodeFrame
  * (internal/lossy/encode.go:1356) encodes those with the serial encodeFrame.
  * out / work must be 16-byte aligned, the planes 4-byte aligned.

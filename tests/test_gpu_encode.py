@@ -1,10 +1,12 @@
-"""GPU parity: the encoder macroblock RD loop (Phase A, method 4) through the
+"""GPU parity: the encoder macroblock RD loop (Phase A, methods 4 and 3) through the
 C ABI vs the C restatement (oracle/lossy_rd.c): every MBEncInfo field
 (modes, levels, nz bookkeeping, skip, score) and the reconstruction,
 bit-exact.  Frames cover image edges (non-multiple-of-16 sizes), all four
 segments with different quantisers, fine / coarse quantisers (I4-heavy and
 I16-heavy), SNS on / off, quality < 50 (2 I4 RD candidates), a batch, and
-the 1920x1080 C2 frame.  Frames have mbh >= 4: smaller ones take the
+the 1920x1080 C2 frame; method 3 (plain quantisation instead of the trellis in
+the I4 RD and the final I16 residuals, encode_parallel.go:793, :1202, TLambdaSD
+0) on the same cases.  Frames have mbh >= 4: smaller ones take the
 reference's serial encodeFrame (encode.go:1356), which wg_encode_mbs refuses.
 
 test_encode_pipeline_* run the whole device encode path of frames.encode_frames
@@ -32,21 +34,21 @@ def planes(w, h, kind, seed):
     return O.import_rgba(gen(), has_alpha=False)
 
 
-def run(imgs, w, h, qs, sns=50, quality=75):
+def run(imgs, w, h, qs, sns=50, quality=75, method=4):
     n = len(imgs)
     mbw, mbh = frames.mb_dims(w, h)
-    segs = np.stack([O.setup_segment(q, sns_strength=sns) for q in qs])
+    segs = np.stack([O.setup_segment(q, method=method, sns_strength=sns) for q in qs])
     seg_ids = np.stack([((np.arange(mbw * mbh) * 7 + i) % 4).astype(np.uint8) for i in range(n)])
     proba = O.default_proba()
     Y = torch.from_numpy(np.stack([p[0] for p in imgs])).cuda()
     U = torch.from_numpy(np.stack([p[1] for p in imgs])).cuda()
     V = torch.from_numpy(np.stack([p[2] for p in imgs])).cuda()
     out, (RY, RU, RV) = frames.encode_mbs(Y, U, V, w, h, torch.from_numpy(seg_ids).cuda(), segs.view(frames.SEGMENT_DTYPE),
-                                          proba, quality=quality, check=True)
+                                          proba, method=method, quality=quality, check=True)
     got = out.cpu().numpy().view(frames.MB_ENC_DTYPE).reshape(n, mbw * mbh)
     RY, RU, RV = RY.cpu().numpy(), RU.cpu().numpy(), RV.cpu().numpy()
     for i, (y, u, v) in enumerate(imgs):
-        enc, ry, ru, rv = O.encode_frame_rd(y, u, v, w, h, seg_ids[i], segs, proba, method=4, quality=quality)
+        enc, ry, ru, rv = O.encode_frame_rd(y, u, v, w, h, seg_ids[i], segs, proba, method=method, quality=quality)
         for f in FIELDS:
             bad = np.argwhere(np.asarray(got[i][f] != enc[f]).reshape(len(enc), -1).any(axis=1))
             assert len(bad) == 0, f"image {i} field {f}: MBs {bad[:5].ravel()} (of {len(enc)})"
@@ -56,20 +58,31 @@ def run(imgs, w, h, qs, sns=50, quality=75):
 @pytest.mark.parametrize("w,h,kind,qs", [(16, 64, "noise", (20, 30, 40, 50)), (48, 64, "blobs", (10, 20, 30, 40)),
                                          (37, 61, "noise", (30, 30, 30, 30)), (80, 64, "grad", (60, 70, 80, 90)),
                                          (100, 64, "blobs", (5, 15, 100, 127))])
-def test_encode_matches_oracle(cuda, w, h, kind, qs):
-    run([planes(w, h, kind, seed=w)], w, h, qs)
+@pytest.mark.parametrize("method", [4, 3])
+def test_encode_matches_oracle(cuda, w, h, kind, qs, method):
+    run([planes(w, h, kind, seed=w)], w, h, qs, method=method)
 
 
-def test_encode_low_quality_and_no_sns(cuda):
-    run([planes(64, 64, "noise", 3)], 64, 64, (25, 35, 45, 55), sns=0, quality=30)
+@pytest.mark.parametrize("method", [4, 3])
+def test_encode_low_quality_and_no_sns(cuda, method):
+    run([planes(64, 64, "noise", 3)], 64, 64, (25, 35, 45, 55), sns=0, quality=30, method=method)
 
 
-def test_encode_batch(cuda):
-    run([planes(96, 80, k, s) for s, k in enumerate(("noise", "blobs", "grad"))], 96, 80, (20, 40, 60, 80))
+@pytest.mark.parametrize("method", [4, 3])
+def test_encode_batch(cuda, method):
+    run([planes(96, 80, k, s) for s, k in enumerate(("noise", "blobs", "grad"))], 96, 80, (20, 40, 60, 80), method=method)
 
 
-def test_encode_1080p(cuda):
-    run([planes(1920, 1080, "blobs", 7)], 1920, 1080, (30, 35, 40, 45))
+@pytest.mark.parametrize("method", [4, 3])
+def test_encode_1080p(cuda, method):
+    run([planes(1920, 1080, "blobs", 7)], 1920, 1080, (30, 35, 40, 45), method=method)
+
+
+def test_methods_below_3_refused(cuda):
+    """Methods 0-2 take the serial encodeFrame with non-RD mode choice (encode.go:1356)."""
+    from webp_amd._lib import WebpGpuError
+    with pytest.raises(WebpGpuError, match="methods 3-6"):
+        run([planes(64, 64, "noise", 3)], 64, 64, (25, 35, 45, 55), method=2)
 
 
 def test_small_frames_refused(cuda):
@@ -117,3 +130,10 @@ def test_encode_pipeline_presets(cuda):
     imgs = [synth.blobs_rgba(w, h, seed=5), synth.noise_rgba(w, h, seed=6)]
     pipeline(imgs, w, h, quality=30, sns_strength=80, filter_strength=35, filter_sharpness=4, preprocessing=1)
     pipeline(imgs, w, h, quality=90, sns_strength=0, segments=2)
+
+
+def test_encode_pipeline_method3(cuda):
+    """webp.Encode with Method 3 (the parallel Phase A without the trellis) on the C1 frame and noise."""
+    rgba = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "test_png_rgba.npz"))["rgba"]
+    pipeline([rgba], 768, 576, method=3)
+    pipeline([synth.noise_rgba(320, 240, seed=9), synth.gradient_rgba(320, 240)], 320, 240, method=3, quality=40)

@@ -1,6 +1,6 @@
 // encode_rd.hip -- the encoder's macroblock RD loop on gfx950 (SURVEY.md
 // 8(a) A20): Phase A of encodeFrameParallel (internal/lossy/
-// encode_parallel.go:168-1495), method >= 4, for whole frames.
+// encode_parallel.go:168-1495), methods 3-6 (method 3: plain quantisation instead of the trellis), for whole frames.
 //
 // Schedule: like decode.hip, one persistent launch; each 64-lane workgroup
 // dequeues a macroblock ROW (ordered counter over (row, image)) and walks it
@@ -920,6 +920,10 @@ __device__ unsigned long long g_enc_phase[16];
 #ifndef WG_ENC_OCC
 #define WG_ENC_OCC 2  // waves per SIMD (VGPR budget 512 / occupancy)
 #endif
+// TRELLIS: method >= 4 (trellis quantisation in the I4 RD and the final I16
+// residuals, encode_parallel.go:793, :1202); method 3 quantises plainly
+// (pickBestI4ModeRDParallel :842-929, QuantizeCoeffs at :1215).
+template <bool TRELLIS>
 __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs a) {
   __shared__ Tables t_lds;
   __shared__ Shared s_waves[WAVES];
@@ -1248,11 +1252,19 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
             int pred[16], co[16];
             pred4_lut(t.pcode[mode], s.pv[half], pred);
             fdct(src, pred, co);
+            if constexpr (TRELLIS) {
 #pragma unroll
-            for (int i = 0; i < 16; i++) s.co_buf[slot][i] = co[i];
+              for (int i = 0; i < 16; i++) s.co_buf[slot][i] = co[i];
+            } else {  // method 3: QuantizeCoeffs (pickBestI4ModeRDParallel :890)
+              int16_t q[16];
+              s.cand_nz[slot] = quantize(co, q, sg.y1, 0);
+#pragma unroll
+              for (int i = 0; i < 16; i++) s.cand_q[slot][i] = q[i];
+            }
             CSTAMP(0);
           }
           lds_sync();
+          if constexpr (TRELLIS) {
           // trellis positions: lane (candidate c, pair pp) prepares positions 2pp, 2pp + 1
           const int lam16 = sg.tlambda_i4 * 16;
           bool pnz = false;
@@ -1280,6 +1292,7 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
             }
           }
           lds_sync();
+          }  // TRELLIS
           // candidates: reconstruction + distortion on the candidate's lane quad
           // (lane 4c + r owns row r; the TDisto column pass reads the row pass
           // results back from LDS; sums are quad reductions)
@@ -1508,8 +1521,15 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
           load4x4(s.yin + off, src);
           load4x4(s.yout + off, pred);
           fdct(src, pred, co);
+          if constexpr (TRELLIS) {
 #pragma unroll
-          for (int i = 1; i < 16; i++) s.co_buf[lane][i] = co[i];
+            for (int i = 1; i < 16; i++) s.co_buf[lane][i] = co[i];
+          } else {  // method 3: the AC levels by QuantizeCoeffs (encodeI16ResidualsParallel :1215)
+            int16_t q[16];
+            s.nzy[lane] = (uint8_t)quantize(co, q, sg.y1, 1);
+#pragma unroll
+            for (int i = 0; i < 16; i++) s.coeffs[lane * 16 + i] = q[i];
+          }
           // the Y2 block, lane-parallel over lanes 0..15
           int dcq = 0, dccost = 0;
           dc_rec = dc_block_lane(t, co[0], lane, sg.y2, 0, &dcq, &dc_nz, &dccost);
@@ -1517,6 +1537,7 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
         }
         nz_dc = __builtin_amdgcn_readfirstlane(dc_nz);
         lds_sync();
+        if constexpr (TRELLIS) {
         // Trellis of the 16 AC blocks.  A block's DP depends on its left / top
         // neighbours' nz only through its initial context min(l + t, 2), so
         // it is run speculatively for every context the block can still get
@@ -1602,6 +1623,7 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
           }
           lds_sync();
         }
+        }  // TRELLIS
       }
       for (int i = 0; i < 16; i++) nzy_mask |= (s.nzy[i] > 0 ? 1u : 0u) << i;
       if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
@@ -1849,7 +1871,8 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
                              uint8_t* ry, uint8_t* ru, uint8_t* rv, void* work, void* stream) {
   WG_REQUIRE(y && u && v && segs && proba && out && ry && ru && rv && work);
   WG_REQUIRE(width > 0 && height > 0 && n_images > 0);
-  if (method < 4) return wg::invalid("wg_encode_mbs implements method >= 4 (the default); method 3 is not built");
+  // methods 0-2 take the serial encodeFrame with non-RD mode choice (encode.go:1356)
+  if (method < 3 || method > 6) return wg::invalid("wg_encode_mbs implements methods 3-6 (encode.go:1356 runs 0-2 serially)");
   const int mbw = (width + 15) >> 4, mbh = (height + 15) >> 4;
   // EncodeFrame (internal/lossy/encode.go:1356) runs the row-parallel Phase A
   // only for mbH >= 4; smaller frames take the serial encodeFrame (chroma DC
@@ -1905,12 +1928,15 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
     return wg::check_launch("hipMemsetAsync(encode ctl)");
   int cus = 0, per_cu = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows, 64 * WAVES, 0) != hipSuccess || per_cu <= 0)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows<true>, 64 * WAVES, 0) != hipSuccess || per_cu <= 0)
     return wg::check_launch("encode occupancy query");
   const int rows = n_images * mbh;
   const int wgs = (rows + WAVES - 1) / WAVES;  // each wave dequeues rows on its own
   const int grid = wgs < per_cu * cus ? wgs : per_cu * cus;
-  hipLaunchKernelGGL(k_encode_rows, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
+  if (method >= 4)
+    hipLaunchKernelGGL(k_encode_rows<true>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_encode_rows<false>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
   return wg::check_launch("k_encode_rows");
 }
 
