@@ -106,6 +106,7 @@ _SIGS = {
     "or_vp8l_inverse_predictor": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
     "or_vp8l_subtract_green": (None, [ctypes.c_void_p, ctypes.c_size_t]),
     "or_vp8l_add_green": (None, [ctypes.c_void_p, ctypes.c_size_t]),
+    "or_vp8l_decode": (_i, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "or_vp8l_color_space_transform": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p]),
     "or_vp8l_color_space_inverse": (None, [ctypes.c_void_p, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
     "or_vp8l_color_index_inverse": (None, [ctypes.c_void_p, _i, _i, _i, _i, ctypes.c_void_p, ctypes.c_void_p]),
@@ -321,6 +322,71 @@ def vp8l_color_index_inverse(palette, xbits, width, src, fill=0):
     out = np.full((h, width), fill, np.uint32)
     lib.or_vp8l_color_index_inverse(pal.ctypes.data, len(pal), xbits, width, h, src.ctypes.data, out.ctypes.data)
     return out
+
+
+class _VP8LInfo(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("has_alpha", ctypes.c_int), ("tw", ctypes.c_int),
+                ("n_transforms", ctypes.c_int), ("type", ctypes.c_int * 4), ("bits", ctypes.c_int * 4),
+                ("xsize", ctypes.c_int * 4), ("dsize", ctypes.c_int * 4)]
+
+
+VP8L_PREDICTOR, VP8L_CROSS_COLOR, VP8L_SUBTRACT_GREEN, VP8L_COLOR_INDEXING = range(4)
+
+
+def riff_chunk(data, fourcc):
+    """The payload of the first `fourcc` chunk of a RIFF/WEBP file."""
+    assert data[:4] == b"RIFF" and data[8:12] == b"WEBP"
+    off = 12
+    while off + 8 <= len(data):
+        size = int.from_bytes(data[off + 4:off + 8], "little")
+        if data[off:off + 4] == fourcc:
+            return data[off + 8:off + 8 + size]
+        off += 8 + size + (size & 1)
+    raise ValueError("no %r chunk" % fourcc)
+
+
+def vp8l_decode_entropy(data):
+    """Entropy-decode a VP8L stream (a .webp file or the bare payload) up to
+    the inverse transforms -> dict(width, height, tw, pixels (h, tw) uint32,
+    transforms=[dict(type, bits, xsize, data)] in bitstream order; predictor /
+    cross-colour data is the (tiles_y, tiles_x) sub-image, colour indexing
+    data the expanded palette)."""
+    payload = riff_chunk(data, b"VP8L") if data[:4] == b"RIFF" else data
+    buf = np.frombuffer(payload, np.uint8).copy()
+    info = _VP8LInfo()
+    assert lib.or_vp8l_decode(buf.ctypes.data, len(buf), ctypes.byref(info), None, None) == 0
+    h = info.height
+    pixels = np.zeros((h, info.tw), np.uint32)
+    tds = []
+    for k in range(info.n_transforms):
+        t, bits, xs = info.type[k], info.bits[k], info.xsize[k]
+        if t in (VP8L_PREDICTOR, VP8L_CROSS_COLOR):
+            tds.append(np.zeros((vp8l_subsample(h, bits), vp8l_subsample(xs, bits)), np.uint32))
+        else:
+            tds.append(np.zeros(max(info.dsize[k], 1), np.uint32))
+    ptrs = (ctypes.c_void_p * 4)(*[d.ctypes.data for d in tds], *([None] * (4 - len(tds))))
+    assert lib.or_vp8l_decode(buf.ctypes.data, len(buf), ctypes.byref(info), pixels.ctypes.data, ptrs) == 0
+    transforms = [dict(type=info.type[k], bits=info.bits[k], xsize=info.xsize[k], data=tds[k])
+                  for k in range(info.n_transforms)]
+    return dict(width=info.width, height=h, has_alpha=info.has_alpha, tw=info.tw, pixels=pixels,
+                transforms=transforms)
+
+
+def vp8l_apply_inverse(dec):
+    """applyInverseTransforms (decode_transform.go:134-156) with the
+    restatement's inverses, last-read transform first -> (h, w) ARGB."""
+    cur = dec["pixels"]
+    for t in reversed(dec["transforms"]):
+        if t["type"] == VP8L_PREDICTOR:
+            cur = vp8l_inverse_predictor(t["data"], t["bits"], cur)
+        elif t["type"] == VP8L_CROSS_COLOR:
+            cur = vp8l_color_space_inverse(t["data"], t["bits"], cur)
+        elif t["type"] == VP8L_SUBTRACT_GREEN:
+            cur = cur.copy()
+            lib.or_vp8l_add_green(cur.ctypes.data, cur.size)
+        else:
+            cur = vp8l_color_index_inverse(t["data"], t["bits"], t["xsize"], cur)
+    return cur
 
 
 # ---------------- alpha plane (SURVEY 8(f)#4) ----------------

@@ -165,6 +165,13 @@ void or_vp8l_color_space_inverse(const uint32_t* data, int bits, int width, int 
 void or_vp8l_color_index_inverse(const uint32_t* palette, int palette_size, int xbits, int width, int height,
                                  const uint32_t* src, uint32_t* dst);
 
+/* vp8l_dec.c: entropy decoding of a VP8L bitstream up to the inverse transforms */
+typedef struct {
+  int width, height, has_alpha, tw, n_transforms;
+  int type[4], bits[4], xsize[4], dsize[4];
+} or_vp8l_info;
+int or_vp8l_decode(const uint8_t* payload, size_t len, or_vp8l_info* info, uint32_t* pixels, uint32_t** tdata);
+
 /* alpha.c: alpha-plane filters and alpha processing */
 void or_alpha_filter(int filter, const uint8_t* in, int width, int height, uint8_t* out);
 void or_alpha_unfilter(int filter, uint8_t* data, int width, int height);

@@ -65,6 +65,7 @@ def main():
     make_bench_bitstreams()
     make_decode_fixtures(img)
     make_sharpyuv_fixtures(img)
+    make_reference_testdata()
     print("wrote", os.path.join(HERE, "libwebp_fixtures.npz"), sum(v.nbytes for v in out.values()), "bytes raw")
 
 
@@ -141,6 +142,27 @@ def make_bench_bitstreams():
            "blobs": L.encode_lossy(synth.blobs_rgba(w, h, seed=2), 75.0)}
     path = os.path.join(HERE, "q75_1080p.npz")
     np.savez(path, **{k: np.frombuffer(bytes(v), np.uint8) for k, v in out.items()})
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+REF_TESTDATA = ["blue_16x16_lossy.webp", "red_4x4_lossy.webp", "red_4x4_lossless.webp",
+                "gradient_8x8_lossless.webp", "lossless/bug-decode/input-vp8l.webp"]
+
+
+def make_reference_testdata():
+    """The .webp files the reference's own tests decode (testdata/, used by
+    webp_test.go:135-221) as raw bytes, next to libwebp 1.6.0's
+    WebPDecodeRGBA of each: they pin the VP8 decode path and, through a VP8L
+    entropy decode in oracle/vp8l_dec.c, the VP8L inverse transforms.  Keys:
+    <name>_webp (bytes), <name>_rgba (h, w, 4)."""
+    out = {}
+    for f in REF_TESTDATA:
+        data = open(os.path.join("/root/reference/testdata", f), "rb").read()
+        key = os.path.basename(f).replace(".webp", "").replace("-", "_")
+        out[key + "_webp"] = np.frombuffer(data, np.uint8)
+        out[key + "_rgba"] = L.decode_rgba(data)
+    path = os.path.join(HERE, "reference_testdata.npz")
+    np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
