@@ -50,17 +50,20 @@ def decode_case(n_img, w, h):
 
 
 def encode_case(kind, w=1920, h=1080):
+    """C2: the encode DSP path of one frame at the reference's q75 defaults
+    (import -> analysis -> segment analysis -> MB RD, frames.encode_frames),
+    and its RD launch alone."""
     mbw, mbh = (w + 15) >> 4, (h + 15) >> 4
     gen = {"gradient": lambda: synth.gradient_rgba(w, h), "noise": lambda: synth.noise_rgba(w, h, seed=3),
            "blobs": lambda: synth.blobs_rgba(w, h, seed=3)}[kind]
-    y, u, v = O.import_rgba(gen(), has_alpha=False)
-    Y, U, V = (torch.from_numpy(a[None]).cuda() for a in (y, u, v))
-    segs = np.stack([frames.setup_segment(q) for q in (22, 25, 28, 31)])
-    seg_ids = torch.from_numpy((np.arange(mbw * mbh) % 4).astype(np.uint8)[None]).cuda()
+    rgba = torch.from_numpy(gen()[None]).cuda()
+    out, rec, seg_ids, segs, _ = frames.encode_frames(rgba)
+    t_full = timed(lambda: frames.encode_frames(rgba, check=False))
+    Y, U, V = frames.import_rgba(rgba, has_alpha=False)
     proba = O.default_proba()
-    out, rec = frames.encode_mbs(Y, U, V, w, h, seg_ids, segs, proba, check=True)
     t = timed(lambda: frames.encode_mbs(Y, U, V, w, h, seg_ids, segs, proba, out=out, recon=rec))
-    print(f"encode RD 1x{w}x{h} {kind}: {t:.3f} ms = {w * h / t / 1e3:.1f} MPix/s")
+    print(f"encode C2 1x{w}x{h} {kind}: import+analysis+segments+RD {t_full:.3f} ms = {w * h / t_full / 1e3:.1f} "
+          f"MPix/s; RD alone {t:.3f} ms")
 
 
 def main():

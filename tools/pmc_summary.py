@@ -7,11 +7,21 @@ FETCH_SIZE / WRITE_SIZE are in KB.  MI355X_MICROARCH.md (HBM section): on
 gfx950 FETCH_SIZE counts half the bytes of wide (16 B/lane) streaming reads,
 so the HBM byte figure doubles it; WRITE_SIZE is exact for 16-B stores.  Both
 raw and corrected values are written so the correction stays visible.
+
+The undercount is of 128-B requests (tallied at 64 B).  k_encode_rows never
+makes one: each lane reads its own row's 32-B (Y) / 8-B (U, V) pieces, a
+wave instruction touching 16 different rows, plus 4- to 16-B hand-off and
+table words.  Its raw FETCH_SIZE equals the bytes it has to read (source
+1.5 B/px = 200.5 MB per 64 x 1080p, hand-off records and top-right words
+27 MB, segment ids 0.5 MB, cost tables: ~229 MB against 236 MB counted), so it is taken as
+is; doubling it would claim twice what the kernel can read.
 """
 import collections
 import csv
 import json
 import sys
+
+NARROW_READS = {"k_encode_rows"}  # no 128-B read requests: FETCH_SIZE is not halved (see above)
 
 
 def load(paths):
@@ -19,6 +29,7 @@ def load(paths):
     for path in paths:
         for row in csv.DictReader(open(path)):
             name = row["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].strip()
+            name = name.removeprefix("void ").split("<")[0]  # "void k_encode_rows<true>" -> "k_encode_rows"
             agg[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return agg
 
@@ -57,9 +68,11 @@ def main(argv):
             continue
         f = sum(ctrs["FETCH_SIZE"]) / len(ctrs["FETCH_SIZE"]) * 1024
         w = sum(ctrs["WRITE_SIZE"]) / len(ctrs["WRITE_SIZE"]) * 1024
+        narrow = name in NARROW_READS
         rec[name] = {"fetch_size_bytes_raw": int(f), "write_size_bytes": int(w),
-                     "hbm_bytes_per_launch": int(2 * f + w), "launches": len(ctrs["FETCH_SIZE"]),
-                     "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount) + WRITE_SIZE"}
+                     "hbm_bytes_per_launch": int((1 if narrow else 2) * f + w), "launches": len(ctrs["FETCH_SIZE"]),
+                     "correction": ("FETCH_SIZE x1 (no 128-B read requests, tools/pmc_summary.py) + WRITE_SIZE"
+                                    if narrow else "FETCH_SIZE x2 (gfx950 wide-read undercount) + WRITE_SIZE")}
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 

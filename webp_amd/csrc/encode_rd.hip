@@ -1001,6 +1001,10 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
     uint32_t left_modes = 0;  // 4 x 8 bits, B_DC_PRED = 0
     int tl_y = 127, tl_u = 127, tl_v = 127;
     int seen = 0;
+    // source rows loaded ahead for the next MBs of the pair / quad (import),
+    // reconstruction rows held back for a whole-sector store (export)
+    uint4 stg0 = make_uint4(0, 0, 0, 0), stg1 = stg0, rst0 = stg0;
+    uint2 rst1 = make_uint2(0, 0);
 
     for (int mbx = 0; mbx < mbw; mbx++) {
       Shared& s = launder(s_waves[wave]);
@@ -1041,19 +1045,46 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
       const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
       const Segment& sg = s.seg[segid];
       // ---- import (importBlockParallel :433-452) with edge replication ----
+      // A lane loads one source row.  Where whole 32-B sectors lie inside the
+      // image, a Y lane loads the rows of MB pairs (x even, x + 1) and a U / V
+      // lane those of MB quads in one go and keeps the rest in registers
+      // (stg0 / stg1), so every sector is fetched once: a 16-B (Y) or 8-B
+      // (U / V) load per MB fetched the whole sector again for the next MB.
       {
         const int x = 16 * mbx, y = 16 * mby;
         const int ww = min(a.width - x, 16), hh = min(a.height - y, 16);
         if (lane < 16) {
           const int r = min(lane, hh - 1);
-          for (int c = 0; c < 16; c++) s.yin[YOFF + lane * BPS + c] = Y[(int64_t)(y + r) * ys + x + min(c, ww - 1)];
+          const uint8_t* src = Y + (int64_t)(y + r) * ys + x;
+          if (16 * ((mbx & ~1) + 2) <= a.width) {  // the pair is whole
+            if ((mbx & 1) == 0) {
+              stg0 = *reinterpret_cast<const uint4*>(src);
+              stg1 = *reinterpret_cast<const uint4*>(src + 16);
+            }
+            const uint4 v = (mbx & 1) ? stg1 : stg0;
+            *reinterpret_cast<uint2*>(s.yin + YOFF + lane * BPS) = make_uint2(v.x, v.y);
+            *reinterpret_cast<uint2*>(s.yin + YOFF + lane * BPS + 8) = make_uint2(v.z, v.w);
+          } else {
+            for (int c = 0; c < 16; c++) s.yin[YOFF + lane * BPS + c] = src[min(c, ww - 1)];
+          }
         } else if (lane < 32) {
           const int k = lane - 16, pl = k >> 3, j = k & 7;
           const int uvw = (ww + 1) >> 1, uvh = (hh + 1) >> 1;
           const int r = min(j, uvh - 1);
-          const uint8_t* P = pl ? V : U;
-          for (int c = 0; c < 8; c++)
-            s.yin[(pl ? VOFF : UOFF) + j * BPS + c] = P[(int64_t)(8 * mby + r) * uvs + 8 * mbx + min(c, uvw - 1)];
+          const uint8_t* P = (pl ? V : U) + (int64_t)(8 * mby + r) * uvs + 8 * mbx;
+          if (16 * ((mbx & ~3) + 4) <= a.width) {  // the quad is whole (rows 8-B aligned: 8-B loads)
+            if ((mbx & 3) == 0) {
+              const uint2 p0 = reinterpret_cast<const uint2*>(P)[0], p1 = reinterpret_cast<const uint2*>(P)[1];
+              const uint2 p2 = reinterpret_cast<const uint2*>(P)[2], p3 = reinterpret_cast<const uint2*>(P)[3];
+              stg0 = make_uint4(p0.x, p0.y, p1.x, p1.y);
+              stg1 = make_uint4(p2.x, p2.y, p3.x, p3.y);
+            }
+            const uint4 h = (mbx & 2) ? stg1 : stg0;
+            *reinterpret_cast<uint2*>(s.yin + (pl ? VOFF : UOFF) + j * BPS) =
+                (mbx & 1) ? make_uint2(h.z, h.w) : make_uint2(h.x, h.y);
+          } else {
+            for (int c = 0; c < 8; c++) s.yin[(pl ? VOFF : UOFF) + j * BPS + c] = P[min(c, uvw - 1)];
+          }
         }
       }
       // ---- prediction context (fillPredContextParallel :455-562) ----
@@ -1706,21 +1737,54 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
         const int x = 16 * mbx, y = 16 * mby;
         const int wy = min(a.width - x, 16), hy = min(a.height - y, 16);
 #ifndef WG_EXP_NO_RECON
+        // Rows leave in whole 32-B sectors where the MB pair (Y) / quad (U, V)
+        // is whole: the earlier MBs' rows wait in registers (rst0 / rst1) and
+        // go out back to back with the last one's, so L2 never writes a
+        // partial sector back (a 16-B / 8-B piece per MB was written back
+        // before the next MB's piece arrived).
         if (lane < hy) {
           const uint8_t* srow = s.yout + YOFF + lane * BPS;  // 8-B aligned in LDS
           uint8_t* drow = RY + (int64_t)(y + lane) * ys + x;
           if (wy == 16) {  // one 16-B store per row
             const uint2 lo = *reinterpret_cast<const uint2*>(srow), hi = *reinterpret_cast<const uint2*>(srow + 8);
-            *reinterpret_cast<uint4*>(drow) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            const uint4 v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            if (16 * ((mbx & ~1) + 2) <= a.width) {
+              if ((mbx & 1) == 0) {
+                rst0 = v;
+              } else {
+                reinterpret_cast<uint4*>(drow)[-1] = rst0;
+                *reinterpret_cast<uint4*>(drow) = v;
+              }
+            } else {
+              *reinterpret_cast<uint4*>(drow) = v;
+            }
           } else {
             for (int c = 0; c < wy; c++) drow[c] = srow[c];
           }
         }
-        if (lane >= 16 && lane < 32) {  // U / V rows: one 8-B store each
+        if (lane >= 16 && lane < 32) {  // U / V rows: 8 B each
           const int k = lane - 16, pl = k >> 3, j = k & 7;
-          uint8_t* P = pl ? RV : RU;
-          *reinterpret_cast<uint2*>(P + (int64_t)(8 * mby + j) * uvs + 8 * mbx) =
-              *reinterpret_cast<const uint2*>(s.yout + (pl ? VOFF : UOFF) + j * BPS);
+          uint2* drow = reinterpret_cast<uint2*>((pl ? RV : RU) + (int64_t)(8 * mby + j) * uvs + 8 * mbx);
+          const uint2 v = *reinterpret_cast<const uint2*>(s.yout + (pl ? VOFF : UOFF) + j * BPS);
+          if (16 * ((mbx & ~3) + 4) <= a.width) {
+            const int q = mbx & 3;
+            if (q == 0) {
+              rst0.x = v.x;
+              rst0.y = v.y;
+            } else if (q == 1) {
+              rst0.z = v.x;
+              rst0.w = v.y;
+            } else if (q == 2) {
+              rst1 = v;
+            } else {
+              drow[-3] = make_uint2(rst0.x, rst0.y);
+              drow[-2] = make_uint2(rst0.z, rst0.w);
+              drow[-1] = rst1;
+              drow[0] = v;
+            }
+          } else {
+            *drow = v;
+          }
         }
 #endif
       }
