@@ -97,6 +97,34 @@ __device__ __forceinline__ uint32_t predict(int mode, uint32_t l, uint32_t t, ui
   }
 }
 
+// The same predictors for a lane-varying mode with little divergence (the
+// inverse walk's lanes sit in up to ~10 tiles at once, and a switch runs the
+// union of their cases).  Modes 1-10 are all avg2(avg2(A, B), avg2(C, D)) with
+// A..D drawn from (L, T, TR, TL) -- L = avg2(L, L) etc. -- so one branch-free
+// form with per-mode input codes (2 bits each: 0 L, 1 T, 2 TR, 3 TL) covers
+// them and mode 13's avg2(L, T); only Select (11) and the clamped
+// predictors (12, 13) branch.  Modes 0, 14, 15: black.
+__device__ __forceinline__ uint32_t predict_lanes(int mode, uint32_t l, uint32_t t, uint32_t tr, uint32_t tl) {
+#define PCODE(a, b, c, d) (uint64_t)((a) | (b) << 2 | (c) << 4 | (d) << 6)
+  constexpr uint64_t K0 = PCODE(0, 0, 0, 0) | PCODE(0, 0, 0, 0) << 8 | PCODE(1, 1, 1, 1) << 16 |
+                          PCODE(2, 2, 2, 2) << 24 | PCODE(3, 3, 3, 3) << 32 | PCODE(0, 2, 1, 1) << 40 |
+                          PCODE(0, 0, 3, 3) << 48 | PCODE(0, 0, 1, 1) << 56;  // modes 0-7
+  constexpr uint64_t K1 = PCODE(3, 3, 1, 1) | PCODE(1, 1, 2, 2) << 8 | PCODE(0, 3, 1, 2) << 16 |
+                          PCODE(0, 0, 1, 1) << 40;  // modes 8-15 (13: avg2(L, T))
+#undef PCODE
+  const uint32_t code = (uint32_t)((mode < 8 ? K0 : K1) >> (8 * (mode & 7)));
+  auto pick = [&](uint32_t i) {
+    const uint32_t lo = (i & 1) ? t : l, hi = (i & 1) ? tl : tr;
+    return (i & 2) ? hi : lo;
+  };
+  const uint32_t avg = avg2(avg2(pick(code & 3), pick((code >> 2) & 3)), avg2(pick((code >> 4) & 3), pick((code >> 6) & 3)));
+  uint32_t p = (mode == 0 || mode >= 14) ? ARGB_BLACK : avg;
+  if (mode == 11) p = select_pred(l, t, tl);
+  else if (mode == 12) p = clamp_add_sub_full(l, t, tl);
+  else if (mode == 13) p = clamp_add_sub_half(avg, tl);
+  return p;
+}
+
 // Go math.Log / math.Log2 (src/math/log.go, log10.go) for counts beyond the
 // LUT (tiles of 512 px at bits = 9); same operation sequence as the host LUT.
 __device__ double go_log(double x) {
@@ -259,13 +287,23 @@ constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
 // their own left neighbour.  A wave takes a band of 64 rows and walks it as a
 // diagonal: at step s lane k reconstructs pixel x = s - 2k of row
 // band*64 + k.  The row above comes from the previous lane's last three
-// outputs (lane shift); every value was produced at an earlier step.  Lane 0
-// reads the band above's last row, 64 columns at a time, into LDS once the
-// band above has published them (sc1 stores + progress counter, as in
-// decode.hip).  Bands are dequeued in (band, image) order from a counter, so
-// a band only ever waits on a band owned by a running wave.
+// outputs (a whole-wave DPP shift); lane 0's row above is the band above's
+// last row, read once that band has published it (sc1 stores + progress
+// counter, as in decode.hip).  Bands are dequeued in (band, image) order from
+// a counter, so a band only ever waits on a band owned by a running wave.
+//
+// The walk runs in chunks of 16 steps, and everything but the predictor
+// itself is done per chunk, one chunk ahead: each lane's 16 residuals and
+// tile modes, lane 0's 18 pixels of the row above (the DPP shift leaves
+// lane 0 its own register: update_dpp's `old`, no per-step branch), the
+// 16 outputs (stored as one 64-B run per lane), the band-above wait and the
+// progress publication.  A step is then the DPP shifts, the predictor
+// (predict_lanes, few branches) and the add: a step used to carry per-step
+// lane-0 LDS reads, a global store, boundary branches and the hand-off
+// checks, ~260 instructions.
+constexpr int INV_PUB = 32;  // the band's last row is published every INV_PUB columns (and at its end)
+
 __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
-  __shared__ uint32_t up_buf[66];  // row above, columns c0-1 .. c0+64
   __shared__ int sh_band;
   const int lane = threadIdx.x;
   const int w = a.width;
@@ -284,15 +322,20 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
     const int* prog_above = a.progress + img * a.bands + band - 1;
     int* prog_mine = a.progress + img * a.bands + band;
     const int last_lane = min(63, a.height - 1 - band * 64);
+    const bool publishes = band + 1 < a.bands;
     const uint32_t* mrow =
         a.modes + (int64_t)img * a.tiles_x * a.tiles_y + (int64_t)(min(y, a.height - 1) >> a.bits) * a.tiles_x;
-    uint32_t o1 = 0, o2 = 0, o3 = 0, first = 0;  // this lane's outputs at x-1, x-2, x-3
-    const int steps = w + 2 * last_lane;
     const uint32_t* inrow = in + (int64_t)min(y, a.height - 1) * w;
-    // residuals and modes of 16 consecutive pixels of this lane's row,
-    // loaded one 16-step chunk ahead: a load per step waited a memory round
-    // trip per step (the whole kernel ran at ~1.8 us per step)
-    auto load_chunk = [&](int x0, uint32_t* r, uint32_t* m) {
+    uint32_t* orow = out + (int64_t)min(y, a.height - 1) * w;
+    const uint32_t* uprow = out + (int64_t)(band * 64 - 1) * w;  // band > 0
+    uint32_t o1 = 0, o2 = 0, o3 = 0, first = 0;  // this lane's outputs at x-1, x-2, x-3; at x = 0
+    const int steps = w + 2 * last_lane;
+    int seen = 0, published = 0;
+    // the chunk at step s: residuals and modes of pixels s - 2k .. s - 2k + 15
+    // of this lane's row, and (band > 0) columns s - 1 .. s + 16 of the row
+    // above, once the band above has published them
+    auto load_chunk = [&](int s, uint32_t* r, uint32_t* m, uint32_t* up) {
+      const int x0 = s - 2 * lane;
 #pragma unroll
       for (int u = 0; u < 16; u++) {
         const int x = x0 + u;
@@ -300,81 +343,91 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
         r[u] = ok ? inrow[x] : 0u;
         m[u] = ok ? mrow[x >> a.bits] : 0u;
       }
-    };
-    uint32_t rc[16], mc[16];
-    load_chunk(-2 * lane, rc, mc);
-    for (int s0 = 0; s0 < steps; s0 += 16) {
-      uint32_t rn[16], mn[16];
-      load_chunk(s0 + 16 - 2 * lane, rn, mn);
-#pragma unroll
-      for (int u = 0; u < 16; u++) {
-        const int s = s0 + u;  // steps past the end run as idle steps (x >= w on every lane)
-        const int x = s - 2 * lane;
-        if (band > 0 && (s & 63) == 0 && s < w) {  // next 64 columns of the band above's last row
-          const int need = min(s + 65, w);
-          int seen = 0;
+      if (band > 0 && s < w) {
+        const int need = min(s + 17, w);
+        if (seen < need) {
+          int v = 0;
           if (lane == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (uint32_t it = 0;; it++) {
-              seen = __hip_atomic_load(prog_above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if (seen >= need) break;
+              v = __hip_atomic_load(prog_above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (v >= need) break;
               if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
                                       __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                 __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v = w;
                 break;
               }
               __builtin_amdgcn_s_sleep(2);
             }
           }
-          const uint32_t* up = out + (int64_t)(band * 64 - 1) * w;
-          const int c = s - 1 + lane;
-          if (c >= 0 && c < w) up_buf[lane] = __hip_atomic_load(up + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (lane < 2 && s + 63 + lane < w)
-            up_buf[64 + lane] = __hip_atomic_load(up + s + 63 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_wave_barrier();
+          seen = __builtin_amdgcn_readfirstlane(__shfl(v, 0, 64));
         }
-        // row-above values from lane-1's previous step: its x+1 (o1), x (o2),
-        // x-1 (o3), by a whole-wave DPP shift (wave_shr:1) instead of an LDS
-        // permute
-        uint32_t up_x1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)o1, 0x138, 0xf, 0xf, false);
-        uint32_t up_x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)o2, 0x138, 0xf, 0xf, false);
-        uint32_t up_xm1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)o3, 0x138, 0xf, 0xf, false);
-        if (lane == 0 && band > 0 && x < w) {
-          const int k = x - (s & ~63) + 1;  // == x - c0 + 1
-          up_xm1 = up_buf[k - 1];
-          up_x = up_buf[k];
-          up_x1 = up_buf[k + 1];
+#pragma unroll
+        for (int j = 0; j < 18; j++) {  // the same address in every lane: one line per load
+          const int c = min(max(s - 1 + j, 0), w - 1);
+          up[j] = __hip_atomic_load(uprow + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (live && x >= 0 && x < w) {
-          const uint32_t r = rc[u];
-          uint32_t v;
-          if (y == 0) {
-            v = add_pixels(r, x == 0 ? ARGB_BLACK : o1);
-          } else if (x == 0) {
-            v = add_pixels(r, up_x);
-          } else {
-            const int mode = (int)((mc[u] >> 8) & 0xf);
-            const uint32_t tr = (x < w - 1) ? up_x1 : first;
-            v = add_pixels(r, predict(mode, o1, up_x, tr, up_xm1));
-          }
-          if (x == 0) first = v;
-          o3 = o2;
-          o2 = o1;
-          o1 = v;
-          uint32_t* dst = out + (int64_t)y * w + x;
-          if (lane == last_lane) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else *dst = v;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 18; j++) up[j] = 0;
+      }
+    };
+    uint32_t rc[16], mc[16], uc[18];
+    load_chunk(0, rc, mc, uc);
+    for (int s0 = 0; s0 < steps; s0 += 16) {
+      uint32_t rn[16], mn[16], un[18], ov[16];
+      load_chunk(s0 + 16, rn, mn, un);
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const int x = s0 + u - 2 * lane;  // steps past the end run idle (x >= w on every lane)
+        // row above: lane k-1's outputs at x+1, x, x-1 from its previous step
+        // (wave_shr:1); lane 0 keeps its own copy of the band above's row
+        const uint32_t up_x1 = (uint32_t)__builtin_amdgcn_update_dpp((int)uc[u + 2], (int)o1, 0x138, 0xf, 0xf, false);
+        const uint32_t up_x = (uint32_t)__builtin_amdgcn_update_dpp((int)uc[u + 1], (int)o2, 0x138, 0xf, 0xf, false);
+        const uint32_t up_xm1 = (uint32_t)__builtin_amdgcn_update_dpp((int)uc[u], (int)o3, 0x138, 0xf, 0xf, false);
+        // the reference's border rules as modes: row 0 L (black at x = 0),
+        // column 0 T; TR past the right edge is this row's first pixel
+        int mode = (int)((mc[u] >> 8) & 0xf);
+        mode = x == 0 ? (y == 0 ? 0 : 2) : (y == 0 ? 1 : mode);
+        const uint32_t tr = x < w - 1 ? up_x1 : first;
+        const uint32_t v = add_pixels(rc[u], predict_lanes(mode, o1, up_x, tr, up_xm1));
+        first = x == 0 ? v : first;
+        o3 = o2;
+        o2 = o1;
+        o1 = (live && x >= 0 && x < w) ? v : 0u;
+        ov[u] = v;
+      }
+      // this chunk's outputs: pixels x0 .. x0 + 15 of the lane's row (8-B aligned)
+      const int x0 = s0 - 2 * lane;
+      const bool mine_last = lane == last_lane && publishes;  // read by the band below: write-through
+      if (live && x0 >= 0 && x0 + 15 < w) {
+        uint64_t* d = reinterpret_cast<uint64_t*>(orow + x0);
+        if (mine_last) {
+#pragma unroll
+          for (int j = 0; j < 8; j++)
+            __hip_atomic_store(d + j, (uint64_t)ov[2 * j + 1] << 32 | ov[2 * j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-          o3 = o2;
-          o2 = o1;
-          o1 = 0;
+#pragma unroll
+          for (int j = 0; j < 8; j++) d[j] = (uint64_t)ov[2 * j + 1] << 32 | ov[2 * j];
         }
-        // publish the band's last row every 64 columns (and at its end)
-        const int xl = s - 2 * last_lane;
-        if (band + 1 < a.bands && xl >= 0 && ((xl & 63) == 63 || xl == w - 1)) {
+      } else if (live) {
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          const int x = x0 + u;
+          if (x >= 0 && x < w) {
+            if (mine_last) __hip_atomic_store(orow + x, ov[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else orow[x] = ov[u];
+          }
+        }
+      }
+      // publish the band's last row every INV_PUB columns and at its end
+      if (publishes) {
+        const int p = min(max(s0 + 16 - 2 * last_lane, 0), w);  // columns of the last row stored
+        if (p > published && (p - published >= INV_PUB || p == w)) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lane == last_lane) __hip_atomic_store(prog_mine, xl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) __hip_atomic_store(prog_mine, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          published = p;
         }
       }
 #pragma unroll
@@ -382,6 +435,8 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
         rc[u] = rn[u];
         mc[u] = mn[u];
       }
+#pragma unroll
+      for (int j = 0; j < 18; j++) uc[j] = un[j];
     }
   }
 }
