@@ -328,8 +328,9 @@ int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, int32_t hei
                                 uint32_t* modes, uint32_t* residuals, void* stream);
 /* predictorInverseTransform (internal/lossless/decode_transform.go:202-360):
  * out = residuals +mod prediction from reconstructed pixels.  `work` needs
- * wg_vp8l_inverse_work_bytes(height, n_images) bytes. */
-size_t wg_vp8l_inverse_work_bytes(int32_t height, int32_t n_images);
+ * wg_vp8l_inverse_work_bytes(width, height, n_images) bytes, 16-B aligned (the
+ * band-to-band hand-off of each band's last row). */
+size_t wg_vp8l_inverse_work_bytes(int32_t width, int32_t height, int32_t n_images);
 int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, int32_t width, int32_t height,
                               int64_t image_pitch, int32_t n_images, const uint32_t* residuals, uint32_t* out,
                               void* work, void* stream);

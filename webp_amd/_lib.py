@@ -63,7 +63,7 @@ SIGNATURES = {
     "wg_plane_ssim": [_vp, _i32, _i64, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp],
     "wg_vp8l_residual_image_rows": [_vp, _i32, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp],
     "wg_vp8l_residual_image": [_vp, _i32, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp],
-    "wg_vp8l_inverse_work_bytes": [_i32, _i32],
+    "wg_vp8l_inverse_work_bytes": [_i32, _i32, _i32],
     "wg_vp8l_inverse_predictor": [_vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _vp, _vp],
     "wg_vp8l_inverse_status": [_vp, _vp],
     "wg_vp8l_green": [_vp, _i64, _i32, _vp],

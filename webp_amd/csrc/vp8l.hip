@@ -275,8 +275,8 @@ struct InvArgs {
   const uint32_t* modes;
   const uint32_t* in;
   uint32_t* out;
-  int* ctl;       // [0] band dequeue counter, [1] error flag (wait timeout)
-  int* progress;  // [n_img][bands]: columns of the band's last row completed (multiples of 64, or width)
+  int* ctl;        // [0] band dequeue counter, [1] error flag (wait timeout)
+  uint64_t* hand;  // [n_img][bands][width] {pixel, tag} granules of each band's last row
   int64_t pitch;
   int width, height, bits, tiles_x, tiles_y, bands, n_img;
 };
@@ -288,20 +288,26 @@ constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
 // diagonal: at step s lane k reconstructs pixel x = s - 2k of row
 // band*64 + k.  The row above comes from the previous lane's last three
 // outputs (a whole-wave DPP shift); lane 0's row above is the band above's
-// last row, read once that band has published it (sc1 stores + progress
-// counter, as in decode.hip).  Bands are dequeued in (band, image) order from
-// a counter, so a band only ever waits on a band owned by a running wave.
+// last row.  Bands are dequeued in (band, image) order from a counter, so a
+// band only ever waits on a band owned by a running wave.
 //
-// The walk runs in chunks of 16 steps, and everything but the predictor
-// itself is done per chunk, one chunk ahead: each lane's 16 residuals and
-// tile modes, lane 0's 18 pixels of the row above (the DPP shift leaves
-// lane 0 its own register: update_dpp's `old`, no per-step branch), the
-// 16 outputs (stored as one 64-B run per lane), the band-above wait and the
-// progress publication.  A step is then the DPP shifts, the predictor
-// (predict_lanes, few branches) and the add: a step used to carry per-step
-// lane-0 LDS reads, a global store, boundary branches and the hand-off
-// checks, ~260 instructions.
-constexpr int INV_PUB = 32;  // the band's last row is published every INV_PUB columns (and at its end)
+// Hand-off between bands: the band's last lane writes every pixel of its row
+// as it makes it, as an 8-B {pixel, tag} granule with one sc1 (write-through)
+// store (MI355X_MICROARCH.md, R2 granules: untorn, no flag, no drain); the
+// band below loads the granules it needs with sc1 loads and re-polls any
+// whose tag is not set yet.  The band below then trails by the diagonal's
+// 128 steps plus a store's flight and its own lookahead (a progress counter
+// published every 32 columns behind a store drain cost it ~90 more steps per
+// band: 6.2 -> 4.x ms at 4096^2).
+//
+// The walk runs in chunks of 16 steps, and everything but the predictor is
+// done per chunk, one chunk ahead: each lane's 16 residuals and tile modes,
+// lane 0's 18 pixels of the row above (the DPP shift leaves lane 0 its own
+// register: update_dpp's `old`, no per-step branch) and the 16 outputs
+// (stored as one 64-B run per lane).
+#ifndef UP_AT
+#define UP_AT 12  // step of the chunk at which the next chunk's row-above loads are issued
+#endif
 
 __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
   __shared__ int sh_band;
@@ -319,22 +325,18 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
     const bool live = y < a.height;
     const uint32_t* in = a.in + img * a.pitch;
     uint32_t* out = a.out + img * a.pitch;
-    const int* prog_above = a.progress + img * a.bands + band - 1;
-    int* prog_mine = a.progress + img * a.bands + band;
+    const uint64_t* hand_above = a.hand + ((int64_t)img * a.bands + band - 1) * w;  // band > 0
+    uint64_t* hand_mine = a.hand + ((int64_t)img * a.bands + band) * w;
     const int last_lane = min(63, a.height - 1 - band * 64);
-    const bool publishes = band + 1 < a.bands;
+    const bool hands_off = band + 1 < a.bands && lane == last_lane;
     const uint32_t* mrow =
         a.modes + (int64_t)img * a.tiles_x * a.tiles_y + (int64_t)(min(y, a.height - 1) >> a.bits) * a.tiles_x;
     const uint32_t* inrow = in + (int64_t)min(y, a.height - 1) * w;
     uint32_t* orow = out + (int64_t)min(y, a.height - 1) * w;
-    const uint32_t* uprow = out + (int64_t)(band * 64 - 1) * w;  // band > 0
     uint32_t o1 = 0, o2 = 0, o3 = 0, first = 0;  // this lane's outputs at x-1, x-2, x-3; at x = 0
     const int steps = w + 2 * last_lane;
-    int seen = 0, published = 0;
-    // the chunk at step s: residuals and modes of pixels s - 2k .. s - 2k + 15
-    // of this lane's row, and (band > 0) columns s - 1 .. s + 16 of the row
-    // above, once the band above has published them
-    auto load_chunk = [&](int s, uint32_t* r, uint32_t* m, uint32_t* up) {
+    // residuals and modes of pixels s - 2k .. s - 2k + 15 of this lane's row
+    auto load_chunk = [&](int s, uint32_t* r, uint32_t* m) {
       const int x0 = s - 2 * lane;
 #pragma unroll
       for (int u = 0; u < 16; u++) {
@@ -343,43 +345,52 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
         r[u] = ok ? inrow[x] : 0u;
         m[u] = ok ? mrow[x >> a.bits] : 0u;
       }
-      if (band > 0 && s < w) {
-        const int need = min(s + 17, w);
-        if (seen < need) {
-          int v = 0;
-          if (lane == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (uint32_t it = 0;; it++) {
-              v = __hip_atomic_load(prog_above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if (v >= need) break;
-              if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
-                                      __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                v = w;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(2);
-            }
+    };
+    // lane 0's row above for the chunk at step s: columns s - 1 .. s + 16 of
+    // the band above's last row as {pixel, tag} granules.  issue_up loads
+    // them (UP_AT steps before the chunk); take_up, at the chunk's start,
+    // re-polls until every tag is set and keeps the pixels.
+    auto issue_up = [&](int s, uint64_t* g) {
+#pragma unroll
+      for (int j = 0; j < 18; j++)  // the same address in every lane: one line per load
+        g[j] = band > 0 && s < w ? __hip_atomic_load(hand_above + min(max(s - 1 + j, 0), w - 1), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                 : ~0ull;
+    };
+    auto take_up = [&](int s, uint64_t* g, uint32_t* up) {
+      bool ready = true;
+#pragma unroll
+      for (int j = 0; j < 18; j++) ready &= (g[j] >> 32) != 0;
+      if (!__builtin_amdgcn_readfirstlane((int)ready)) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (uint32_t it = 0;; it++) {
+          __builtin_amdgcn_s_sleep(1);
+          issue_up(s, g);
+          ready = true;
+#pragma unroll
+          for (int j = 0; j < 18; j++) ready &= (g[j] >> 32) != 0;
+          if (__builtin_amdgcn_readfirstlane((int)ready)) break;
+          if ((it & 15) == 15 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+                                  __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            if (lane == 0) __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
           }
-          seen = __builtin_amdgcn_readfirstlane(__shfl(v, 0, 64));
         }
-#pragma unroll
-        for (int j = 0; j < 18; j++) {  // the same address in every lane: one line per load
-          const int c = min(max(s - 1 + j, 0), w - 1);
-          up[j] = __hip_atomic_load(uprow + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 18; j++) up[j] = 0;
       }
+#pragma unroll
+      for (int j = 0; j < 18; j++) up[j] = band > 0 ? (uint32_t)g[j] : 0u;
     };
     uint32_t rc[16], mc[16], uc[18];
-    load_chunk(0, rc, mc, uc);
+    uint64_t ug[18];
+    load_chunk(0, rc, mc);
+    issue_up(0, ug);
     for (int s0 = 0; s0 < steps; s0 += 16) {
-      uint32_t rn[16], mn[16], un[18], ov[16];
-      load_chunk(s0 + 16, rn, mn, un);
+      uint32_t rn[16], mn[16], ov[16];
+      take_up(s0, ug, uc);
+      load_chunk(s0 + 16, rn, mn);
 #pragma unroll
       for (int u = 0; u < 16; u++) {
+        if (u == UP_AT) issue_up(s0 + 16, ug);  // the next chunk's row above, UP_AT steps into this one
         const int x = s0 + u - 2 * lane;  // steps past the end run idle (x >= w on every lane)
         // row above: lane k-1's outputs at x+1, x, x-1 from its previous step
         // (wave_shr:1); lane 0 keeps its own copy of the band above's row
@@ -392,42 +403,25 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
         mode = x == 0 ? (y == 0 ? 0 : 2) : (y == 0 ? 1 : mode);
         const uint32_t tr = x < w - 1 ? up_x1 : first;
         const uint32_t v = add_pixels(rc[u], predict_lanes(mode, o1, up_x, tr, up_xm1));
+        const bool valid = live && x >= 0 && x < w;
+        if (hands_off && valid) __hip_atomic_store(hand_mine + x, 1ull << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         first = x == 0 ? v : first;
         o3 = o2;
         o2 = o1;
-        o1 = (live && x >= 0 && x < w) ? v : 0u;
+        o1 = valid ? v : 0u;
         ov[u] = v;
       }
       // this chunk's outputs: pixels x0 .. x0 + 15 of the lane's row (8-B aligned)
       const int x0 = s0 - 2 * lane;
-      const bool mine_last = lane == last_lane && publishes;  // read by the band below: write-through
       if (live && x0 >= 0 && x0 + 15 < w) {
         uint64_t* d = reinterpret_cast<uint64_t*>(orow + x0);
-        if (mine_last) {
 #pragma unroll
-          for (int j = 0; j < 8; j++)
-            __hip_atomic_store(d + j, (uint64_t)ov[2 * j + 1] << 32 | ov[2 * j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; j++) d[j] = (uint64_t)ov[2 * j + 1] << 32 | ov[2 * j];
-        }
+        for (int j = 0; j < 8; j++) d[j] = (uint64_t)ov[2 * j + 1] << 32 | ov[2 * j];
       } else if (live) {
 #pragma unroll
         for (int u = 0; u < 16; u++) {
           const int x = x0 + u;
-          if (x >= 0 && x < w) {
-            if (mine_last) __hip_atomic_store(orow + x, ov[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else orow[x] = ov[u];
-          }
-        }
-      }
-      // publish the band's last row every INV_PUB columns and at its end
-      if (publishes) {
-        const int p = min(max(s0 + 16 - 2 * last_lane, 0), w);  // columns of the last row stored
-        if (p > published && (p - published >= INV_PUB || p == w)) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lane == 0) __hip_atomic_store(prog_mine, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          published = p;
+          if (x >= 0 && x < w) orow[x] = ov[u];
         }
       }
 #pragma unroll
@@ -435,8 +429,6 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
         rc[u] = rn[u];
         mc[u] = mn[u];
       }
-#pragma unroll
-      for (int j = 0; j < 18; j++) uc[j] = un[j];
     }
   }
 }
@@ -511,9 +503,9 @@ extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32
                                      n_images, modes, residuals, stream);
 }
 
-extern "C" size_t wg_vp8l_inverse_work_bytes(int32_t height, int32_t n_images) {
-  if (height <= 0 || n_images <= 0) return 0;
-  return sizeof(int) * ((size_t)n_images * ((height + 63) / 64) + 4);
+extern "C" size_t wg_vp8l_inverse_work_bytes(int32_t width, int32_t height, int32_t n_images) {
+  if (width <= 0 || height <= 0 || n_images <= 0) return 0;
+  return 16 + sizeof(uint64_t) * (size_t)n_images * ((height + 63) / 64) * width;
 }
 
 extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, int32_t width, int32_t height,
@@ -521,6 +513,7 @@ extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, in
                                          uint32_t* out, void* work, void* stream) {
   WG_REQUIRE(modes && residuals && out && work && width > 0 && height > 0 && n_images > 0);
   WG_REQUIRE(bits >= 2 && bits <= 9 && image_pitch >= (int64_t)width * height);
+  WG_REQUIRE(reinterpret_cast<uintptr_t>(work) % 16 == 0);
   hipStream_t s = wg::as_stream(stream);
   InvArgs a;
   a.modes = modes;
@@ -529,14 +522,15 @@ extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, in
   a.bands = (height + 63) / 64;
   a.n_img = n_images;
   a.ctl = static_cast<int*>(work);
-  a.progress = a.ctl + 4;
+  a.hand = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(work) + 16);
   a.pitch = image_pitch;
   a.width = width;
   a.height = height;
   a.bits = bits;
   a.tiles_x = subsample(width, bits);
   a.tiles_y = subsample(height, bits);
-  if (hipMemsetAsync(work, 0, wg_vp8l_inverse_work_bytes(height, n_images), s) != hipSuccess)
+  // counters and every granule's tag start clear
+  if (hipMemsetAsync(work, 0, wg_vp8l_inverse_work_bytes(width, height, n_images), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(vp8l work)");
   const int total = a.bands * n_images;
   const int grid = total < 2048 ? total : 2048;

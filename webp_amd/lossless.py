@@ -53,7 +53,7 @@ def predictor_inverse(modes, bits, residuals, out=None, check=False):
     n, h, w = r.shape
     if out is None:
         out = torch.empty_like(r)
-    work = torch.empty(lib.wg_vp8l_inverse_work_bytes(h, n), dtype=torch.uint8, device=r.device)
+    work = torch.empty(lib.wg_vp8l_inverse_work_bytes(w, h, n), dtype=torch.uint8, device=r.device)
     call("wg_vp8l_inverse_predictor", modes.data_ptr(), bits, w, h, h * w, n, r.data_ptr(), out.data_ptr(),
          work.data_ptr(), _stream())
     if check:
