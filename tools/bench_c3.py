@@ -69,8 +69,9 @@ def encode_case(kind, w=1920, h=1080):
 def main():
     for n in (1, 4, 16):
         decode_case(n, 4096, 4096)
-    for kind in ("gradient", "blobs", "noise"):
-        encode_case(kind)
+    if os.environ.get("C3_ONLY") != "1":
+        for kind in ("gradient", "blobs", "noise"):
+            encode_case(kind)
 
 
 if __name__ == "__main__":

@@ -24,6 +24,7 @@
 // 4 pixels per lane; chroma lanes 0-15 U, 16-31 V.
 #include <cstddef>
 #include <cstdlib>
+#include <cstring>
 
 #include "wg_common.h"
 #include "wg_dsp.h"
@@ -650,8 +651,467 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
   STAMP_FLUSH();
 }
 
+// ---------------------------------------------------------------------------
+// k_decode_split: the same work as k_decode_bands with reconstruction and loop
+// filtering on two waves per macroblock row.  Intra prediction reads
+// UNFILTERED pixels (the top context is saved before filtering,
+// decode_frame.go:190-194), so the reconstruction chain never waits for the
+// filter: a workgroup takes a band of SW rows with a reconstruction wave (R)
+// and a filter wave (F) per row.
+//   R(y) walks row y: it waits for R(y-1) to have finished MB x (x + 1 when
+//     this MB's I4 blocks on the right column read the top-right pixels:
+//     modes VE / LD / VL), reconstructs, hands the unfiltered top context to
+//     R(y+1) (LDS ring, or the global top records across bands) and the
+//     unfiltered MB (+ its filter parameters) to F(y) through an LDS ring.
+//   F(y) takes MB x from that ring, waits for F(y-1) to have finished MB
+//     x + 1 (its top-edge filter writes the rows above, which are final only
+//     once the MB above-right has run its left-edge filter), filters and
+//     stores exactly as k_decode_bands does.
+// The reconstruction chain -- the critical path of one image -- is then the
+// loads, prediction and residuals alone, and its slope is one MB per row
+// wherever the MB above-right is not needed.  Cross-band hand-off: R by
+// progress_r + the top records, F by progress_f + the frame rows (sc1 stores,
+// drained before the flag), as in k_decode_bands.
+constexpr int SW = 4;         // rows per band (one R and one F wave each)
+constexpr int RING_M = 8;     // R -> F ring depth (unfiltered MBs)
+constexpr int MB_SLOT = 416;  // Y 16 x 16 | U 8 x 8 | V 8 x 8 | wg_mb_info 32
+
+__device__ __forceinline__ bool needs_top_right(uint32_t is_i4, const uint8_t* imodes) {
+  // blocks 3, 7, 11, 15 read the MB above-right in VE4 / LD4 / VL4 (wg_dsp.h pred4_row)
+  if (!is_i4) return false;
+  bool n = false;
+#pragma unroll
+  for (int b = 3; b < 16; b += 4) n |= imodes[b] == 2 || imodes[b] == 6 || imodes[b] == 7;
+  return n;
+}
+
+__global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t wb_all[SW][WB_SIZE];
+  __shared__ __attribute__((aligned(16))) int4 stage_all[SW][50];
+  constexpr int FT_BYTES = 20 * FY_STRIDE + 2 * 12 * FC_STRIDE + 8 * FC_STRIDE;
+  __shared__ __attribute__((aligned(16))) uint8_t ftiles_all[SW][FT_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t top_ring[SW][RING][TOP_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t bot_ring[SW][RING][BOT_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t mb_ring[SW][RING_M][MB_SLOT];
+  __shared__ int prog_r[SW], prog_f[SW], cons_f[SW];
+  __shared__ int sh_word;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool is_f = wave >= SW;
+  const int r = is_f ? wave - SW : wave;  // row of the band
+  int lane = threadIdx.x & 63;
+  const int mbw = a.mbw, mbh = a.mbh;
+  const int bands = (mbh + SW - 1) / SW;
+  const int total = a.n_img * bands;
+  const int ys = 16 * mbw, uvs = 8 * mbw;
+  const bool luma_only = a.filter_type == 1;
+  int* const progress_f = a.progress + (int64_t)a.n_img * mbh;
+
+  for (;;) {
+    if (threadIdx.x == 0) sh_word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+      if (is_f) {
+        prog_f[r] = 0;
+        cons_f[r] = 0;
+      } else {
+        prog_r[r] = 0;
+      }
+    }
+    __syncthreads();
+    const int idx = __builtin_amdgcn_readfirstlane(sh_word);
+    __syncthreads();
+    if (idx >= total) break;
+    const int band = idx / a.n_img, img = idx % a.n_img;
+    const int mby = band * SW + r;
+    const int last_row = min(SW, mbh - band * SW) - 1;
+    const bool from_lds = r > 0, to_lds = r < last_row;
+    uint8_t* top = a.top + (int64_t)img * mbw * TOP_BYTES;
+    if (r <= last_row && !is_f) {
+      // ============================ R: reconstruction ============================
+      uint8_t* const wb = wb_all[r];
+      int16_t* const cof = reinterpret_cast<int16_t*>(stage_all[r]);
+      int4* const stage = stage_all[r];
+      int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
+      int* prog_mine = a.progress + (int64_t)img * mbh + mby;
+      if (lane < 16) wb[LY - 1 + lane * WG_BPS] = 129;
+      else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = 129;
+      else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = 129;
+      else if (lane < 35) wb[(lane == 32 ? LY : lane == 33 ? LU : LV) - WG_BPS - 1] = mby > 0 ? 129 : 127;
+      int seen = 0;
+      const int64_t row_mb0 = ((int64_t)img * mbh + mby) * mbw;
+      int4 pf = make_int4(0, 0, 0, 0);
+      if (lane < 48) pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384) + lane);
+      else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + row_mb0)[lane - 48];
+      for (int mbx = 0; mbx < mbw; mbx++) {
+        const int64_t mbi = row_mb0 + mbx;
+        const int slot = mbx & (RING - 1), mslot = mbx & (RING_M - 1);
+        lane = opaque_lane() & 63;
+        if (lane < 50) stage[lane] = pf;
+        lds_sync();
+        const uint32_t* iw = reinterpret_cast<const uint32_t*>(stage + 48);  // wg_mb_info words
+        const uint32_t w6 = __builtin_amdgcn_readfirstlane(iw[6]);
+        const uint8_t* imodes = reinterpret_cast<const uint8_t*>(stage + 48) + 8;
+        const bool tr_needed = mbx + 1 < mbw && needs_top_right(w6 & 0xff, imodes);
+        // ---- dependency on the row above; ring space below (top ring) and in F's ring ----
+        if (mby > 0) {
+          const int need = tr_needed ? mbx + 2 : mbx + 1;
+          if (seen < need) {
+            int v = 0;
+            if (lane == 0)
+              v = from_lds ? wait_progress<false>(&prog_r[r - 1], need, &a.ctl[1], mbw)
+                           : wait_progress<true>(prog_above, need, &a.ctl[1], mbw);
+            seen = __shfl(v, 0, 64);
+          }
+        }
+        if (lane == 0) {
+          if (to_lds && mbx >= RING - 1) wait_progress<false>(&prog_r[r + 1], mbx - RING + 2, &a.ctl[1], mbw);
+          if (mbx >= RING_M) wait_progress<false>(&cons_f[r], mbx - RING_M + 1, &a.ctl[1], mbw);
+        }
+        lds_sync();
+        // ---- top context (unfiltered) ----
+        if (mby > 0 && from_lds) {
+          const uint8_t* tc = top_ring[r - 1][slot];
+          if (lane >= 48 && lane < 52) {
+            const int k = lane - 48;
+            uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
+            *reinterpret_cast<uint64_t*>(dst) = lds64(tc + 8 * k);
+          }
+          if (lane == 0) {
+            uint32_t tr;
+            if (mbx < mbw - 1) tr = lds32(top_ring[r - 1][(mbx + 1) & (RING - 1)]);
+            else tr = 0x01010101u * (uint32_t)tc[15];
+            *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
+          }
+        } else if (mby > 0) {
+          const uint8_t* tc = top + mbx * TOP_BYTES;
+          if (lane >= 48 && lane < 52) {
+            const uint64_t w = ld_sc1_64(tc + 8 * (lane - 48));
+            const int k = lane - 48;
+            uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
+            *reinterpret_cast<uint64_t*>(dst) = w;
+          }
+          if (lane == 0) {
+            uint32_t tr;
+            if (mbx < mbw - 1) tr = (uint32_t)ld_sc1_64(tc + TOP_BYTES);
+            else tr = 0x01010101u * (uint32_t)(ld_sc1_64(tc + 8) >> 56);
+            *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
+          }
+        } else {
+          if (lane < 21) wb[LY - WG_BPS + lane - 1] = 127;
+          else if (lane < 30) wb[LU - WG_BPS + lane - 22] = 127;
+          else if (lane < 39) wb[LV - WG_BPS + lane - 31] = 127;
+        }
+        lds_sync();
+        if (mbx + 1 < mbw) {  // prefetch the next MB
+          if (lane < 48) pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384) + lane);
+          else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + mbi + 1)[lane - 48];
+        }
+        const uint32_t nz_y = __builtin_amdgcn_readfirstlane(iw[0]), nz_uv = __builtin_amdgcn_readfirstlane(iw[1]);
+        const uint32_t im0 = __builtin_amdgcn_readfirstlane(iw[2]);
+        const int is_i4 = w6 & 0xff, uv_mode = (w6 >> 8) & 0xff;
+        if (is_i4 && lane < 12) {  // replicate top-right down to rows 3, 7, 11 (:155-160)
+          const int rr = 4 * (lane / 4 + 1) - 1, i = lane & 3;
+          wb[LY + rr * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
+        }
+        lds_sync();
+        lane = opaque_lane() & 63;
+        // ---- luma prediction + residual ----
+        {
+          const int blk = lane >> 2, rr = lane & 3, bx = blk & 3, by = blk >> 2;
+          const int off = LY + (4 * by + rr) * WG_BPS + 4 * bx;
+          const int code = (nz_y >> (30 - 2 * blk)) & 3;
+          int res[4];
+          dec_residual_row(cof + blk * 16, code, rr, res);
+          if (!is_i4) {
+            const int mode = check_mode(mbx, mby, im0 & 0xff);
+            const int dc = predsq_dc(mode, wb + LY, 16);
+            const uint32_t pred = predsq_row4(mode, wb + LY, 4 * bx, 4 * by + rr, dc);
+            *reinterpret_cast<uint32_t*>(wb + off) =
+                pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
+                      clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+          } else {
+            const int my_step = bx + 2 * by;
+            const int mode = imodes[blk];
+            for (int st = 0; st < 10; st++) {
+              if (st == my_step) {
+                int X, T[8], L[4];
+                pred4_ctx(wb, LY + 4 * by * WG_BPS + 4 * bx, X, T, L);
+                const uint32_t pred = pred4_row(mode, rr, X, T, L);
+                *reinterpret_cast<uint32_t*>(wb + off) =
+                    pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
+                          clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+              }
+              lds_sync();
+            }
+          }
+        }
+        lane = opaque_lane() & 63;
+        // ---- chroma prediction + residual (doUVTransform :47-68) ----
+        if (lane < 32) {
+          const int pl = lane >> 4, cblk = (lane >> 2) & 3, rr = lane & 3;
+          const int cbx = cblk & 1, cby = cblk >> 1;
+          const int base = pl ? LV : LU;
+          const int mode = check_mode(mbx, mby, uv_mode);
+          const int dc = predsq_dc(mode, wb + base, 8);
+          const uint32_t pred = predsq_row4(mode, wb + base, 4 * cbx, 4 * cby + rr, dc);
+          const uint32_t bits = nz_uv >> (8 * pl);
+          const int16_t* bco = cof + (16 + 4 * pl + cblk) * 16;
+          int res[4] = {0, 0, 0, 0};
+          if (bits & 0xff) {
+            if (bits & 0xaa) dec_residual_row(bco, 3, rr, res);
+            else if (bco[0] != 0) dec_residual_row(bco, 1, rr, res);
+          }
+          *reinterpret_cast<uint32_t*>(wb + base + (4 * cby + rr) * WG_BPS + 4 * cbx) =
+              pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
+                    clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+        }
+        lds_sync();
+        lane = opaque_lane() & 63;
+        // ---- hand-offs: unfiltered top context for R(y+1), the MB and its info for F(y) ----
+        if (mby < mbh - 1 && lane >= 32 && lane < 36) {
+          const int k = lane - 32;
+          const uint8_t* src =
+              k < 2 ? wb + LY + 15 * WG_BPS + 8 * k : (k == 2 ? wb + LU + 7 * WG_BPS : wb + LV + 7 * WG_BPS);
+          if (to_lds) *reinterpret_cast<uint64_t*>(top_ring[r][slot] + 8 * k) = lds64(src);
+          else st_sc1_64(top + mbx * TOP_BYTES + 8 * k, lds64(src));
+        }
+        {
+          uint8_t* ms = mb_ring[r][mslot];
+          if (lane < 16) {
+            *reinterpret_cast<uint4*>(ms + 16 * lane) = *reinterpret_cast<const uint4*>(wb + LY + lane * WG_BPS);
+          } else if (lane < 32) {
+            const int pl = lane >= 24, j = (lane - 16) & 7;
+            *reinterpret_cast<uint64_t*>(ms + 256 + 64 * pl + 8 * j) = lds64(wb + (pl ? LV : LU) + j * WG_BPS);
+          } else if (lane < 34) {
+            *reinterpret_cast<int4*>(ms + 384 + 16 * (lane - 32)) = stage[48 + lane - 32];
+          }
+        }
+        lds_sync();
+        // ---- rotate the reconstruction context for the next MB (:118-126) ----
+        if (lane < 16) wb[LY - 1 + lane * WG_BPS] = wb[LY + 15 + lane * WG_BPS];
+        else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = wb[LU + 7 + (lane - 16) * WG_BPS];
+        else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = wb[LV + 7 + (lane - 24) * WG_BPS];
+        else if (lane == 32) wb[LY - WG_BPS - 1] = wb[LY - WG_BPS + 15];
+        else if (lane == 33) wb[LU - WG_BPS - 1] = wb[LU - WG_BPS + 7];
+        else if (lane == 34) wb[LV - WG_BPS - 1] = wb[LV - WG_BPS + 7];
+        lds_sync();
+        // ---- publish: LDS for F(y) and R(y+1) in the band; global for the next band ----
+        if (!to_lds && mby < mbh - 1) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the top record is out before the flag
+          if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) __hip_atomic_store(&prog_r[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else if (r <= last_row) {
+      // ============================ F: loop filter + frame stores ============================
+      uint8_t* const fy = ftiles_all[r];
+      uint8_t* const fu = fy + 20 * FY_STRIDE;
+      uint8_t* const fv = fu + 12 * FC_STRIDE;
+      int* prog_above = progress_f + (int64_t)img * mbh + mby - 1;
+      int* prog_mine = progress_f + (int64_t)img * mbh + mby;
+      uint8_t* Yp = a.Y + (int64_t)img * ys * 16 * mbh;
+      uint8_t* Up = a.U + (int64_t)img * uvs * 8 * mbh;
+      uint8_t* Vp = a.V + (int64_t)img * uvs * 8 * mbh;
+      int seen = 0, have = 0;
+      for (int mbx = 0; mbx < mbw; mbx++) {
+        const int slot = mbx & (RING - 1), mslot = mbx & (RING_M - 1);
+        lane = opaque_lane() & 63;
+        // ---- this row's MB from R, the row above's filtered rows, ring space below ----
+        if (lane == 0) {
+          if (have < mbx + 1) have = wait_progress<false>(&prog_r[r], mbx + 1, &a.ctl[1], mbw);
+          if (mby > 0) {
+            const int need = min(mbx + 2, mbw);
+            if (seen < need)
+              seen = from_lds ? wait_progress<false>(&prog_f[r - 1], need, &a.ctl[1], mbw)
+                              : wait_progress<true>(prog_above, need, &a.ctl[1], mbw);
+          }
+          if (to_lds && mbx >= RING - 1) wait_progress<false>(&prog_f[r + 1], mbx - RING + 2, &a.ctl[1], mbw);
+        }
+        lds_sync();
+        // rotate the filter tiles: the MBs to the left move one MB further left
+        if (mbx > 0) {
+          uint4 y0 = make_uint4(0, 0, 0, 0);
+          uint64_t c[2] = {0, 0};
+          if (lane < 40) y0 = *reinterpret_cast<const uint4*>(fy + (lane >> 1) * FY_STRIDE + FY_X0 - 16 + 16 * (lane & 1));
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const int i = lane + 64 * h;
+            if (i < 96) {
+              const int row = i >> 2, pl = row >= 12;
+              c[h] = lds64((pl ? fv : fu) + (row - 12 * pl) * FC_STRIDE + FC_X0 - 24 + 8 * (i & 3));
+            }
+          }
+          lds_sync();
+          if (lane < 40) *reinterpret_cast<uint4*>(fy + (lane >> 1) * FY_STRIDE + FY_X0 - 32 + 16 * (lane & 1)) = y0;
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const int i = lane + 64 * h;
+            if (i < 96) {
+              const int row = i >> 2, pl = row >= 12;
+              *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (row - 12 * pl) * FC_STRIDE + FC_X0 - 32 + 8 * (i & 3)) = c[h];
+            }
+          }
+        }
+        // the MB into the tiles (rows 4..) and the filter rows above (rows 0..3)
+        const uint8_t* ms = mb_ring[r][mslot];
+        if (lane < 16) {
+          *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) = *reinterpret_cast<const uint4*>(ms + 16 * lane);
+        } else if (lane < 32) {
+          const int pl = lane >= 24, j = (lane - 16) & 7;
+          *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0) = lds64(ms + 256 + 64 * pl + 8 * j);
+        }
+        if (mby > 0 && from_lds) {
+          const uint8_t* bt = bot_ring[r - 1][slot];
+          if (lane >= 52 && lane < 60) {
+            const int k = lane - 52, rr = k >> 1, half = k & 1;
+            *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = lds64(bt + 16 * rr + 8 * half);
+          } else if (lane >= 60) {
+            const int rr = lane - 60;
+            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) = lds64(bt + 64 + 8 * rr);
+          } else if (lane >= 44 && lane < 48) {
+            const int rr = lane - 44;
+            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = lds64(bt + 96 + 8 * rr);
+          }
+        } else if (mby > 0) {
+          if (lane >= 52 && lane < 60) {
+            const int k = lane - 52, rr = k >> 1, half = k & 1;
+            *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) =
+                ld_sc1_64(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half);
+          } else if (lane >= 60) {
+            const int rr = lane - 60;
+            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) =
+                ld_sc1_64(Up + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
+          } else if (lane >= 44 && lane < 48) {
+            const int rr = lane - 44;
+            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) =
+                ld_sc1_64(Vp + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
+          }
+        }
+        const uint32_t w7 = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(ms + 384)[7]);
+        lds_sync();
+        if (lane == 0) __hip_atomic_store(&cons_f[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int f_limit = w7 & 0xff, ilevel = (w7 >> 8) & 0xff, f_inner = (w7 >> 16) & 0xff, hev_t = w7 >> 24;
+        lane = opaque_lane() & 63;
+        // ---- loop filter (doFilter :293-342) ----
+        const bool do_filter = a.filter_type > 0 && f_limit > 0;
+        const bool inner = f_inner != 0;
+        if (do_filter) {
+          if (a.filter_type == 2) filter_mb<true>(fy, fu, fv, lane, true, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
+          else filter_mb<false>(fy, fu, fv, lane, false, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
+        }
+        lane = opaque_lane() & 63;
+        // ---- stores (as k_decode_bands) ----
+        {
+          const bool last = mbx == mbw - 1;
+          int y0 = -1, y1 = -1;
+          if (last) {
+            y0 = mbx > 0 ? (mbx - 1) & ~1 : 0;
+            y1 = mbx;
+          } else if (mbx >= 2 && (mbx & 1) == 0) {
+            y0 = mbx - 2;
+            y1 = mbx - 1;
+          }
+          int c0 = -1, c1 = -1;
+          if (last) {
+            c0 = mbx > 0 ? (mbx - 1) & ~3 : 0;
+            c1 = mbx;
+          } else if (mbx >= 4 && (mbx & 3) == 0) {
+            c0 = mbx - 4;
+            c1 = mbx - 1;
+          }
+          const int ylim = to_lds ? 13 : 12, clim = to_lds ? 5 : 4;
+          if (lane < 48) {
+            const int j = lane & 15, x = y0 + (lane >> 4);
+            if (y0 >= 0 && j < ylim && x <= y1) {
+              const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
+              *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby + j) * ys + 16 * x) = w;
+            }
+          }
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const int i = lane + 64 * h, pl = (i >> 3) & 1, j = i & 7, x = c0 + (i >> 4);
+            if (c0 >= 0 && i < 80 && j < clim && x <= c1)
+              *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x) =
+                  lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx));
+          }
+          if (!to_lds) {
+            const int which = lane >> 5, k = lane & 31, x = mbx - 1 + which;
+            if (which == 0 ? mbx > 0 : last) {
+              if (k < 4) {
+                const int j = 12 + k;
+                const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
+                uint8_t* dst = Yp + (int64_t)(16 * mby + j) * ys + 16 * x;
+                st_sc1_64(dst, (uint64_t)w.y << 32 | w.x);
+                st_sc1_64(dst + 8, (uint64_t)w.w << 32 | w.z);
+              } else if (k < 12) {
+                const int pl = k >= 8, j = 4 + (k & 3);
+                st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x,
+                          lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
+              }
+            }
+          }
+          if (mby > 0) {
+            int t0 = -1, t1 = -1;
+            if ((mbx & 1) == 1 || last) {
+              t0 = mbx & ~1;
+              t1 = mbx;
+            }
+            int u0 = -1, u1 = -1;
+            if ((mbx & 3) == 3 || last) {
+              u0 = mbx & ~3;
+              u1 = mbx;
+            }
+            if (lane < 6) {
+              const int rr = 1 + (lane >> 1), part = lane & 1, x = t0 + part;
+              if (t0 >= 0 && x <= t1)
+                *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * x) =
+                    *reinterpret_cast<const uint4*>(fy + rr * FY_STRIDE + FY_X0 + 16 * (x - mbx));
+            } else if ((from_lds || !luma_only) && lane >= 8 && lane < 32) {
+              const int k = lane - 8, pl = k >= 12, rr = 1 + (k % 12) / 4, q = k & 3, x = u0 + q;
+              if (u0 >= 0 && x <= u1)
+                *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * x) =
+                    lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0 + 8 * (x - mbx));
+            }
+          }
+        }
+        if (to_lds) {
+          uint8_t* bt = bot_ring[r][slot];
+          if (lane < 8) {
+            const int rr = lane >> 1, half = lane & 1;
+            *reinterpret_cast<uint64_t*>(bt + 16 * rr + 8 * half) = lds64(fy + (16 + rr) * FY_STRIDE + FY_X0 + 8 * half);
+          } else if (lane < 16) {
+            const int k = lane - 8, pl = k >= 4, rr = k & 3;
+            *reinterpret_cast<uint64_t*>(bt + 64 + 32 * pl + 8 * rr) = lds64((pl ? fv : fu) + (8 + rr) * FC_STRIDE + FC_X0);
+          } else if (mbx > 0 && do_filter && lane < 28) {
+            uint8_t* bl = bot_ring[r][(mbx - 1) & (RING - 1)];
+            const int k = lane - 16;
+            if (k < 4) {
+              *reinterpret_cast<uint32_t*>(bl + 16 * k + 12) = lds32(fy + (16 + k) * FY_STRIDE + FY_X0 - 4);
+            } else if (!luma_only) {
+              const int pl = k >= 8, rr = k & 3;
+              *reinterpret_cast<uint32_t*>(bl + 64 + 32 * pl + 8 * rr + 4) =
+                  lds32((pl ? fv : fu) + (8 + rr) * FC_STRIDE + FC_X0 - 4);
+            }
+          }
+        }
+        lds_sync();
+        lane = opaque_lane() & 63;
+        if (!to_lds && mby < mbh - 1) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this MB is out before the flag
+          if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) __hip_atomic_store(&prog_f[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // the band's LDS rings are reused by the next band
+  }
+}
+
 int g_num_cus = 0;
-int g_rows_per_cu = 0;  // resident workgroups per CU (occupancy)
+int g_rows_per_cu = 0;   // resident k_decode_bands workgroups per CU (occupancy)
+int g_split_per_cu = 0;  // resident k_decode_split workgroups per CU
+int g_use_split = 1;     // WG_DECODE_KERNEL=bands selects k_decode_bands (A/B)
 
 }  // namespace
 
@@ -665,7 +1125,8 @@ extern "C" int wg_debug_phases(unsigned long long* host, int n) {
 
 extern "C" size_t wg_decode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images) {
   if (mbw <= 0 || mbh <= 0 || n_images <= 0) return 0;
-  return (size_t)n_images * mbw * TOP_BYTES + sizeof(int) * ((size_t)n_images * mbh + 4);
+  // top records | ctl[4] | progress (reconstruction) | progress_f (filter, k_decode_split)
+  return (size_t)n_images * mbw * TOP_BYTES + sizeof(int) * (2 * (size_t)n_images * mbh + 4);
 }
 
 extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int32_t filter_type, int32_t mbw,
@@ -692,17 +1153,27 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   a.n_img = n_images;
   hipStream_t s = wg::as_stream(stream);
   if (g_num_cus == 0) {
-    int dev = 0, cus = 0, per_cu = 0;
+    int dev = 0, cus = 0, per_cu = 0, per_cu_s = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0 ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_bands, 64 * DW, 0) != hipSuccess || per_cu <= 0)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_bands, 64 * DW, 0) != hipSuccess || per_cu <= 0 ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, k_decode_split, 128 * SW, 0) != hipSuccess ||
+        per_cu_s <= 0)
       return wg::check_launch("decode occupancy query");
     g_num_cus = cus;
     g_rows_per_cu = per_cu;
+    g_split_per_cu = per_cu_s;
     if (const char* e = getenv("WG_DECODE_WG_PER_CU")) g_rows_per_cu = atoi(e) > 0 ? atoi(e) : per_cu;  // tuning
+    if (const char* e = getenv("WG_DECODE_KERNEL")) g_use_split = strcmp(e, "bands") != 0;
   }
-  if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
+  if (hipMemsetAsync(a.ctl, 0, sizeof(int) * (2 * (size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(decode ctl)");
+  if (g_use_split) {
+    const int bands = n_images * ((mbh + SW - 1) / SW);
+    const int grid = bands < g_split_per_cu * g_num_cus ? bands : g_split_per_cu * g_num_cus;
+    hipLaunchKernelGGL(k_decode_split, dim3((unsigned)grid), dim3(128 * SW), 0, s, a);
+    return wg::check_launch("k_decode_split");
+  }
   const int bands = n_images * ((mbh + DW - 1) / DW);
   const int grid = bands < g_rows_per_cu * g_num_cus ? bands : g_rows_per_cu * g_num_cus;
   hipLaunchKernelGGL(k_decode_bands, dim3((unsigned)grid), dim3(64 * DW), 0, s, a);
