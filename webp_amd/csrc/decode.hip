@@ -673,8 +673,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
 // progress_r + the top records, F by progress_f + the frame rows (sc1 stores,
 // drained before the flag), as in k_decode_bands.
 constexpr int SW = 4;         // rows per band (one R and one F wave each)
-constexpr int RING_M = 8;     // R -> F ring depth (unfiltered MBs)
-constexpr int MB_SLOT = 416;  // Y 16 x 16 | U 8 x 8 | V 8 x 8 | wg_mb_info 32
+constexpr int RING_M = 8;     // R -> F ring depth (R's work buffers of unfiltered MBs)
 
 __device__ __forceinline__ bool needs_top_right(uint32_t is_i4, const uint8_t* imodes) {
   // blocks 3, 7, 11, 15 read the MB above-right in VE4 / LD4 / VL4 (wg_dsp.h pred4_row)
@@ -686,13 +685,14 @@ __device__ __forceinline__ bool needs_top_right(uint32_t is_i4, const uint8_t* i
 }
 
 __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t wb_all[SW][WB_SIZE];
+  // R reconstructs MB x in wb_all[row][x % RING_M]; F filters it from there
+  __shared__ __attribute__((aligned(16))) uint8_t wb_all[SW][RING_M][WB_SIZE];
   __shared__ __attribute__((aligned(16))) int4 stage_all[SW][50];
   constexpr int FT_BYTES = 20 * FY_STRIDE + 2 * 12 * FC_STRIDE + 8 * FC_STRIDE;
   __shared__ __attribute__((aligned(16))) uint8_t ftiles_all[SW][FT_BYTES];
   __shared__ __attribute__((aligned(16))) uint8_t top_ring[SW][RING][TOP_BYTES];
   __shared__ __attribute__((aligned(16))) uint8_t bot_ring[SW][RING][BOT_BYTES];
-  __shared__ __attribute__((aligned(16))) uint8_t mb_ring[SW][RING_M][MB_SLOT];
+  __shared__ __attribute__((aligned(16))) uint8_t info_ring[SW][RING_M][32];  // each MB's wg_mb_info, R -> F
   __shared__ int prog_r[SW], prog_f[SW], cons_f[SW];
   __shared__ int sh_word;
 
@@ -706,6 +706,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
   const int ys = 16 * mbw, uvs = 8 * mbw;
   const bool luma_only = a.filter_type == 1;
   int* const progress_f = a.progress + (int64_t)a.n_img * mbh;
+  STAMP_DECL;
 
   for (;;) {
     if (threadIdx.x == 0) sh_word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -728,15 +729,10 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
     uint8_t* top = a.top + (int64_t)img * mbw * TOP_BYTES;
     if (r <= last_row && !is_f) {
       // ============================ R: reconstruction ============================
-      uint8_t* const wb = wb_all[r];
       int16_t* const cof = reinterpret_cast<int16_t*>(stage_all[r]);
       int4* const stage = stage_all[r];
       int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
       int* prog_mine = a.progress + (int64_t)img * mbh + mby;
-      if (lane < 16) wb[LY - 1 + lane * WG_BPS] = 129;
-      else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = 129;
-      else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = 129;
-      else if (lane < 35) wb[(lane == 32 ? LY : lane == 33 ? LU : LV) - WG_BPS - 1] = mby > 0 ? 129 : 127;
       int seen = 0;
       const int64_t row_mb0 = ((int64_t)img * mbh + mby) * mbw;
       int4 pf = make_int4(0, 0, 0, 0);
@@ -745,6 +741,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
       for (int mbx = 0; mbx < mbw; mbx++) {
         const int64_t mbi = row_mb0 + mbx;
         const int slot = mbx & (RING - 1), mslot = mbx & (RING_M - 1);
+        STAMP(0);
         lane = opaque_lane() & 63;
         if (lane < 50) stage[lane] = pf;
         lds_sync();
@@ -767,7 +764,24 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           if (to_lds && mbx >= RING - 1) wait_progress<false>(&prog_r[r + 1], mbx - RING + 2, &a.ctl[1], mbw);
           if (mbx >= RING_M) wait_progress<false>(&cons_f[r], mbx - RING_M + 1, &a.ctl[1], mbw);
         }
+        // ---- this MB's work buffer: left context from the previous MB's (:118-126), or the row start (:93-110) ----
+        uint8_t* const wb = wb_all[r][mslot];
+        if (mbx == 0) {
+          if (lane < 16) wb[LY - 1 + lane * WG_BPS] = 129;
+          else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = 129;
+          else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = 129;
+          else if (lane < 35) wb[(lane == 32 ? LY : lane == 33 ? LU : LV) - WG_BPS - 1] = mby > 0 ? 129 : 127;
+        } else {
+          const uint8_t* pw = wb_all[r][(mbx - 1) & (RING_M - 1)];
+          if (lane < 16) wb[LY - 1 + lane * WG_BPS] = pw[LY + 15 + lane * WG_BPS];
+          else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = pw[LU + 7 + (lane - 16) * WG_BPS];
+          else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = pw[LV + 7 + (lane - 24) * WG_BPS];
+          else if (lane == 32) wb[LY - WG_BPS - 1] = pw[LY - WG_BPS + 15];
+          else if (lane == 33) wb[LU - WG_BPS - 1] = pw[LU - WG_BPS + 7];
+          else if (lane == 34) wb[LV - WG_BPS - 1] = pw[LV - WG_BPS + 7];
+        }
         lds_sync();
+        STAMP(1);
         // ---- top context (unfiltered) ----
         if (mby > 0 && from_lds) {
           const uint8_t* tc = top_ring[r - 1][slot];
@@ -814,6 +828,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           wb[LY + rr * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
         }
         lds_sync();
+        STAMP(2);
         lane = opaque_lane() & 63;
         // ---- luma prediction + residual ----
         {
@@ -845,6 +860,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
             }
           }
         }
+        STAMP(3);
         lane = opaque_lane() & 63;
         // ---- chroma prediction + residual (doUVTransform :47-68) ----
         if (lane < 32) {
@@ -866,6 +882,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                     clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
         }
         lds_sync();
+        STAMP(4);
         lane = opaque_lane() & 63;
         // ---- hand-offs: unfiltered top context for R(y+1), the MB and its info for F(y) ----
         if (mby < mbh - 1 && lane >= 32 && lane < 36) {
@@ -875,32 +892,17 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           if (to_lds) *reinterpret_cast<uint64_t*>(top_ring[r][slot] + 8 * k) = lds64(src);
           else st_sc1_64(top + mbx * TOP_BYTES + 8 * k, lds64(src));
         }
-        {
-          uint8_t* ms = mb_ring[r][mslot];
-          if (lane < 16) {
-            *reinterpret_cast<uint4*>(ms + 16 * lane) = *reinterpret_cast<const uint4*>(wb + LY + lane * WG_BPS);
-          } else if (lane < 32) {
-            const int pl = lane >= 24, j = (lane - 16) & 7;
-            *reinterpret_cast<uint64_t*>(ms + 256 + 64 * pl + 8 * j) = lds64(wb + (pl ? LV : LU) + j * WG_BPS);
-          } else if (lane < 34) {
-            *reinterpret_cast<int4*>(ms + 384 + 16 * (lane - 32)) = stage[48 + lane - 32];
-          }
-        }
+        if (lane >= 48 && lane < 50)
+          *reinterpret_cast<int4*>(info_ring[r][mslot] + 16 * (lane - 48)) = stage[lane];
         lds_sync();
-        // ---- rotate the reconstruction context for the next MB (:118-126) ----
-        if (lane < 16) wb[LY - 1 + lane * WG_BPS] = wb[LY + 15 + lane * WG_BPS];
-        else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = wb[LU + 7 + (lane - 16) * WG_BPS];
-        else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = wb[LV + 7 + (lane - 24) * WG_BPS];
-        else if (lane == 32) wb[LY - WG_BPS - 1] = wb[LY - WG_BPS + 15];
-        else if (lane == 33) wb[LU - WG_BPS - 1] = wb[LU - WG_BPS + 7];
-        else if (lane == 34) wb[LV - WG_BPS - 1] = wb[LV - WG_BPS + 7];
-        lds_sync();
+        STAMP(5);
         // ---- publish: LDS for F(y) and R(y+1) in the band; global for the next band ----
         if (!to_lds && mby < mbh - 1) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the top record is out before the flag
           if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (lane == 0) __hip_atomic_store(&prog_r[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        STAMP(6);
       }
     } else if (r <= last_row) {
       // ============================ F: loop filter + frame stores ============================
@@ -915,6 +917,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
       int seen = 0, have = 0;
       for (int mbx = 0; mbx < mbw; mbx++) {
         const int slot = mbx & (RING - 1), mslot = mbx & (RING_M - 1);
+        STAMP(0);
         lane = opaque_lane() & 63;
         // ---- this row's MB from R, the row above's filtered rows, ring space below ----
         if (lane == 0) {
@@ -928,6 +931,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           if (to_lds && mbx >= RING - 1) wait_progress<false>(&prog_f[r + 1], mbx - RING + 2, &a.ctl[1], mbw);
         }
         lds_sync();
+        STAMP(7);
         // rotate the filter tiles: the MBs to the left move one MB further left
         if (mbx > 0) {
           uint4 y0 = make_uint4(0, 0, 0, 0);
@@ -953,12 +957,13 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           }
         }
         // the MB into the tiles (rows 4..) and the filter rows above (rows 0..3)
-        const uint8_t* ms = mb_ring[r][mslot];
+        const uint8_t* ms = wb_all[r][mslot];
         if (lane < 16) {
-          *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) = *reinterpret_cast<const uint4*>(ms + 16 * lane);
+          *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) =
+              *reinterpret_cast<const uint4*>(ms + LY + lane * WG_BPS);
         } else if (lane < 32) {
           const int pl = lane >= 24, j = (lane - 16) & 7;
-          *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0) = lds64(ms + 256 + 64 * pl + 8 * j);
+          *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0) = lds64(ms + (pl ? LV : LU) + j * WG_BPS);
         }
         if (mby > 0 && from_lds) {
           const uint8_t* bt = bot_ring[r - 1][slot];
@@ -987,10 +992,11 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                 ld_sc1_64(Vp + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
           }
         }
-        const uint32_t w7 = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(ms + 384)[7]);
+        const uint32_t w7 = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(info_ring[r][mslot])[7]);
         lds_sync();
         if (lane == 0) __hip_atomic_store(&cons_f[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int f_limit = w7 & 0xff, ilevel = (w7 >> 8) & 0xff, f_inner = (w7 >> 16) & 0xff, hev_t = w7 >> 24;
+        STAMP(8);
         lane = opaque_lane() & 63;
         // ---- loop filter (doFilter :293-342) ----
         const bool do_filter = a.filter_type > 0 && f_limit > 0;
@@ -999,6 +1005,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           if (a.filter_type == 2) filter_mb<true>(fy, fu, fv, lane, true, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
           else filter_mb<false>(fy, fu, fv, lane, false, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
         }
+        STAMP(9);
         lane = opaque_lane() & 63;
         // ---- stores (as k_decode_bands) ----
         {
@@ -1101,11 +1108,13 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (lane == 0) __hip_atomic_store(&prog_f[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        STAMP(10);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // the band's LDS rings are reused by the next band
   }
+  STAMP_FLUSH();
 }
 
 int g_num_cus = 0;
