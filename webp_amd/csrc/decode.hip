@@ -131,15 +131,9 @@ __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// Loop filter of one MB on the LDS tiles (doFilter, decode_frame.go:293-342):
-// lanes 0-15 luma line 0-15, lanes 16-31 chroma line 0-7 of U / V.  A line is
-// 20 (luma) / 12 (chroma) pixels: 4 of the left / upper neighbour, then the
-// MB.  Each lane filters all edges of its line in registers (rf_line); the
-// row pass (H edges) completes before the column pass (V edges).  One wave:
-// the passes are ordered with wave-level LDS syncs.
 template <bool COMPLEX>
-__device__ __forceinline__ void filter_mb(uint8_t* fy, uint8_t* fu, uint8_t* fv, int lane, bool chroma, bool left,
-                                          bool top, bool inner, int limit, int ilevel, int hev_t) {
+__device__ __forceinline__ void filter_mb_rows(uint8_t* fy, uint8_t* fu, uint8_t* fv, int lane, bool chroma, bool left,
+                                               bool inner, int limit, int ilevel, int hev_t) {
   const bool luma = lane < 16;
   const bool active = luma || (chroma && lane < 32);
   const int pl = lane >= 24, j = (lane - 16) & 7;
@@ -163,6 +157,13 @@ __device__ __forceinline__ void filter_mb(uint8_t* fy, uint8_t* fu, uint8_t* fv,
     }
   }
   lds_sync();
+}
+template <bool COMPLEX>
+__device__ __forceinline__ void filter_mb_cols(uint8_t* fy, uint8_t* fu, uint8_t* fv, int lane, bool chroma, bool top,
+                                               bool inner, int limit, int ilevel, int hev_t) {
+  const bool luma = lane < 16;
+  const bool active = luma || (chroma && lane < 32);
+  const int pl = lane >= 24, j = (lane - 16) & 7;
   if (active) {
     uint8_t* col = luma ? fy + FY_X0 + lane : (pl ? fv : fu) + FC_X0 + j;
     const int st = luma ? FY_STRIDE : FC_STRIDE;
@@ -178,6 +179,18 @@ __device__ __forceinline__ void filter_mb(uint8_t* fy, uint8_t* fu, uint8_t* fv,
     }
   }
   lds_sync();
+}
+// Loop filter of one MB on the LDS tiles (doFilter, decode_frame.go:293-342):
+// lanes 0-15 luma line 0-15, lanes 16-31 chroma line 0-7 of U / V.  A line is
+// 20 (luma) / 12 (chroma) pixels: 4 of the left / upper neighbour, then the
+// MB.  Each lane filters all edges of its line in registers (rf_line); the
+// row pass (H edges) completes before the column pass (V edges).  One wave:
+// the passes are ordered with wave-level LDS syncs.
+template <bool COMPLEX>
+__device__ __forceinline__ void filter_mb(uint8_t* fy, uint8_t* fu, uint8_t* fv, int lane, bool chroma, bool left,
+                                          bool top, bool inner, int limit, int ilevel, int hev_t) {
+  filter_mb_rows<COMPLEX>(fy, fu, fv, lane, chroma, left, inner, limit, ilevel, hev_t);
+  filter_mb_cols<COMPLEX>(fy, fu, fv, lane, chroma, top, inner, limit, ilevel, hev_t);
 }
 
 // threadIdx.x through an opaque move, re-read at every phase of the MB loop:
@@ -672,8 +685,14 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
 // wherever the MB above-right is not needed.  Cross-band hand-off: R by
 // progress_r + the top records, F by progress_f + the frame rows (sc1 stores,
 // drained before the flag), as in k_decode_bands.
-constexpr int SW = 4;         // rows per band (one R and one F wave each)
-constexpr int RING_M = 8;     // R -> F ring depth (R's work buffers of unfiltered MBs)
+#ifndef WG_DEC_SW
+#define WG_DEC_SW 4
+#endif
+#ifndef WG_DEC_RING_M
+#define WG_DEC_RING_M 8
+#endif
+constexpr int SW = WG_DEC_SW;          // rows per band (one R and one F wave each)
+constexpr int RING_M = WG_DEC_RING_M;  // R -> F ring depth (R's work buffers of unfiltered MBs)
 
 __device__ __forceinline__ bool needs_top_right(uint32_t is_i4, const uint8_t* imodes) {
   // blocks 3, 7, 11, 15 read the MB above-right in VE4 / LD4 / VL4 (wg_dsp.h pred4_row)
@@ -693,7 +712,9 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t top_ring[SW][RING][TOP_BYTES];
   __shared__ __attribute__((aligned(16))) uint8_t bot_ring[SW][RING][BOT_BYTES];
   __shared__ __attribute__((aligned(16))) uint8_t info_ring[SW][RING_M][32];  // each MB's wg_mb_info, R -> F
-  __shared__ int prog_r[SW], prog_f[SW], cons_f[SW];
+  // prog_f: MBs F finished; bot_f: MBs whose final bottom rows are in bot_ring
+  // (MB x's once MB x + 1's left-edge filter, in its row pass, has run)
+  __shared__ int prog_r[SW], prog_f[SW], cons_f[SW], bot_f[SW];
   __shared__ int sh_word;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -714,6 +735,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
       if (is_f) {
         prog_f[r] = 0;
         cons_f[r] = 0;
+        bot_f[r] = 0;
       } else {
         prog_r[r] = 0;
       }
@@ -923,9 +945,11 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         if (lane == 0) {
           if (have < mbx + 1) have = wait_progress<false>(&prog_r[r], mbx + 1, &a.ctl[1], mbw);
           if (mby > 0) {
-            const int need = min(mbx + 2, mbw);
+            // in the band: MB x's bottom rows above (bot_f); across bands the
+            // frame rows, final once the row above has finished MB x + 1
+            const int need = from_lds ? mbx + 1 : min(mbx + 2, mbw);
             if (seen < need)
-              seen = from_lds ? wait_progress<false>(&prog_f[r - 1], need, &a.ctl[1], mbw)
+              seen = from_lds ? wait_progress<false>(&bot_f[r - 1], need, &a.ctl[1], mbw)
                               : wait_progress<true>(prog_above, need, &a.ctl[1], mbw);
           }
           if (to_lds && mbx >= RING - 1) wait_progress<false>(&prog_f[r + 1], mbx - RING + 2, &a.ctl[1], mbw);
@@ -1002,8 +1026,29 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         const bool do_filter = a.filter_type > 0 && f_limit > 0;
         const bool inner = f_inner != 0;
         if (do_filter) {
-          if (a.filter_type == 2) filter_mb<true>(fy, fu, fv, lane, true, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
-          else filter_mb<false>(fy, fu, fv, lane, false, mbx > 0, mby > 0, inner, f_limit, ilevel, hev_t);
+          if (a.filter_type == 2) filter_mb_rows<true>(fy, fu, fv, lane, true, mbx > 0, inner, f_limit, ilevel, hev_t);
+          else filter_mb_rows<false>(fy, fu, fv, lane, false, mbx > 0, inner, f_limit, ilevel, hev_t);
+        }
+        if (to_lds && mbx > 0) {
+          // the left MB's bottom rows are final now (our left-edge filter was
+          // the last to touch them): its columns 12..15 into its bot_ring slot
+          if (do_filter && lane >= 16 && lane < 28) {
+            uint8_t* bl = bot_ring[r][(mbx - 1) & (RING - 1)];
+            const int k = lane - 16;
+            if (k < 4) {
+              *reinterpret_cast<uint32_t*>(bl + 16 * k + 12) = lds32(fy + (16 + k) * FY_STRIDE + FY_X0 - 4);
+            } else if (!luma_only) {
+              const int pl = k >= 8, rr = k & 3;
+              *reinterpret_cast<uint32_t*>(bl + 64 + 32 * pl + 8 * rr + 4) =
+                  lds32((pl ? fv : fu) + (8 + rr) * FC_STRIDE + FC_X0 - 4);
+            }
+          }
+          lds_sync();
+          if (lane == 0) __hip_atomic_store(&bot_f[r], mbx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (do_filter) {
+          if (a.filter_type == 2) filter_mb_cols<true>(fy, fu, fv, lane, true, mby > 0, inner, f_limit, ilevel, hev_t);
+          else filter_mb_cols<false>(fy, fu, fv, lane, false, mby > 0, inner, f_limit, ilevel, hev_t);
         }
         STAMP(9);
         lane = opaque_lane() & 63;
@@ -1089,16 +1134,6 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           } else if (lane < 16) {
             const int k = lane - 8, pl = k >= 4, rr = k & 3;
             *reinterpret_cast<uint64_t*>(bt + 64 + 32 * pl + 8 * rr) = lds64((pl ? fv : fu) + (8 + rr) * FC_STRIDE + FC_X0);
-          } else if (mbx > 0 && do_filter && lane < 28) {
-            uint8_t* bl = bot_ring[r][(mbx - 1) & (RING - 1)];
-            const int k = lane - 16;
-            if (k < 4) {
-              *reinterpret_cast<uint32_t*>(bl + 16 * k + 12) = lds32(fy + (16 + k) * FY_STRIDE + FY_X0 - 4);
-            } else if (!luma_only) {
-              const int pl = k >= 8, rr = k & 3;
-              *reinterpret_cast<uint32_t*>(bl + 64 + 32 * pl + 8 * rr + 4) =
-                  lds32((pl ? fv : fu) + (8 + rr) * FC_STRIDE + FC_X0 - 4);
-            }
           }
         }
         lds_sync();
@@ -1107,7 +1142,10 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this MB is out before the flag
           if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (lane == 0) __hip_atomic_store(&prog_f[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) {
+          __hip_atomic_store(&prog_f[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (mbx == mbw - 1) __hip_atomic_store(&bot_f[r], mbw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         STAMP(10);
       }
     }
