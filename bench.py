@@ -51,7 +51,7 @@ BYTES_PER_PX = {
     "upsample": 1.5 + 4.0,            # YUV in, NRGBA out
 }
 KERNELS = {"import": "k_import", "analysis": "k_analysis", "segments": "k_segments", "encode": "k_encode_rows",
-           "decode": "k_decode_bands", "upsample": "k_upsample"}
+           "decode": "k_decode_split", "upsample": "k_upsample"}
 CONTENTS = ("grad", "noise", "blobs")
 BITSTREAMS = os.path.join(ROOT, "tests", "golden", "q75_1080p.npz")
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")

@@ -1,0 +1,16 @@
+#!/bin/bash
+# GPU box, round 2 final evidence (part A): the -m gpu suite, smoke, the bench
+# line with the CPU baseline, C3 / C2, C5 and aux stage timings.
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name, limit, command...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 $lim "$@" > gpurun_out/$name.log 2>&1 || { echo "$name failed rc=$?"; tail -40 gpurun_out/$name.log; exit 1; }
+  tail -${TAILN:-2} gpurun_out/$name.log
+}
+step gpu 500 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
+step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+TAILN=1 step bench 400 python bench.py --steps 10 --warmup 3
+TAILN=7 step c3 300 python tools/bench_c3.py
+TAILN=1 step c5 300 python tools/bench_c5.py
+TAILN=1 step aux 300 python tools/bench_aux.py
