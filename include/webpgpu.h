@@ -225,6 +225,12 @@ int wg_segment_analysis(const wg_enc_config* cfg, const int32_t* alphas, const i
                         int32_t mbh, int32_t n_images, uint8_t* seg_ids, void* segs, int64_t segs_pitch,
                         wg_frame_segs* info, void* stream);
 size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images);
+/* Phase A of encodeFrameParallel (encode_parallel.go:168-232) for n frames of
+ * one size: y / u / v planes [n] at y_pitch / uv_pitch bytes apart, rows
+ * 16*mbw / 8*mbw bytes (the reference's padded layout); y and ry 16-byte
+ * aligned with y_pitch a multiple of 16, u, v, ru, rv 8-byte aligned with
+ * uv_pitch a multiple of 8; out (wg_mb_enc [n][mbh][mbw]) and work 16-byte
+ * aligned.  Methods 3-6, mbh >= 4 (else WG_EINVAL). */
 int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t y_pitch, int64_t uv_pitch,
                   int32_t width, int32_t height, int32_t n_images, const uint8_t* segments, const void* segs,
                   int64_t segs_pitch, const uint8_t* proba, int32_t method, int32_t quality, void* out, uint8_t* ry, uint8_t* ru,

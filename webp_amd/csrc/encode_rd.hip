@@ -1943,12 +1943,14 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   // error diffusion, mid-frame proba refresh), which this kernel is not.
   if (mbh < 4) return wg::invalid("wg_encode_mbs needs mbh >= 4 (height > 48): encode.go:1356 encodes smaller frames serially");
   WG_REQUIRE(((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(work)) & 15) == 0);
-  WG_REQUIRE(((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(v) |
-               reinterpret_cast<uintptr_t>(ry) | reinterpret_cast<uintptr_t>(ru) | reinterpret_cast<uintptr_t>(rv) |
-               reinterpret_cast<uintptr_t>(segs)) & 3) == 0);
+  // Y rows move as 16-B pieces, U / V rows as 8-B pieces (k_encode_rows import / export)
+  WG_REQUIRE(((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(ry)) & 15) == 0 &&
+             ((reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(ru) |
+               reinterpret_cast<uintptr_t>(rv)) & 7) == 0);
   WG_REQUIRE((reinterpret_cast<uintptr_t>(segs) & 15) == 0 && (segs_pitch == 0 || segs_pitch >= (int64_t)(4 * sizeof(Segment))) &&
              (segs_pitch & 15) == 0);
-  WG_REQUIRE(y_pitch >= (int64_t)256 * mbw * mbh && uv_pitch >= (int64_t)64 * mbw * mbh && ((y_pitch | uv_pitch) & 3) == 0);
+  WG_REQUIRE(y_pitch >= (int64_t)256 * mbw * mbh && uv_pitch >= (int64_t)64 * mbw * mbh && (y_pitch & 15) == 0 &&
+             (uv_pitch & 7) == 0);
   hipStream_t s = wg::as_stream(stream);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return wg::check_launch("hipGetDevice");
