@@ -137,3 +137,15 @@ def test_encode_pipeline_method3(cuda):
     rgba = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "test_png_rgba.npz"))["rgba"]
     pipeline([rgba], 768, 576, method=3)
     pipeline([synth.noise_rgba(320, 240, seed=9), synth.gradient_rgba(320, 240)], 320, 240, method=3, quality=40)
+
+
+@pytest.mark.parametrize("schedule", ["0", "1"])
+@pytest.mark.parametrize("method", [4, 3])
+def test_encode_row_schedules(cuda, monkeypatch, schedule, method):
+    """Both row schedules of k_encode_rows on the same frames: one wave a row
+    (the batch schedule) and a wave pair a row (I4 RD beside the I16 / chroma
+    work, the schedule of launches whose rows fit the wave slots twice);
+    WG_ENCODE_PAIR forces either."""
+    monkeypatch.setenv("WG_ENCODE_PAIR", schedule)
+    run([planes(160, 96, k, s) for s, k in enumerate(("noise", "blobs", "grad"))], 160, 96, (20, 40, 60, 80), method=method)
+    run([planes(64, 64, "noise", 3)], 64, 64, (25, 35, 45, 55), sns=0, quality=30, method=method)

@@ -23,6 +23,7 @@
 //              (each needs its left / top neighbour's nz), DC and chroma in
 //              parallel, then reconstruction and export
 // All integer; bit-exact with the C restatement (oracle/lossy_rd.c).
+#include <cstdlib>
 #include <mutex>
 
 #include "vp8_tables.h"
@@ -170,6 +171,12 @@ struct Shared {
   int cand_nz[6], cand_rate[6];
   alignas(16) uint8_t pv[2][64];  // per half-wave: the I4 block's prediction value table
   int word;
+  // pair mode (k_encode_rows<., true>): the I4 wave (A) hands the MB's
+  // neighbour context to the I16 / chroma wave (B) in ctxw; B posts the I16
+  // score for A's early exit (s16v, then s16_flag) and its results (post_*)
+  uint32_t ctxw[4];  // top_nz, top_nz_dc, left_nz, left_nz_dc
+  int s16_flag, post_best16, post_best_uv, post_nz_dc;
+  uint64_t s16v, post_s16;
 };
 constexpr int WAVES = 4;  // waves (macroblock rows in flight) per workgroup
 
@@ -828,6 +835,11 @@ __device__ __forceinline__ int opaque_lane() {
   asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"((int)threadIdx.x & 63));
   return l;
 }
+// a wave-uniform 64-bit value into SGPRs (the builtin takes 32 bits)
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32;
+}
 template <typename T>
 __device__ __forceinline__ T& launder(T& s) {
   typedef __attribute__((address_space(3))) T LdsT;
@@ -923,19 +935,31 @@ __device__ unsigned long long g_enc_phase[16];
 // TRELLIS: method >= 4 (trellis quantisation in the I4 RD and the final I16
 // residuals, encode_parallel.go:793, :1202); method 3 quantises plainly
 // (pickBestI4ModeRDParallel :842-929, QuantizeCoeffs at :1215).
-template <bool TRELLIS>
-__global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs a) {
+//
+// PAIR: a row is walked by a pair of waves (a 2-wave workgroup).  The luma
+// and chroma chains of a macroblock are independent up to the export (the
+// I4 / I16 choice reads luma only, the chroma mode chroma only), so wave A
+// (wave 0) runs import, context and the I4 RD while wave B (wave 1) runs the
+// I16 RD, the UV RD, the final residuals of I16 (speculatively) and chroma
+// and their reconstruction; A joins the two and exports.  A's early exit
+// takes B's I16 score once B has posted it; until then it runs on (an I4
+// pass the reference would have cut short loses to I16 all the same).  This
+// roughly halves a macroblock's latency for launches whose rows fit the
+// wave slots twice over (one frame, C2); a full batch keeps one wave a row.
+template <bool TRELLIS, bool PAIR>
+__global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_rows(EncArgs a) {
+  constexpr int NW = PAIR ? 2 : WAVES;
   __shared__ Tables t_lds;
-  __shared__ Shared s_waves[WAVES];
+  __shared__ Shared s_waves[NW];
   Tables& t = t_lds;
   const int tid = threadIdx.x;
-  constexpr int NT = 64 * WAVES;
+  constexpr int NT = 64 * NW;
   for (int i = tid; i < 1056; i += NT) t.proba[i] = a.proba[i];
   for (int i = tid; i < 256; i += NT) t.ecost[i] = vp8_entropy_cost[i];
   for (int i = tid; i < 2048; i += NT) t.lfixed[i] = vp8_level_fixed_costs[i];
   for (int i = tid; i < 1000; i += NT) t.fixed_i4[i] = c_fixed_i4[i];
   if (tid < 16) t.wtr[tid] = c_wtrellis[tid];
-  if (tid < 160) t.pcode[tid >> 4][tid & 15] = kPred4Code[tid >> 4][tid & 15];
+  for (int i = tid; i < 160; i += NT) t.pcode[i >> 4][i & 15] = kPred4Code[i >> 4][i & 15];
   __syncthreads();
   for (int i = tid; i < 4 * 8 * 68; i += NT) {
     const int tb = i / 68, level = i % 68;
@@ -965,6 +989,8 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
   __builtin_amdgcn_s_setprio(1);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
+  // roles (wave-uniform): one wave a row does both; in PAIR wave 0 is A, wave 1 is B
+  const bool isA = !PAIR || wave == 0, isB = !PAIR || wave == 1;
   Shared& s = s_waves[wave];
   const int mbw = a.mbw, mbh = a.mbh;
   const int ys = 16 * mbw, uvs = 8 * mbw;
@@ -973,10 +999,17 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
   ESTAMP_DECL;
 
   for (;;) {
-    if (lane == 0) s.word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    lds_sync();
-    const int row = __builtin_amdgcn_readfirstlane(s.word);
-    lds_sync();
+    int row;
+    if constexpr (PAIR) {  // the pair dequeues together (the next write of word is two barriers on)
+      if (tid == 0) s_waves[0].word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      row = __builtin_amdgcn_readfirstlane(s_waves[0].word);
+    } else {
+      if (lane == 0) s.word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lds_sync();
+      row = __builtin_amdgcn_readfirstlane(s.word);
+      lds_sync();
+    }
     if (row >= total_rows) break;
     const int mby = row / a.n_img, img = row % a.n_img;
     const uint8_t* Y = a.y + img * a.y_pitch;
@@ -1008,6 +1041,7 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
 
     for (int mbx = 0; mbx < mbw; mbx++) {
       Shared& s = launder(s_waves[wave]);
+      Shared& c = launder(s_waves[PAIR ? 0 : wave]);  // the MB's pixels and context (A's)
       Tables& t = launder(t_lds);
       const int lane = opaque_lane();
       const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
@@ -1040,10 +1074,13 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
           seen = __shfl(v, 0, 64);
         }
       };
-      wait_above(mbx + 1);
+      if (isA) wait_above(mbx + 1);
       ESTAMP(1);
       const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
       const Segment& sg = s.seg[segid];
+      uint32_t top_nz = 0, top_modes = 0;
+      int top_nz_dc = 0;
+      if (isA) {
       // ---- import (importBlockParallel :433-452) with edge replication ----
       // A lane loads one source row.  Where whole 32-B sectors lie inside the
       // image, a Y lane loads the rows of MB pairs (x even, x + 1) and a U / V
@@ -1088,8 +1125,6 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
         }
       }
       // ---- prediction context (fillPredContextParallel :455-562) ----
-      uint32_t top_nz = 0, top_modes = 0;
-      int top_nz_dc = 0;
       {
         const uint8_t* rec = top + mbx * REC;
         if (mby > 0) {
@@ -1115,30 +1150,58 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
       top_nz = __builtin_amdgcn_readfirstlane(top_nz);
       top_modes = __builtin_amdgcn_readfirstlane(top_modes);
       top_nz_dc = __builtin_amdgcn_readfirstlane(top_nz_dc);
+      if constexpr (PAIR) {  // B's inputs; A's working copy of the context for I4 (B writes yout from here on)
+        if (lane == 0) {
+          s.ctxw[0] = top_nz;
+          s.ctxw[1] = (uint32_t)top_nz_dc;
+          s.ctxw[2] = left_nz;
+          s.ctxw[3] = (uint32_t)left_nz_dc;
+          s.s16_flag = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < (YUV / 4 + 63) / 64; k++) {
+          const int i = lane + 64 * k;
+          if (i < YUV / 4) reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
+        }
+      }
+      }  // isA
+      if constexpr (PAIR) {
+        __syncthreads();
+        if (isB) {
+          top_nz = __builtin_amdgcn_readfirstlane(c.ctxw[0]);
+          top_nz_dc = __builtin_amdgcn_readfirstlane((int)c.ctxw[1]);
+          left_nz = __builtin_amdgcn_readfirstlane(c.ctxw[2]);
+          left_nz_dc = __builtin_amdgcn_readfirstlane((int)c.ctxw[3]);
+        }
+      }
 
       ESTAMP(2);
+      const int b = lane & 15, bx = b & 3, by = b >> 2;  // I16 lane = (mode, block)
+      int best16 = 0;
+      uint64_t s16 = ~0ull;
+      if (isB) {
       // ================= I16 RD (pickBestI16ModeRDParallel :624-737) =================
       bool src_flat;
       {
         // isFlatSource16 (encode_analysis.go:358)
-        const uint8_t v0 = s.yin[YOFF];
+        const uint8_t v0 = c.yin[YOFF];
         bool mine = true;
 #pragma unroll
         for (int k = 0; k < 4; k++) {  // fixed trip count (lane is opaque to the compiler)
           const int i = lane + 64 * k;
-          mine &= s.yin[YOFF + (i >> 4) * BPS + (i & 15)] == v0;
+          mine &= c.yin[YOFF + (i >> 4) * BPS + (i & 15)] == v0;
         }
         src_flat = __all(mine);
       }
-      const int m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
+      const int m = lane >> 4;
       const bool mvalid = !((m == 2 && mby == 0) || (m == 3 && mbx == 0) || (m == 1 && (mbx == 0 || mby == 0)));
       P4 src16, pred16;
       Q16 q16;
       int nz16 = 0, dc_in = 0;
       {
         const int off = YOFF + 4 * by * BPS + 4 * bx;
-        src16 = ld4(s.yin + off);
-        pred16 = predsq_p(check_mode(mbx, mby, m), s.yout + YOFF, 16, 4 * bx, 4 * by);
+        src16 = ld4(c.yin + off);
+        pred16 = predsq_p(check_mode(mbx, mby, m), c.yout + YOFF, 16, 4 * bx, 4 * by);
         int co[16];
         fdct_p(src16, pred16, co);
         dc_in = co[0];
@@ -1178,7 +1241,7 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
         }
         lds_sync();
       }
-      int best16 = 0, rate16 = 0, disto16 = 0;
+      int rate16 = 0, disto16 = 0;
       {
         uint64_t best = ~0ull;
         for (int mm = 0; mm < 4; mm++) {
@@ -1192,9 +1255,19 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
           }
         }
       }
-      const uint64_t s16 = rd_score(disto16, rate16, sg.lambda_mode);
+      s16 = rd_score(disto16, rate16, sg.lambda_mode);
+      if constexpr (PAIR) {  // for A's early exit: the score, then the flag
+        if (lane == 0) {
+          *reinterpret_cast<volatile uint64_t*>(&c.s16v) = s16;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          *reinterpret_cast<volatile int*>(&c.s16_flag) = 1;
+        }
+      }
+      }  // isB
 
       ESTAMP(3);
+      uint64_t s4 = ~0ull;
+      if (isA) {
       __builtin_amdgcn_s_setprio(2);
       // ================= I4 RD (tryI4ModesRDParallel :739-846) =================
       // The 16 blocks run as a wavefront, step st = bx + 2 by: a block's left,
@@ -1204,13 +1277,14 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
       // applied afterwards from the per-block results: a block reads only
       // reconstructions of raster-earlier blocks, so every block evaluated
       // before the exit point sees exactly the reference's inputs.
+      if constexpr (!PAIR) {  // (PAIR: copied before the pair's barrier)
 #pragma unroll
-      for (int k = 0; k < (YUV / 4 + 63) / 64; k++) {
-        const int i = lane + 64 * k;
-        if (i < YUV / 4) reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
+        for (int k = 0; k < (YUV / 4 + 63) / 64; k++) {
+          const int i = lane + 64 * k;
+          if (i < YUV / 4) reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
+        }
       }
       lds_sync();
-      uint64_t s4;
       {
         // running totals over the finished blocks: rate, distortion and header
         // bits only grow, so once the finished blocks alone reach the exit
@@ -1458,20 +1532,27 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
               run_disto += __builtin_amdgcn_readlane(disto, w1);
               run_header += __builtin_amdgcn_readlane(hdr, w1);
             }
-            early = rd_score(run_disto, run_rate + 211, sg.lambda_mode) >= s16 || run_header > 15000;
+            uint64_t s16_now = s16;
+            if constexpr (PAIR) {  // B's I16 score once posted (no exit before)
+              s16_now = ~0ull;
+              if (*reinterpret_cast<volatile int*>(&s.s16_flag)) s16_now = *reinterpret_cast<volatile uint64_t*>(&s.s16v);
+              s16_now = uniform64(s16_now);
+            }
+            early = rd_score(run_disto, run_rate + 211, sg.lambda_mode) >= s16_now || run_header > 15000;
           }
           lds_sync();
           SSTAMP(3);
         }
         s4 = early ? ~0ull : rd_score(run_disto, run_rate + 211, sg.lambda_mode);
       }
-      const bool is_i4 = s4 < s16;
       __builtin_amdgcn_s_setprio(1);
+      }  // isA
+      bool is_i4 = s4 < s16;  // (PAIR: decided at the join)
 
       ESTAMP(4);
       // ================= UV RD (pickBestUVModeRDParallel :1030-1114) =================
       int best_uv = 0;
-      {
+      if (isB) {
         const int um = lane >> 3, k = lane & 7, pl = k >> 2, ub = k & 3, ubx = ub & 1, uby = ub >> 1;
         const bool act = lane < 32;
         const bool uvalid = act && !((um == 2 && mby == 0) || (um == 3 && mbx == 0) || (um == 1 && (mbx == 0 || mby == 0)));
@@ -1480,8 +1561,8 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
         Q16 q;
         int nz = 0;
         if (act) {
-          src = ld4(s.yin + base + 4 * uby * BPS + 4 * ubx);
-          pred = predsq_p(check_mode(mbx, mby, um), s.yout + base, 8, 4 * ubx, 4 * uby);
+          src = ld4(c.yin + base + 4 * uby * BPS + 4 * ubx);
+          pred = predsq_p(check_mode(mbx, mby, um), c.yout + base, 8, 4 * ubx, 4 * uby);
           int co[16];
           fdct_p(src, pred, co);
           nz = quantize(co, q, sg.uv, 0);
@@ -1522,35 +1603,39 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
 
       // ================= predictions into yout (pickBestModeParallel :586-604) =================
       // (the square predictors read only the borders, so lanes write their blocks directly)
-      if (is_i4) {  // I4 reconstruction from the RD pass (I4Cached)
+      // PAIR: B runs the I16 residuals (and reconstruction) whatever A's I4 RD
+      // decides; A keeps them at the join if I16 wins
+      const bool run16 = PAIR || !is_i4;
+      uint32_t nzy_mask = 0, nzuv_mask = 0;
+      int nz_dc = 0, dc_rec = 0;  // dc_rec: lane b's reconstructed DC (I16)
+      if (isB) {
+      if (!PAIR && is_i4) {  // I4 reconstruction from the RD pass (I4Cached)
         if (lane < 16)
-          *reinterpret_cast<uint4*>(s.yout + YOFF + lane * BPS) = *reinterpret_cast<const uint4*>(s.yout2 + YOFF + lane * BPS);
+          *reinterpret_cast<uint4*>(c.yout + YOFF + lane * BPS) = *reinterpret_cast<const uint4*>(s.yout2 + YOFF + lane * BPS);
         else if (lane < 32)
           s.coeffs[384 + lane - 16] = 0;  // no WHT block for I4
-      } else if (lane < 16) {
+      } else if (run16 && lane < 16) {
         int p[16];
-        predsq_block(check_mode(mbx, mby, best16), s.yout + YOFF, 16, 4 * bx, 4 * by, p);
-        store4x4(s.yout + YOFF + 4 * by * BPS + 4 * bx, p);
+        predsq_block(check_mode(mbx, mby, best16), c.yout + YOFF, 16, 4 * bx, 4 * by, p);
+        store4x4(c.yout + YOFF + 4 * by * BPS + 4 * bx, p);
       }
       if (lane >= 32 && lane < 40) {
         const int k = lane - 32, pl = k >> 2, ub = k & 3;
         int p[16];
-        predsq_block(check_mode(mbx, mby, best_uv), s.yout + (pl ? VOFF : UOFF), 8, 4 * (ub & 1), 4 * (ub >> 1), p);
-        store4x4(s.yout + (pl ? VOFF : UOFF) + 4 * (ub >> 1) * BPS + 4 * (ub & 1), p);
+        predsq_block(check_mode(mbx, mby, best_uv), c.yout + (pl ? VOFF : UOFF), 8, 4 * (ub & 1), 4 * (ub >> 1), p);
+        store4x4(c.yout + (pl ? VOFF : UOFF) + 4 * (ub >> 1) * BPS + 4 * (ub & 1), p);
       }
       lds_sync();
 
       ESTAMP(5);
       // ================= final residuals (encodeResidualsParallel :1166-1356) =================
-      uint32_t nzy_mask = 0, nzuv_mask = 0;
-      int nz_dc = 0, dc_rec = 0;  // dc_rec: lane b's reconstructed DC (I16)
-      if (!is_i4) {
+      if (run16) {
         int dc_nz = 0;
         if (lane < 16) {
           const int off = YOFF + 4 * by * BPS + 4 * bx;
           int src[16], pred[16], co[16];
-          load4x4(s.yin + off, src);
-          load4x4(s.yout + off, pred);
+          load4x4(c.yin + off, src);
+          load4x4(c.yout + off, pred);
           fdct(src, pred, co);
           if constexpr (TRELLIS) {
 #pragma unroll
@@ -1656,15 +1741,13 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
         }
         }  // TRELLIS
       }
-      for (int i = 0; i < 16; i++) nzy_mask |= (s.nzy[i] > 0 ? 1u : 0u) << i;
-      if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
       if (lane < 8) {  // chroma
         const int pl = lane >> 2, ub = lane & 3;
         const int off = (pl ? VOFF : UOFF) + 4 * (ub >> 1) * BPS + 4 * (ub & 1);
         int src[16], pred[16], co[16];
         int16_t q[16];
-        load4x4(s.yin + off, src);
-        load4x4(s.yout + off, pred);
+        load4x4(c.yin + off, src);
+        load4x4(c.yout + off, pred);
         fdct(src, pred, co);
         const int nz = quantize(co, q, sg.uv, 0);
         s.nzuv[lane] = (uint8_t)nz;
@@ -1672,11 +1755,10 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
         for (int i = 0; i < 16; i++) s.coeffs[(16 + lane) * 16 + i] = q[i];
       }
       lds_sync();
-      for (int i = 0; i < 8; i++) nzuv_mask |= (s.nzuv[i] > 0 ? 1u : 0u) << i;
 
       ESTAMP(6);
       // ================= reconstruction (reconstructMBParallel :1358-1410) =================
-      if (!is_i4) {
+      if (run16) {
         if (lane < 16) {
           const int off = YOFF + 4 * by * BPS + 4 * bx;
           int16_t q[16];
@@ -1685,9 +1767,9 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
           for (int i = 0; i < 16; i++) q[i] = s.coeffs[lane * 16 + i];
           dequant(q, dq, sg.y1);
           dq[0] = dc_rec;
-          load4x4(s.yout + off, pred);
+          load4x4(c.yout + off, pred);
           recon4(pred, dq, rec);
-          store4x4(s.yout + off, rec);
+          store4x4(c.yout + off, rec);
         }
       }
       if (lane >= 16 && lane < 24) {
@@ -1698,11 +1780,51 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
 #pragma unroll
         for (int i = 0; i < 16; i++) q[i] = s.coeffs[(16 + k) * 16 + i];
         dequant(q, dq, sg.uv);
-        load4x4(s.yout + off, pred);
+        load4x4(c.yout + off, pred);
         recon4(pred, dq, rec);
-        store4x4(s.yout + off, rec);
+        store4x4(c.yout + off, rec);
       }
       lds_sync();
+      if constexpr (PAIR) {
+        if (lane == 0) {
+          s.post_best16 = best16;
+          s.post_best_uv = best_uv;
+          s.post_nz_dc = nz_dc;
+          s.post_s16 = s16;
+        }
+      }
+      }  // isB
+      if constexpr (PAIR) {
+        // ---- the join: A keeps B's I16 residuals and reconstruction or its own I4 ones ----
+        __syncthreads();
+        if (isA) {
+          const Shared& sb = launder(s_waves[1]);
+          best16 = __builtin_amdgcn_readfirstlane(sb.post_best16);
+          best_uv = __builtin_amdgcn_readfirstlane(sb.post_best_uv);
+          s16 = uniform64(sb.post_s16);
+          is_i4 = s4 < s16;
+          nz_dc = is_i4 ? 0 : __builtin_amdgcn_readfirstlane(sb.post_nz_dc);
+          const uint4* bq = reinterpret_cast<const uint4*>(sb.coeffs);  // 50 x 16 B
+          uint4* cq = reinterpret_cast<uint4*>(s.coeffs);
+          if (is_i4) {
+            if (lane < 16)  // the I4 reconstruction (I4Cached)
+              *reinterpret_cast<uint4*>(s.yout + YOFF + lane * BPS) = *reinterpret_cast<const uint4*>(s.yout2 + YOFF + lane * BPS);
+            else if (lane < 32)  // chroma levels (coeffs[256..383] = 16-B pieces 32..47)
+              cq[lane + 16] = bq[lane + 16];
+            else if (lane < 48)
+              s.coeffs[384 + lane - 32] = 0;  // no WHT block for I4
+          } else {
+            if (lane < 50) cq[lane] = bq[lane];  // luma, chroma and WHT levels
+            else if (lane < 54) reinterpret_cast<uint32_t*>(s.nzy)[lane - 50] = reinterpret_cast<const uint32_t*>(sb.nzy)[lane - 50];
+          }
+          if (lane >= 56 && lane < 58) reinterpret_cast<uint32_t*>(s.nzuv)[lane - 56] = reinterpret_cast<const uint32_t*>(sb.nzuv)[lane - 56];
+          lds_sync();
+        }
+      }
+      if (isA) {
+      for (int i = 0; i < 16; i++) nzy_mask |= (s.nzy[i] > 0 ? 1u : 0u) << i;
+      if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
+      for (int i = 0; i < 8; i++) nzuv_mask |= (s.nzuv[i] > 0 ? 1u : 0u) << i;
 
       // ================= outputs, export, contexts (exportParallel :1412-1495) =================
       MbEnc* o = a.out + mbi;
@@ -1871,6 +1993,7 @@ __global__ __launch_bounds__(64 * WAVES, WG_ENC_OCC) void k_encode_rows(EncArgs 
       lds_sync();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }  // isA
       ESTAMP(7);
     }
   }
@@ -1992,17 +2115,33 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   a.quality = quality;
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(encode ctl)");
-  int cus = 0, per_cu = 0;
+  int cus = 0, per_cu = 0, per_cu_pair = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows<true>, 64 * WAVES, 0) != hipSuccess || per_cu <= 0)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows<true, false>, 64 * WAVES, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pair, k_encode_rows<true, true>, 128, 0) != hipSuccess ||
+      per_cu <= 0 || per_cu_pair <= 0)
     return wg::check_launch("encode occupancy query");
   const int rows = n_images * mbh;
-  const int wgs = (rows + WAVES - 1) / WAVES;  // each wave dequeues rows on its own
-  const int grid = wgs < per_cu * cus ? wgs : per_cu * cus;
-  if (method >= 4)
-    hipLaunchKernelGGL(k_encode_rows<true>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
-  else
-    hipLaunchKernelGGL(k_encode_rows<false>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
+  // a wave pair per row when every row fits at once (one frame, a few
+  // frames); a full batch has more rows than wave slots and keeps one wave
+  // per row (two waves a row would halve the rows in flight).
+  // WG_ENCODE_PAIR=0 / 1 forces either schedule (A/B, tests).
+  bool pair = rows <= per_cu_pair * cus;
+  if (const char* e = getenv("WG_ENCODE_PAIR")) pair = e[0] == '1';
+  if (pair) {
+    const int grid = rows < per_cu_pair * cus ? rows : per_cu_pair * cus;
+    if (method >= 4)
+      hipLaunchKernelGGL((k_encode_rows<true, true>), dim3((unsigned)grid), dim3(128), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_encode_rows<false, true>), dim3((unsigned)grid), dim3(128), 0, s, a);
+  } else {
+    const int wgs = (rows + WAVES - 1) / WAVES;  // each wave dequeues rows on its own
+    const int grid = wgs < per_cu * cus ? wgs : per_cu * cus;
+    if (method >= 4)
+      hipLaunchKernelGGL((k_encode_rows<true, false>), dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_encode_rows<false, false>), dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
+  }
   return wg::check_launch("k_encode_rows");
 }
 
