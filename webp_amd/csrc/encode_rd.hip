@@ -1826,6 +1826,81 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
       if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
       for (int i = 0; i < 8; i++) nzuv_mask |= (s.nzuv[i] > 0 ? 1u : 0u) << i;
 
+      // The hand-off record and the progress flag go first: the row below
+      // waits on them (at its MB start and its I4 step 3), while the MBEncInfo
+      // record and the reconstruction rows are outputs only and leave after.
+      // NZ context update (updateNZContextParallel :343-430)
+      uint32_t out_t, out_l;
+      {
+        const int first = is_i4 ? 0 : 1;
+        uint32_t tnz = top_nz & 0x0f, lnz = left_nz & 0x0f;
+        for (int yy = 0; yy < 4; yy++) {
+          uint32_t l = lnz & 1;
+          for (int xx = 0; xx < 4; xx++) {
+            l = s.nzy[yy * 4 + xx] > first;
+            tnz = (tnz >> 1) | (l << 7);
+          }
+          tnz >>= 4;
+          lnz = (lnz >> 1) | (l << 7);
+        }
+        out_t = tnz;
+        out_l = lnz >> 4;
+        for (int ch = 0; ch < 4; ch += 2) {
+          tnz = (top_nz >> (4 + ch)) & 0x0f;
+          lnz = (left_nz >> (4 + ch)) & 0x0f;
+          for (int yy = 0; yy < 2; yy++) {
+            uint32_t l = lnz & 1;
+            for (int xx = 0; xx < 2; xx++) {
+              l = s.nzuv[(ch / 2) * 4 + yy * 2 + xx] > 0;
+              tnz = (tnz >> 1) | (l << 3);
+            }
+            tnz >>= 2;
+            lnz = (lnz >> 1) | (l << 5);
+          }
+          out_t |= (tnz << 4) << ch;
+          out_l |= (lnz & 0xf0) << ch;
+        }
+      }
+      int new_top_dc = top_nz_dc;
+      if (!is_i4) {
+        new_top_dc = nz_dc > 0;
+        left_nz_dc = nz_dc > 0;
+      }
+      uint32_t new_top_modes;
+      if (is_i4) {
+        new_top_modes = (uint32_t)s.modes4[12] | ((uint32_t)s.modes4[13] << 8) | ((uint32_t)s.modes4[14] << 16) |
+                        ((uint32_t)s.modes4[15] << 24);
+        left_modes = (uint32_t)s.modes4[3] | ((uint32_t)s.modes4[7] << 8) | ((uint32_t)s.modes4[11] << 16) |
+                     ((uint32_t)s.modes4[15] << 24);
+      } else {
+        new_top_modes = 0;
+        left_modes = 0;
+      }
+      left_nz = out_l;
+      // hand-off record for the row below, then publish: staged in LDS and
+      // written as three 16-B write-through stores
+      if (mby < mbh - 1) {
+        if (lane < 8) {
+          const int so = lane < 4 ? YOFF + 15 * BPS + 4 * lane : (lane < 6 ? UOFF + 7 * BPS + 4 * (lane - 4) : VOFF + 7 * BPS + 4 * (lane - 6));
+          s.handoff[lane] = *reinterpret_cast<const uint32_t*>(s.yout + so);
+        } else if (lane == 8) {
+          s.handoff[8] = out_t;
+        } else if (lane == 9) {
+          s.handoff[9] = new_top_modes;
+        } else if (lane == 10) {
+          s.handoff[10] = (uint32_t)new_top_dc;
+        } else if (lane == 11) {
+          s.handoff[11] = 0;
+        }
+        lds_sync();
+        if (lane < 3) {
+          const uint4 w = reinterpret_cast<const uint4*>(s.handoff)[lane];
+          u32x4_t v = {w.x, w.y, w.z, w.w};
+          st_sc1_128(top + mbx * REC + 16 * lane, v);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record is visible before the flag
+      if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // ================= outputs, export, contexts (exportParallel :1412-1495) =================
       MbEnc* o = a.out + mbi;
       {  // the record's tail (bytes 800..863) staged next to the levels in LDS
@@ -1914,76 +1989,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
       tl_y = s.yout[YOFF - BPS + 15];
       tl_u = s.yout[UOFF - BPS + 7];
       tl_v = s.yout[VOFF - BPS + 7];
-      // NZ context update (updateNZContextParallel :343-430)
-      uint32_t out_t, out_l;
-      {
-        const int first = is_i4 ? 0 : 1;
-        uint32_t tnz = top_nz & 0x0f, lnz = left_nz & 0x0f;
-        for (int yy = 0; yy < 4; yy++) {
-          uint32_t l = lnz & 1;
-          for (int xx = 0; xx < 4; xx++) {
-            l = s.nzy[yy * 4 + xx] > first;
-            tnz = (tnz >> 1) | (l << 7);
-          }
-          tnz >>= 4;
-          lnz = (lnz >> 1) | (l << 7);
-        }
-        out_t = tnz;
-        out_l = lnz >> 4;
-        for (int ch = 0; ch < 4; ch += 2) {
-          tnz = (top_nz >> (4 + ch)) & 0x0f;
-          lnz = (left_nz >> (4 + ch)) & 0x0f;
-          for (int yy = 0; yy < 2; yy++) {
-            uint32_t l = lnz & 1;
-            for (int xx = 0; xx < 2; xx++) {
-              l = s.nzuv[(ch / 2) * 4 + yy * 2 + xx] > 0;
-              tnz = (tnz >> 1) | (l << 3);
-            }
-            tnz >>= 2;
-            lnz = (lnz >> 1) | (l << 5);
-          }
-          out_t |= (tnz << 4) << ch;
-          out_l |= (lnz & 0xf0) << ch;
-        }
-      }
-      int new_top_dc = top_nz_dc;
-      if (!is_i4) {
-        new_top_dc = nz_dc > 0;
-        left_nz_dc = nz_dc > 0;
-      }
-      uint32_t new_top_modes;
-      if (is_i4) {
-        new_top_modes = (uint32_t)s.modes4[12] | ((uint32_t)s.modes4[13] << 8) | ((uint32_t)s.modes4[14] << 16) |
-                        ((uint32_t)s.modes4[15] << 24);
-        left_modes = (uint32_t)s.modes4[3] | ((uint32_t)s.modes4[7] << 8) | ((uint32_t)s.modes4[11] << 16) |
-                     ((uint32_t)s.modes4[15] << 24);
-      } else {
-        new_top_modes = 0;
-        left_modes = 0;
-      }
-      left_nz = out_l;
-      // hand-off record for the row below, then publish: staged in LDS and
-      // written as three 16-B write-through stores
-      if (mby < mbh - 1) {
-        if (lane < 8) {
-          const int so = lane < 4 ? YOFF + 15 * BPS + 4 * lane : (lane < 6 ? UOFF + 7 * BPS + 4 * (lane - 4) : VOFF + 7 * BPS + 4 * (lane - 6));
-          s.handoff[lane] = *reinterpret_cast<const uint32_t*>(s.yout + so);
-        } else if (lane == 8) {
-          s.handoff[8] = out_t;
-        } else if (lane == 9) {
-          s.handoff[9] = new_top_modes;
-        } else if (lane == 10) {
-          s.handoff[10] = (uint32_t)new_top_dc;
-        } else if (lane == 11) {
-          s.handoff[11] = 0;
-        }
-        lds_sync();
-        if (lane < 3) {
-          const uint4 w = reinterpret_cast<const uint4*>(s.handoff)[lane];
-          u32x4_t v = {w.x, w.y, w.z, w.w};
-          st_sc1_128(top + mbx * REC + 16 * lane, v);
-        }
-      }
       // rotate the left context: column 15 / 7 becomes column -1
       lds_sync();
       if (lane < 16) s.yout[YOFF - 1 + lane * BPS] = s.yout[YOFF + 15 + lane * BPS];
@@ -1991,8 +1996,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
       else if (lane < 32) s.yout[VOFF - 1 + (lane - 24) * BPS] = s.yout[VOFF + 7 + (lane - 24) * BPS];
       if (lane < 16) s.nzy[lane] = 0;
       lds_sync();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }  // isA
       ESTAMP(7);
     }
