@@ -1053,6 +1053,29 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         STAMP(9);
         lane = opaque_lane() & 63;
         // ---- stores (as k_decode_bands) ----
+        // A band's last row first stores the rows the next band reads (MB
+        // x - 1's bottom rows, final after this MB's left-edge filter) and
+        // publishes; the other frame rows are outputs only and follow.
+        if (!to_lds) {
+          const int which = lane >> 5, k = lane & 31, x = mbx - 1 + which;
+          if (which == 0 ? mbx > 0 : mbx == mbw - 1) {
+            if (k < 4) {
+              const int j = 12 + k;
+              const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
+              uint8_t* dst = Yp + (int64_t)(16 * mby + j) * ys + 16 * x;
+              st_sc1_64(dst, (uint64_t)w.y << 32 | w.x);
+              st_sc1_64(dst + 8, (uint64_t)w.w << 32 | w.z);
+            } else if (k < 12) {
+              const int pl = k >= 8, j = 4 + (k & 3);
+              st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x,
+                        lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
+            }
+          }
+          if (mby < mbh - 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows are out before the flag
+            if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
         {
           const bool last = mbx == mbw - 1;
           int y0 = -1, y1 = -1;
@@ -1085,22 +1108,6 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
             if (c0 >= 0 && i < 80 && j < clim && x <= c1)
               *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x) =
                   lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx));
-          }
-          if (!to_lds) {
-            const int which = lane >> 5, k = lane & 31, x = mbx - 1 + which;
-            if (which == 0 ? mbx > 0 : last) {
-              if (k < 4) {
-                const int j = 12 + k;
-                const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
-                uint8_t* dst = Yp + (int64_t)(16 * mby + j) * ys + 16 * x;
-                st_sc1_64(dst, (uint64_t)w.y << 32 | w.x);
-                st_sc1_64(dst + 8, (uint64_t)w.w << 32 | w.z);
-              } else if (k < 12) {
-                const int pl = k >= 8, j = 4 + (k & 3);
-                st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x,
-                          lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
-              }
-            }
           }
           if (mby > 0) {
             int t0 = -1, t1 = -1;
@@ -1138,10 +1145,6 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         }
         lds_sync();
         lane = opaque_lane() & 63;
-        if (!to_lds && mby < mbh - 1) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this MB is out before the flag
-          if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
         if (lane == 0) {
           __hip_atomic_store(&prog_f[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           if (mbx == mbw - 1) __hip_atomic_store(&bot_f[r], mbw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
