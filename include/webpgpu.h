@@ -230,7 +230,10 @@ size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images);
  * 16*mbw / 8*mbw bytes (the reference's padded layout); y and ry 16-byte
  * aligned with y_pitch a multiple of 16, u, v, ru, rv 8-byte aligned with
  * uv_pitch a multiple of 8; out (wg_mb_enc [n][mbh][mbw]) and work 16-byte
- * aligned.  Methods 3-6, mbh >= 4 (else WG_EINVAL). */
+ * aligned.  Methods 3-6, mbh >= 4 (else WG_EINVAL).  Launches whose rows fit
+ * the device's wave slots twice walk each row with a wave pair (I4 RD beside
+ * the I16 / chroma work), larger ones with one wave a row; the outputs are the
+ * same (environment WG_ENCODE_PAIR=0 / 1 forces either schedule). */
 int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t y_pitch, int64_t uv_pitch,
                   int32_t width, int32_t height, int32_t n_images, const uint8_t* segments, const void* segs,
                   int64_t segs_pitch, const uint8_t* proba, int32_t method, int32_t quality, void* out, uint8_t* ry, uint8_t* ru,

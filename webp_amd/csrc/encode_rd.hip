@@ -163,7 +163,7 @@ struct Shared {
   alignas(16) uint32_t handoff[12];  // the 48-B hand-off record, staged for three 16-B write-through stores
   uint8_t modes4[16];
   uint8_t nzy[16], nzuv[8];
-  int mode_rate[4], mode_disto[4];
+  int mode_rate[4], mode_disto[4], uv_rate[4], uv_disto[4];
   int co_buf[16][16];      // transform coefficients handed to the trellis prep lanes
   TRec trec[6][16];        // trellis position records: I4 (half, candidate) / final I16 (diagonal slot)
   int l0s[6][16];          // per position: L0 << 3 | negative << 2 | min(L0, 2)
@@ -1177,10 +1177,13 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
 
       ESTAMP(2);
       const int b = lane & 15, bx = b & 3, by = b >> 2;  // I16 lane = (mode, block)
-      int best16 = 0;
+      int best16 = 0, best_uv = 0;
       uint64_t s16 = ~0ull;
       if (isB) {
       // ================= I16 RD (pickBestI16ModeRDParallel :624-737) =================
+      // and UV RD (pickBestUVModeRDParallel :1030-1114) in one pass: the two
+      // are independent, and as one straight-line stream their dependency
+      // chains interleave instead of running back to back
       bool src_flat;
       {
         // isFlatSource16 (encode_analysis.go:358)
@@ -1208,6 +1211,23 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
         co[0] = 0;
         nz16 = quantize(co, q16, sg.y1, 1);
       }
+      // UV lane = (mode, plane, block) over lanes 0..31; lanes 32..63 repeat
+      // them (discarded) so that no branch splits the stream
+      const int ul = lane & 31, um = ul >> 3, uk = ul & 7, upl = uk >> 2, uub = uk & 3, uubx = uub & 1, uuby = uub >> 1;
+      P4 usrc, upred;
+      Q16 uq;
+      int unz;
+      {
+        const int base = upl ? VOFF : UOFF;
+        usrc = ld4(c.yin + base + 4 * uuby * BPS + 4 * uubx);
+        upred = predsq_p(check_mode(mbx, mby, um), c.yout + base, 8, 4 * uubx, 4 * uuby);
+        int co[16];
+        fdct_p(usrc, upred, co);
+        unz = quantize(co, uq, sg.uv, 0);
+      }
+      // left / top block of the same plane (only read when ubx / uby > 0): DPP row shifts
+      const int unzl = __builtin_amdgcn_update_dpp(0, unz, 0x111, 0xf, 0xf, false);  // row_shr:1
+      const int unzt = __builtin_amdgcn_update_dpp(0, unz, 0x112, 0xf, 0xf, false);  // row_shr:2
       // contexts from the neighbours' nz within the same mode
       // left / top neighbour within the mode's 16-lane row (only read when bx / by > 0): DPP row shifts
       const int nz_left = __builtin_amdgcn_update_dpp(0, nz16, 0x111, 0xf, 0xf, false);  // row_shr:1
@@ -1216,7 +1236,19 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
         const int l = bx > 0 ? (nz_left > 0) : (int)((left_nz >> by) & 1);
         const int tp = by > 0 ? (nz_top > 0) : (int)((top_nz >> bx) & 1);
         const int ctx = min(l + tp, 2);
-        int rate = mvalid ? token_cost(t, q16, nz16, 0, ctx, 1) : 0;
+        int rate = token_cost(t, q16, nz16, 0, ctx, 1);
+        rate = mvalid ? rate : 0;
+        int urate, usse, uacn = 0;
+        {
+          const int ul_ = uubx > 0 ? (unzl > 0) : (int)((left_nz >> (4 + 2 * upl + uuby)) & 1);
+          const int ut_ = uuby > 0 ? (unzt > 0) : (int)((top_nz >> (4 + 2 * upl + uubx)) & 1);
+          urate = token_cost(t, uq, unz, 2, min(ul_ + ut_, 2), 0);
+          int dq[16];
+          dequant(uq, dq, sg.uv);
+          usse = sse_p(usrc, recon_p(upred, dq));
+#pragma unroll
+          for (int i = 1; i < 16; i++) uacn += uq.get(i) != 0;
+        }
         bool acnz = false;
 #pragma unroll
         for (int i = 1; i < 16; i++) acnz |= q16.get(i) != 0;
@@ -1231,6 +1263,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
         const int td = sg.tlambda_sd > 0 ? tdisto_p(src16, rec16) : 0;
         const int rsum = group_sum_first<16>(rate), ssum = group_sum_first<16>(sse), tsum = group_sum_first<16>(td);  // used by lane b == 0
         const unsigned long long acmask = __ballot(acnz);
+        const int ursum = group_sum_first<8>(urate), ussum = group_sum_first<8>(usse), uasum = group_sum_first<8>(uacn);  // lane uk == 0
         if (b == 0 && mvalid) {
           const int total_rate = vp8_mode_fixed_cost16[m] + dccost + rsum;
           int disto = ssum;
@@ -1239,7 +1272,24 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
           s.mode_rate[m] = total_rate;
           s.mode_disto[m] = disto;
         }
+        if (lane < 32 && uk == 0) {
+          int total = vp8_mode_fixed_cost_uv[um] + ursum;
+          if (um > 0 && uasum <= 2) total += 140 * 8;
+          s.uv_rate[um] = total;
+          s.uv_disto[um] = ussum;
+        }
         lds_sync();
+      }
+      {
+        uint64_t best = ~0ull;
+        for (int mm = 0; mm < 4; mm++) {
+          if ((mm == 2 && mby == 0) || (mm == 3 && mbx == 0) || (mm == 1 && (mbx == 0 || mby == 0))) continue;
+          const uint64_t sc = rd_score(s.uv_disto[mm], s.uv_rate[mm], sg.lambda_uv);
+          if (sc < best) {
+            best = sc;
+            best_uv = mm;
+          }
+        }
       }
       int rate16 = 0, disto16 = 0;
       {
@@ -1550,57 +1600,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
       bool is_i4 = s4 < s16;  // (PAIR: decided at the join)
 
       ESTAMP(4);
-      // ================= UV RD (pickBestUVModeRDParallel :1030-1114) =================
-      int best_uv = 0;
-      if (isB) {
-        const int um = lane >> 3, k = lane & 7, pl = k >> 2, ub = k & 3, ubx = ub & 1, uby = ub >> 1;
-        const bool act = lane < 32;
-        const bool uvalid = act && !((um == 2 && mby == 0) || (um == 3 && mbx == 0) || (um == 1 && (mbx == 0 || mby == 0)));
-        const int base = pl ? VOFF : UOFF;
-        P4 src, pred;
-        Q16 q;
-        int nz = 0;
-        if (act) {
-          src = ld4(c.yin + base + 4 * uby * BPS + 4 * ubx);
-          pred = predsq_p(check_mode(mbx, mby, um), c.yout + base, 8, 4 * ubx, 4 * uby);
-          int co[16];
-          fdct_p(src, pred, co);
-          nz = quantize(co, q, sg.uv, 0);
-        }
-        // left / top block of the same plane (only read when ubx / uby > 0): DPP row shifts
-        const int nzl = __builtin_amdgcn_update_dpp(0, nz, 0x111, 0xf, 0xf, false);  // row_shr:1
-        const int nzt = __builtin_amdgcn_update_dpp(0, nz, 0x112, 0xf, 0xf, false);  // row_shr:2
-        int rate = 0, sse = 0, acn = 0;
-        if (act) {
-          const int l = ubx > 0 ? (nzl > 0) : (int)((left_nz >> (4 + 2 * pl + uby)) & 1);
-          const int tp = uby > 0 ? (nzt > 0) : (int)((top_nz >> (4 + 2 * pl + ubx)) & 1);
-          rate = uvalid ? token_cost(t, q, nz, 2, min(l + tp, 2), 0) : 0;
-          int dq[16];
-          dequant(q, dq, sg.uv);
-          sse = sse_p(src, recon_p(pred, dq));
-#pragma unroll
-          for (int i = 1; i < 16; i++) acn += q.get(i) != 0;
-        }
-        const int rsum = group_sum_first<8>(rate), ssum = group_sum_first<8>(sse), asum = group_sum_first<8>(acn);  // used by lane k == 0
-        if (act && k == 0) {
-          int total = vp8_mode_fixed_cost_uv[um] + rsum;
-          if (um > 0 && asum <= 2) total += 140 * 8;
-          s.mode_rate[um] = total;
-          s.mode_disto[um] = ssum;
-        }
-        lds_sync();
-        uint64_t best = ~0ull;
-        for (int mm = 0; mm < 4; mm++) {
-          if ((mm == 2 && mby == 0) || (mm == 3 && mbx == 0) || (mm == 1 && (mbx == 0 || mby == 0))) continue;
-          const uint64_t sc = rd_score(s.mode_disto[mm], s.mode_rate[mm], sg.lambda_uv);
-          if (sc < best) {
-            best = sc;
-            best_uv = mm;
-          }
-        }
-        lds_sync();
-      }
-
       // ================= predictions into yout (pickBestModeParallel :586-604) =================
       // (the square predictors read only the borders, so lanes write their blocks directly)
       // PAIR: B runs the I16 residuals (and reconstruction) whatever A's I4 RD
