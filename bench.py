@@ -426,7 +426,7 @@ def main():
             rec["valu"] = valu
         if gather is not None:
             rec["gather"] = gather
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is timed at N = 1 only
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds, parsed)
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -240,6 +240,21 @@ int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t 
                   uint8_t* rv, void* work, void* stream);
 /* After wg_encode_mbs on the same stream: WG_OK or WG_EHIP on a row-wait timeout.  Synchronises. */
 int wg_encode_status(const void* work, int32_t mbw, int32_t n_images, void* stream);
+/* The multi-device batch variant of the encode DSP path (one host process
+ * driving several GPUs, as a cgo host would): n_images RGBA frames (w x h,
+ * tightly packed, n_images * w * h * 4 bytes of HOST memory); frame i is
+ * encoded on devices[i % n_devices] (each device listed once), each device
+ * running wg_import_rgba -> wg_analysis_alphas -> wg_segment_analysis (cfg,
+ * host) -> wg_encode_mbs over its frames on its own stream, with the default
+ * token probabilities (CoeffsProba0).  The outputs are gathered into HOST
+ * buffers in frame order: mb_out wg_mb_enc [n][mbh*mbw]; ry [n][16*mbh][16*mbw],
+ * ru / rv [n][8*mbh][8*mbw], seg_ids [n][mbh*mbw], info [n] (each may be NULL
+ * but mb_out).  Replaces the per-frame EncodeFrame calls up to Phase A
+ * (internal/lossy/encode.go:1324-1366) for a batch of independent frames
+ * (C4); blocks until every device is done.  WG_EINVAL for mbh < 4. */
+int wg_encode_frames_devices(const int32_t* devices, int32_t n_devices, const uint8_t* rgba, int32_t w, int32_t h,
+                             int32_t n_images, int32_t has_alpha, const wg_enc_config* cfg, void* mb_out, uint8_t* ry,
+                             uint8_t* ru, uint8_t* rv, uint8_t* seg_ids, wg_frame_segs* info);
 /* VP8FixedCostsI4[top][left][mode] (encode_analysis.go:1498-1520) as
  * uploaded by wg_encode_mbs; host memory, 1000 uint16. */
 int wg_fixed_costs_i4_host(uint16_t* out);

@@ -106,6 +106,7 @@ SIGNATURES = {
     "wg_encoder_config": [_i32] * 8 + [_vp],
     "wg_segment_analysis": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp],
     "wg_encode_status": [_vp, _i32, _i32, _vp],
+    "wg_encode_frames_devices": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
 }
 _RES = {"wg_last_error": ctypes.c_char_p, "wg_decode_work_bytes": ctypes.c_size_t,
         "wg_plane_ssim_work_bytes": ctypes.c_size_t, "wg_vp8l_inverse_work_bytes": ctypes.c_size_t,

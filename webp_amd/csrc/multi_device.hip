@@ -1,0 +1,151 @@
+// multi_device.hip -- the multi-device batch variant of the encode DSP path
+// (last bullet; 8(e) C4) for a host that drives every GPU from
+// one process, as the reference's Go program would through cgo.
+//
+// Frame i belongs to device devices[i % n_devices] (round-robin, the ownership
+// webp_amd/shard.py frames_of uses for the one-process-per-GPU path).  Each
+// device runs the whole device encode path over its frames on a stream of
+// its own -- import (importImage, internal/lossy/encode.go:671-943) ->
+// computeAlphas (encode_analysis.go:245-307) -> analysis() segments
+// (encode_analysis.go:29-903) -> Phase A of encodeFrameParallel
+// (encode_parallel.go:168-232) -- with no exchange between devices.  The only
+// cross-device step is the final gather: every frame's MBEncInfo records,
+// reconstruction, segment map and segment header come back to the caller's
+// host buffers in frame order, which is where the reference's Phase B
+// (recordAllTokens, encode_parallel.go:1497) and the bitstream writer run.
+#include <vector>
+
+#include "vp8_tables.h"
+#include "wg_common.h"
+
+namespace {
+
+struct DevJob {
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  std::vector<int> frames;  // global frame indices, in order
+  void* mem = nullptr;      // one allocation, carved below
+  uint8_t *rgba = nullptr, *y = nullptr, *u = nullptr, *v = nullptr, *seg_ids = nullptr, *segs = nullptr;
+  uint8_t *proba = nullptr, *out = nullptr, *work = nullptr, *ry = nullptr, *ru = nullptr, *rv = nullptr;
+  int32_t *alphas = nullptr, *uv_sum = nullptr;
+  wg_frame_segs* info = nullptr;
+};
+
+inline size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+int fail_hip(hipError_t e, const char* what) {
+  wg::set_error(std::string(what) + ": " + hipGetErrorString(e));
+  return WG_EHIP;
+}
+
+}  // namespace
+
+extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_devices, const uint8_t* rgba, int32_t w,
+                                        int32_t h, int32_t n_images, int32_t has_alpha, const wg_enc_config* cfg,
+                                        void* mb_out, uint8_t* ry, uint8_t* ru, uint8_t* rv, uint8_t* seg_ids_out,
+                                        wg_frame_segs* info_out) {
+  WG_REQUIRE(devices && n_devices > 0 && rgba && cfg && mb_out);
+  WG_REQUIRE(w > 0 && h > 0 && n_images > 0);
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess) return wg::check_launch("hipGetDeviceCount");
+  for (int k = 0; k < n_devices; k++) {
+    WG_REQUIRE(devices[k] >= 0 && devices[k] < count);
+    for (int j = 0; j < k; j++) WG_REQUIRE(devices[j] != devices[k]);  // a device appears once
+  }
+  const int mbw = (w + 15) >> 4, mbh = (h + 15) >> 4;
+  if (mbh < 4) return wg::invalid("mbh >= 4 (encode.go:1356 encodes smaller frames serially)");
+  const int64_t n_mb = (int64_t)mbw * mbh;
+  const int64_t rgba_b = (int64_t)w * h * 4, y_b = 256 * n_mb, uv_b = 64 * n_mb, seg_pitch = 4 * sizeof(wg_segment);
+  int prev_dev = 0;
+  if (hipGetDevice(&prev_dev) != hipSuccess) return wg::check_launch("hipGetDevice");
+
+  std::vector<DevJob> jobs((size_t)n_devices);
+  for (int i = 0; i < n_images; i++) jobs[(size_t)(i % n_devices)].frames.push_back(i);
+  int rc = WG_OK;
+  // enqueue every device's work first, so the devices run at once
+  for (auto& j : jobs) {
+    j.dev = devices[&j - jobs.data()];
+    const int nk = (int)j.frames.size();
+    if (nk == 0) continue;
+    hipError_t e = hipSetDevice(j.dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&j.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      rc = fail_hip(e, "device setup");
+      break;
+    }
+    const size_t work_b = wg_encode_work_bytes(mbw, mbh, nk);
+    size_t sz[15] = {(size_t)(rgba_b * nk), (size_t)(y_b * nk), (size_t)(uv_b * nk), (size_t)(uv_b * nk),
+                     (size_t)(n_mb * nk), (size_t)(seg_pitch * nk), sizeof(vp8_coeffs_proba0),
+                     (size_t)(n_mb * nk) * sizeof(wg_mb_enc), work_b, (size_t)(y_b * nk), (size_t)(uv_b * nk),
+                     (size_t)(uv_b * nk), (size_t)(n_mb * nk) * 4, (size_t)nk * 4, (size_t)nk * sizeof(wg_frame_segs)};
+    size_t total = 0;
+    for (size_t s : sz) total += align_up(s);
+    if ((e = hipMalloc(&j.mem, total)) != hipSuccess) {
+      rc = fail_hip(e, "hipMalloc (encode batch)");
+      break;
+    }
+    uint8_t* p = static_cast<uint8_t*>(j.mem);
+    uint8_t* parts[15];
+    for (int q = 0; q < 15; q++) {
+      parts[q] = p;
+      p += align_up(sz[q]);
+    }
+    j.rgba = parts[0], j.y = parts[1], j.u = parts[2], j.v = parts[3], j.seg_ids = parts[4], j.segs = parts[5];
+    j.proba = parts[6], j.out = parts[7], j.work = parts[8], j.ry = parts[9], j.ru = parts[10], j.rv = parts[11];
+    j.alphas = reinterpret_cast<int32_t*>(parts[12]), j.uv_sum = reinterpret_cast<int32_t*>(parts[13]);
+    j.info = reinterpret_cast<wg_frame_segs*>(parts[14]);
+    for (int q = 0; q < nk && e == hipSuccess; q++)
+      e = hipMemcpyAsync(j.rgba + q * rgba_b, rgba + (int64_t)j.frames[(size_t)q] * rgba_b, (size_t)rgba_b,
+                         hipMemcpyHostToDevice, j.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(j.proba, vp8_coeffs_proba0, sizeof(vp8_coeffs_proba0), hipMemcpyHostToDevice, j.stream);
+    if (e != hipSuccess) {
+      rc = fail_hip(e, "hipMemcpyAsync (frames to device)");
+      break;
+    }
+    void* st = j.stream;
+    if ((rc = wg_import_rgba(j.rgba, w, h, 4 * w, rgba_b, has_alpha, j.y, j.u, j.v, y_b, uv_b, nk, st)) != WG_OK) break;
+    if ((rc = wg_analysis_alphas(j.y, j.u, j.v, w, h, y_b, uv_b, nk, j.alphas, nullptr, nullptr, j.uv_sum, st)) != WG_OK)
+      break;
+    if ((rc = wg_segment_analysis(cfg, j.alphas, j.uv_sum, mbw, mbh, nk, j.seg_ids, j.segs, seg_pitch, j.info, st)) !=
+        WG_OK)
+      break;
+    if ((rc = wg_encode_mbs(j.y, j.u, j.v, y_b, uv_b, w, h, nk, j.seg_ids, j.segs, seg_pitch, j.proba, cfg->method,
+                            cfg->quality, j.out, j.ry, j.ru, j.rv, j.work, st)) != WG_OK)
+      break;
+  }
+  // the gather: each device's frames back to their places in the host buffers
+  for (auto& j : jobs) {
+    if (!j.mem) continue;
+    if (hipSetDevice(j.dev) != hipSuccess) continue;
+    if (rc == WG_OK) {
+      const int st = wg_encode_status(j.work, mbw, (int)j.frames.size(), j.stream);  // synchronises the stream
+      if (st != WG_OK) rc = st;
+    }
+    hipError_t e = hipSuccess;
+    for (size_t q = 0; q < j.frames.size() && rc == WG_OK && e == hipSuccess; q++) {
+      const int64_t i = j.frames[q];
+      const int64_t rec_b = n_mb * (int64_t)sizeof(wg_mb_enc);
+      e = hipMemcpyAsync(static_cast<uint8_t*>(mb_out) + i * rec_b, j.out + (int64_t)q * rec_b, (size_t)rec_b,
+                         hipMemcpyDeviceToHost, j.stream);
+      if (e == hipSuccess && ry) e = hipMemcpyAsync(ry + i * y_b, j.ry + q * y_b, (size_t)y_b, hipMemcpyDeviceToHost, j.stream);
+      if (e == hipSuccess && ru) e = hipMemcpyAsync(ru + i * uv_b, j.ru + q * uv_b, (size_t)uv_b, hipMemcpyDeviceToHost, j.stream);
+      if (e == hipSuccess && rv) e = hipMemcpyAsync(rv + i * uv_b, j.rv + q * uv_b, (size_t)uv_b, hipMemcpyDeviceToHost, j.stream);
+      if (e == hipSuccess && seg_ids_out)
+        e = hipMemcpyAsync(seg_ids_out + i * n_mb, j.seg_ids + q * n_mb, (size_t)n_mb, hipMemcpyDeviceToHost, j.stream);
+      if (e == hipSuccess && info_out)
+        e = hipMemcpyAsync(info_out + i, j.info + q, sizeof(wg_frame_segs), hipMemcpyDeviceToHost, j.stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(j.stream);
+    if (e != hipSuccess && rc == WG_OK) rc = fail_hip(e, "gather (device to host)");
+  }
+  for (auto& j : jobs) {
+    if (!j.stream && !j.mem) continue;
+    (void)hipSetDevice(j.dev);
+    if (j.stream) (void)hipStreamSynchronize(j.stream);
+    if (j.mem) (void)hipFree(j.mem);
+    if (j.stream) (void)hipStreamDestroy(j.stream);
+  }
+  (void)hipSetDevice(prev_dev);
+  return rc;
+}

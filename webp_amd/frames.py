@@ -295,6 +295,28 @@ def encoder_config(quality=75, method=4, sns_strength=50, filter_strength=60, fi
     return cfg
 
 
+def encode_frames_devices(rgba, devices, cfg=None, has_alpha=False):
+    """The multi-device batch variant (wg_encode_frames_devices): rgba (n, h, w, 4)
+    uint8 HOST array, frame i encoded on devices[i % len(devices)] by the whole
+    device encode path; returns host arrays in frame order: (mb_enc bytes
+    (n*mbh*mbw, 864), (RY, RU, RV) planes, seg_ids (n, mbh*mbw), info (n, 112))."""
+    rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
+    n, h, w, _ = rgba.shape
+    mbw, mbh = mb_dims(w, h)
+    cfg = encoder_config() if cfg is None else cfg
+    devs = np.ascontiguousarray(devices, dtype=np.int32)
+    out = np.empty((n * mbw * mbh, MB_ENC_DTYPE.itemsize), np.uint8)
+    ry = np.empty((n, 16 * mbh, 16 * mbw), np.uint8)
+    ru = np.empty((n, 8 * mbh, 8 * mbw), np.uint8)
+    rv = np.empty_like(ru)
+    seg_ids = np.empty((n, mbw * mbh), np.uint8)
+    info = np.empty((n, FRAME_SEGS_DTYPE.itemsize), np.uint8)
+    call("wg_encode_frames_devices", devs.ctypes.data, len(devs), rgba.ctypes.data, w, h, n, int(has_alpha),
+         cfg.ctypes.data, out.ctypes.data, ry.ctypes.data, ru.ctypes.data, rv.ctypes.data, seg_ids.ctypes.data,
+         info.ctypes.data)
+    return out, (ry, ru, rv), seg_ids, info
+
+
 def segment_analysis(cfg, alphas, uv_sum, mbw, mbh, out=None, info=True):
     """assignSegments + setSegmentParams + setSegmentProbas + setupSegment per
     image on the device: alphas (n, mbh*mbw) int32, uv_sum (n,) int32 ->
