@@ -243,7 +243,8 @@ int wg_encode_status(const void* work, int32_t mbw, int32_t n_images, void* stre
 /* The multi-device batch variant of the encode DSP path (one host process
  * driving several GPUs, as a cgo host would): n_images RGBA frames (w x h,
  * tightly packed, n_images * w * h * 4 bytes of HOST memory); frame i is
- * encoded on devices[i % n_devices] (each device listed once), each device
+ * encoded on devices[i % n_devices] (an entry may repeat a device: each
+ * entry gets its own stream and buffers), each device
  * running wg_import_rgba -> wg_analysis_alphas -> wg_segment_analysis (cfg,
  * host) -> wg_encode_mbs over its frames on its own stream, with the default
  * token probabilities (CoeffsProba0).  The outputs are gathered into HOST
@@ -324,6 +325,13 @@ int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uin
 int wg_plane_ssim_rows(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uint8_t* b, int32_t b_stride,
                        int64_t b_pitch, int32_t w, int32_t h, int32_t ty_begin, int32_t ty_end, int32_t n_images,
                        double* partial, void* stream);
+/* Plane SSIM of one large pair over several devices (C5, from one host
+ * process): 16-row tile bands, device k computing band k from its rows plus
+ * 3 halo rows each side (wg_plane_ssim_rows); the per-tile partial sums are
+ * gathered and reduced on the first device in the one-device order, so *out
+ * (HOST) equals wg_plane_ssim's sum bit for bit.  a, b: HOST planes. */
+int wg_plane_ssim_devices(const int32_t* devices, int32_t n_devices, const uint8_t* a, int32_t a_stride,
+                          const uint8_t* b, int32_t b_stride, int32_t w, int32_t h, double* out);
 /* out[img] = the fixed-order sum of partial[img][0 .. per_image) */
 int wg_plane_ssim_reduce(const double* partial, int64_t per_image, int32_t n_images, double* out, void* stream);
 
@@ -350,6 +358,15 @@ int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32_t height, 
 int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, int32_t height, int64_t image_pitch,
                                 int32_t bits, int32_t quality, int32_t ty_begin, int32_t ty_end, int32_t n_images,
                                 uint32_t* modes, uint32_t* residuals, void* stream);
+/* One large image over several devices (C5), from one host
+ * process: device k of n_devices takes the contiguous tile-row band k (the
+ * first tiles % n devices one row more) and computes it through
+ * wg_vp8l_residual_image_rows from its rows plus the row above; modes
+ * [tiles_y*tiles_x] and residuals [height*width] land in HOST memory at
+ * their places, identical to wg_vp8l_residual_image.  argb: HOST, width *
+ * height words.  Blocks until done. */
+int wg_vp8l_residual_image_devices(const int32_t* devices, int32_t n_devices, const uint32_t* argb, int32_t width,
+                                   int32_t height, int32_t bits, int32_t quality, uint32_t* modes, uint32_t* residuals);
 /* predictorInverseTransform (internal/lossless/decode_transform.go:202-360):
  * out = residuals +mod prediction from reconstructed pixels.  `work` needs
  * wg_vp8l_inverse_work_bytes(width, height, n_images) bytes, 16-B aligned (the

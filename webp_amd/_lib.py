@@ -107,6 +107,8 @@ SIGNATURES = {
     "wg_segment_analysis": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp],
     "wg_encode_status": [_vp, _i32, _i32, _vp],
     "wg_encode_frames_devices": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "wg_vp8l_residual_image_devices": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp],
+    "wg_plane_ssim_devices": [_vp, _i32, _vp, _i32, _vp, _i32, _i32, _i32, _vp],
 }
 _RES = {"wg_last_error": ctypes.c_char_p, "wg_decode_work_bytes": ctypes.c_size_t,
         "wg_plane_ssim_work_bytes": ctypes.c_size_t, "wg_vp8l_inverse_work_bytes": ctypes.c_size_t,

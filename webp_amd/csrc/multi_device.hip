@@ -13,6 +13,7 @@
 // reconstruction, segment map and segment header come back to the caller's
 // host buffers in frame order, which is where the reference's Phase B
 // (recordAllTokens, encode_parallel.go:1497) and the bitstream writer run.
+#include <algorithm>
 #include <vector>
 
 #include "vp8_tables.h"
@@ -48,10 +49,9 @@ extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_device
   WG_REQUIRE(w > 0 && h > 0 && n_images > 0);
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess) return wg::check_launch("hipGetDeviceCount");
-  for (int k = 0; k < n_devices; k++) {
-    WG_REQUIRE(devices[k] >= 0 && devices[k] < count);
-    for (int j = 0; j < k; j++) WG_REQUIRE(devices[j] != devices[k]);  // a device appears once
-  }
+  // a device may appear more than once: each entry gets its own stream and
+  // buffers (how the tests split work on a one-GPU box)
+  for (int k = 0; k < n_devices; k++) WG_REQUIRE(devices[k] >= 0 && devices[k] < count);
   const int mbw = (w + 15) >> 4, mbh = (h + 15) >> 4;
   if (mbh < 4) return wg::invalid("mbh >= 4 (encode.go:1356 encodes smaller frames serially)");
   const int64_t n_mb = (int64_t)mbw * mbh;
@@ -147,5 +147,176 @@ extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_device
     if (j.stream) (void)hipStreamDestroy(j.stream);
   }
   (void)hipSetDevice(prev_dev);
+  return rc;
+}
+
+// ---------------- one large image over several devices: row bands (C5) ----------------
+//
+// the streaming stages of C5 shard by row bands with a halo --
+// VP8L ResidualImage by tile rows (1 pixel row above the band: the
+// predictors read the row above), plane SSIM by 16-row tiles (3 rows each
+// side).  Device k of n takes the contiguous tile-row band band_of(k) (the
+// first tiles % n devices one tile row more, as webp_amd/shard.py band_of),
+// computes it through the *_rows entry points from its rows plus the halo,
+// and the bands come back to host memory at their places.  The SSIM bands'
+// per-tile partial sums are reduced on the first device in the one-device
+// order, so the sum is bit-identical to wg_plane_ssim's.
+namespace {
+
+void band_of(int tiles, int n, int k, int* b0, int* b1) {
+  const int base = tiles / n, rem = tiles % n;
+  *b0 = k * base + (k < rem ? k : rem);
+  *b1 = *b0 + base + (k < rem ? 1 : 0);
+}
+
+int check_devices(const int32_t* devices, int32_t n_devices) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess) return wg::check_launch("hipGetDeviceCount");
+  for (int k = 0; k < n_devices; k++) WG_REQUIRE(devices[k] >= 0 && devices[k] < count);
+  return WG_OK;
+}
+
+struct Band {
+  int dev = 0, t0 = 0, t1 = 0;
+  hipStream_t stream = nullptr;
+  void* mem = nullptr;
+};
+
+void release(std::vector<Band>& bands, int prev_dev) {
+  for (auto& b : bands) {
+    if (!b.stream && !b.mem) continue;
+    (void)hipSetDevice(b.dev);
+    if (b.stream) (void)hipStreamSynchronize(b.stream);
+    if (b.mem) (void)hipFree(b.mem);
+    if (b.stream) (void)hipStreamDestroy(b.stream);
+  }
+  (void)hipSetDevice(prev_dev);
+}
+
+}  // namespace
+
+extern "C" int wg_vp8l_residual_image_devices(const int32_t* devices, int32_t n_devices, const uint32_t* argb,
+                                              int32_t width, int32_t height, int32_t bits, int32_t quality,
+                                              uint32_t* modes, uint32_t* residuals) {
+  WG_REQUIRE(devices && n_devices > 0 && argb && modes && residuals);
+  WG_REQUIRE(width > 0 && height > 0 && bits >= 2 && bits <= 9);
+  if (int rc = check_devices(devices, n_devices)) return rc;
+  const int ts = 1 << bits, tx = (width + ts - 1) >> bits, ty = (height + ts - 1) >> bits;
+  const int64_t px = (int64_t)width * height, row_b = (int64_t)width * 4;
+  int prev_dev = 0;
+  if (hipGetDevice(&prev_dev) != hipSuccess) return wg::check_launch("hipGetDevice");
+  std::vector<Band> bands((size_t)n_devices);
+  int rc = WG_OK;
+  for (int k = 0; k < n_devices && rc == WG_OK; k++) {
+    Band& b = bands[(size_t)k];
+    b.dev = devices[k];
+    band_of(ty, n_devices, k, &b.t0, &b.t1);
+    if (b.t1 <= b.t0) continue;
+    hipError_t e = hipSetDevice(b.dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking);
+    // full-image layouts (the *_rows entry points address rows at their image positions)
+    const size_t img_b = (size_t)align_up((size_t)px * 4), modes_b = align_up((size_t)tx * ty * 4);
+    if (e == hipSuccess) e = hipMalloc(&b.mem, 2 * img_b + modes_b);
+    if (e != hipSuccess) {
+      rc = fail_hip(e, "device setup (residual bands)");
+      break;
+    }
+    uint8_t* base = static_cast<uint8_t*>(b.mem);
+    uint32_t *d_argb = reinterpret_cast<uint32_t*>(base), *d_res = reinterpret_cast<uint32_t*>(base + img_b);
+    uint32_t* d_modes = reinterpret_cast<uint32_t*>(base + 2 * img_b);
+    const int r0 = (b.t0 << bits) - (b.t0 > 0 ? 1 : 0), r1 = std::min(b.t1 << bits, (int)height);  // + the row above
+    e = hipMemcpyAsync(d_argb + (int64_t)r0 * width, argb + (int64_t)r0 * width, (size_t)((r1 - r0) * row_b),
+                       hipMemcpyHostToDevice, b.stream);
+    if (e != hipSuccess) {
+      rc = fail_hip(e, "hipMemcpyAsync (band to device)");
+      break;
+    }
+    rc = wg_vp8l_residual_image_rows(d_argb, width, height, px, bits, quality, b.t0, b.t1, 1, d_modes, d_res, b.stream);
+  }
+  for (auto& b : bands) {  // gather: the band's tile modes and residual rows at their places
+    if (!b.mem || rc != WG_OK) continue;
+    (void)hipSetDevice(b.dev);
+    uint8_t* base = static_cast<uint8_t*>(b.mem);
+    const size_t img_b = (size_t)align_up((size_t)px * 4);
+    const int r0 = b.t0 << bits, r1 = std::min(b.t1 << bits, (int)height);
+    hipError_t e = hipMemcpyAsync(modes + (int64_t)b.t0 * tx, base + 2 * img_b + (size_t)b.t0 * tx * 4,
+                                  (size_t)(b.t1 - b.t0) * tx * 4, hipMemcpyDeviceToHost, b.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(residuals + (int64_t)r0 * width, base + img_b + (size_t)r0 * row_b, (size_t)((r1 - r0) * row_b),
+                         hipMemcpyDeviceToHost, b.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(b.stream);
+    if (e != hipSuccess) rc = fail_hip(e, "gather (residual bands)");
+  }
+  release(bands, prev_dev);
+  return rc;
+}
+
+extern "C" int wg_plane_ssim_devices(const int32_t* devices, int32_t n_devices, const uint8_t* a, int32_t a_stride,
+                                     const uint8_t* b_plane, int32_t b_stride, int32_t w, int32_t h, double* out) {
+  WG_REQUIRE(devices && n_devices > 0 && a && b_plane && out);
+  WG_REQUIRE(w > 0 && h > 0 && a_stride >= w && b_stride >= w);
+  if (int rc = check_devices(devices, n_devices)) return rc;
+  constexpr int TILE = 16, HALO = 3;
+  const int tx = (w + TILE - 1) / TILE, ty = (h + TILE - 1) / TILE;
+  int prev_dev = 0;
+  if (hipGetDevice(&prev_dev) != hipSuccess) return wg::check_launch("hipGetDevice");
+  std::vector<Band> bands((size_t)n_devices);
+  std::vector<double> partial((size_t)tx * ty);
+  int rc = WG_OK;
+  const size_t a_b = align_up((size_t)a_stride * h), b_b = align_up((size_t)b_stride * h);
+  for (int k = 0; k < n_devices && rc == WG_OK; k++) {
+    Band& b = bands[(size_t)k];
+    b.dev = devices[k];
+    band_of(ty, n_devices, k, &b.t0, &b.t1);
+    if (b.t1 <= b.t0) continue;
+    hipError_t e = hipSetDevice(b.dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking);
+    const size_t part_b = align_up((size_t)tx * (b.t1 - b.t0) * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&b.mem, a_b + b_b + part_b + 256);
+    if (e != hipSuccess) {
+      rc = fail_hip(e, "device setup (ssim bands)");
+      break;
+    }
+    uint8_t* base = static_cast<uint8_t*>(b.mem);
+    const int r0 = std::max(TILE * b.t0 - HALO, 0), r1 = std::min(TILE * b.t1 + HALO, (int)h);  // band + halo
+    e = hipMemcpyAsync(base + (size_t)r0 * a_stride, a + (size_t)r0 * a_stride, (size_t)(r1 - r0) * a_stride,
+                       hipMemcpyHostToDevice, b.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(base + a_b + (size_t)r0 * b_stride, b_plane + (size_t)r0 * b_stride, (size_t)(r1 - r0) * b_stride,
+                         hipMemcpyHostToDevice, b.stream);
+    if (e != hipSuccess) {
+      rc = fail_hip(e, "hipMemcpyAsync (ssim band to device)");
+      break;
+    }
+    rc = wg_plane_ssim_rows(base, a_stride, (int64_t)a_stride * h, base + a_b, b_stride, (int64_t)b_stride * h, w, h, b.t0,
+                            b.t1, 1, reinterpret_cast<double*>(base + a_b + b_b), b.stream);
+  }
+  for (auto& b : bands) {  // gather the per-tile partial sums in tile-row order
+    if (!b.mem || rc != WG_OK) continue;
+    (void)hipSetDevice(b.dev);
+    const uint8_t* base = static_cast<const uint8_t*>(b.mem);
+    hipError_t e = hipMemcpyAsync(partial.data() + (size_t)b.t0 * tx, base + a_b + b_b,
+                                  (size_t)tx * (b.t1 - b.t0) * sizeof(double), hipMemcpyDeviceToHost, b.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(b.stream);
+    if (e != hipSuccess) rc = fail_hip(e, "gather (ssim bands)");
+  }
+  if (rc == WG_OK) {  // the one-device reduction order, on the first device that holds a band (its buffer is big enough)
+    for (auto& b : bands) {
+      if (!b.mem) continue;
+      (void)hipSetDevice(b.dev);
+      uint8_t* base = static_cast<uint8_t*>(b.mem);  // reuse the band's plane buffer for all partials + the sum
+      double* d_part = reinterpret_cast<double*>(base);
+      double* d_out = reinterpret_cast<double*>(base + align_up(partial.size() * sizeof(double)));
+      hipError_t e = hipMemcpyAsync(d_part, partial.data(), partial.size() * sizeof(double), hipMemcpyHostToDevice, b.stream);
+      if (e == hipSuccess) {
+        rc = wg_plane_ssim_reduce(d_part, (int64_t)partial.size(), 1, d_out, b.stream);
+        if (rc == WG_OK) e = hipMemcpyAsync(out, d_out, sizeof(double), hipMemcpyDeviceToHost, b.stream);
+        if (rc == WG_OK && e == hipSuccess) e = hipStreamSynchronize(b.stream);
+      }
+      if (e != hipSuccess && rc == WG_OK) rc = fail_hip(e, "ssim reduce");
+      break;
+    }
+  }
+  release(bands, prev_dev);
   return rc;
 }

@@ -153,6 +153,18 @@ def plane_ssim(a, b, work=None):
     return out
 
 
+def plane_ssim_devices(a, b, devices):
+    """Plane SSIM of one (h, w) HOST uint8 pair by 16-row bands over `devices`
+    (wg_plane_ssim_devices); equals plane_ssim's sum bit for bit."""
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    b = np.ascontiguousarray(b, dtype=np.uint8)
+    h, w = a.shape
+    devs = np.ascontiguousarray(devices, dtype=np.int32)
+    out = np.zeros(1, np.float64)
+    call("wg_plane_ssim_devices", devs.ctypes.data, len(devs), a.ctypes.data, w, b.ctypes.data, w, w, h, out.ctypes.data)
+    return float(out[0])
+
+
 def vp8_parse(data):
     """Parse a lossy WebP (RIFF "VP8 " chunk or raw VP8 frame) on the host:
     returns (dims dict, mb_info structured array, coeffs int16 (n_mb, 384))."""

@@ -48,6 +48,20 @@ def ResidualImage(argb, bits, quality, out=None):
     return modes, res
 
 
+def ResidualImage_devices(argb, bits, quality, devices):
+    """ResidualImage of one (h, w) HOST image (uint32 / int32 numpy) by tile-row
+    bands over `devices` (wg_vp8l_residual_image_devices) -> host (modes
+    (tiles_y, tiles_x), residuals (h, w)) as uint32."""
+    a = np.ascontiguousarray(argb).view(np.uint32)
+    h, w = a.shape
+    devs = np.ascontiguousarray(devices, dtype=np.int32)
+    modes = np.empty((subsample(h, bits), subsample(w, bits)), np.uint32)
+    res = np.empty((h, w), np.uint32)
+    call("wg_vp8l_residual_image_devices", devs.ctypes.data, len(devs), a.ctypes.data, w, h, bits, quality,
+         modes.ctypes.data, res.ctypes.data)
+    return modes, res
+
+
 def predictor_inverse(modes, bits, residuals, out=None, check=False):
     r = _batched(residuals)
     n, h, w = r.shape
