@@ -1453,11 +1453,20 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
           // results back from LDS; sums are quad reductions)
           const bool qact = bvalid && hl < 4 * K;
           const int qc = min(hl >> 2, 2), qr = hl & 3, qsl = half * 3 + qc;
-          const int qmode = pick3(qc, cm[0], cm[1], cm[2]);
+          // (unconditional, so that the reconstruction, TDisto and token-cost
+          // streams interleave: lanes past the candidates repeat candidate 2's
+          // work, or work on an unused slot, and nothing reads their results)
+          const int qmode = min(pick3(qc, cm[0], cm[1], cm[2]) & 15, 9);
           int16_t qv[16];
           int qnz = 0, sse_r = 0, cnt = 0;
           uint32_t rec_row = 0;
-          if (qact) {
+          int part;  // token cost, lane-parallel over positions: lane 8c + p takes positions 2p, 2p + 1
+          {
+            const int c = min(hl >> 3, 2), n0 = 2 * (hl & 7), sl = half * 3 + c;
+            const int nzc = s.cand_nz[sl];
+            part = token_cost_pos<3>(t, s.cand_q[sl], n0, nzc, nz_ctx, 0) + token_cost_pos<3>(t, s.cand_q[sl], n0 + 1, nzc, nz_ctx, 0);
+          }
+          {
             CSTAMP(1);
 #pragma unroll
             for (int i = 0; i < 16; i++) qv[i] = s.cand_q[qsl][i];
@@ -1476,26 +1485,25 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
             rec_row = pack4(rr[0], rr[1], rr[2], rr[3]);
             // tTransform row pass (ssim.go:266-304) of the reconstruction and the source
             int* th = &s.co_buf[2 * qsl][0] + 8 * qr;  // co_buf is free again after the trellis prep
+            int4 tr, ts;
             {
               const int a0 = rr[0] + rr[2], a1 = rr[1] + rr[3], a2 = rr[1] - rr[3], a3 = rr[0] - rr[2];
-              th[0] = a0 + a1;
-              th[1] = a3 + a2;
-              th[2] = a3 - a2;
-              th[3] = a0 - a1;
+              tr = make_int4(a0 + a1, a3 + a2, a3 - a2, a0 - a1);
             }
             {
               const int a0 = sr[0] + sr[2], a1 = sr[1] + sr[3], a2 = sr[1] - sr[3], a3 = sr[0] - sr[2];
-              th[4] = a0 + a1;
-              th[5] = a3 + a2;
-              th[6] = a3 - a2;
-              th[7] = a0 - a1;
+              ts = make_int4(a0 + a1, a3 + a2, a3 - a2, a0 - a1);
+            }
+            if (qact) {
+              reinterpret_cast<int4*>(th)[0] = tr;
+              reinterpret_cast<int4*>(th)[1] = ts;
             }
 #pragma unroll
             for (int i = 1; i < 16; i++) cnt += qv[i] != 0;
           }
           lds_sync();
           int wrec = 0, wsrc = 0;  // weighted column sums of column qr
-          if (qact) {
+          {
             const int* tx = &s.co_buf[2 * qsl][0];
             int cr[4], cs[4];
 #pragma unroll
@@ -1519,14 +1527,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
           int disto = sse_q;
           if (sg.tlambda_sd > 0) disto += (sg.tlambda_sd * (abs(wrec_q - wsrc_q) >> 5) + 128) >> 8;
           CSTAMP(2);
-          // token cost, lane-parallel over positions, summed over each candidate's 8 lanes
-          int part = 0;
-          if (bvalid && hl < 8 * K) {
-            const int c = hl >> 3, n0 = 2 * (hl & 7), sl = half * 3 + c;
-            const int nzc = s.cand_nz[sl];
-            part = token_cost_pos<3>(t, s.cand_q[sl], n0, nzc, nz_ctx, 0) + token_cost_pos<3>(t, s.cand_q[sl], n0 + 1, nzc, nz_ctx, 0);
-          }
-          // candidate c's rate sits in lane 32 * half + 8c; read the six with
+          // the token cost summed over each candidate's 8 lanes: candidate c's
+          // rate sits in lane 32 * half + 8c; read the six with
           // v_readlane (wave-uniform lanes) instead of LDS permutes
           part = group_sum_first<8>(part);
           int tok_rate;
