@@ -210,6 +210,7 @@ class Pipeline:
         f.analysis_alphas(sl.Y, sl.U, sl.V, W, H, out=(sl.alphas, sl.uv_sum, None, None))
         mark()
         f.segment_analysis(self.cfg, sl.alphas, sl.uv_sum, MBW, MBH, out=(sl.seg_ids, sl.segs, sl.seg_info))
+        f.encode_row_order(sl.alphas, MBW, MBH, work=sl.enc_work)
         mark()
         f.encode_mbs(sl.Y, sl.U, sl.V, W, H, sl.seg_ids, sl.segs, self.proba, method=ENC_CFG["method"],
                      quality=ENC_CFG["quality"], out=sl.enc_out, recon=(sl.rY, sl.rU, sl.rV), work=sl.enc_work)

@@ -238,6 +238,14 @@ int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t 
                   int32_t width, int32_t height, int32_t n_images, const uint8_t* segments, const void* segs,
                   int64_t segs_pitch, const uint8_t* proba, int32_t method, int32_t quality, void* out, uint8_t* ry, uint8_t* ru,
                   uint8_t* rv, void* work, void* stream);
+/* The row schedule of wg_encode_mbs for a batch, from computeAlphas' per-MB
+ * alphas [n_images][mbw*mbh] (device): the rows of frames with textured
+ * macroblocks (low mean alpha; the slow ones, whose wavefront ends the
+ * launch) are dequeued up to mbh/4 rows ahead of the others.  Written into
+ * `work` (wg_encode_work_bytes; kept across wg_encode_mbs calls on the same
+ * work and row count, until the next wg_encode_row_order); without it the
+ * rows go in (row, frame) order.  Scheduling only: the outputs are the same. */
+int wg_encode_row_order(const int32_t* alphas, int32_t mbw, int32_t mbh, int32_t n_images, void* work, void* stream);
 /* After wg_encode_mbs on the same stream: WG_OK or WG_EHIP on a row-wait timeout.  Synchronises. */
 int wg_encode_status(const void* work, int32_t mbw, int32_t n_images, void* stream);
 /* The multi-device batch variant of the encode DSP path (one host process

@@ -149,3 +149,31 @@ def test_encode_row_schedules(cuda, monkeypatch, schedule, method):
     monkeypatch.setenv("WG_ENCODE_PAIR", schedule)
     run([planes(160, 96, k, s) for s, k in enumerate(("noise", "blobs", "grad"))], 160, 96, (20, 40, 60, 80), method=method)
     run([planes(64, 64, "noise", 3)], 64, 64, (25, 35, 45, 55), sns=0, quality=30, method=method)
+
+
+@pytest.mark.parametrize("schedule", ["0", "1"])
+def test_row_schedule_keeps_outputs(cuda, monkeypatch, schedule):
+    """wg_encode_row_order only reorders the row dequeue (textured frames' rows
+    first): the outputs equal the (row, frame)-order launch and the oracle."""
+    monkeypatch.setenv("WG_ENCODE_PAIR", schedule)
+    w, h = 320, 240
+    rgba = np.stack([[synth.gradient_rgba, synth.noise_rgba, synth.blobs_rgba][i % 3](w, h, **({} if i % 3 == 0 else
+                     {"seed": i})) for i in range(9)])
+    t = torch.from_numpy(rgba).cuda()
+    mbw, mbh = frames.mb_dims(w, h)
+    Y, U, V = frames.import_rgba(t, has_alpha=False)
+    alphas, uv_sum = frames.analysis_alphas(Y, U, V, w, h)
+    seg_ids, segs, _ = frames.segment_analysis(frames.encoder_config(), alphas, uv_sum, mbw, mbh)
+    proba = frames.default_proba()
+    plain, rec0 = frames.encode_mbs(Y, U, V, w, h, seg_ids, segs, proba, check=True)
+    work = frames.encode_row_order(alphas, mbw, mbh)
+    ordered, rec1 = frames.encode_mbs(Y, U, V, w, h, seg_ids, segs, proba, work=work, check=True)
+    again, _ = frames.encode_mbs(Y, U, V, w, h, seg_ids, segs, proba, work=work, check=True)  # the schedule persists
+    assert torch.equal(plain, ordered) and torch.equal(plain, again)
+    assert all(torch.equal(a, b) for a, b in zip(rec0, rec1))
+    got = ordered.cpu().numpy().view(frames.MB_ENC_DTYPE).reshape(9, mbw * mbh)
+    for i in (1, 2):
+        y, u, v = O.import_rgba(rgba[i], has_alpha=False)
+        enc, _, _, _ = O.encode_frame(y, u, v, w, h, O.encoder_config())
+        for f in FIELDS:
+            assert (got[i][f] == enc[f]).all(), (i, f)

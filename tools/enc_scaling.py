@@ -25,12 +25,13 @@ for B in [int(b) for b in os.environ.get("BATCHES", "1,3,8,16,32,64").split(",")
     alphas, uv_sum = frames.analysis_alphas(Y, U, V, W, H)
     seg_ids, segs, _ = frames.segment_analysis(frames.encoder_config(), alphas, uv_sum, MBW, MBH)
     proba = O.default_proba()
-    out, rec = frames.encode_mbs(Y, U, V, W, H, seg_ids, segs, proba, check=True)
+    work = frames.encode_row_order(alphas, MBW, MBH) if os.environ.get("ROW_ORDER", "1") == "1" else None
+    out, rec = frames.encode_mbs(Y, U, V, W, H, seg_ids, segs, proba, work=work, check=True)
     ts = []
     for _ in range(5):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        frames.encode_mbs(Y, U, V, W, H, seg_ids, segs, proba, out=out, recon=rec)
+        frames.encode_mbs(Y, U, V, W, H, seg_ids, segs, proba, out=out, recon=rec, work=work)
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))

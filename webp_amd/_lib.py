@@ -106,6 +106,7 @@ SIGNATURES = {
     "wg_encoder_config": [_i32] * 8 + [_vp],
     "wg_segment_analysis": [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp],
     "wg_encode_status": [_vp, _i32, _i32, _vp],
+    "wg_encode_row_order": [_vp, _i32, _i32, _i32, _vp, _vp],
     "wg_encode_frames_devices": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "wg_vp8l_residual_image_devices": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp],
     "wg_plane_ssim_devices": [_vp, _i32, _vp, _i32, _vp, _i32, _i32, _i32, _vp],

@@ -877,11 +877,14 @@ struct EncArgs {
   uint8_t* top;   // [n_img][mbw][REC]
   int* progress;  // [n_img][mbh]
   int* ctl;       // [0] dequeue, [1] error
+  const int* order;  // the work buffer's row schedule (wg_encode_row_order): dequeue index -> row * n_img + image
+  const int* order_tag;  // {ORDER_TAG ^ rows, ~that} when the schedule was built for this many rows, else (row, image) order
   int64_t y_pitch, uv_pitch;
   int width, height, mbw, mbh, n_img, quality;
 };
 
 constexpr uint64_t SPIN_TICKS = 200000000ull;
+constexpr int ORDER_TAG = 0x5e0d0000;  // marks a row schedule in the work buffer (xor the row count)
 
 #ifdef WG_STAMPS
 // Diagnostic build only: cycles per phase summed over macroblocks.
@@ -998,6 +1001,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
   const int total_rows = a.n_img * mbh;
   ESTAMP_DECL;
 
+  const bool use_order = a.order_tag[0] == (ORDER_TAG ^ total_rows) && a.order_tag[1] == ~(ORDER_TAG ^ total_rows);
   for (;;) {
     int row;
     if constexpr (PAIR) {  // the pair dequeues together (the next write of word is two barriers on)
@@ -1011,7 +1015,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
       lds_sync();
     }
     if (row >= total_rows) break;
-    const int mby = row / a.n_img, img = row % a.n_img;
+    const int ro = use_order ? __builtin_amdgcn_readfirstlane(a.order[row]) : row;
+    const int mby = ro / a.n_img, img = ro % a.n_img;
     const uint8_t* Y = a.y + img * a.y_pitch;
     const uint8_t* U = a.u + img * a.uv_pitch;
     const uint8_t* V = a.v + img * a.uv_pitch;
@@ -2051,10 +2056,75 @@ extern "C" int wg_debug_enc_phases(unsigned long long* host, int n) {
 }
 #endif
 
+// work: hand-off records [n][mbw][REC] | ctl[4] | progress[n*mbh] (cleared by
+// every wg_encode_mbs) | tag[4] | row schedule order[n*mbh] | slack[n]
+// (wg_encode_row_order; kept across calls)
 extern "C" size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images) {
   if (mbw <= 0 || mbh <= 0 || n_images <= 0) return 0;
-  return (size_t)n_images * mbw * REC + sizeof(int) * ((size_t)n_images * mbh + 4);
+  return (size_t)n_images * mbw * REC + sizeof(int) * ((size_t)n_images * mbh + 4) +
+         sizeof(int) * (4 + (size_t)n_images * mbh + (size_t)n_images);
 }
+
+namespace {
+// ---- the row schedule (wg_encode_row_order) ----
+// A launch over many frames ends on the critical path of its slowest frame:
+// mbw + ~2 (mbh - 1) macroblock times of the frame whose macroblocks take
+// longest (textured content, where the I4 RD dominates).  Its rows are
+// therefore dequeued up to mbh / 4 rows ahead of the others: frame i's row y
+// takes the key (y - slack_i, y, i), slack_i = (mbh / 4) * (255 - mean alpha_i)
+// / 255 (computeAlphas' alpha is low for textured macroblocks).  Keys grow
+// with y within a frame, so a row is always dequeued after the row above
+// (the kernel's waits stay on running waves); the outputs do not depend on
+// the order.  64 mixed 1080p frames: 25.4 -> 23.3 ms.
+__global__ __launch_bounds__(256) void k_row_slack(const int32_t* alphas, int n_mb, int mbh, int rows, int* tag, int* slack) {
+  __shared__ long long part[256];
+  long long sum = 0;
+  const int32_t* al = alphas + (int64_t)blockIdx.x * n_mb;
+  for (int i = threadIdx.x; i < n_mb; i += 256) sum += min(max(al[i], 0), 255);
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int mean = (int)(part[0] / n_mb);
+    slack[blockIdx.x] = (mbh / 4) * (255 - mean) / 255;
+    if (blockIdx.x == 0) {  // the encoder reads it after k_row_order (same stream)
+      tag[0] = ORDER_TAG ^ rows;
+      tag[1] = ~(ORDER_TAG ^ rows);
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_row_order(const int* slack, int n_img, int mbh, int* order) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n_img * mbh) return;
+  const int y = k / n_img, i = k % n_img, di = slack[i], r = y - di;
+  int pos = 0;  // rows with a smaller key (r', y', i')
+  for (int j = 0; j < n_img; j++) {
+    const int dj = slack[j], yj = r + dj;  // frame j's row with the same r
+    pos += min(max(yj, 0), mbh) + ((yj >= 0 && yj < mbh && (dj < di || (dj == di && j < i))) ? 1 : 0);
+  }
+  order[pos] = k;
+}
+
+}  // namespace
+
+extern "C" int wg_encode_row_order(const int32_t* alphas, int32_t mbw, int32_t mbh, int32_t n_images, void* work,
+                                   void* stream) {
+  WG_REQUIRE(alphas && work && mbw > 0 && mbh > 0 && n_images > 0);
+  WG_REQUIRE((reinterpret_cast<uintptr_t>(work) & 15) == 0);
+  const int rows = n_images * mbh;
+  int* progress = reinterpret_cast<int*>(static_cast<uint8_t*>(work) + (size_t)n_images * mbw * REC) + 4;
+  int* tag = progress + rows;
+  int* order = tag + 4;
+  int* slack = order + rows;
+  hipStream_t s = wg::as_stream(stream);
+  hipLaunchKernelGGL(k_row_slack, dim3((unsigned)n_images), dim3(256), 0, s, alphas, mbw * mbh, mbh, rows, tag, slack);
+  hipLaunchKernelGGL(k_row_order, dim3(wg::blocks_for(rows, 256)), dim3(256), 0, s, slack, n_images, mbh, order);
+  return wg::check_launch("k_row_order");
+}
+
 
 extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t y_pitch, int64_t uv_pitch,
                              int32_t width, int32_t height, int32_t n_images, const uint8_t* segments,
@@ -2117,6 +2187,8 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   a.mbh = mbh;
   a.n_img = n_images;
   a.quality = quality;
+  a.order = a.progress + (size_t)n_images * mbh + 4;  // work: ... | progress | tag[4] | order | slack
+  a.order_tag = a.order - 4;
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(encode ctl)");
   int cus = 0, per_cu = 0, per_cu_pair = 0;

@@ -110,6 +110,7 @@ extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_device
     if ((rc = wg_segment_analysis(cfg, j.alphas, j.uv_sum, mbw, mbh, nk, j.seg_ids, j.segs, seg_pitch, j.info, st)) !=
         WG_OK)
       break;
+    if ((rc = wg_encode_row_order(j.alphas, mbw, mbh, nk, j.work, st)) != WG_OK) break;
     if ((rc = wg_encode_mbs(j.y, j.u, j.v, y_b, uv_b, w, h, nk, j.seg_ids, j.segs, seg_pitch, j.proba, cfg->method,
                             cfg->quality, j.out, j.ry, j.ru, j.rv, j.work, st)) != WG_OK)
       break;

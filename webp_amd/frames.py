@@ -269,6 +269,16 @@ def encode_mbs(Y, U, V, width, height, segments, segs, proba, method=4, quality=
     return out, recon
 
 
+def encode_row_order(alphas, mbw, mbh, work=None):
+    """The batch's row schedule (wg_encode_row_order) from the (n, mbh*mbw) int32
+    alphas, written into (and returning) the encoder work buffer."""
+    n = alphas.shape[0]
+    if work is None:
+        work = torch.empty(lib.wg_encode_work_bytes(mbw, mbh, n), dtype=torch.uint8, device=alphas.device)
+    call("wg_encode_row_order", alphas.data_ptr(), mbw, mbh, n, work.data_ptr(), _stream())
+    return work
+
+
 def encode_status(work, mbw, n):
     """Raises if a row-dependency wait of the last wg_encode_mbs on `work` timed out (synchronises)."""
     call("wg_encode_status", work.data_ptr(), mbw, n, _stream())
@@ -362,8 +372,9 @@ def encode_frames(rgba, cfg=None, has_alpha=False, proba=None, check=True):
     seg_ids, segs, info = segment_analysis(cfg, alphas, uv_sum, mbw, mbh)
     if proba is None:
         proba = default_proba()
+    work = encode_row_order(alphas, mbw, mbh)
     out, recon = encode_mbs(Y, U, V, w, h, seg_ids, segs, proba, method=int(cfg["method"][0]),
-                            quality=int(cfg["quality"][0]), check=check)
+                            quality=int(cfg["quality"][0]), work=work, check=check)
     return out, recon, seg_ids, segs, info
 
 
