@@ -42,6 +42,9 @@ def test_invalid_arguments_are_rejected_without_gpu():
     assert lib.wg_import_rgba(None, 0, 0, 0, 0, 0, None, None, None, 0, 0, 1, None) == -1
     assert lib.wg_transform(9, None, 0, None, 0, 1, None) == -1
     assert lib.wg_filter(12, None, 0, 0, 0, 0, None, None, None, 1, None) == -1
+    assert lib.wg_encode_row_order(None, 120, 68, 1, None, None) == -1
+    assert lib.wg_encode_frames_devices(None, 1, None, 64, 64, 1, 0, None, None, None, None, None, None, None) == -1
+    assert lib.wg_plane_ssim_devices(None, 1, None, 8, None, 8, 8, 8, None) == -1
 
 
 def test_work_size_helpers():
@@ -53,6 +56,9 @@ def test_work_size_helpers():
     assert _lib.lib.wg_vp8l_inverse_work_bytes(100, 130, 2) == 16 + 8 * 2 * 3 * 100
     assert _lib.lib.wg_vp8l_inverse_work_bytes(100, 0, 2) == 0
     assert _lib.lib.wg_plane_ssim_work_bytes(33, 17, 1) == 8 * 3 * 2
+    # hand-off records | ctl[4] | progress | row-schedule tag[4] | order | slack (wg_encode_row_order)
+    assert _lib.lib.wg_encode_work_bytes(120, 68, 2) == 2 * 120 * 64 + 4 * (2 * 68 + 4) + 4 * (4 + 2 * 68 + 2)
+    assert _lib.lib.wg_encode_work_bytes(120, 0, 2) == 0
 
 
 def test_library_is_gfx950_only():

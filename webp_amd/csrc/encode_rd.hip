@@ -878,13 +878,13 @@ struct EncArgs {
   int* progress;  // [n_img][mbh]
   int* ctl;       // [0] dequeue, [1] error
   const int* order;  // the work buffer's row schedule (wg_encode_row_order): dequeue index -> row * n_img + image
-  const int* order_tag;  // {ORDER_TAG ^ rows, ~that} when the schedule was built for this many rows, else (row, image) order
+  const int* order_tag;  // {ORDER_TAG ^ n_img, ~(ORDER_TAG ^ mbh)} when the schedule was built for this batch shape, else (row, image) order
   int64_t y_pitch, uv_pitch;
   int width, height, mbw, mbh, n_img, quality;
 };
 
 constexpr uint64_t SPIN_TICKS = 200000000ull;
-constexpr int ORDER_TAG = 0x5e0d0000;  // marks a row schedule in the work buffer (xor the row count)
+constexpr int ORDER_TAG = 0x5e0d0000;  // marks a row schedule in the work buffer (xor the batch shape)
 
 #ifdef WG_STAMPS
 // Diagnostic build only: cycles per phase summed over macroblocks.
@@ -1001,7 +1001,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
   const int total_rows = a.n_img * mbh;
   ESTAMP_DECL;
 
-  const bool use_order = a.order_tag[0] == (ORDER_TAG ^ total_rows) && a.order_tag[1] == ~(ORDER_TAG ^ total_rows);
+  const bool use_order = a.order_tag[0] == (ORDER_TAG ^ a.n_img) && a.order_tag[1] == ~(ORDER_TAG ^ mbh);
   for (;;) {
     int row;
     if constexpr (PAIR) {  // the pair dequeues together (the next write of word is two barriers on)
@@ -2076,7 +2076,7 @@ namespace {
 // with y within a frame, so a row is always dequeued after the row above
 // (the kernel's waits stay on running waves); the outputs do not depend on
 // the order.  64 mixed 1080p frames: 25.4 -> 23.3 ms.
-__global__ __launch_bounds__(256) void k_row_slack(const int32_t* alphas, int n_mb, int mbh, int rows, int* tag, int* slack) {
+__global__ __launch_bounds__(256) void k_row_slack(const int32_t* alphas, int n_mb, int mbh, int* tag, int* slack) {
   __shared__ long long part[256];
   long long sum = 0;
   const int32_t* al = alphas + (int64_t)blockIdx.x * n_mb;
@@ -2091,8 +2091,8 @@ __global__ __launch_bounds__(256) void k_row_slack(const int32_t* alphas, int n_
     const int mean = (int)(part[0] / n_mb);
     slack[blockIdx.x] = (mbh / 4) * (255 - mean) / 255;
     if (blockIdx.x == 0) {  // the encoder reads it after k_row_order (same stream)
-      tag[0] = ORDER_TAG ^ rows;
-      tag[1] = ~(ORDER_TAG ^ rows);
+      tag[0] = ORDER_TAG ^ (int)gridDim.x;
+      tag[1] = ~(ORDER_TAG ^ mbh);
     }
   }
 }
@@ -2120,7 +2120,7 @@ extern "C" int wg_encode_row_order(const int32_t* alphas, int32_t mbw, int32_t m
   int* order = tag + 4;
   int* slack = order + rows;
   hipStream_t s = wg::as_stream(stream);
-  hipLaunchKernelGGL(k_row_slack, dim3((unsigned)n_images), dim3(256), 0, s, alphas, mbw * mbh, mbh, rows, tag, slack);
+  hipLaunchKernelGGL(k_row_slack, dim3((unsigned)n_images), dim3(256), 0, s, alphas, mbw * mbh, mbh, tag, slack);
   hipLaunchKernelGGL(k_row_order, dim3(wg::blocks_for(rows, 256)), dim3(256), 0, s, slack, n_images, mbh, order);
   return wg::check_launch("k_row_order");
 }
