@@ -689,7 +689,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
 #define WG_DEC_SW 4
 #endif
 #ifndef WG_DEC_RING_M
-#define WG_DEC_RING_M 8
+#define WG_DEC_RING_M 4
 #endif
 constexpr int SW = WG_DEC_SW;          // rows per band (one R and one F wave each)
 constexpr int RING_M = WG_DEC_RING_M;  // R -> F ring depth (R's work buffers of unfiltered MBs)
