@@ -2065,6 +2065,9 @@ extern "C" size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_image
          sizeof(int) * (4 + (size_t)n_images * mbh + (size_t)n_images);
 }
 
+#ifndef WG_ENC_SLACK_DIV
+#define WG_ENC_SLACK_DIV 4  // the largest head start is mbh / WG_ENC_SLACK_DIV rows
+#endif
 namespace {
 // ---- the row schedule (wg_encode_row_order) ----
 // A launch over many frames ends on the critical path of its slowest frame:
@@ -2089,7 +2092,7 @@ __global__ __launch_bounds__(256) void k_row_slack(const int32_t* alphas, int n_
   }
   if (threadIdx.x == 0) {
     const int mean = (int)(part[0] / n_mb);
-    slack[blockIdx.x] = (mbh / 4) * (255 - mean) / 255;
+    slack[blockIdx.x] = (mbh / WG_ENC_SLACK_DIV) * (255 - mean) / 255;
     if (blockIdx.x == 0) {  // the encoder reads it after k_row_order (same stream)
       tag[0] = ORDER_TAG ^ (int)gridDim.x;
       tag[1] = ~(ORDER_TAG ^ mbh);
