@@ -177,3 +177,27 @@ def test_row_schedule_keeps_outputs(cuda, monkeypatch, schedule):
         enc, _, _, _ = O.encode_frame(y, u, v, w, h, O.encoder_config())
         for f in FIELDS:
             assert (got[i][f] == enc[f]).all(), (i, f)
+
+
+def test_row_schedule_table(cuda):
+    """k_row_slack / k_row_order build exactly the order the key (y - slack_i, y, i)
+    sorts to, slack_i = (mbh / 4) * (255 - mean alpha_i) / 255 (integer), and
+    every frame's rows appear in row order (the kernel's waits stay on running waves)."""
+    w, h = 320, 240
+    rgba = np.stack([[synth.gradient_rgba, synth.noise_rgba, synth.blobs_rgba][i % 3](w, h, **({} if i % 3 == 0 else
+                     {"seed": i})) for i in range(7)])
+    t = torch.from_numpy(rgba).cuda()
+    mbw, mbh = frames.mb_dims(w, h)
+    Y, U, V = frames.import_rgba(t, has_alpha=False)
+    alphas, _ = frames.analysis_alphas(Y, U, V, w, h)
+    n, rows = 7, 7 * mbh
+    work = frames.encode_row_order(alphas, mbw, mbh).cpu().numpy()
+    base = n * mbw * 64 // 4 + 4 + rows  # int32 index of the tag: records | ctl[4] | progress | tag
+    words = work.view(np.int32)
+    order, slack = words[base + 4:base + 4 + rows], words[base + 4 + rows:base + 4 + rows + n]
+    a = np.clip(alphas.cpu().numpy().astype(np.int64), 0, 255)
+    mean = a.sum(axis=1) // a.shape[1]
+    assert (slack == (mbh // 4) * (255 - mean) // 255).all()
+    keys = sorted(((y - slack[i], y, i) for y in range(mbh) for i in range(n)))
+    assert order.tolist() == [y * n + i for (_, y, i) in keys]
+    assert slack[1] > slack[0] and slack[1] > slack[2]  # the noise frame goes ahead
