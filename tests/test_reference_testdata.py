@@ -155,3 +155,60 @@ def test_vp8_files_gpu(cuda, name):
         assert (rgba.cpu().numpy()[0] == exp).all()
     if name == "blue_16x16_lossy":
         assert tuple(rgba.cpu().numpy()[0][8, 8]) == (1, 128, 255, 255)
+
+
+# ---------------- select_predictor_test.go: the reference's Select grid ----------------
+
+def select_grid_image():
+    """TestSelectPredictorEncoderMatchesDecoder's grid (select_predictor_test.go:17-31):
+    left / top / topLeft built from 9 values per channel pair, 531441 triples.
+    Triple j sits in a 2 x 2 cell of a 2-wide image (rows 2j, 2j + 1): topLeft,
+    top / left, target; every x > 0, y > 0 pixel uses the Select predictor
+    (mode 11, 4 x 4 tiles), the target's residual is 0, and the other residuals
+    are chosen so that the pixels reconstruct to the triple -- so the decoded
+    target is Select(left, top, topLeft).  Select is restated here from
+    selectPredictor (decode_transform.go:376-414): top if sum(|L - TL|) -
+    sum(|T - TL|) <= 0, else left."""
+    vals = np.array([0, 1, 7, 64, 127, 128, 200, 254, 255], np.uint32)
+    g = np.stack(np.meshgrid(*([vals] * 6), indexing="ij"), -1).reshape(-1, 6)
+    lr, lg, tr, tg, cr, cg = g.T
+    left = 0xff000000 | lr << 16 | lg << 8 | lr
+    top = 0xff000000 | tr << 16 | tg << 8 | tg
+    tl = 0xff000000 | cr << 16 | cg << 8 | cr
+
+    def chans(p):
+        return np.stack([(p >> s) & 0xff for s in (0, 8, 16, 24)]).astype(np.int64)
+
+    def select(L, T, TL):
+        pa = (np.abs(chans(L) - chans(TL)) - np.abs(chans(T) - chans(TL))).sum(axis=0)
+        return np.where(pa <= 0, T, L).astype(np.uint32)
+
+    def sub(a, b):  # per-channel a - b mod 256
+        return (((chans(a) - chans(b)) & 0xff) << np.array([0, 8, 16, 24])[:, None]).sum(axis=0).astype(np.uint32)
+
+    n = len(g)
+    target = select(left, top, tl)
+    img = np.empty((2 * n, 2), np.uint32)
+    img[0::2, 0], img[0::2, 1], img[1::2, 0], img[1::2, 1] = tl, top, left, target
+    res = np.empty_like(img)
+    res[0, 0] = sub(tl[:1], np.array([0xff000000], np.uint32))[0]    # black predictor
+    res[0, 1] = sub(top[:1], tl[:1])[0]                              # row 0: L
+    res[1:, 0] = sub(img[1:, 0], img[:-1, 0])                        # column 0: T
+    res[1::2, 1] = 0                                                 # the targets
+    res[2::2, 1] = sub(top[1:], select(tl[1:], target[:-1], left[:-1]))  # Select onto the next cell's top
+    modes = np.full(((2 * n + 3) // 4, 1), 0xff000000 | 11 << 8, np.uint32)
+    return img, res, modes
+
+
+def test_select_grid_oracle():
+    img, res, modes = select_grid_image()
+    assert (O.vp8l_inverse_predictor(modes, 2, res) == img).all()
+
+
+@pytest.mark.gpu
+def test_select_grid_gpu(cuda):
+    """The GPU inverse predictor's Select on the reference's test grid."""
+    from webp_amd import lossless as L
+    img, res, modes = select_grid_image()
+    out = L.predictor_inverse(L.to_argb_tensor(modes[None]), 2, L.to_argb_tensor(res[None]), check=True)
+    assert (L.from_argb_tensor(out)[0] == img).all()
