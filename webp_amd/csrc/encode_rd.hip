@@ -2201,11 +2201,12 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
       per_cu <= 0 || per_cu_pair <= 0)
     return wg::check_launch("encode occupancy query");
   const int rows = n_images * mbh;
-  // a wave pair per row when every row fits at once (one frame, a few
-  // frames); a full batch has more rows than wave slots and keeps one wave
-  // per row (two waves a row would halve the rows in flight).
-  // WG_ENCODE_PAIR=0 / 1 forces either schedule (A/B, tests).
-  bool pair = rows <= per_cu_pair * cus;
+  // a wave pair per row up to three times as many rows as pair workgroups
+  // fit at once (mixed 1080p frames with the row schedule: 16 frames 20.2 ->
+  // 15.6 ms, 32 frames 20.9 -> 19.5 ms; at 40 frames one wave a row wins,
+  // 21.2 vs 21.7 ms, and at 64 clearly, 23.1 vs 30.8 ms: two waves a row
+  // halve the rows in flight).  WG_ENCODE_PAIR=0 / 1 forces either schedule.
+  bool pair = rows <= 3 * per_cu_pair * cus;
   if (const char* e = getenv("WG_ENCODE_PAIR")) pair = e[0] == '1';
   if (pair) {
     const int grid = rows < per_cu_pair * cus ? rows : per_cu_pair * cus;
