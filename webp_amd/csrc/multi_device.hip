@@ -118,7 +118,10 @@ extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_device
   // the gather: each device's frames back to their places in the host buffers
   for (auto& j : jobs) {
     if (!j.mem) continue;
-    if (hipSetDevice(j.dev) != hipSuccess) continue;
+    if (hipError_t e = hipSetDevice(j.dev); e != hipSuccess) {
+      if (rc == WG_OK) rc = fail_hip(e, "hipSetDevice (gather)");
+      continue;
+    }
     if (rc == WG_OK) {
       const int st = wg_encode_status(j.work, mbw, (int)j.frames.size(), j.stream);  // synchronises the stream
       if (st != WG_OK) rc = st;
@@ -236,7 +239,10 @@ extern "C" int wg_vp8l_residual_image_devices(const int32_t* devices, int32_t n_
   }
   for (auto& b : bands) {  // gather: the band's tile modes and residual rows at their places
     if (!b.mem || rc != WG_OK) continue;
-    (void)hipSetDevice(b.dev);
+    if (hipError_t e = hipSetDevice(b.dev); e != hipSuccess) {
+      rc = fail_hip(e, "hipSetDevice (residual gather)");
+      continue;
+    }
     uint8_t* base = static_cast<uint8_t*>(b.mem);
     const size_t img_b = (size_t)align_up((size_t)px * 4);
     const int r0 = b.t0 << bits, r1 = std::min(b.t1 << bits, (int)height);
@@ -294,7 +300,10 @@ extern "C" int wg_plane_ssim_devices(const int32_t* devices, int32_t n_devices, 
   }
   for (auto& b : bands) {  // gather the per-tile partial sums in tile-row order
     if (!b.mem || rc != WG_OK) continue;
-    (void)hipSetDevice(b.dev);
+    if (hipError_t e = hipSetDevice(b.dev); e != hipSuccess) {
+      rc = fail_hip(e, "hipSetDevice (ssim gather)");
+      continue;
+    }
     const uint8_t* base = static_cast<const uint8_t*>(b.mem);
     hipError_t e = hipMemcpyAsync(partial.data() + (size_t)b.t0 * tx, base + a_b + b_b,
                                   (size_t)tx * (b.t1 - b.t0) * sizeof(double), hipMemcpyDeviceToHost, b.stream);
@@ -304,7 +313,10 @@ extern "C" int wg_plane_ssim_devices(const int32_t* devices, int32_t n_devices, 
   if (rc == WG_OK) {  // the one-device reduction order, on the first device that holds a band (its buffer is big enough)
     for (auto& b : bands) {
       if (!b.mem) continue;
-      (void)hipSetDevice(b.dev);
+      if (hipError_t e = hipSetDevice(b.dev); e != hipSuccess) {
+        rc = fail_hip(e, "hipSetDevice (ssim reduce)");
+        break;
+      }
       uint8_t* base = static_cast<uint8_t*>(b.mem);  // reuse the band's plane buffer for all partials + the sum
       double* d_part = reinterpret_cast<double*>(base);
       double* d_out = reinterpret_cast<double*>(base + align_up(partial.size() * sizeof(double)));
