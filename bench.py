@@ -6,28 +6,39 @@ frames, all inputs resident in HBM before timing starts:
                -> segment analysis (k_segments: assignSegments k-means,
                   setSegmentParams, setupSegment at the reference's q75 defaults)
                -> macroblock RD loop, Phase A of encodeFrameParallel (k_encode_rows)
-  decode side  reconstruct + loop filter (k_decode_bands) of libwebp q75
+  decode side  reconstruct + loop filter (k_decode_split) of libwebp q75
                bitstreams of the same three contents, parsed once on the host by
                wg_vp8_parse (tests/golden/q75_1080p.npz), -> fancy upsample to
                NRGBA (k_upsample)
 The encode configuration is webp.Encode's DefaultOptions (quality 75, method
 4, SNS 50, filter strength 60, 4 segments; internal/lossy/encode.go:66-86).
 
-After the timed region every slot's in-kernel dependency-wait flags are
-checked (wg_encode_status / wg_decode_status), and an untimed one-batch pass
-measures each kernel's isolated launch time for the roofline.
+After the timed region the in-kernel dependency waits are checked
+(wg_encode_status / wg_decode_status: the last launch of each slot plus the
+library's device-wide count of timed-out waits, which covers every timed
+launch).  Then, untimed for `value`:
+  - `runs`: the median of --runs repeats of a short timed region, for the
+    whole path and for the encode side and the decode side alone (BASELINE.md 2);
+  - an isolated one-batch pass for each kernel's launch time (the roofline);
+  - one-frame encodes (C2), whose RD launch is the macroblock wavefront's
+    critical path: the per-MB latency bench reports as the encoder's limiter;
+  - the measured copy-kernel HBM ceiling (tools/libprobe.so).
 
-Multi-GPU: one process per GPU (torch.distributed.run), frames sharded across
-ranks with no data-path collective in the timed region ("weak" scaling);
-value = all pixels / max rank time.  With N > 1, each rank then sends its last
-batch's outputs (wg_mb_enc records, reconstruction, NRGBA) to rank 0 with
-grouped RCCL send/recv (webp_amd/shard.py), timed and reported separately
-("gather"), outside `value`.
+Multi-GPU: one process per GPU, frames sharded across ranks with no data-path
+collective in the timed region ("weak" scaling); value = all pixels / max rank
+time.  `python bench.py --gpus N` with N > 1 starts the N ranks itself
+(torch.distributed.run in a child process, before anything touches the GPU);
+under an external torch.distributed.run, WORLD_SIZE must equal --gpus.  With
+N > 1, each rank then sends its last batch's outputs (wg_mb_enc records,
+reconstruction, NRGBA) to rank 0 with grouped RCCL send/recv
+(webp_amd/shard.py), timed and reported separately ("gather"), outside `value`.
 Rank 0 prints one JSON line.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -102,6 +113,11 @@ def parse():
     p.add_argument("--iso-steps", type=int, default=2, help="untimed one-batch passes for the isolated kernel times")
     p.add_argument("--no-gather", action="store_true",
                    help="with N > 1, skip the gather of the last batch's outputs to rank 0 (timed apart from value)")
+    p.add_argument("--runs", type=int, default=10, help="repeats of the short timed region for the medians")
+    p.add_argument("--run-steps", type=int, default=6, help="steps per median run")
+    p.add_argument("--launcher-check", action="store_true",
+                   help="CPU/gloo: start the ranks, join them and time an empty step; no GPU work, no measurement "
+                        "(tests/test_bench_launch.py)")
     return p.parse_args()
 
 
@@ -186,16 +202,25 @@ class Pipeline:
         self.slots = [Slot(batch, device, frames, _lib.lib) for _ in range(slots)]
         self.k = 0
         self.events = []
+        # Bind every slot stream to its hardware queue now: the first kernel on
+        # a new stream makes the runtime create and map a queue, and doing that
+        # while a persistent kernel runs on another queue stalled that kernel
+        # past its 2 s dependency-wait bound (the first overlapped step timed
+        # out; tools/debug_timeouts.py).
+        for sl in self.slots:
+            with torch.cuda.stream(sl.stream):
+                sl.uv_sum.zero_()
         torch.cuda.synchronize(device)  # inputs made on the default stream are ready for every slot stream
 
-    def step(self, record=False):
+    def step(self, record=False, side=None):
+        """One pass over the batch; side "encode" / "decode" runs that half alone (the per-side medians)."""
         sl = self.slots[self.k % len(self.slots)]
         self.k += 1
         sl.used = True
         with torch.cuda.stream(sl.stream):
-            self._stages(sl, record)
+            self._stages(sl, record and side is None, side)
 
-    def _stages(self, sl, record):
+    def _stages(self, sl, record, side=None):
         f = self.frames
         ev = []
 
@@ -205,20 +230,22 @@ class Pipeline:
                 ev[-1].record()  # on the slot's stream (the current stream here)
 
         mark()
-        f.import_rgba(self.rgba, has_alpha=False, out=(sl.Y, sl.U, sl.V))
-        mark()
-        f.analysis_alphas(sl.Y, sl.U, sl.V, W, H, out=(sl.alphas, sl.uv_sum, None, None))
-        mark()
-        f.segment_analysis(self.cfg, sl.alphas, sl.uv_sum, MBW, MBH, out=(sl.seg_ids, sl.segs, sl.seg_info))
-        f.encode_row_order(sl.alphas, MBW, MBH, work=sl.enc_work)
-        mark()
-        f.encode_mbs(sl.Y, sl.U, sl.V, W, H, sl.seg_ids, sl.segs, self.proba, method=ENC_CFG["method"],
-                     quality=ENC_CFG["quality"], out=sl.enc_out, recon=(sl.rY, sl.rU, sl.rV), work=sl.enc_work)
-        mark()
-        f.decode_frames(self.mb, self.co, 2, MBW, MBH, self.batch, out=(sl.dY, sl.dU, sl.dV), work=sl.work)
-        mark()
-        f.build_nrgba(sl.dY, sl.dU, sl.dV, W, H, out=sl.out)
-        mark()
+        if side != "decode":
+            f.import_rgba(self.rgba, has_alpha=False, out=(sl.Y, sl.U, sl.V))
+            mark()
+            f.analysis_alphas(sl.Y, sl.U, sl.V, W, H, out=(sl.alphas, sl.uv_sum, None, None))
+            mark()
+            f.segment_analysis(self.cfg, sl.alphas, sl.uv_sum, MBW, MBH, out=(sl.seg_ids, sl.segs, sl.seg_info))
+            f.encode_row_order(sl.alphas, MBW, MBH, work=sl.enc_work)
+            mark()
+            f.encode_mbs(sl.Y, sl.U, sl.V, W, H, sl.seg_ids, sl.segs, self.proba, method=ENC_CFG["method"],
+                         quality=ENC_CFG["quality"], out=sl.enc_out, recon=(sl.rY, sl.rU, sl.rV), work=sl.enc_work)
+            mark()
+        if side != "encode":
+            f.decode_frames(self.mb, self.co, 2, MBW, MBH, self.batch, out=(sl.dY, sl.dU, sl.dV), work=sl.work)
+            mark()
+            f.build_nrgba(sl.dY, sl.dU, sl.dV, W, H, out=sl.out)
+            mark()
         if record:
             self.events.append(ev)
 
@@ -235,7 +262,9 @@ class Pipeline:
         return {k: v / n for k, v in acc.items()}
 
     def check_status(self):
-        """Raises if any in-kernel dependency wait of the slots' last launches timed out."""
+        """Raises if an in-kernel dependency wait timed out: the slots' last
+        launches (their work-buffer flags) or any earlier launch (the library's
+        device-wide count of timed-out waits, never reset)."""
         for sl in self.slots:
             if sl.used:
                 with torch.cuda.stream(sl.stream):
@@ -349,23 +378,133 @@ def isolated_stage_ms(rgba, mb, co, batch, device, steps):
     return ms
 
 
+def median_runs(pipe, runs, steps, world, device):
+    """BASELINE.md 2's statistic: the median over `runs` short timed regions
+    (each bracketed like the main one, MAX over ranks) of MPix/s for the whole
+    path and for each side alone.  One untimed step before each side."""
+    out = {}
+    for side in (None, "encode", "decode"):
+        pipe.step(side=side)
+        vals = []
+        for _ in range(runs):
+            el = timed_region(lambda record=False: pipe.step(side=side), steps, 0, world, torch.cuda.synchronize,
+                              device)
+            vals.append(aggregate_mpix_s(world, pipe.batch, steps, el))
+        vals.sort()
+        m = len(vals)
+        med = vals[m // 2] if m % 2 else (vals[m // 2 - 1] + vals[m // 2]) / 2
+        out[side or "encode+decode"] = {"median": round(med, 1), "min": round(vals[0], 1), "max": round(vals[-1], 1)}
+    pipe.events = []
+    return {"runs": runs, "steps_per_run": steps, "unit": "MPixels/s", **out}
+
+
+def single_frame_encode(device, reps=3):
+    """C2 (one 1920x1080 frame, q75 defaults) per content: the encode DSP path
+    (import -> analysis -> segments -> RD) and the RD launch alone, best of
+    `reps`, event-timed on the current stream.  A one-frame RD launch is the
+    macroblock wavefront's critical path: (mbw + 2 (mbh - 1)) macroblock
+    times of the row's wave pair, which gives the per-MB latency."""
+    from webp_amd import frames
+    cfg = frames.encoder_config(**ENC_CFG)
+    proba = frames.default_proba(device)
+    steps_cp = MBW + 2 * (MBH - 1)
+    res = {}
+    for j, kind in enumerate(CONTENTS):
+        rgba = torch.from_numpy(content_rgba(kind, j)[None]).to(device)
+        best_path = best_rd = None
+        for rep in range(reps + 1):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record()
+            Y, U, V = frames.import_rgba(rgba, has_alpha=False)
+            al, uvs = frames.analysis_alphas(Y, U, V, W, H)
+            ids, segs, _ = frames.segment_analysis(cfg, al, uvs, MBW, MBH, info=False)
+            work = frames.encode_row_order(al, MBW, MBH)
+            e[1].record()
+            frames.encode_mbs(Y, U, V, W, H, ids, segs, proba, method=ENC_CFG["method"], quality=ENC_CFG["quality"],
+                              work=work)
+            e[2].record()
+            frames.encode_status(work, MBW, 1)
+            rd, path = e[1].elapsed_time(e[2]), e[0].elapsed_time(e[2])
+            if rep > 0:  # the first pass builds the per-device tables
+                best_rd = rd if best_rd is None else min(best_rd, rd)
+                best_path = path if best_path is None else min(best_path, path)
+        res[kind] = {"path_ms": round(best_path, 3), "rd_ms": round(best_rd, 3),
+                     "mpix_s": round(W * H / best_path / 1e3, 1),
+                     "per_mb_us": round(best_rd * 1e3 / steps_cp, 2)}
+    return {"frames": res, "critical_path_mb_steps": steps_cp}
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv, n):
+    """`python bench.py --gpus N` (N > 1) without a launcher: run N ranks under
+    torch.distributed.run in a child process and return its exit code.  This
+    process never touches the GPU (importing torch does not initialise HIP),
+    so nothing is re-executed after a device was opened; rank 0's JSON line
+    reaches stdout through the child."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this pool
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launcher_check(args, world, rank):
+    """--launcher-check: the launch / join / timing path on gloo with an empty
+    step (no GPU, nothing measured); rank 0 prints the ranks that joined."""
+    dev = torch.device("cpu")
+    if world > 1:
+        torch.distributed.init_process_group("gloo")
+    joined = torch.ones(1)
+    if world > 1:
+        torch.distributed.all_reduce(joined)
+    elapsed = timed_region(lambda record=False: None, args.steps, args.warmup, world, lambda: None, dev)
+    if rank == 0:
+        print(json.dumps({"metric": "launcher check (no GPU work; not a measurement)", "value": None,
+                          "n_gpus": world, "ranks_joined": int(joined.item()), "steps": args.steps,
+                          "warmup": args.warmup, "elapsed_s": elapsed}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: {world} ranks were launched (WORLD_SIZE) but --gpus is {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launcher_check:
+        return launcher_check(args, world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     import webp_amd
     webp_amd.device_check()
+    joined = torch.ones(1, device=device)
+    if world > 1:
+        torch.distributed.all_reduce(joined)  # every rank that joined the process group (RCCL)
+    joined = int(joined.item())
+    if joined != args.gpus:
+        print(f"bench.py: {joined} ranks joined, --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
 
     rgba, mb, co, parsed = make_inputs(args.batch, rank, device)
     pipe = Pipeline(rgba, mb, co, args.batch, device, slots=args.slots)
     elapsed = timed_region(pipe.step, args.steps, args.warmup, world, torch.cuda.synchronize, device)
     overlapped = pipe.stage_ms()
-    pipe.check_status()  # raises if any timed launch hit an in-kernel wait timeout
+    pipe.check_status()  # raises if any launch so far hit an in-kernel wait timeout
+    runs = median_runs(pipe, args.runs, args.run_steps, world, device) if args.runs > 0 else None
+    pipe.check_status()
     iso = isolated_stage_ms(rgba, mb, co, args.batch, device, args.iso_steps)
     gather = None
     if world > 1 and not args.no_gather:
@@ -373,6 +512,12 @@ def main():
         sl = pipe.slots[(pipe.k - 1) % len(pipe.slots)]
         gather = shard.timed_gather_to_root([sl.enc_out, sl.rY, sl.rU, sl.rV, sl.out], world, rank, device)
     del pipe
+    c2 = single_frame_encode(device) if rank == 0 else None
+    copy = None
+    if rank == 0:
+        from tools import fetch_calib
+        copy = fetch_calib.copy_peak(device)
+    torch.cuda.synchronize()
 
     if rank == 0:
         value = aggregate_mpix_s(world, args.batch, args.steps, elapsed)
@@ -388,6 +533,7 @@ def main():
             "value": round(value, 1),
             "unit": "MPixels/s",
             "n_gpus": world,
+            "ranks_joined": joined,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(step_ms, 3),
@@ -405,6 +551,8 @@ def main():
                                   "(k_segments)",
                        "frames_per_gpu": args.batch, "width": W, "height": H, "parallelism": f"frames sharded x{world}",
                        "batches_in_flight": args.slots},
+            "value_stat": f"mean over the {args.steps} timed steps (the contract's K-step region); medians in `runs`",
+            "runs": runs,
             "stage_ms_isolated": {k: round(v, 3) for k, v in iso.items()},
             "stage_ms_overlapped": {k: round(v, 3) for k, v in overlapped.items()},
             "roofline": {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -413,21 +561,37 @@ def main():
                          "algorithmic_bytes_per_launch": int(alg),
                          "avg_launch_ms": round(iso[dominant], 4), "launch_ms_source": "isolated one-batch pass",
                          "launches_per_step": 1,
+                         "measured_copy_peak": copy,
+                         "frac_of_measured_copy_peak": round(achieved / copy["GB/s"], 4) if copy else None,
                          # with batches in flight the launches overlap: bytes per step over the step time
                          "achieved_per_step": round(alg / (step_ms / 1e3) / 1e9, 1),
                          "frac_per_step": round(alg / (step_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "launches_in_flight": args.slots},
+                         "launches_in_flight": args.slots,
+                         "isolated_vs_step": "the isolated launch is longer than ms_per_step because consecutive "
+                                             "batches' launches overlap on their own streams",
+                         "limiter": "critical path of the macroblock wavefront (latency), not HBM: see critical_path "
+                                    "and valu"},
             "stage_roofline": {k: {"kernel": KERNELS[k],
                                    "GB/s": round(BYTES_PER_PX[k] * px_rank_step / (v / 1e3) / 1e9, 1),
                                    "frac": round(BYTES_PER_PX[k] * px_rank_step / (v / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
                                for k, v in iso.items()},
         }
+        if c2 is not None:
+            slow = max(c2["frames"].values(), key=lambda r: r["rd_ms"])
+            rec["roofline"]["critical_path"] = {
+                "model": "a one-frame RD launch = (mbw + 2 (mbh - 1)) macroblock latencies of the row's wave pair; "
+                         "a batch launch ends on its slowest frame's path plus slot contention",
+                "mb_steps": c2["critical_path_mb_steps"],
+                "per_mb_us": {k: r["per_mb_us"] for k, r in c2["frames"].items()},
+                "slowest_frame_rd_ms": slow["rd_ms"],
+                "batch_launch_over_slowest_frame": round(iso[dominant] / slow["rd_ms"], 3)}
+            rec["c2_single_frame"] = c2["frames"]
         valu = pmc_valu(kernel, iso[dominant], step_ms)
         if valu is not None:
             rec["valu"] = valu
         if gather is not None:
             rec["gather"] = gather
-        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is timed at N = 1 only
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is timed at N = 1 only, after the GPU phase
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds, parsed)
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -16,6 +16,14 @@
  *    independent instances.  Instance i's buffer starts at base + i*stride.
  *  - Frame entry points take `n_images` same-sized images laid out back to
  *    back with the given per-image byte pitch (image_pitch).
+ *  - Persistent kernels (wg_encode_mbs, wg_decode_frames,
+ *    wg_vp8l_inverse_predictor, the gradient wg_alpha_unfilter) hand rows
+ *    across workgroups and bound every wait (2 s); a wait that times out makes
+ *    the *_status call fail.  Issue a first kernel on every stream before
+ *    running them concurrently with other streams: the first kernel on a new
+ *    stream makes the runtime create a hardware queue, which on MI355X
+ *    stalled a persistent kernel already running on another queue past that
+ *    bound.
  *
  * The Go-side binding a maintainer adds (cgo) is shown in INTEGRATION.md.
  */
@@ -246,7 +254,9 @@ int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t 
  * work and row count, until the next wg_encode_row_order); without it the
  * rows go in (row, frame) order.  Scheduling only: the outputs are the same. */
 int wg_encode_row_order(const int32_t* alphas, int32_t mbw, int32_t mbh, int32_t n_images, void* work, void* stream);
-/* After wg_encode_mbs on the same stream: WG_OK or WG_EHIP on a row-wait timeout.  Synchronises. */
+/* After wg_encode_mbs on the same stream: WG_OK, or WG_EHIP if a row wait of
+ * the last launch on `work` -- or of any encoder launch since the library
+ * loaded (a device-wide count that is never reset) -- timed out.  Synchronises. */
 int wg_encode_status(const void* work, int32_t mbw, int32_t n_images, void* stream);
 /* The multi-device batch variant of the encode DSP path (one host process
  * driving several GPUs, as a cgo host would): n_images RGBA frames (w x h,
@@ -269,8 +279,9 @@ int wg_encode_frames_devices(const int32_t* devices, int32_t n_devices, const ui
 int wg_fixed_costs_i4_host(uint16_t* out);
 
 /* After wg_decode_frames on the same stream: WG_OK, or WG_EHIP if a row
- * dependency wait timed out inside the kernel (output invalid).  Synchronises
- * the stream. */
+ * dependency wait of the last launch on `work`, or of any decoder launch since
+ * the library loaded, timed out inside the kernel (output invalid).
+ * Synchronises the stream. */
 int wg_decode_status(const void* work, int32_t mbw, int32_t n_images, void* stream);
 
 /* RGBA -> YUV420 import: replaces VP8Encoder.importImage

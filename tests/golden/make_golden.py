@@ -66,6 +66,7 @@ def main():
     make_decode_fixtures(img)
     make_sharpyuv_fixtures(img)
     make_reference_testdata()
+    make_c3_bitstream()
     print("wrote", os.path.join(HERE, "libwebp_fixtures.npz"), sum(v.nbytes for v in out.values()), "bytes raw")
 
 
@@ -142,6 +143,35 @@ def make_bench_bitstreams():
            "blobs": L.encode_lossy(synth.blobs_rgba(w, h, seed=2), 75.0)}
     path = os.path.join(HERE, "q75_1080p.npz")
     np.savez(path, **{k: np.frombuffer(bytes(v), np.uint8) for k, v in out.items()})
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+C3_PNG = "/root/reference/testdata/test_color.png"
+
+
+def c3_rgba():
+    """SURVEY 8(d) C3 input "P": testdata/test_color.png (1536x1024) tiled to 4096x4096."""
+    from PIL import Image
+    img = np.array(Image.open(C3_PNG).convert("RGBA"))
+    reps = (-(-4096 // img.shape[0]), -(-4096 // img.shape[1]), 1)
+    return np.ascontiguousarray(np.tile(img, reps)[:4096, :4096])
+
+
+def make_c3_bitstream():
+    """C3 on real content: a libwebp 1.6.0 q75 encode (WebPEncodeRGBA) of the
+    tiled test_color.png at 4096x4096, and the SHA-256 of libwebp's
+    WebPDecodeRGBA / WebPDecodeYUV of it (67 MB of pixels: only the hashes are
+    kept).  tests/test_gpu_c3.py decodes the stream with wg_vp8_parse ->
+    wg_decode_frames -> wg_upsample_nrgba and compares with the oracle at full
+    size and with these hashes (under libwebp's skip rule)."""
+    import hashlib
+    data = L.encode_lossy(c3_rgba(), 75.0)
+    rgba = L.decode_rgba(data)
+    Y, U, V = L.decode_yuv(data)
+    sha = lambda a: np.frombuffer(hashlib.sha256(np.ascontiguousarray(a).tobytes()).digest(), np.uint8)
+    path = os.path.join(HERE, "c3_4096_q75.npz")
+    np.savez(path, webp=np.frombuffer(bytes(data), np.uint8), rgba_sha256=sha(rgba), y_sha256=sha(Y),
+             u_sha256=sha(U), v_sha256=sha(V))
     print("wrote", path, os.path.getsize(path), "bytes")
 
 

@@ -1,8 +1,11 @@
 """C3 (BASELINE.json configs[2]) and single-frame latencies on one GPU.
 
-  C3: one 4096x4096 lossy decode = reconstruct + loop filter (k_decode_bands)
-      + fancy upsample to NRGBA (k_upsample), from seeded synthetic parsed
-      macroblocks (SURVEY.md 8(d) recipe, normal filter, half I4);
+  C3 real: one 4096x4096 lossy decode of a libwebp q75 bitstream of the tiled
+      testdata/test_color.png (tests/golden/c3_4096_q75.npz): the host parse
+      (wg_vp8_parse) timed apart, then reconstruct + loop filter
+      (k_decode_split) + fancy upsample to NRGBA (k_upsample) on the GPU;
+  C3 synthetic: the same decode from seeded synthetic parsed macroblocks
+      (SURVEY.md 8(d) recipe, normal filter, half I4), also at batch 4 / 16;
   C2: one 1920x1080 q75 encode RD pass (k_encode_rows) on each content type;
   plus the same decode at batch 4 / 16 to show where a single image stops
   filling the chip.
@@ -49,6 +52,27 @@ def decode_case(n_img, w, h):
           f"total {t_dec + t_up:.3f} ms = {px / (t_dec + t_up) / 1e3:.1f} MPix/s")
 
 
+def decode_real():
+    import time
+    z = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                             "c3_4096_q75.npz"))
+    data = z["webp"].tobytes()
+    t0 = time.perf_counter()
+    dims, mb, co = frames.vp8_parse(data)
+    t_parse = (time.perf_counter() - t0) * 1e3
+    w, h, mbw, mbh, ft = dims["width"], dims["height"], dims["mbw"], dims["mbh"], dims["filter_type"]
+    mbt = frames.mb_info_tensor(mb)
+    cot = torch.from_numpy(co).cuda()
+    Y, U, V = frames.decode_frames(mbt, cot, ft, mbw, mbh, 1, check=True)
+    out = frames.build_nrgba(Y, U, V, w, h)
+    t_dec = timed(lambda: frames.decode_frames(mbt, cot, ft, mbw, mbh, 1, out=(Y, U, V)))
+    t_up = timed(lambda: frames.build_nrgba(Y, U, V, w, h, out=out))
+    i4 = float(mb["is_i4x4"].mean())
+    print(f"decode C3 real q75 {w}x{h} (test_color tiled, {len(data)} B, {i4:.2f} I4, filter {ft}): host parse "
+          f"{t_parse:.1f} ms; reconstruct+filter {t_dec:.3f} ms, upsample {t_up:.3f} ms, total {t_dec + t_up:.3f} ms "
+          f"= {w * h / (t_dec + t_up) / 1e3:.1f} MPix/s")
+
+
 def encode_case(kind, w=1920, h=1080):
     """C2: the encode DSP path of one frame at the reference's q75 defaults
     (import -> analysis -> segment analysis -> MB RD, frames.encode_frames),
@@ -67,6 +91,7 @@ def encode_case(kind, w=1920, h=1080):
 
 
 def main():
+    decode_real()
     for n in (1, 4, 16):
         decode_case(n, 4096, 4096)
     if os.environ.get("C3_ONLY") != "1":

@@ -4,24 +4,24 @@
   python tools/pmc_summary.py --json out.json fetch.csv write.csv      # HBM bytes per launch
 
 FETCH_SIZE / WRITE_SIZE are in KB.  MI355X_MICROARCH.md (HBM section): on
-gfx950 FETCH_SIZE counts half the bytes of wide (16 B/lane) streaming reads,
-so the HBM byte figure doubles it; WRITE_SIZE is exact for 16-B stores.  Both
-raw and corrected values are written so the correction stays visible.
-
-The undercount is of 128-B requests (tallied at 64 B).  k_encode_rows never
-makes one: each lane reads its own row's 32-B (Y) / 8-B (U, V) pieces, a
-wave instruction touching 16 different rows, plus 4- to 16-B hand-off and
-table words.  Its raw FETCH_SIZE equals the bytes it has to read (source
-1.5 B/px = 200.5 MB per 64 x 1080p, hand-off records and top-right words
-27 MB, segment ids 0.5 MB, cost tables: ~229 MB against 236 MB counted), so it is taken as
-is; doubling it would claim twice what the kernel can read.
+gfx950 FETCH_SIZE counts half the bytes of wide (16 B/lane) streaming reads.
+tools/fetch_calib.py measured the same factor for every read width the
+kernels here use (profiles/r03_fetch_calibration.json): 32-B and 8-B per-lane
+row pieces, 16 rows per wave instruction, count 0.50 of their bytes when a
+line's pieces are read close together, i.e. every L2 miss fills a 128-B line
+and is tallied at 64 B; read far apart (k_encode_rows' pattern) they count
+0.83 and 2.09, which is 0.5 x the real re-fetch (lines evicted between
+pieces).  So FETCH_SIZE is doubled for every kernel (round 2 took k_encode_rows'
+raw count, which the calibration does not support).  WRITE_SIZE is exact for
+32-B stores close together (1.01) and counts the real partial-line write
+traffic when they are far apart (1.86 for 32-B, 6.8 for 8-B pieces).  Raw and
+corrected values are both written.
 """
 import collections
 import csv
 import json
 import sys
 
-NARROW_READS = {"k_encode_rows"}  # no 128-B read requests: FETCH_SIZE is not halved (see above)
 
 
 def load(paths):
@@ -68,11 +68,10 @@ def main(argv):
             continue
         f = sum(ctrs["FETCH_SIZE"]) / len(ctrs["FETCH_SIZE"]) * 1024
         w = sum(ctrs["WRITE_SIZE"]) / len(ctrs["WRITE_SIZE"]) * 1024
-        narrow = name in NARROW_READS
         rec[name] = {"fetch_size_bytes_raw": int(f), "write_size_bytes": int(w),
-                     "hbm_bytes_per_launch": int((1 if narrow else 2) * f + w), "launches": len(ctrs["FETCH_SIZE"]),
-                     "correction": ("FETCH_SIZE x1 (no 128-B read requests, tools/pmc_summary.py) + WRITE_SIZE"
-                                    if narrow else "FETCH_SIZE x2 (gfx950 wide-read undercount) + WRITE_SIZE")}
+                     "hbm_bytes_per_launch": int(2 * f + w), "launches": len(ctrs["FETCH_SIZE"]),
+                     "correction": "FETCH_SIZE x2 (128-B line fills tallied at 64 B; measured for these access widths "
+                                   "in profiles/r03_fetch_calibration.json) + WRITE_SIZE"}
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 

@@ -16,6 +16,12 @@ class WebpGpuError(RuntimeError):
 
 
 def _load():
+    # torch first: libwebpgpu.so and torch must share one HIP runtime.  Loaded
+    # before torch, the library pulls in /opt/rocm's libamdhip64 and torch then
+    # binds to that copy instead of its own, after which the library saw no HIP
+    # device (hipGetDevice failed in a pytest run that imported a test module
+    # using webp_amd before any module imported torch).
+    import torch  # noqa: F401
     if not os.path.exists(LIB_PATH):
         raise WebpGpuError(
             f"{LIB_PATH} not found: build it with `make -C webp_amd` (hipcc --offload-arch=gfx950); "

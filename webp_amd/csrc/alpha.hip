@@ -210,6 +210,7 @@ __global__ __launch_bounds__(1024) void k_alpha_vseg(uint8_t* data, int w, int h
 struct GArgs {
   uint8_t* data;
   int* ctl;       // [0] band dequeue, [1] error
+  int* diag;      // wg::diag_words + DIAG_ALPHA
   int* progress;  // [n_img][bands]
   int64_t pitch;
   int w, h, bands, n_img;
@@ -300,6 +301,7 @@ __global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
               if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
                                       __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                 __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                wg::note_timeout(a.diag, need, seen, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0);
                 break;
               }
               __builtin_amdgcn_s_sleep(2);
@@ -694,6 +696,9 @@ extern "C" int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, i
   GArgs a;
   a.data = data;
   a.ctl = static_cast<int*>(work);
+  a.diag = wg::diag_words(s);
+  if (!a.diag) return WG_EHIP;
+  a.diag += wg::DIAG_ALPHA;
   a.progress = a.ctl + 4;
   a.pitch = pitch;
   a.w = width;
@@ -713,16 +718,8 @@ extern "C" int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, i
 
 extern "C" int wg_alpha_unfilter_status(const void* work, void* stream) {
   WG_REQUIRE(work);
-  int flag = 0;
-  hipStream_t s = wg::as_stream(stream);
-  if (hipMemcpyAsync(&flag, static_cast<const int*>(work) + 1, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return wg::check_launch("wg_alpha_unfilter_status");
-  if (flag) {
-    wg::set_error("alpha unfilter: a band wait timed out (output invalid)");
-    return WG_EHIP;
-  }
-  return WG_OK;
+  return wg::wait_status(static_cast<const int*>(work) + 1, wg::DIAG_ALPHA, wg::as_stream(stream),
+                         "wg_alpha_unfilter_status: alpha unfilter band", "needed, seen, ticks, block, -, -");
 }
 
 extern "C" size_t wg_alpha_estimate_work_bytes(int32_t n_images) {

@@ -98,6 +98,7 @@ struct DecArgs {
   uint8_t* top;   // [n_img][mbw][TOP_BYTES]
   int* progress;  // [n_img][mbh]: macroblocks completed (reconstructed + filtered + stored)
   int* ctl;       // [0] row dequeue counter, [1] error flag (wait timeout)
+  int* diag;      // wg::diag_words + DIAG_DECODE
   int filter_type, mbw, mbh, n_img;
 };
 
@@ -212,7 +213,7 @@ constexpr int BOT_BYTES = 128;  // final rows 12..15 of an MB: Y 4 x 16, U 4 x 8
 
 // bounded spin on a progress word (LDS or agent-scope global) by lane 0
 template <bool GLOBAL>
-__device__ __forceinline__ int wait_progress(const int* p, int need, int* err_flag, int give_up) {
+__device__ __forceinline__ int wait_progress(const int* p, int need, int* err_flag, int give_up, int* diag) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t it = 0;; it++) {
     int v;
@@ -224,6 +225,8 @@ __device__ __forceinline__ int wait_progress(const int* p, int need, int* err_fl
     if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
                             __hip_atomic_load(err_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
       __hip_atomic_fetch_or(err_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      wg::note_timeout(diag, need, v, GLOBAL ? 1 : 0, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x,
+                       (int)(threadIdx.x >> 6));
       return give_up;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -317,13 +320,13 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
           if (seen < need) {
             int v = 0;
             if (lane == 0)
-              v = from_lds ? wait_progress<false>(&prog_lds[wave - 1], need, &a.ctl[1], mbw)
-                           : wait_progress<true>(prog_above, need, &a.ctl[1], mbw);
+              v = from_lds ? wait_progress<false>(&prog_lds[wave - 1], need, &a.ctl[1], mbw, a.diag)
+                           : wait_progress<true>(prog_above, need, &a.ctl[1], mbw, a.diag);
             seen = __shfl(v, 0, 64);
           }
         }
         if (to_lds && mbx >= RING - 1) {  // ring slot `slot` must have been read by the row below
-          if (lane == 0) wait_progress<false>(&prog_lds[wave + 1], mbx - RING + 2, &a.ctl[1], mbw);
+          if (lane == 0) wait_progress<false>(&prog_lds[wave + 1], mbx - RING + 2, &a.ctl[1], mbw, a.diag);
           lds_sync();
         }
         STAMP(1);
@@ -777,14 +780,14 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           if (seen < need) {
             int v = 0;
             if (lane == 0)
-              v = from_lds ? wait_progress<false>(&prog_r[r - 1], need, &a.ctl[1], mbw)
-                           : wait_progress<true>(prog_above, need, &a.ctl[1], mbw);
+              v = from_lds ? wait_progress<false>(&prog_r[r - 1], need, &a.ctl[1], mbw, a.diag)
+                           : wait_progress<true>(prog_above, need, &a.ctl[1], mbw, a.diag);
             seen = __shfl(v, 0, 64);
           }
         }
         if (lane == 0) {
-          if (to_lds && mbx >= RING - 1) wait_progress<false>(&prog_r[r + 1], mbx - RING + 2, &a.ctl[1], mbw);
-          if (mbx >= RING_M) wait_progress<false>(&cons_f[r], mbx - RING_M + 1, &a.ctl[1], mbw);
+          if (to_lds && mbx >= RING - 1) wait_progress<false>(&prog_r[r + 1], mbx - RING + 2, &a.ctl[1], mbw, a.diag);
+          if (mbx >= RING_M) wait_progress<false>(&cons_f[r], mbx - RING_M + 1, &a.ctl[1], mbw, a.diag);
         }
         // ---- this MB's work buffer: left context from the previous MB's (:118-126), or the row start (:93-110) ----
         uint8_t* const wb = wb_all[r][mslot];
@@ -943,16 +946,16 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         lane = opaque_lane() & 63;
         // ---- this row's MB from R, the row above's filtered rows, ring space below ----
         if (lane == 0) {
-          if (have < mbx + 1) have = wait_progress<false>(&prog_r[r], mbx + 1, &a.ctl[1], mbw);
+          if (have < mbx + 1) have = wait_progress<false>(&prog_r[r], mbx + 1, &a.ctl[1], mbw, a.diag);
           if (mby > 0) {
             // in the band: MB x's bottom rows above (bot_f); across bands the
             // frame rows, final once the row above has finished MB x + 1
             const int need = from_lds ? mbx + 1 : min(mbx + 2, mbw);
             if (seen < need)
-              seen = from_lds ? wait_progress<false>(&bot_f[r - 1], need, &a.ctl[1], mbw)
-                              : wait_progress<true>(prog_above, need, &a.ctl[1], mbw);
+              seen = from_lds ? wait_progress<false>(&bot_f[r - 1], need, &a.ctl[1], mbw, a.diag)
+                              : wait_progress<true>(prog_above, need, &a.ctl[1], mbw, a.diag);
           }
-          if (to_lds && mbx >= RING - 1) wait_progress<false>(&prog_f[r + 1], mbx - RING + 2, &a.ctl[1], mbw);
+          if (to_lds && mbx >= RING - 1) wait_progress<false>(&prog_f[r + 1], mbx - RING + 2, &a.ctl[1], mbw, a.diag);
         }
         lds_sync();
         STAMP(7);
@@ -1202,6 +1205,9 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   a.mbh = mbh;
   a.n_img = n_images;
   hipStream_t s = wg::as_stream(stream);
+  a.diag = wg::diag_words(s);
+  if (!a.diag) return WG_EHIP;
+  a.diag += wg::DIAG_DECODE;
   if (g_num_cus == 0) {
     int dev = 0, cus = 0, per_cu = 0, per_cu_s = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -1234,14 +1240,6 @@ extern "C" int wg_decode_status(const void* work, int32_t mbw, int32_t n_images,
   WG_REQUIRE(work && mbw > 0 && n_images > 0);
   const int* ctl =
       reinterpret_cast<const int*>(static_cast<const uint8_t*>(work) + (size_t)n_images * mbw * TOP_BYTES);
-  int flag = 0;
-  hipStream_t s = wg::as_stream(stream);
-  if (hipMemcpyAsync(&flag, ctl + 1, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return wg::check_launch("wg_decode_status");
-  if (flag) {
-    wg::set_error("decode: a row dependency wait timed out (output invalid)");
-    return WG_EHIP;
-  }
-  return WG_OK;
+  return wg::wait_status(ctl + 1, wg::DIAG_DECODE, wg::as_stream(stream), "wg_decode_status: decode row",
+                         "needed, seen, global, ticks, block, wave");
 }

@@ -877,6 +877,7 @@ struct EncArgs {
   uint8_t* top;   // [n_img][mbw][REC]
   int* progress;  // [n_img][mbh]
   int* ctl;       // [0] dequeue, [1] error
+  int* diag;      // wg::diag_words + DIAG_ENCODE
   const int* order;  // the work buffer's row schedule (wg_encode_row_order): dequeue index -> row * n_img + image
   const int* order_tag;  // {ORDER_TAG ^ n_img, ~(ORDER_TAG ^ mbh)} when the schedule was built for this batch shape, else (row, image) order
   int64_t y_pitch, uv_pitch;
@@ -884,6 +885,7 @@ struct EncArgs {
 };
 
 constexpr uint64_t SPIN_TICKS = 200000000ull;
+
 constexpr int ORDER_TAG = 0x5e0d0000;  // marks a row schedule in the work buffer (xor the batch shape)
 
 #ifdef WG_STAMPS
@@ -1070,6 +1072,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
               if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
                                       __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                 __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                wg::note_timeout(a.diag, mby, img, need, v, (int)(__builtin_amdgcn_s_memrealtime() - t0),
+                                 (int)blockIdx.x);
                 v = mbw;
                 break;
               }
@@ -2192,6 +2196,9 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   a.quality = quality;
   a.order = a.progress + (size_t)n_images * mbh + 4;  // work: ... | progress | tag[4] | order | slack
   a.order_tag = a.order - 4;
+  a.diag = wg::diag_words(s);
+  if (!a.diag) return WG_EHIP;
+  a.diag += wg::DIAG_ENCODE;
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(encode ctl)");
   int cus = 0, per_cu = 0, per_cu_pair = 0;
@@ -2228,14 +2235,6 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
 extern "C" int wg_encode_status(const void* work, int32_t mbw, int32_t n_images, void* stream) {
   WG_REQUIRE(work && mbw > 0 && n_images > 0);
   const int* ctl = reinterpret_cast<const int*>(static_cast<const uint8_t*>(work) + (size_t)n_images * mbw * REC);
-  int flag = 0;
-  hipStream_t s = wg::as_stream(stream);
-  if (hipMemcpyAsync(&flag, ctl + 1, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return wg::check_launch("wg_encode_status");
-  if (flag) {
-    wg::set_error("encode: a row dependency wait timed out (output invalid)");
-    return WG_EHIP;
-  }
-  return WG_OK;
+  return wg::wait_status(ctl + 1, wg::DIAG_ENCODE, wg::as_stream(stream), "wg_encode_status: encode row",
+                         "row, image, needed, seen, ticks, block");
 }

@@ -39,6 +39,14 @@ int fail_hip(hipError_t e, const char* what) {
   return WG_EHIP;
 }
 
+// A first kernel on a new stream (its hardware queue is created then), issued
+// before any persistent kernel runs: creating a queue while wg_encode_mbs runs
+// on another one stalled it past its dependency-wait bound (webpgpu.h).
+hipError_t bind_stream(void* mem, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(mem, 0, 256, s);
+  return e == hipSuccess ? hipStreamSynchronize(s) : e;
+}
+
 }  // namespace
 
 extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_devices, const uint8_t* rgba, int32_t w,
@@ -62,7 +70,9 @@ extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_device
   std::vector<DevJob> jobs((size_t)n_devices);
   for (int i = 0; i < n_images; i++) jobs[(size_t)(i % n_devices)].frames.push_back(i);
   int rc = WG_OK;
-  // enqueue every device's work first, so the devices run at once
+  // every device's stream and buffers first (the streams bound to their
+  // queues before any persistent kernel runs), then every device's work, so
+  // the devices run at once
   for (auto& j : jobs) {
     j.dev = devices[&j - jobs.data()];
     const int nk = (int)j.frames.size();
@@ -94,6 +104,15 @@ extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_device
     j.proba = parts[6], j.out = parts[7], j.work = parts[8], j.ry = parts[9], j.ru = parts[10], j.rv = parts[11];
     j.alphas = reinterpret_cast<int32_t*>(parts[12]), j.uv_sum = reinterpret_cast<int32_t*>(parts[13]);
     j.info = reinterpret_cast<wg_frame_segs*>(parts[14]);
+    if ((e = bind_stream(j.mem, j.stream)) != hipSuccess) {
+      rc = fail_hip(e, "stream setup");
+      break;
+    }
+  }
+  for (auto& j : jobs) {
+    const int nk = (int)j.frames.size();
+    if (nk == 0 || rc != WG_OK) continue;
+    hipError_t e = hipSetDevice(j.dev);
     for (int q = 0; q < nk && e == hipSuccess; q++)
       e = hipMemcpyAsync(j.rgba + q * rgba_b, rgba + (int64_t)j.frames[(size_t)q] * rgba_b, (size_t)rgba_b,
                          hipMemcpyHostToDevice, j.stream);
@@ -218,19 +237,22 @@ extern "C" int wg_vp8l_residual_image_devices(const int32_t* devices, int32_t n_
     if (b.t1 <= b.t0) continue;
     hipError_t e = hipSetDevice(b.dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking);
-    // full-image layouts (the *_rows entry points address rows at their image positions)
-    const size_t img_b = (size_t)align_up((size_t)px * 4), modes_b = align_up((size_t)tx * ty * 4);
-    if (e == hipSuccess) e = hipMalloc(&b.mem, 2 * img_b + modes_b);
+    // the band's rows (+ the row above) and its tile modes only: the *_rows
+    // entry points address rows at their image positions, so they get base
+    // pointers moved back by the band's first row / tile row (only the band's
+    // own rows are ever touched)
+    const int r0 = (b.t0 << bits) - (b.t0 > 0 ? 1 : 0), r1 = std::min(b.t1 << bits, (int)height);  // + the row above
+    const size_t in_b = align_up((size_t)(r1 - r0) * row_b), modes_b = align_up((size_t)tx * (b.t1 - b.t0) * 4);
+    if (e == hipSuccess) e = hipMalloc(&b.mem, 2 * in_b + modes_b);
     if (e != hipSuccess) {
       rc = fail_hip(e, "device setup (residual bands)");
       break;
     }
     uint8_t* base = static_cast<uint8_t*>(b.mem);
-    uint32_t *d_argb = reinterpret_cast<uint32_t*>(base), *d_res = reinterpret_cast<uint32_t*>(base + img_b);
-    uint32_t* d_modes = reinterpret_cast<uint32_t*>(base + 2 * img_b);
-    const int r0 = (b.t0 << bits) - (b.t0 > 0 ? 1 : 0), r1 = std::min(b.t1 << bits, (int)height);  // + the row above
-    e = hipMemcpyAsync(d_argb + (int64_t)r0 * width, argb + (int64_t)r0 * width, (size_t)((r1 - r0) * row_b),
-                       hipMemcpyHostToDevice, b.stream);
+    uint32_t* d_argb = reinterpret_cast<uint32_t*>(base) - (int64_t)r0 * width;
+    uint32_t* d_res = reinterpret_cast<uint32_t*>(base + in_b) - (int64_t)r0 * width;
+    uint32_t* d_modes = reinterpret_cast<uint32_t*>(base + 2 * in_b) - (int64_t)b.t0 * tx;
+    e = hipMemcpyAsync(base, argb + (int64_t)r0 * width, (size_t)((r1 - r0) * row_b), hipMemcpyHostToDevice, b.stream);
     if (e != hipSuccess) {
       rc = fail_hip(e, "hipMemcpyAsync (band to device)");
       break;
@@ -244,13 +266,14 @@ extern "C" int wg_vp8l_residual_image_devices(const int32_t* devices, int32_t n_
       continue;
     }
     uint8_t* base = static_cast<uint8_t*>(b.mem);
-    const size_t img_b = (size_t)align_up((size_t)px * 4);
+    const int h0 = (b.t0 << bits) - (b.t0 > 0 ? 1 : 0);  // the buffer's first row
     const int r0 = b.t0 << bits, r1 = std::min(b.t1 << bits, (int)height);
-    hipError_t e = hipMemcpyAsync(modes + (int64_t)b.t0 * tx, base + 2 * img_b + (size_t)b.t0 * tx * 4,
-                                  (size_t)(b.t1 - b.t0) * tx * 4, hipMemcpyDeviceToHost, b.stream);
+    const size_t in_b = align_up((size_t)(r1 - h0) * row_b);
+    hipError_t e = hipMemcpyAsync(modes + (int64_t)b.t0 * tx, base + 2 * in_b, (size_t)(b.t1 - b.t0) * tx * 4,
+                                  hipMemcpyDeviceToHost, b.stream);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(residuals + (int64_t)r0 * width, base + img_b + (size_t)r0 * row_b, (size_t)((r1 - r0) * row_b),
-                         hipMemcpyDeviceToHost, b.stream);
+      e = hipMemcpyAsync(residuals + (int64_t)r0 * width, base + in_b + (size_t)(r0 - h0) * row_b,
+                         (size_t)((r1 - r0) * row_b), hipMemcpyDeviceToHost, b.stream);
     if (e == hipSuccess) e = hipStreamSynchronize(b.stream);
     if (e != hipSuccess) rc = fail_hip(e, "gather (residual bands)");
   }
@@ -270,7 +293,11 @@ extern "C" int wg_plane_ssim_devices(const int32_t* devices, int32_t n_devices, 
   std::vector<Band> bands((size_t)n_devices);
   std::vector<double> partial((size_t)tx * ty);
   int rc = WG_OK;
-  const size_t a_b = align_up((size_t)a_stride * h), b_b = align_up((size_t)b_stride * h);
+  // each band's buffer: its rows + halo of both planes, then its partial sums
+  auto rows_of = [&](const Band& b, int* r0, int* r1) {
+    *r0 = std::max(TILE * b.t0 - HALO, 0);
+    *r1 = std::min(TILE * b.t1 + HALO, (int)h);
+  };
   for (int k = 0; k < n_devices && rc == WG_OK; k++) {
     Band& b = bands[(size_t)k];
     b.dev = devices[k];
@@ -278,25 +305,28 @@ extern "C" int wg_plane_ssim_devices(const int32_t* devices, int32_t n_devices, 
     if (b.t1 <= b.t0) continue;
     hipError_t e = hipSetDevice(b.dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking);
+    int r0, r1;
+    rows_of(b, &r0, &r1);
+    const size_t a_b = align_up((size_t)(r1 - r0) * a_stride), b_b = align_up((size_t)(r1 - r0) * b_stride);
     const size_t part_b = align_up((size_t)tx * (b.t1 - b.t0) * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&b.mem, a_b + b_b + part_b + 256);
+    if (e == hipSuccess) e = hipMalloc(&b.mem, a_b + b_b + part_b);
     if (e != hipSuccess) {
       rc = fail_hip(e, "device setup (ssim bands)");
       break;
     }
     uint8_t* base = static_cast<uint8_t*>(b.mem);
-    const int r0 = std::max(TILE * b.t0 - HALO, 0), r1 = std::min(TILE * b.t1 + HALO, (int)h);  // band + halo
-    e = hipMemcpyAsync(base + (size_t)r0 * a_stride, a + (size_t)r0 * a_stride, (size_t)(r1 - r0) * a_stride,
-                       hipMemcpyHostToDevice, b.stream);
+    e = hipMemcpyAsync(base, a + (size_t)r0 * a_stride, (size_t)(r1 - r0) * a_stride, hipMemcpyHostToDevice, b.stream);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(base + a_b + (size_t)r0 * b_stride, b_plane + (size_t)r0 * b_stride, (size_t)(r1 - r0) * b_stride,
-                         hipMemcpyHostToDevice, b.stream);
+      e = hipMemcpyAsync(base + a_b, b_plane + (size_t)r0 * b_stride, (size_t)(r1 - r0) * b_stride, hipMemcpyHostToDevice,
+                         b.stream);
     if (e != hipSuccess) {
       rc = fail_hip(e, "hipMemcpyAsync (ssim band to device)");
       break;
     }
-    rc = wg_plane_ssim_rows(base, a_stride, (int64_t)a_stride * h, base + a_b, b_stride, (int64_t)b_stride * h, w, h, b.t0,
-                            b.t1, 1, reinterpret_cast<double*>(base + a_b + b_b), b.stream);
+    // plane bases moved back by r0 rows: the rows entry point addresses rows at their image positions
+    rc = wg_plane_ssim_rows(base - (int64_t)r0 * a_stride, a_stride, (int64_t)a_stride * h,
+                            base + a_b - (int64_t)r0 * b_stride, b_stride, (int64_t)b_stride * h, w, h, b.t0, b.t1, 1,
+                            reinterpret_cast<double*>(base + a_b + b_b), b.stream);
   }
   for (auto& b : bands) {  // gather the per-tile partial sums in tile-row order
     if (!b.mem || rc != WG_OK) continue;
@@ -305,27 +335,31 @@ extern "C" int wg_plane_ssim_devices(const int32_t* devices, int32_t n_devices, 
       continue;
     }
     const uint8_t* base = static_cast<const uint8_t*>(b.mem);
+    int r0, r1;
+    rows_of(b, &r0, &r1);
+    const size_t a_b = align_up((size_t)(r1 - r0) * a_stride), b_b = align_up((size_t)(r1 - r0) * b_stride);
     hipError_t e = hipMemcpyAsync(partial.data() + (size_t)b.t0 * tx, base + a_b + b_b,
                                   (size_t)tx * (b.t1 - b.t0) * sizeof(double), hipMemcpyDeviceToHost, b.stream);
     if (e == hipSuccess) e = hipStreamSynchronize(b.stream);
     if (e != hipSuccess) rc = fail_hip(e, "gather (ssim bands)");
   }
-  if (rc == WG_OK) {  // the one-device reduction order, on the first device that holds a band (its buffer is big enough)
+  if (rc == WG_OK) {  // the one-device reduction order, on the first device that holds a band
     for (auto& b : bands) {
       if (!b.mem) continue;
-      if (hipError_t e = hipSetDevice(b.dev); e != hipSuccess) {
-        rc = fail_hip(e, "hipSetDevice (ssim reduce)");
-        break;
-      }
-      uint8_t* base = static_cast<uint8_t*>(b.mem);  // reuse the band's plane buffer for all partials + the sum
-      double* d_part = reinterpret_cast<double*>(base);
-      double* d_out = reinterpret_cast<double*>(base + align_up(partial.size() * sizeof(double)));
-      hipError_t e = hipMemcpyAsync(d_part, partial.data(), partial.size() * sizeof(double), hipMemcpyHostToDevice, b.stream);
+      void* red = nullptr;
+      hipError_t e = hipSetDevice(b.dev);
+      if (e == hipSuccess) e = hipMalloc(&red, align_up(partial.size() * sizeof(double)) + 256);
       if (e == hipSuccess) {
-        rc = wg_plane_ssim_reduce(d_part, (int64_t)partial.size(), 1, d_out, b.stream);
-        if (rc == WG_OK) e = hipMemcpyAsync(out, d_out, sizeof(double), hipMemcpyDeviceToHost, b.stream);
-        if (rc == WG_OK && e == hipSuccess) e = hipStreamSynchronize(b.stream);
+        double* d_part = static_cast<double*>(red);
+        double* d_out = reinterpret_cast<double*>(static_cast<uint8_t*>(red) + align_up(partial.size() * sizeof(double)));
+        e = hipMemcpyAsync(d_part, partial.data(), partial.size() * sizeof(double), hipMemcpyHostToDevice, b.stream);
+        if (e == hipSuccess) {
+          rc = wg_plane_ssim_reduce(d_part, (int64_t)partial.size(), 1, d_out, b.stream);
+          if (rc == WG_OK) e = hipMemcpyAsync(out, d_out, sizeof(double), hipMemcpyDeviceToHost, b.stream);
+          if (rc == WG_OK && e == hipSuccess) e = hipStreamSynchronize(b.stream);
+        }
       }
+      if (red) (void)hipFree(red);
       if (e != hipSuccess && rc == WG_OK) rc = fail_hip(e, "ssim reduce");
       break;
     }

@@ -92,6 +92,12 @@ __global__ __launch_bounds__(NT) void k_segments(SegArgs a) {
   __shared__ int num_segs_s, smooth_s, reset_s;
   __shared__ SegState dqm[4];
   __shared__ int dq_s[2];
+  // thread 0's k-means state lives in LDS, not in dynamically indexed private
+  // arrays: a kernel with scratch (private segment) memory, dispatched on a
+  // queue for the first time while a persistent kernel runs on another, stalled
+  // that kernel's waves for seconds on MI355X (bench.py's first overlapped
+  // steps; tools/debug_timeouts.py), so no kernel here uses scratch.
+  __shared__ int centers[4], accum[4], dist[4];
   const int tid = threadIdx.x, img = blockIdx.x;
   const int mbw = a.mbw, mbh = a.mbh, total = mbw * mbh;
   const int32_t* al = a.alphas + (int64_t)img * total;
@@ -106,7 +112,12 @@ __global__ __launch_bounds__(NT) void k_segments(SegArgs a) {
     for (int i = tid; i < total; i += NT) atomicAdd(&histo[al[i] & 255], 1);
   __syncthreads();
   if (tid == 0) {
-    SegState d[4] = {};
+    SegState* d = dqm;
+    int* map = seg_map;
+    for (int k = 0; k < 4; k++) {
+      d[k] = SegState{};
+      map[k] = k;
+    }
     int num_segs = num_segs0;
     if (num_segs > 1) {
       // assignSegments (:737-849)
@@ -115,11 +126,11 @@ __global__ __launch_bounds__(NT) void k_segments(SegArgs a) {
       int max_a = 255;
       while (max_a > min_a && histo[max_a] == 0) max_a--;
       const int range_a = max_a - min_a;
-      int centers[4] = {0, 0, 0, 0};
+      for (int k = 0; k < 4; k++) centers[k] = 0;
       for (int k = 0; k < num_segs; k++) centers[k] = min_a + ((2 * k + 1) * range_a) / (2 * num_segs);
       int weighted_avg = 0;
       for (int iter = 0; iter < 6; iter++) {
-        int accum[4] = {0, 0, 0, 0}, dist[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 4; k++) accum[k] = dist[k] = 0;
         int n = 0;
         for (int al_ = min_a; al_ <= max_a; al_++) {
           const int h = histo[al_];
@@ -171,7 +182,6 @@ __global__ __launch_bounds__(NT) void k_segments(SegArgs a) {
       }
     }
     // simplifySegments (:197-242)
-    int map[4] = {0, 1, 2, 3};
     if (num_segs > 1) {
       int num_final = 1;
       for (int s1 = 1; s1 < num_segs; s1++) {
@@ -190,10 +200,6 @@ __global__ __launch_bounds__(NT) void k_segments(SegArgs a) {
       if (num_final < num_segs)
         for (int i = num_final; i < num_segs; i++) d[i] = d[num_final - 1];
       num_segs = num_final;
-    }
-    for (int s = 0; s < 4; s++) {
-      dqm[s] = d[s];
-      seg_map[s] = map[s];
     }
     num_segs_s = num_segs;
     smooth_s = num_segs0 > 1 && cfg.segments > 1 && (cfg.preprocessing & 1) && mbw >= 3 && mbh >= 3;
@@ -223,11 +229,12 @@ __global__ __launch_bounds__(NT) void k_segments(SegArgs a) {
     const int pa[3] = {counts[0] + counts[1], counts[0], counts[2]};
     const int pb[3] = {counts[2] + counts[3], counts[1], counts[3]};
     int all255 = 1;
-    uint8_t p[3];
+    uint32_t p = 0;  // three probabilities, a byte each (no private array)
     for (int k = 0; k < 3; k++) {
       const int t = pa[k] + pb[k];
-      p[k] = (uint8_t)(t == 0 ? 255 : (255 * pa[k] + t / 2) / t);
-      all255 &= p[k] == 255;
+      const uint32_t pk = t == 0 ? 255u : (uint32_t)((255 * pa[k] + t / 2) / t);
+      p |= pk << (8 * k);
+      all255 &= pk == 255;
     }
     reset_s = all255;
     if (a.info) {
@@ -246,7 +253,7 @@ __global__ __launch_bounds__(NT) void k_segments(SegArgs a) {
         o.alpha[k] = dqm[k].alpha;
         o.beta[k] = dqm[k].beta;
       }
-      for (int k = 0; k < 3; k++) o.seg_proba[k] = p[k];
+      for (int k = 0; k < 3; k++) o.seg_proba[k] = (uint8_t)(p >> (8 * k));
       o.seg_proba[3] = 0;
       o.pad2[0] = o.pad2[1] = o.pad2[2] = 0;
     }

@@ -276,6 +276,7 @@ struct InvArgs {
   const uint32_t* in;
   uint32_t* out;
   int* ctl;        // [0] band dequeue counter, [1] error flag (wait timeout)
+  int* diag;       // wg::diag_words + DIAG_VP8L_INVERSE
   uint64_t* hand;  // [n_img][bands][width] {pixel, tag} granules of each band's last row
   int64_t pitch;
   int width, height, bits, tiles_x, tiles_y, bands, n_img;
@@ -372,7 +373,10 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
           if (__builtin_amdgcn_readfirstlane((int)ready)) break;
           if ((it & 15) == 15 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
                                   __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-            if (lane == 0) __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+              __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              wg::note_timeout(a.diag, s, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0, 0);
+            }
             break;
           }
         }
@@ -522,6 +526,9 @@ extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, in
   a.bands = (height + 63) / 64;
   a.n_img = n_images;
   a.ctl = static_cast<int*>(work);
+  a.diag = wg::diag_words(s);
+  if (!a.diag) return WG_EHIP;
+  a.diag += wg::DIAG_VP8L_INVERSE;
   a.hand = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(work) + 16);
   a.pitch = image_pitch;
   a.width = width;
@@ -540,16 +547,8 @@ extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, in
 
 extern "C" int wg_vp8l_inverse_status(const void* work, void* stream) {
   WG_REQUIRE(work);
-  int flag = 0;
-  hipStream_t s = wg::as_stream(stream);
-  if (hipMemcpyAsync(&flag, static_cast<const int*>(work) + 1, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return wg::check_launch("wg_vp8l_inverse_status");
-  if (flag) {
-    wg::set_error("vp8l inverse: a band dependency wait timed out (output invalid)");
-    return WG_EHIP;
-  }
-  return WG_OK;
+  return wg::wait_status(static_cast<const int*>(work) + 1, wg::DIAG_VP8L_INVERSE, wg::as_stream(stream),
+                         "wg_vp8l_inverse_status: vp8l inverse band", "step, ticks, block, -, -, -");
 }
 
 extern "C" int wg_vp8l_green(uint32_t* argb, int64_t n, int32_t add, void* stream) {

@@ -29,6 +29,52 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 inline unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
+// Timed-out dependency waits of the persistent kernels, per device: a
+// zeroed, never-reset block of 16 ints per kernel family (DIAG_ENCODE ...):
+// [0] timed-out waits of every launch since the library loaded, [1] set once
+// the first one is recorded, [2..7] its coordinates (kernel-specific).
+// Returns nullptr (error set) if the block cannot be made.
+enum { DIAG_ENCODE = 0, DIAG_DECODE = 16, DIAG_VP8L_INVERSE = 32, DIAG_ALPHA = 48 };
+int* diag_words(hipStream_t s);
+
+// lane-0 call on a timed-out wait: counts it and records the first one
+__device__ inline void note_timeout(int* diag, int c2, int c3, int c4, int c5, int c6, int c7) {
+  __hip_atomic_fetch_add(&diag[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int z = 0;
+  if (__hip_atomic_compare_exchange_strong(&diag[1], &z, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)) {
+    const int v[6] = {c2, c3, c4, c5, c6, c7};
+#pragma unroll
+    for (int k = 0; k < 6; k++) __hip_atomic_store(&diag[2 + k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// The status entry points of the persistent kernels: `flag` is the launch's
+// own timeout word in its work buffer (cleared by each launch), `diag` the
+// device's never-reset record of timed-out waits of every launch of that
+// kernel family (diag_words), so a timeout in any launch -- not only the last
+// one on `work` -- is reported.  `fields` names diag[2..7].  Synchronises `s`.
+inline int wait_status(const int* flag, int family, hipStream_t s, const char* what, const char* fields) {
+  int* diag = diag_words(s);
+  if (!diag) return WG_EHIP;
+  int f = 0, d[8] = {0};
+  if (hipMemcpyAsync(&f, flag, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(d, diag + family, sizeof(d), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return check_launch(what);
+  if (f || d[0]) {
+    std::string m = std::string(what) + ": a dependency wait timed out (output invalid)" +
+                    (f ? "" : " in an earlier launch") + "; " + std::to_string(d[0]) + " timed-out waits so far";
+    if (d[1]) {
+      m += ", the first at (" + std::string(fields) + ") =";
+      for (int k = 2; k < 8; k++) m += " " + std::to_string(d[k]);
+    }
+    set_error(m);
+    return WG_EHIP;
+  }
+  return WG_OK;
+}
+
 }  // namespace wg
 
 #define WG_REQUIRE(cond)                   \
