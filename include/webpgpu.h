@@ -108,6 +108,63 @@ int wg_ssim_get(const uint8_t* s1, const uint8_t* s2, int64_t buf_stride, int32_
 int wg_filter(int32_t kind, uint8_t* p, int64_t buf_stride, int32_t base, int32_t stride, int32_t uv_delta,
               const int32_t* thresh, const int32_t* ithresh, const int32_t* hev, int32_t n, void* stream);
 
+/* UpsampleLinePair (internal/dsp/upsample.go:45, format 0: RGB, 3 B/px) and
+ * UpsampleLinePairNRGBA (upsample_direct_amd64.go:10 / upsample_direct_noasm.go,
+ * format 1: NRGBA, 4 B/px; alpha rows may be NULL -> 255) over n line pairs:
+ * pair i reads top_y/bot_y + i*y_step, the four chroma rows + i*uv_step, and
+ * writes top_dst/bot_dst + i*dst_step (and alpha_* + i*alpha_step).  bot_y
+ * NULL = the last row of an odd-height image (bot_dst unused), as in Go.
+ * width >= 0; n <= 65535; NRGBA rows 4-byte aligned. */
+int wg_upsample_line_pairs(int32_t format, const uint8_t* top_y, const uint8_t* bot_y, int64_t y_step,
+                           const uint8_t* top_u, const uint8_t* top_v, const uint8_t* bot_u, const uint8_t* bot_v,
+                           int64_t uv_step, uint8_t* top_dst, uint8_t* bot_dst, int64_t dst_step,
+                           const uint8_t* alpha_top, const uint8_t* alpha_bot, int64_t alpha_step, int32_t width,
+                           int32_t n, void* stream);
+
+/* AccumulateRGBA(r, g, b, a, stride, dst, width) (internal/dsp/yuv.go:486-547)
+ * over n row pairs: planar channel rows at r/g/b/a + i*in_pitch (second row
+ * at +stride), dst uint16 (R, G, B, A) quads at dst + i*dst_pitch (elements).
+ * n <= 65535. */
+int wg_accumulate_rgba(const uint8_t* r, const uint8_t* g, const uint8_t* b, const uint8_t* a, int32_t stride,
+                       int64_t in_pitch, uint16_t* dst, int64_t dst_pitch, int32_t width, int32_t n, void* stream);
+/* ConvertRGBA32ToUV(rgb, u, v, width) (yuv.go:553) over n rows: rgb uint16
+ * quads at rgb + i*rgb_pitch (elements), u/v + i*uv_pitch.  n <= 65535. */
+int wg_convert_rgba32_to_uv(const uint16_t* rgb, int64_t rgb_pitch, uint8_t* u, uint8_t* v, int64_t uv_pitch,
+                            int32_t width, int32_t n, void* stream);
+/* VP8Random (internal/dsp/random.go:17-21): the generator state a dithered
+ * conversion advances.  232 bytes. */
+typedef struct wg_random {
+  int32_t index1, index2;
+  uint32_t tab[55];
+  int32_t amp;
+} wg_random;
+/* InitRandom(rg, dithering) (random.go:39-52), host memory */
+void wg_random_init_host(wg_random* rg, float dithering);
+/* ConvertRGBA32ToUVDithered(rgb, u, v, width, rg) (yuv.go:568-576) over n
+ * rows, row i with its own generator state[i] (device), advanced in place
+ * exactly as the Go call advances rg (two RandomBits(18) draws per pixel). */
+int wg_convert_rgba32_to_uv_dithered(const uint16_t* rgb, int64_t rgb_pitch, uint8_t* u, uint8_t* v, int64_t uv_pitch,
+                                     int32_t width, wg_random* state, int32_t n, void* stream);
+
+/* SSE(pix, ref, width, height, pixStride, refStride) (ssim.go:172) over n
+ * blocks at pix + i*pix_pitch / ref + i*ref_pitch: out uint64[n]. n <= 65535. */
+int wg_sse_planes(const uint8_t* pix, const uint8_t* ref, int32_t width, int32_t height, int32_t pix_stride,
+                  int32_t ref_stride, int64_t pix_pitch, int64_t ref_pitch, uint64_t* out, int32_t n, void* stream);
+/* PSNRFromSSE(sse, count) (ssim.go:163): out double[n] (Go's math.Log10). */
+int wg_psnr_from_sse(const uint64_t* sse, const int64_t* count, double* out, int32_t n, void* stream);
+/* DistoStats (ssim.go:12-17), Go's uint32 fields (wrapping sums). */
+typedef struct wg_disto_stats {
+  uint32_t w, xm, ym, xxm, xym, yym;
+} wg_disto_stats;
+/* The DistoStats SSIMFromBlocks accumulates (Accumulate per pixel,
+ * ssim.go:19-27, :103-112) over n blocks: out[n]. n <= 65535. */
+int wg_disto_stats_blocks(const uint8_t* pix, const uint8_t* ref, int32_t width, int32_t height, int32_t pix_stride,
+                          int32_t ref_stride, int64_t pix_pitch, int64_t ref_pitch, wg_disto_stats* out, int32_t n,
+                          void* stream);
+/* SSIMFromStats (ssim.go:88, clipped = 0) / SSIMFromStatsClipped (:97,
+ * clipped = 1) of n stats: out double[n]. */
+int wg_ssim_from_stats(const wg_disto_stats* stats, int32_t clipped, double* out, int32_t n, void* stream);
+
 /* ===================================================================== *
  * 2. Frame layer: the reference's row/frame seams.
  * ===================================================================== */

@@ -91,6 +91,11 @@ _SIGS = {
     "or_ssim_get_clipped": (ctypes.c_double, [_u8p, _i, _u8p, _i, _i, _i, _i, _i]),
     "or_plane_ssim": (ctypes.c_double, [_u8p, _i, _u8p, _i, _i, _i]),
     "or_sse_plane": (ctypes.c_uint64, [_u8p, _i, _u8p, _i, _i, _i]),
+    "or_disto_stats": (None, [_u8p, _i, _u8p, _i, _i, _i, ctypes.c_void_p]),
+    "or_ssim_from_stats": (ctypes.c_double, [ctypes.c_void_p, _i]),
+    "or_psnr_from_sse": (ctypes.c_double, [ctypes.c_uint64, ctypes.c_int64]),
+    "or_random_init": (None, [ctypes.c_void_p, ctypes.c_float]),
+    "or_convert_rgba32_to_uv_dithered": (None, [_u16p, _u8p, _u8p, _i, ctypes.c_void_p]),
     "or_import_rgba": (None, [_u8p, _i, _i, _i, _i, _u8p, _u8p, _u8p]),
     "or_dithering_strength": (ctypes.c_float, [ctypes.c_float]),
     "or_import_rgba_dithered": (None, [_u8p, _i, _i, _i, _i, ctypes.c_float, _u8p, _u8p, _u8p]),
@@ -632,3 +637,67 @@ def encode_frame(Y, U, V, width, height, cfg=None, proba=None):
     enc, ry, ru, rv = encode_frame_rd(Y, U, V, width, height, seg_ids, segs, proba, method=int(cfg[1]),
                                       quality=int(cfg[0]))
     return enc, (ry, ru, rv), seg_ids, info
+
+
+# ---------------- block-level yuv / metric helpers (tests/test_gpu_blockops_yuv.py) ----------------
+
+RANDOM_DTYPE = np.dtype([("index1", "<i4"), ("index2", "<i4"), ("tab", "<u4", (55,)), ("amp", "<i4")])  # or_random
+
+
+def random_init(dithering):
+    """InitRandom (internal/dsp/random.go:39): one VP8Random state record."""
+    st = np.zeros(1, RANDOM_DTYPE)
+    lib.or_random_init(st.ctypes.data, float(dithering))
+    return st
+
+
+def accumulate_rgba(r, g, b, a, stride, width):
+    """AccumulateRGBA (yuv.go:486) of one row pair: 1-D planes, row 2 at +stride."""
+    out = np.zeros(4 * ((width + 1) // 2), np.uint16)
+    lib.or_accumulate_rgba(u8(r), u8(g), u8(b), u8(a), stride, out.ctypes.data_as(_u16p), width)
+    return out
+
+
+def convert_rgba32_to_uv(rgb, width, state=None):
+    """ConvertRGBA32ToUV[Dithered] (yuv.go:553, :568); `state` (RANDOM_DTYPE) is advanced in place."""
+    rgb = np.ascontiguousarray(rgb, np.uint16)
+    u = np.zeros(width, np.uint8)
+    v = np.zeros(width, np.uint8)
+    if state is None:
+        lib.or_convert_rgba32_to_uv(rgb.ctypes.data_as(_u16p), u8(u), u8(v), width)
+    else:
+        lib.or_convert_rgba32_to_uv_dithered(rgb.ctypes.data_as(_u16p), u8(u), u8(v), width, state.ctypes.data)
+    return u, v
+
+
+def upsample_line_pair(ty, by, tu, tv, bu, bv, width, nrgba, at=None, ab=None):
+    """UpsampleLinePair (upsample.go:45, RGB) / UpsampleLinePairNRGBA (:130); by may be None."""
+    bpp = 4 if nrgba else 3
+    td = np.zeros(bpp * width, np.uint8)
+    bd = np.zeros(bpp * width, np.uint8)
+    byp = u8(by) if by is not None else None
+    if nrgba:
+        lib.or_upsample_line_pair_nrgba(u8(ty), byp, u8(tu), u8(tv), u8(bu), u8(bv), u8(td), u8(bd),
+                                        u8(at) if at is not None else None, u8(ab) if ab is not None else None, width)
+    else:
+        lib.or_upsample_line_pair_rgb(u8(ty), byp, u8(tu), u8(tv), u8(bu), u8(bv), u8(td), u8(bd), width)
+    return td, (bd if by is not None else None)
+
+
+def disto_stats(pix, ref):
+    """DistoStats of SSIMFromBlocks (ssim.go:103): [w, xm, ym, xxm, xym, yym] uint32."""
+    pix = np.ascontiguousarray(pix, np.uint8)
+    ref = np.ascontiguousarray(ref, np.uint8)
+    out = np.zeros(6, np.uint32)
+    h, w = pix.shape
+    lib.or_disto_stats(u8(pix), w, u8(ref), w, w, h, out.ctypes.data)
+    return out
+
+
+def ssim_from_stats(stats, clipped):
+    st = np.ascontiguousarray(stats, np.uint32)
+    return float(lib.or_ssim_from_stats(st.ctypes.data, int(clipped)))
+
+
+def psnr_from_sse(sse, count):
+    return float(lib.or_psnr_from_sse(int(sse), int(count)))

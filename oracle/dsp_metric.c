@@ -112,6 +112,28 @@ double or_plane_ssim(const uint8_t* a, int sa, const uint8_t* b, int sb, int w, 
   return sum;
 }
 
+/* DistoStats.Accumulate over a block (SSIMFromBlocks :103-112): Go's uint32
+ * fields wrap exactly like these */
+void or_disto_stats(const uint8_t* pix, int ps, const uint8_t* ref, int rs, int w, int h, uint32_t out[6]) {
+  stats_t s = {0};
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) acc(&s, pix[x + y * ps], ref[x + y * rs], 1);
+  out[0] = s.w, out[1] = s.xm, out[2] = s.ym, out[3] = s.xxm, out[4] = s.xym, out[5] = s.yym;
+}
+/* SSIMFromStats :88 (clipped = 0) / SSIMFromStatsClipped :97 (clipped = 1) */
+double or_ssim_from_stats(const uint32_t st[6], int clipped) {
+  const stats_t s = {st[0], st[1], st[2], st[3], st[4], st[5]};
+  if (clipped) return ssim_calc(&s, s.w);
+  return s.w == 0 ? 0.0 : ssim_calc(&s, 256);
+}
+/* PSNRFromSSE :163-170 with Go's math.Log10 = log2(x) * (Ln2/Ln10) (src/math/log10.go) */
+double or_go_log2(double x);
+double or_psnr_from_sse(uint64_t sse, int64_t count) {
+  if (sse == 0 || count == 0) return 99.0;
+  const double mse = (double)sse / (double)count;
+  return 10.0 * (or_go_log2(255.0 * 255.0 / mse) * 0x1.34413509f79ffp-2 /* Ln2/Ln10 */);
+}
+
 uint64_t or_sse_plane(const uint8_t* a, int sa, const uint8_t* b, int sb, int w, int h) { /* SSE :172 */
   uint64_t s = 0;
   for (int y = 0; y < h; y++)

@@ -116,6 +116,14 @@ void or_convert_rgba32_to_uv(const uint16_t* rgb, uint8_t* u, uint8_t* v, int wi
 }
 
 /* ---------------- VP8Random, random.go ---------------- */
+void or_convert_rgba32_to_uv_dithered(const uint16_t* rgb, uint8_t* u, uint8_t* v, int width, or_random* rg) { /* :568 */
+  for (int i = 0; i < width; i++) {
+    const int r = rgb[4 * i], g = rgb[4 * i + 1], b = rgb[4 * i + 2];
+    u[i] = (uint8_t)or_rgb_to_u(r, g, b, or_random_bits2(rg, 18, rg->amp));
+    v[i] = (uint8_t)or_rgb_to_v(r, g, b, or_random_bits2(rg, 18, rg->amp));
+  }
+}
+
 static const uint32_t k_random_table[55] = { /* random.go:24-35 (libwebp random_utils.c) */
   0x0de15230, 0x03b31886, 0x775faccb, 0x1c88626a, 0x68385c55, 0x14b3b828, 0x4a85fef8, 0x49ddb84b,
   0x64fcf397, 0x5c550289, 0x4a290000, 0x0d7ec1da, 0x5940b7ab, 0x5492577d, 0x4e19ca72, 0x38d38c69,

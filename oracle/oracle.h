@@ -80,6 +80,8 @@ void or_convert_rgba32_to_uv(const uint16_t* rgb, uint8_t* u, uint8_t* v, int wi
 typedef struct { int index1, index2; uint32_t tab[55]; int amp; } or_random;
 void or_random_init(or_random* rg, float dithering);            /* :39 */
 int or_random_bits2(or_random* rg, int num_bits, int amp);      /* :54 */
+void or_convert_rgba32_to_uv_dithered(const uint16_t* rgb, uint8_t* u, uint8_t* v, int width,
+                                      or_random* rg);            /* yuv.go:568 */
 float or_dithering_strength(float quality);                      /* encode.go (root):517-521 */
 void or_import_rgba_dithered(const uint8_t* rgba, int w, int h, int stride, int has_alpha, float dithering,
                              uint8_t* Y, uint8_t* U, uint8_t* V); /* internal/lossy/encode.go:690-940 */
@@ -109,6 +111,9 @@ double or_ssim_get_clipped(const uint8_t* s1, int st1, const uint8_t* s2, int st
 /* plane SSIM sum = libwebp AccumulateSSIM: sum over all pixels of SSIMGetClipped */
 double or_plane_ssim(const uint8_t* a, int sa, const uint8_t* b, int sb, int w, int h);
 uint64_t or_sse_plane(const uint8_t* a, int sa, const uint8_t* b, int sb, int w, int h); /* SSE :172 */
+void or_disto_stats(const uint8_t* pix, int ps, const uint8_t* ref, int rs, int w, int h, uint32_t out[6]); /* :103 */
+double or_ssim_from_stats(const uint32_t st[6], int clipped);   /* :88, :97 */
+double or_psnr_from_sse(uint64_t sse, int64_t count);           /* :163 */
 
 /* ---- lossy encoder DSP drivers ---- */
 /* importImage (internal/lossy/encode.go:671-943), non-dithered direct path:

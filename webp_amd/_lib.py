@@ -51,6 +51,16 @@ SIGNATURES = {
     "wg_metric": [_i32, _vp, _vp, _i64, _vp, _i32, _vp],
     "wg_ssim_get": [_vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp],
     "wg_filter": [_i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp],
+    "wg_upsample_line_pairs": [_i32, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32,
+                               _i32, _vp],
+    "wg_accumulate_rgba": [_vp, _vp, _vp, _vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp],
+    "wg_convert_rgba32_to_uv": [_vp, _i64, _vp, _vp, _i64, _i32, _i32, _vp],
+    "wg_random_init_host": [_vp, ctypes.c_float],
+    "wg_convert_rgba32_to_uv_dithered": [_vp, _i64, _vp, _vp, _i64, _i32, _vp, _i32, _vp],
+    "wg_sse_planes": [_vp, _vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i32, _vp],
+    "wg_psnr_from_sse": [_vp, _vp, _vp, _i32, _vp],
+    "wg_disto_stats_blocks": [_vp, _vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i32, _vp],
+    "wg_ssim_from_stats": [_vp, _i32, _vp, _i32, _vp],
     "wg_decode_work_bytes": [_i32, _i32, _i32],
     "wg_decode_frames": [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
     "wg_vp8_parse": [_vp, ctypes.c_size_t, _vp, _vp, _vp, _i64],
@@ -122,7 +132,7 @@ _RES = {"wg_last_error": ctypes.c_char_p, "wg_decode_work_bytes": ctypes.c_size_
         "wg_sharpyuv_work_bytes": ctypes.c_size_t, "wg_encode_work_bytes": ctypes.c_size_t,
         "wg_alpha_unfilter_work_bytes": ctypes.c_size_t, "wg_alpha_estimate_work_bytes": ctypes.c_size_t,
         "wg_rescaler_plan_bytes": ctypes.c_size_t, "wg_dither_plan_bytes": ctypes.c_size_t,
-        "wg_dither_amp": ctypes.c_int32}
+        "wg_dither_amp": ctypes.c_int32, "wg_random_init_host": None}
 
 for _name, _args in SIGNATURES.items():
     _f = getattr(lib, _name)

@@ -25,48 +25,10 @@
 
 #include "wg_common.h"
 #include "wg_dsp.h"
+#include "wg_yuv.h"
 
 namespace {
 using namespace wg;
-
-struct GammaTabs {
-  uint32_t to_lin[256];  // kGammaToLinearTab
-  uint32_t to_gamma[34]; // kLinearToGammaTab
-};
-
-GammaTabs host_tabs() {  // InitGammaTables, yuv.go:193-215
-  static GammaTabs t;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    for (int i = 0; i < 256; i++) {
-      const double v = (double)i / 255.0;
-      t.to_lin[i] = (uint32_t)((v <= 0 ? 0.0 : pow(v, 0.80)) * 4095.0 + 0.5);
-    }
-    const double scale = 128.0 / 4095.0;
-    for (int i = 0; i <= 32; i++) {
-      const double v = scale * (double)i;
-      t.to_gamma[i] = (uint32_t)((v <= 0 ? 0.0 : pow(v, 1.0 / 0.80)) * 255.0 + 0.5);
-    }
-    t.to_gamma[33] = 255;
-  });
-  return t;
-}
-
-__device__ __forceinline__ int lin_to_gamma(const uint32_t* tg, uint32_t base, int shift) {  // yuv.go:236-249
-  const int v = (int)base << shift;
-  const int pos = min(v >> 9, 31);
-  const int x = v & 511;
-  const int y = (int)tg[pos + 1] * x + (int)tg[pos] * (512 - x);
-  return (y + 64) >> 7;
-}
-
-__device__ __forceinline__ int rgb_to_y(int r, int g, int b) {  // yuv.go:151
-  return (16839 * r + 33059 * g + 6420 * b + (1 << 15) + (16 << 16)) >> 16;
-}
-__device__ __forceinline__ int clip_uv(int uv, int rnd = 1 << 17) {  // VP8ClipUV :138 (rounding YUV_HALF<<2 by default)
-  uv = (uv + rnd + (128 << 18)) >> 18;
-  return (uv & ~0xff) == 0 ? uv : (uv < 0 ? 0 : 255);
-}
 
 // One 2x2 quad: gamma-correct (alpha-weighted when 0 < sum(A) < 1020) average
 // of R, G, B, then RGBToU / RGBToV on the sum-of-4 values.  Returns u | v << 8.

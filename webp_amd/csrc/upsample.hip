@@ -16,31 +16,10 @@
 
 #include "wg_common.h"
 #include "wg_dsp.h"
+#include "wg_yuv.h"
 
 namespace {
 using namespace wg;
-
-// clip to [0, 16383] then >> 6 (v < 0 -> 0, v > 16383 -> 255): one v_med3
-__device__ __forceinline__ int yuv_clip(int v) { return min(max(v, 0), 16383) >> 6; }
-
-// MultHi (yuv.go:38) of a byte and a 16-bit constant on the full-rate 24-bit
-// multiplier.  Written as asm: hipcc turned both "*" and __umul24 into the
-// quarter-rate v_mul_lo_u32 once it lost the operands' range.
-template <uint32_t K>
-__device__ __forceinline__ int mult_hi(int x) {
-  uint32_t r;
-  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(x), "v"(K));
-  return (int)(r >> 8);
-}
-
-// YUVToRGB (yuv.go:71-109)
-__device__ __forceinline__ uint32_t yuv_to_rgba(int y, int u, int v, int a) {
-  const int yy = mult_hi<19077>(y);
-  const int r = yuv_clip(yy + mult_hi<26149>(v) - 14234);
-  const int g = yuv_clip(yy - mult_hi<6419>(u) - mult_hi<13320>(v) + 8708);
-  const int b = yuv_clip(yy + mult_hi<33050>(u) - 17685);
-  return pack4(r, g, b, a);
-}
 
 struct UpArgs {
   const uint8_t *y, *u, *v, *alpha;

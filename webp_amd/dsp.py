@@ -218,3 +218,145 @@ def filter_edge(name, p, base, stride, thresh, ithresh=None, hev=None, uv_delta=
     t, it, h = vec(thresh), vec(ithresh), vec(hev)
     call("wg_filter", FILTER_KINDS[name], p.data_ptr(), p.stride(0), base, stride, uv_delta, t.data_ptr(),
          it.data_ptr() if it is not None else None, h.data_ptr() if h is not None else None, n, _stream())
+
+
+# ---- line-pair upsampler (upsample.go:45-236, upsample_direct_amd64.go:10) ----
+
+def _rows(t, n=None):
+    _dev(t, torch.uint8)
+    assert t.dim() == 2 and (n is None or t.shape[0] == n)
+    return t
+
+
+def _line_pairs(fmt, top_y, bot_y, top_u, top_v, bot_u, bot_v, width, alpha_top=None, alpha_bot=None):
+    n = _rows(top_y).shape[0]
+    for t in (top_u, top_v, bot_u, bot_v):
+        _rows(t, n)
+        assert t.stride(0) == top_u.stride(0)
+    if bot_y is not None:
+        assert _rows(bot_y, n).stride(0) == top_y.stride(0)
+    bpp = 4 if fmt else 3
+    top_dst = torch.empty((n, bpp * width), dtype=torch.uint8, device=top_y.device)
+    bot_dst = torch.empty_like(top_dst) if bot_y is not None else None
+    if alpha_top is not None and alpha_bot is not None:
+        assert alpha_top.stride(0) == alpha_bot.stride(0)
+    a_step = alpha_top.stride(0) if alpha_top is not None else (alpha_bot.stride(0) if alpha_bot is not None else 0)
+    call("wg_upsample_line_pairs", fmt, top_y.data_ptr(), bot_y.data_ptr() if bot_y is not None else None,
+         top_y.stride(0), top_u.data_ptr(), top_v.data_ptr(), bot_u.data_ptr(), bot_v.data_ptr(), top_u.stride(0),
+         top_dst.data_ptr(), bot_dst.data_ptr() if bot_dst is not None else None, top_dst.stride(0),
+         alpha_top.data_ptr() if alpha_top is not None else None,
+         alpha_bot.data_ptr() if alpha_bot is not None else None, a_step, width, n, _stream())
+    return top_dst, bot_dst
+
+
+def UpsampleLinePair(top_y, bot_y, top_u, top_v, bot_u, bot_v, width):
+    """UpsampleLinePair (upsample.go:45) for n line pairs: rows are (n, L)
+    uint8 CUDA tensors (bot_y None = an odd height's last row); returns
+    (topDst, botDst) as (n, 3*width) RGB rows."""
+    return _line_pairs(0, top_y, bot_y, top_u, top_v, bot_u, bot_v, width)
+
+
+def UpsampleLinePairNRGBA(top_y, bot_y, top_u, top_v, bot_u, bot_v, width, alpha_top=None, alpha_bot=None):
+    """UpsampleLinePairNRGBA (upsample_direct_amd64.go:10): (n, 4*width) NRGBA
+    rows; alpha rows None -> 255."""
+    return _line_pairs(1, top_y, bot_y, top_u, top_v, bot_u, bot_v, width, alpha_top, alpha_bot)
+
+
+# ---- RGBA -> YUV420 chroma helpers (yuv.go:486-576, random.go) ----
+
+def AccumulateRGBA(r, g, b, a, stride, width):
+    """AccumulateRGBA(r, g, b, a, stride, dst, width) (yuv.go:486) for n row
+    pairs: r/g/b/a are (n, L) uint8 planar rows (second row at +stride);
+    returns dst as (n, 4 * ceil(width / 2)) uint16."""
+    n = _rows(r).shape[0]
+    for t in (g, b, a):
+        assert _rows(t, n).stride(0) == r.stride(0)
+    dst = torch.empty((n, 4 * ((width + 1) // 2)), dtype=torch.uint16, device=r.device)
+    call("wg_accumulate_rgba", r.data_ptr(), g.data_ptr(), b.data_ptr(), a.data_ptr(), stride, r.stride(0),
+         dst.data_ptr(), dst.stride(0), width, n, _stream())
+    return dst
+
+
+def ConvertRGBA32ToUV(rgb, width):
+    """ConvertRGBA32ToUV(rgb, u, v, width) (yuv.go:553): rgb (n, >= 4*width) uint16; returns (u, v) (n, width)."""
+    _dev(rgb, torch.uint16)
+    n = rgb.shape[0]
+    u = torch.empty((n, width), dtype=torch.uint8, device=rgb.device)
+    v = torch.empty_like(u)
+    call("wg_convert_rgba32_to_uv", rgb.data_ptr(), rgb.stride(0), u.data_ptr(), v.data_ptr(), u.stride(0), width, n,
+         _stream())
+    return u, v
+
+
+RANDOM_BYTES = 232  # wg_random (VP8Random)
+
+
+def InitRandom(dithering, n=1, device="cuda"):
+    """InitRandom(rg, dithering) (random.go:39) -> (n, 232) uint8 CUDA tensor of wg_random states."""
+    import ctypes
+
+    import numpy as np
+    from ._lib import lib
+    host = np.zeros(RANDOM_BYTES, np.uint8)
+    lib.wg_random_init_host(host.ctypes.data_as(ctypes.c_void_p), float(dithering))
+    return torch.from_numpy(np.tile(host, (n, 1))).to(device)
+
+
+def ConvertRGBA32ToUVDithered(rgb, width, states):
+    """ConvertRGBA32ToUVDithered(rgb, u, v, width, rg) (yuv.go:568): row i
+    draws from states[i] (InitRandom), which advance in place."""
+    _dev(rgb, torch.uint16)
+    _dev(states, torch.uint8)
+    n = rgb.shape[0]
+    assert states.shape == (n, RANDOM_BYTES)
+    u = torch.empty((n, width), dtype=torch.uint8, device=rgb.device)
+    v = torch.empty_like(u)
+    call("wg_convert_rgba32_to_uv_dithered", rgb.data_ptr(), rgb.stride(0), u.data_ptr(), v.data_ptr(), u.stride(0),
+         width, states.data_ptr(), n, _stream())
+    return u, v
+
+
+# ---- SSE / PSNR / DistoStats (ssim.go:12-181) ----
+
+def SSE(pix, ref, width, height, pix_stride, ref_stride):
+    """SSE(pix, ref, width, height, pixStride, refStride) (ssim.go:172) per
+    buffer pair: pix / ref (n, L) uint8; returns (n,) int64 (uint64 bits)."""
+    n = _rows(pix).shape[0]
+    _rows(ref, n)
+    out = torch.empty(n, dtype=torch.int64, device=pix.device)
+    call("wg_sse_planes", pix.data_ptr(), ref.data_ptr(), width, height, pix_stride, ref_stride, pix.stride(0),
+         ref.stride(0), out.data_ptr(), n, _stream())
+    return out
+
+
+def PSNRFromSSE(sse, count):
+    """PSNRFromSSE(sse, count) (ssim.go:163): sse / count (n,) int64 -> (n,) float64."""
+    _dev(sse, torch.int64)
+    _dev(count, torch.int64)
+    out = torch.empty(sse.shape[0], dtype=torch.float64, device=sse.device)
+    call("wg_psnr_from_sse", sse.data_ptr(), count.data_ptr(), out.data_ptr(), sse.shape[0], _stream())
+    return out
+
+
+def DistoStatsOfBlocks(pix, ref, width, height, pix_stride, ref_stride):
+    """The DistoStats that SSIMFromBlocks (ssim.go:103) accumulates, per block
+    pair: (n, 6) int32 holding the uint32 fields (W, Xm, Ym, Xxm, Xym, Yym)."""
+    n = _rows(pix).shape[0]
+    _rows(ref, n)
+    out = torch.empty((n, 6), dtype=torch.int32, device=pix.device)
+    call("wg_disto_stats_blocks", pix.data_ptr(), ref.data_ptr(), width, height, pix_stride, ref_stride,
+         pix.stride(0), ref.stride(0), out.data_ptr(), n, _stream())
+    return out
+
+
+def SSIMFromStats(stats, clipped=False):
+    """SSIMFromStats (ssim.go:88) / SSIMFromStatsClipped (:97): (n, 6) stats -> (n,) float64."""
+    _dev(stats, torch.int32)
+    out = torch.empty(stats.shape[0], dtype=torch.float64, device=stats.device)
+    call("wg_ssim_from_stats", stats.data_ptr(), int(bool(clipped)), out.data_ptr(), stats.shape[0], _stream())
+    return out
+
+
+def SSIMFromBlocks(pix, ref, width, height, pix_stride, ref_stride):
+    """SSIMFromBlocks (ssim.go:103): SSIMFromStatsClipped of the blocks' DistoStats."""
+    return SSIMFromStats(DistoStatsOfBlocks(pix, ref, width, height, pix_stride, ref_stride), clipped=True)
