@@ -2,26 +2,43 @@
 // 8(a) A20): Phase A of encodeFrameParallel (internal/lossy/
 // encode_parallel.go:168-1495), methods 3-6 (method 3: plain quantisation instead of the trellis), for whole frames.
 //
-// Schedule: like decode.hip, one persistent launch; each 64-lane workgroup
-// dequeues a macroblock ROW (ordered counter over (row, image)) and walks it
-// left to right exactly as the reference's encodeRow does, with row y
-// allowed to start MB x once row y-1 has finished MB x+1 (:286-295).  The
-// shared top arrays of the reference (topY/U/V, topModes, topNz, topNzDC)
-// become one 48-byte record per MB column, handed down with sc1 stores +
-// a progress counter; the left context stays in LDS.
+// Schedule: one persistent launch.  A wave dequeues a
+// macroblock ROW from an ordered counter -- in the order of the row schedule
+// wg_encode_row_order leaves in the work buffer (textured frames' rows up to
+// mbh/4 rows early), always after the row above -- and walks it left to right
+// as the reference's encodeRow does.  Row y starts MB x once row y-1 has
+// finished MB x and waits for MB x+1 only at I4 step 3, the first read of the
+// top-right pixels (the reference waits for x+1 up front, :286-295; the
+// outputs are the same).  The shared top arrays (topY/U/V, topModes, topNz,
+// topNzDC) become one 48-byte record per MB column (64-B granule), handed
+// down with sc1 stores + a per-row progress counter; the left context stays
+// in LDS.  Two workgroup shapes:
+//   4-wave workgroups, one wave a row, sharing the cost tables in LDS (batch
+//   launches with more rows than twice the pair slots); and
+//   PAIR workgroups, two waves a row (launches with few rows, e.g. one
+//   frame): wave A imports, builds the context and runs the I4 RD; wave B
+//   runs the I16 RD, posts its score (A's early exit reads it), the UV RD, the
+//   I16 final residuals speculatively and the chroma residuals; one barrier
+//   joins them and A exports.
 //
 // Inside a macroblock the lanes take the reference's independent loops:
 //   I16 RD     lane = (mode, block): 4 x 16 blocks predicted, transformed,
 //              quantised, costed and reconstructed at once; contexts from the
-//              neighbours' nz (exchanged in LDS); one lane per mode runs the
-//              DC WHT path; per-mode sums reduced with lane shuffles
+//              neighbours' nz; one lane per mode runs the DC WHT path;
+//              per-mode sums by DPP reductions
 //   UV RD      lane = (mode, plane, block): 4 x 8 blocks
-//   I4 RD      the 16 blocks stay sequential (each predicts from its
-//              reconstructed neighbours); per block, lanes 0-9 pre-screen the
-//              10 modes, lanes 0..K-1 run the K trellis candidates at once
-//   final      I16 AC blocks trellis-quantised along the 7 block diagonals
-//              (each needs its left / top neighbour's nz), DC and chroma in
-//              parallel, then reconstruction and export
+//   I4 RD      the 16 blocks as a wavefront of 10 steps (block (bx, by) at
+//              step bx + 2 by; the two blocks of a step one per half-wave);
+//              per block lanes 0-9 pre-screen the 10 modes, the candidate
+//              pick is the reference's first-argmin on 32-bit keys, and the K
+//              candidates run in parallel: transform per lane, trellis prep
+//              per (candidate, position pair), the 16-step DP on a lane quad
+//              per candidate, reconstruction + TDisto one row per quad lane
+//   final      I16 AC blocks trellis-quantised speculatively, three rounds
+//              of one DP per (block, initial context it can still get), each
+//              followed by the reference's raster-order resolution of the
+//              actual contexts; DC and chroma in parallel; then
+//              reconstruction and export
 // All integer; bit-exact with the C restatement (oracle/lossy_rd.c).
 #include <cstdlib>
 #include <mutex>
