@@ -5,7 +5,7 @@
 //   k_sharp_init   import + gray Y, target W, target / initial chroma
 //                  residuals (convertSharp phase 1, :196-222): one thread per
 //                  2x2 block, fully parallel
-//   k_sharp_band   the iterative refinement (:224-264).  Each iteration sweeps
+//   k_sharp_wave   the iterative refinement (:224-264).  Each iteration sweeps
 //                  the row pairs in order and updates the chroma residuals in
 //                  place, so row pair j reads row pair j-1's values from the
 //                  SAME iteration (Gauss-Seidel): a sweep is sequential by
@@ -14,10 +14,11 @@
 //                  as a pipeline, each reading state k and writing state k+1
 //                  (five states per image, out of place), iteration k+1
 //                  trailing k by three row pairs behind progress counters
-//                  (published one step late, when every wave has drained its
-//                  stores); and an iteration's columns split into bands of
-//                  BAND that recompute a HALO on each side and meet their
-//                  neighbours once every HALO row pairs (see the kernel).
+//                  (published every WB_PUB row pairs, once the wave's stores
+//                  have drained); and an iteration's columns split into
+//                  one-wave bands of WB_OWN columns that recompute a WB_HALO
+//                  halo on each side and meet their neighbours once every
+//                  WB_HALO row pairs (see the kernel).
 //                  The early exit (:254-263) needs each iteration's global
 //                  |dY| sum; all four iterations run speculatively and
 //                  k_sharp_final picks the state the reference would stop at.
@@ -144,7 +145,7 @@ constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 // Hand-off loads / stores between the iteration workgroups: agent-scope
 // relaxed atomics, i.e. sc1 (write-through stores, L1-bypassing loads); every
 // load of handed-off bytes is one, every store of them too, and the progress
-// counter is stored after every wave's vmcnt(0) and a workgroup barrier
+// counter is stored after the wave's vmcnt(0)
 // (MI355X_MICROARCH.md, inter-workgroup visibility).
 __device__ __forceinline__ uint32_t ld_sc1(const void* p) {
   return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -152,49 +153,47 @@ __device__ __forceinline__ uint32_t ld_sc1(const void* p) {
 __device__ __forceinline__ void st_sc1(void* p, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint16_t ld_sc1_16(const void* p) {
-  return __hip_atomic_load(reinterpret_cast<const uint16_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void st_sc1_16(void* p, uint16_t v) {
   __hip_atomic_store(reinterpret_cast<uint16_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// phase 2: workgroup = (image, iteration, column band).  A refinement
-// iteration is a Gauss-Seidel sweep over the row pairs: row pair j reads the
-// chroma row j-1 updated by the SAME iteration (prev), so a sweep is
+// phase 2: workgroup = ONE WAVE = (image, iteration, column band).  A
+// refinement iteration is a Gauss-Seidel sweep over the row pairs: row pair j
+// reads the chroma row j-1 updated by the SAME iteration (prev), so a sweep is
 // sequential in j; but the update of UV column i reads prev only at columns
 // i-1..i+1, so a band of columns can run ahead of its neighbours by
-// recomputing a halo: with HALO extra columns on each side (computed but not
-// stored), the band's own columns stay exact for HALO row pairs after prev
-// was last taken from the neighbours, and every HALO row pairs the band
-// reloads its halo's prev row from the neighbour bands' output.  So one
-// image's iteration spreads over ceil(uvw / BAND) workgroups that meet once
-// every HALO row pairs.  Iteration k+1 trails iteration k (its input state)
-// by three row pairs behind per-band progress counters, as before; each
-// workgroup (thread = UV column) keeps its prev / cur / next chroma rows in
-// LDS.  Blocks are ordered (image, iteration, band), so every wait is on a
-// block dispatched earlier or on a neighbour of the same iteration, and a
-// launch holds only as many images as are resident at once.
-constexpr int BAND = 128, HALO = 32, BAND_T = BAND + 2 * HALO;  // threads per workgroup = columns incl. halo
-constexpr int PUB = 8;  // progress is published every PUB row pairs
-static_assert(HALO % PUB == 0, "resynchronisation rows must be published rows");
-constexpr int SLOTS = BAND_T + 2;                                // LDS row entries per channel (+1 each side)
+// recomputing a halo.  Iteration k+1 trails iteration k (its input state) by
+// three row pairs behind per-band progress counters.  Blocks are ordered
+// (image, iteration, band), so every wait is on a block dispatched earlier or
+// on a neighbour of the same iteration, and a launch holds only as many
+// images as are resident at once.
+//
+// Lane = UV column (WB_OWN own columns and WB_HALO halo columns each side), the prev / cur /
+// next chroma rows in registers and the neighbour columns by whole-wave DPP
+// shifts (wave_shr / wave_shl), so a step has no workgroup barrier and no
+// LDS row traffic -- only the gamma tables stay in LDS.  The band's edge
+// lanes read garbage neighbours, which eats one halo column per step (through
+// prev, the only row this iteration produces itself; cur / next / luma come
+// from the previous state in memory every step), so every WB_HALO row pairs
+// the halo lanes reload prev from the neighbour bands' published output.
+constexpr int WB_OWN = 32, WB_HALO = 16, WB_PUB = 16;
+static_assert(WB_OWN + 2 * WB_HALO == 64 && WB_HALO % WB_PUB == 0, "wave band layout");
+
+__device__ __forceinline__ int dpp_from_left(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false); }   // wave_shr:1: lane i <- i - 1
+__device__ __forceinline__ int dpp_from_right(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false); }  // wave_shl:1: lane i <- i + 1
 
 template <bool LUT>
-__global__ __launch_bounds__(BAND_T) void k_sharp_band(SharpArgs a, int nb) {
+__global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
   __shared__ SharpTabs t;
-  __shared__ int16_t rows[3][3][SLOTS];  // [prev / cur / next][channel][column - c_lo]
-  __shared__ unsigned long long part[(BAND_T + 63) / 64];
-  __shared__ int timed_out;
   const int blk = blockIdx.x, band = blk % nb, it = (blk / nb) & 3, img = blk / (4 * nb);
   if (img >= a.n_img) return;  // uniform over the block
   load_tabs(t, a.tabs);
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x;
   const int uvw = a.uvw, uvh = a.uvh, w = a.w, rs = a.uv_rs;
-  const int c_lo = band * BAND - HALO - 1;       // column of LDS slot 0
-  const int c = c_lo + 1 + tid;                  // this thread's UV column
+  const int c = band * WB_OWN - WB_HALO + lane;  // this lane's UV column
   const bool act = c >= 0 && c < uvw;
-  const bool interior = act && c >= band * BAND && c < (band + 1) * BAND;
+  const bool own = act && lane >= WB_HALO && lane < WB_HALO + WB_OWN;
+  const int cl = act ? c : 0;  // a valid column for address arithmetic
   const uint16_t* in_y = a.best_y + img * a.img_y + it * a.state_y;
   uint16_t* out_y = const_cast<uint16_t*>(in_y) + a.state_y;
   const int16_t* in_uv = a.best_uv + img * a.img_uv + it * a.state_uv;
@@ -203,19 +202,19 @@ __global__ __launch_bounds__(BAND_T) void k_sharp_band(SharpArgs a, int nb) {
   const int16_t* tuv = a.target_uv + img * a.img_uv;
   int* prog_img = a.prog + (int64_t)img * 4 * nb;  // [iteration][band]: row pairs finished
   int* prog_out = prog_img + it * nb + band;
-  if (tid == 0) timed_out = 0;
+  bool timed_out = false;  // wave-uniform
 
-  // thread 0: wait until band bb of iteration ii has finished `need` row
-  // pairs; returns the progress it saw (uvh for a band that does not exist)
+  // wait (the whole wave, on one wave-uniform address) until band bb of
+  // iteration ii has finished `need` row pairs; the progress seen (uvh for a band that does not exist)
   auto wait_for = [&](int ii, int bb, int need) -> int {
-    if (bb < 0 || bb >= nb) return uvh;
+    if (bb < 0 || bb >= nb || timed_out) return uvh;
     const int* p = prog_img + ii * nb + bb;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t k = 0;; k++) {
-      const int v = (int)ld_sc1(p);
+      const int v = __builtin_amdgcn_readfirstlane((int)ld_sc1(p));
       if (v >= need) return v;
       if ((k & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
-        timed_out = 1;
+        timed_out = true;
         return uvh;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -223,116 +222,101 @@ __global__ __launch_bounds__(BAND_T) void k_sharp_band(SharpArgs a, int nb) {
   };
   int seen_in = it == 0 ? uvh : 0;  // input state rows known ready (iteration it-1, bands band-1..band+1)
   auto wait_input = [&](int need) {
-    if (tid == 0 && seen_in < need && !timed_out) {
-      int s = uvh;
-      for (int d = -1; d <= 1; d++) s = min(s, wait_for(it - 1, band + d, need));
-      seen_in = s;
+    if (seen_in < need) {
+      int m = uvh;
+      for (int d = -1; d <= 1; d++) m = min(m, wait_for(it - 1, band + d, need));
+      seen_in = m;
     }
   };
-  // LDS slot s (column c_lo + s) of a chroma row of a state, for s = tid + 1 and
-  // the two edge slots 0 and SLOTS - 1 (loaded by threads 0 and 1)
-  auto load_row = [&](int16_t (*dst)[SLOTS], const int16_t* src_row) {
-    for (int s2 = tid; s2 < SLOTS; s2 += BAND_T) {
-      const int cc = c_lo + s2;
-      if (cc >= 0 && cc < uvw)
-        for (int ch = 0; ch < 3; ch++) dst[ch][s2] = (int16_t)ld_sc1_16(src_row + ch * uvw + cc);
-    }
+  // a chroma row of 3 int16 channels at this lane's column, from a state row.
+  // The loads are unconditional (clamped columns / rows) and keep the raw
+  // zero-extended halves: a load inside a branch, or one whose value is
+  // sign-extended right away, makes the compiler wait for it there, which
+  // would serialise the prefetch two row pairs ahead.
+  // 16-bit values travel as the aligned 32-bit word holding them (a 16-bit
+  // load's result gets masked right away, which again forces the wait):
+  // element e of a 4-byte-aligned state base is in word e >> 1, half e & 1.
+  // Rows are 16-byte aligned, so a channel's half depends only on the
+  // column and the channel (hs[ch]).  The other half may be a neighbour's
+  // value being stored concurrently: it is never used.
+  int hs[3];
+  for (int ch = 0; ch < 3; ch++) hs[ch] = 16 * ((ch * uvw + cl) & 1);
+  auto word = [](const int16_t* base, int64_t e) { return reinterpret_cast<const uint32_t*>(base) + (e >> 1); };
+  struct Row {
+    uint32_t v[3];
   };
-
-  uint64_t my_sum = 0;
-  int pi = 0, ci = 1, ni = 2;
-  const int sl = tid + 1;                                   // this column's LDS slot
-  const int pe = tid == 0 ? 0 : SLOTS - 1, ce = c_lo + pe;  // threads 0 / 1 also fetch the edge slots
-  // Input rows run two row pairs ahead of their use, so the load latency of
-  // the previous iteration's output never sits on a step: the luma pair and
-  // targets of row pair jp, and UV row `row` of the input state.
+  auto load_row = [&](int row) {
+    Row r;
+    const int64_t e0 = (int64_t)min(row, uvh - 1) * rs + cl;  // clamped: the last row pair's next is its cur
+    for (int ch = 0; ch < 3; ch++) r.v[ch] = ld_sc1(word(in_uv, e0 + ch * uvw));
+    return r;
+  };
   struct In {
-    uint32_t y[2], ty[2];
-    int16_t tuv[3];
+    uint32_t y[2], ty[2], tuv[3];
   };
   auto load_in = [&](int jp) {
-    In r = {{0, 0}, {0, 0}, {0, 0, 0}};
-    if (act && jp < uvh) {
-      const int64_t yo = (int64_t)(2 * jp) * w + 2 * c;
-      r.y[0] = ld_sc1(in_y + yo);
-      r.y[1] = ld_sc1(in_y + yo + w);
-      r.ty[0] = *reinterpret_cast<const uint32_t*>(ty + yo);
-      r.ty[1] = *reinterpret_cast<const uint32_t*>(ty + yo + w);
-      for (int ch = 0; ch < 3; ch++) r.tuv[ch] = tuv[(int64_t)jp * rs + ch * uvw + c];
-    }
+    In r;
+    const int jc = min(jp, uvh - 1);
+    const int64_t yo = (int64_t)(2 * jc) * w + 2 * cl;
+    r.y[0] = ld_sc1(in_y + yo);
+    r.y[1] = ld_sc1(in_y + yo + w);
+    r.ty[0] = *reinterpret_cast<const uint32_t*>(ty + yo);
+    r.ty[1] = *reinterpret_cast<const uint32_t*>(ty + yo + w);
+    for (int ch = 0; ch < 3; ch++) r.tuv[ch] = *word(tuv, (int64_t)jc * rs + ch * uvw + cl);
     return r;
   };
-  struct Pf {
-    int16_t v[3], e[3];  // slot sl; edge slot pe (threads 0 / 1)
-  };
-  auto load_pf = [&](int row) {
-    Pf r = {{0, 0, 0}, {0, 0, 0}};
-    if (row < uvh) {
-      const int16_t* src = in_uv + (int64_t)row * rs;
-      if (act)
-        for (int ch = 0; ch < 3; ch++) r.v[ch] = (int16_t)ld_sc1_16(src + ch * uvw + c);
-      if (tid < 2 && ce >= 0 && ce < uvw)
-        for (int ch = 0; ch < 3; ch++) r.e[ch] = (int16_t)ld_sc1_16(src + ch * uvw + ce);
-    }
-    return r;
-  };
-  // rows 0 and 1 of the input state: prev(row 0) = cur(row 0) = row 0; row 2
-  // and luma pairs 0, 1 in registers
-  wait_input(min(3, uvh));
-  __syncthreads();
-  load_row(rows[ci], in_uv);
-  load_row(rows[pi], in_uv);
-  load_row(rows[ni], uvh > 1 ? in_uv + rs : in_uv);
-  Pf pf_a = load_pf(2);
-  In in_cur = load_in(0), in_nxt = load_in(1);
-  for (int ju = 0; ju < uvh; ju++) {
-    wait_input(min(ju + 4, uvh));  // UV row ju + 3 and luma pair ju + 2 of the input state
-    const bool resync = ju > 0 && ju % HALO == 0;
-    if (resync && tid == 0 && !timed_out) {  // the neighbours' row ju - 1 of this iteration
+  // the signed 16-bit value of this column's channel ch in a loaded word
+  auto sx16 = [&](uint32_t v, int ch) { return (int)(int16_t)(uint16_t)(v >> hs[ch]); };
+
+  uint64_t my_sum = 0;
+  // rings of four row pairs, indexed by ju % 4 (compile-time after the
+  // unrolled loop below, so no register moves): the input state's chroma row
+  // and luma / target pair of row pairs ju .. ju + 3, prefetched three ahead
+  Row R[4];
+  In I[4];
+  wait_input(min(4, uvh));
+  R[0] = load_row(0);
+  R[1] = load_row(1);
+  R[2] = load_row(2);
+  I[0] = load_in(0);
+  I[1] = load_in(1);
+  I[2] = load_in(2);
+  Row P = R[0];  // prev(row 0) = cur(row 0)
+  auto step = [&](int ju, const Row& C, const Row& N, Row& pf_row, const In& in_cur, In& pf_in) {
+    wait_input(min(ju + 4, uvh));  // UV row ju + 3 and luma pair ju + 3 of the input state
+    if (ju > 0 && ju % WB_HALO == 0) {  // the halo lanes' prev: the neighbours' row ju - 1 of this iteration
       wait_for(it, band - 1, ju);
       wait_for(it, band + 1, ju);
+      if (act && !own)
+        for (int ch = 0; ch < 3; ch++) P.v[ch] = ld_sc1(word(out_uv, (int64_t)(ju - 1) * rs + ch * uvw + cl));
     }
-    __syncthreads();
-    if (resync && (sl < HALO + 1 || sl >= SLOTS - HALO - 1) && c < uvw && c >= 0)  // halo slots of prev
-      for (int ch = 0; ch < 3; ch++) rows[pi][ch][sl] = (int16_t)ld_sc1_16(out_uv + (int64_t)(ju - 1) * rs + ch * uvw + c);
-    if (resync && tid < 2) {  // slots 0 and SLOTS - 1
-      const int s2 = tid == 0 ? 0 : SLOTS - 1, cc = c_lo + s2;
-      if (cc >= 0 && cc < uvw)
-        for (int ch = 0; ch < 3; ch++) rows[pi][ch][s2] = (int16_t)ld_sc1_16(out_uv + (int64_t)(ju - 1) * rs + ch * uvw + cc);
-    }
-    if (resync) __syncthreads();
     const int j = 2 * ju;
-    const Pf pf_b = load_pf(ju + 3);
-    const In in_2 = load_in(ju + 2);
-    const uint32_t* ycur = in_cur.y;
-    const uint32_t* tycur = in_cur.ty;
-    const int16_t* tuvcur = in_cur.tuv;
-    int16_t upd[3] = {0, 0, 0};
+    pf_row = load_row(ju + 3);
+    pf_in = load_in(ju + 3);
+    int upd[3] = {0, 0, 0};
     uint32_t ynew[2] = {0, 0};
-    if (act) {
-      const int16_t (*P)[SLOTS] = rows[pi];
-      const int16_t (*C)[SLOTS] = rows[ci];
-      const int16_t (*N)[SLOTS] = rows[ni];
+    {
       // interpolateTwoRows (:322-359) for pixels x = 2c, 2c+1 of rows j, j+1
       int iv[2][2][3];
-      const uint32_t r0 = ycur[0], r1 = ycur[1];
+      const uint32_t r0 = in_cur.y[0], r1 = in_cur.y[1];
       const int by00 = r0 & 0xffff, by01 = r0 >> 16, by10 = r1 & 0xffff, by11 = r1 >> 16;
+#pragma unroll
       for (int ch = 0; ch < 3; ch++) {
-        const int a1 = C[ch][sl], b1 = P[ch][sl], n1 = N[ch][sl];
+        const int a1 = sx16(C.v[ch], ch), b1 = sx16(P.v[ch], ch), n1 = sx16(N.v[ch], ch);
+        const int a0 = dpp_from_left(a1), b0 = dpp_from_left(b1), n0 = dpp_from_left(n1);
+        const int a2 = dpp_from_right(a1), b2 = dpp_from_right(b1), n2 = dpp_from_right(n1);
         int e0, e1, f0, f1;  // x = 2c: row j / j+1
         if (c == 0) {
-          e0 = ((a1 * 3 + b1 + 2) >> 2);  // filter2(cur[0], prev[0])
-          f0 = ((a1 * 3 + n1 + 2) >> 2);
+          e0 = (a1 * 3 + b1 + 2) >> 2;  // filter2(cur[0], prev[0])
+          f0 = (a1 * 3 + n1 + 2) >> 2;
         } else {
-          const int a0 = C[ch][sl - 1], b0 = P[ch][sl - 1], n0 = N[ch][sl - 1];
           e0 = (a1 * 9 + a0 * 3 + b1 * 3 + b0 + 8) >> 4;
           f0 = (a1 * 9 + a0 * 3 + n1 * 3 + n0 + 8) >> 4;
         }
         if (c == uvw - 1) {  // x = w-1: filter2(cur[uvw-1], prev[uvw-1])
-          e1 = ((a1 * 3 + b1 + 2) >> 2);
-          f1 = ((a1 * 3 + n1 + 2) >> 2);
+          e1 = (a1 * 3 + b1 + 2) >> 2;
+          f1 = (a1 * 3 + n1 + 2) >> 2;
         } else {
-          const int a2 = C[ch][sl + 1], b2 = P[ch][sl + 1], n2 = N[ch][sl + 1];
           e1 = (a1 * 9 + a2 * 3 + b1 * 3 + b2 + 8) >> 4;
           f1 = (a1 * 9 + a2 * 3 + n1 * 3 + n2 + 8) >> 4;
         }
@@ -344,76 +328,66 @@ __global__ __launch_bounds__(BAND_T) void k_sharp_band(SharpArgs a, int nb) {
       // updateW -> bestRGBY, sharpYUVUpdateY (:361-381)
       uint32_t lin[2][2][3];
       int yv[2][2];
+#pragma unroll
       for (int r = 0; r < 2; r++)
+#pragma unroll
         for (int cc = 0; cc < 2; cc++) {
+#pragma unroll
           for (int ch = 0; ch < 3; ch++) lin[r][cc][ch] = to_linear(t.g2l, iv[r][cc][ch]);
           yv[r][cc] = from_lin<LUT>(t.l2g, a.lut, a.lut_n, (uint32_t)gray(lin[r][cc][0], lin[r][cc][1], lin[r][cc][2]));
         }
       const int byv[2][2] = {{by00, by01}, {by10, by11}};
       int ny[2][2];
+#pragma unroll
       for (int r = 0; r < 2; r++)
+#pragma unroll
         for (int cc = 0; cc < 2; cc++) {
-          const int d = (int)((tycur[r] >> (16 * cc)) & 0xffff) - yv[r][cc];
+          const int d = (int)((in_cur.ty[r] >> (16 * cc)) & 0xffff) - yv[r][cc];
           ny[r][cc] = clip_bd(byv[r][cc] + d);
-          if (interior) my_sum += (uint64_t)(d < 0 ? -d : d);
+          if (own) my_sum += (uint64_t)(d < 0 ? -d : d);
         }
       ynew[0] = (uint32_t)ny[0][0] | (uint32_t)ny[0][1] << 16;
       ynew[1] = (uint32_t)ny[1][0] | (uint32_t)ny[1][1] << 16;
       // updateChroma -> bestRGBUV, sharpYUVUpdateRGB (:383-388)
       int rgbv[3];
+#pragma unroll
       for (int ch = 0; ch < 3; ch++)
         rgbv[ch] = from_lin<LUT>(t.l2g, a.lut, a.lut_n, (lin[0][0][ch] + lin[0][1][ch] + lin[1][0][ch] + lin[1][1][ch] + 2) >> 2);
       const int gv = gray(rgbv[0], rgbv[1], rgbv[2]);
+#pragma unroll
       for (int ch = 0; ch < 3; ch++) {
         const int16_t srcv = (int16_t)(rgbv[ch] - gv);
-        const int16_t d = (int16_t)(tuvcur[ch] - srcv);
-        upd[ch] = (int16_t)(C[ch][sl] + d);
+        const int16_t d = (int16_t)(sx16(in_cur.tuv[ch], ch) - srcv);
+        upd[ch] = (int16_t)(sx16(C.v[ch], ch) + d);
       }
     }
-    __syncthreads();  // every read of P/C/N for this step is done
-    // rotate: prev <- updated cur (into the old prev slot), cur <- next,
-    // next <- row ju + 2 (loaded a step ago; on the last row pair, a copy of cur)
-    const bool have_nn = ju + 2 < uvh;
-    const int npi = pi, nci = ni, nni = ci;
-    if (act)
-      for (int ch = 0; ch < 3; ch++) rows[npi][ch][sl] = upd[ch];
-    for (int ch = 0; ch < 3; ch++) {
-      rows[nni][ch][sl] = have_nn ? pf_a.v[ch] : rows[nci][ch][sl];
-      if (tid < 2) rows[nni][ch][pe] = have_nn ? pf_a.e[ch] : rows[nci][ch][pe];
-    }
-    pf_a = pf_b;
-    in_cur = in_nxt;
-    in_nxt = in_2;
-    pi = npi;
-    ci = nci;
-    ni = nni;
-    __syncthreads();
     // publish this band's own columns of the updated UV row ju and luma pair (write-through)
-    if (interior) {
+    if (own) {
       for (int ch = 0; ch < 3; ch++) st_sc1_16(out_uv + (int64_t)ju * rs + ch * uvw + c, (uint16_t)upd[ch]);
       st_sc1(out_y + (int64_t)j * w + 2 * c, ynew[0]);
       st_sc1(out_y + (int64_t)(j + 1) * w + 2 * c, ynew[1]);
     }
-    if ((ju + 1) % PUB == 0 || ju + 1 == uvh) {
-      // publish row pairs <= ju once every wave drained its stores of them.
-      // Every PUB row pairs only: a drain also waits for the loads in flight
-      // (vmcnt counts both), so per row pair it would put a memory round
-      // trip on every step.  HALO is a multiple of PUB, so the neighbours'
-      // resynchronisation on row ju (at the next step) finds it published.
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) P.v[ch] = (uint32_t)(uint16_t)upd[ch] << hs[ch];  // prev <- the updated cur (in its half)
+    if ((ju + 1) % WB_PUB == 0 || ju + 1 == uvh) {
+      // publish row pairs <= ju once this wave's stores of them are done (a
+      // drain also waits for the loads in flight, so only every WB_PUB steps)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) st_sc1(prog_out, (uint32_t)(ju + 1));
+      if (lane == 0) st_sc1(prog_out, (uint32_t)(ju + 1));
+    }
+  };
+  for (int j0 = 0; j0 < uvh; j0 += 4) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (j0 + k >= uvh) break;  // wave-uniform
+      step(j0 + k, R[k], R[(k + 1) & 3], R[(k + 3) & 3], I[k], I[(k + 3) & 3]);
     }
   }
   // the band's share of the iteration's |dY| sum (:254-263); k_sharp_final applies the exit rule
   unsigned long long sm = my_sum;
   for (int off = 32; off > 0; off >>= 1) sm += __shfl_down(sm, off, 64);
-  if ((tid & 63) == 0) part[tid >> 6] = sm;
-  __syncthreads();
-  if (tid == 0) {
-    uint64_t sum = 0;
-    for (int k = 0; k < (BAND_T + 63) / 64; k++) sum += part[k];
-    atomicAdd(reinterpret_cast<unsigned long long*>(a.sums + img * 4 + it), (unsigned long long)sum);
+  if (lane == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.sums + img * 4 + it), sm);
     if (timed_out) a.iters[img] = -1;
   }
 }
@@ -535,17 +509,18 @@ SharpLayout sharp_layout(int width, int height) {
   L.bytes_img = 2 * (L.img_y + L.img_uv);
   return L;
 }
-// column bands of one refinement iteration (k_sharp_band)
+// one-wave column bands of one refinement iteration (k_sharp_wave)
 int sharp_bands(int width) {
   const int uvw = ((width + 1) & ~1) / 2;
-  return (uvw + BAND - 1) / BAND;
+  return (uvw + WB_OWN - 1) / WB_OWN;
 }
 }  // namespace
 
 extern "C" size_t wg_sharpyuv_work_bytes(int32_t width, int32_t height, int32_t n_images) {
   if (width <= 0 || height <= 0 || n_images <= 0) return 0;
   const SharpLayout L = sharp_layout(width, height);
-  return n_images * L.bytes_img + (size_t)n_images * (4 * 8 + 4 + 4 * 4 * sharp_bands(width)) + 16;
+  const int nb = sharp_bands(width);
+  return n_images * L.bytes_img + (size_t)n_images * (4 * 8 + 4 + 4 * 4 * nb) + 16;
 }
 
 extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t height, int32_t rgb_stride,
@@ -632,7 +607,8 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
   // images as the device holds at once (4 iterations x nb bands each)
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sharp_band<false>, BAND_T, 0) != hipSuccess || per_cu <= 0)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sharp_wave<false>, 64, 0) != hipSuccess ||
+      per_cu <= 0)
     return wg::check_launch("sharpyuv occupancy");
   const int chunk = std::max(1, per_cu * cus / (4 * nb));  // images per launch
   if (4 * nb > per_cu * cus) return wg::invalid("sharpyuv: image too wide for one device's resident workgroups");
@@ -648,10 +624,10 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
     c.iters += i0;
     const unsigned grid = (unsigned)(c.n_img * 4 * nb);
     if (lut)
-      hipLaunchKernelGGL(k_sharp_band<true>, dim3(grid), dim3(BAND_T), 0, s, c, nb);
+      hipLaunchKernelGGL(k_sharp_wave<true>, dim3(grid), dim3(64), 0, s, c, nb);
     else
-      hipLaunchKernelGGL(k_sharp_band<false>, dim3(grid), dim3(BAND_T), 0, s, c, nb);
-    rc = wg::check_launch("k_sharp_band");
+      hipLaunchKernelGGL(k_sharp_wave<false>, dim3(grid), dim3(64), 0, s, c, nb);
+    rc = wg::check_launch("k_sharp_wave");
     if (rc != WG_OK) return rc;
   }
   FinalArgs f;

@@ -5,10 +5,11 @@
 // SSIMGet since N = 256 there).
 //
 // A 16x16 tile of pixels per 256-thread workgroup; the 22x22 source tiles
-// (3-pixel halo) of both planes are staged in LDS.  Window statistics are
-// exact integers (any summation order), the per-pixel SSIM is the same
-// float64 expression as the reference; the plane sum is a per-tile partial
-// plus a second deterministic pass.
+// (3-pixel halo) of both planes are staged in LDS, and the window sums are
+// separable (a horizontal, then a vertical 7-tap hat pass).  Window
+// statistics are exact integers (any summation order), the per-pixel SSIM is
+// the same float64 expression as the reference; the plane sum is a per-tile
+// partial plus a second deterministic pass.
 #include "wg_common.h"
 #include "wg_dsp.h"
 
@@ -27,6 +28,7 @@ struct SsimArgs {
 
 __global__ __launch_bounds__(256) void k_plane_ssim(const SsimArgs p) {
   __shared__ uint8_t ta[TS * TS], tb[TS * TS];
+  __shared__ uint32_t hs[5][TS][TILE];  // horizontal 7-tap hat sums of x, y, xx, xy, yy per (row, output column)
   __shared__ double red[4];
   const int tiles = p.tiles_x * p.tiles_y;
   const int img = blockIdx.x / tiles;
@@ -41,29 +43,53 @@ __global__ __launch_bounds__(256) void k_plane_ssim(const SsimArgs p) {
     tb[i] = in ? B[(int64_t)yy * p.b_stride + xx] : 0;
   }
   __syncthreads();
+  // The hat weights are separable (kw[dx] * kw[dy]) and pixels outside the
+  // image are staged as 0, so a clipped window's sums are a 7-tap horizontal
+  // pass followed by a 7-tap vertical one, and its weight is the product of
+  // the in-image tap sums: the same integers as the 49-term window of
+  // SSIMGetClipped (ssim.go:132-160), at 5 x (7 + 7 x 22/16) MACs per pixel
+  // instead of 6 x 49.
+  constexpr uint32_t kw[7] = {1, 2, 3, 4, 3, 2, 1};
+  for (int i = threadIdx.x; i < TS * TILE; i += blockDim.x) {
+    const int r = i / TILE, cx = i % TILE;
+    const uint8_t* pa = ta + r * TS + cx;
+    const uint8_t* pb = tb + r * TS + cx;
+    uint32_t sx = 0, sy = 0, sxx = 0, sxy = 0, syy = 0;
+#pragma unroll
+    for (int dx = 0; dx < 7; dx++) {
+      const uint32_t x = pa[dx], y = pb[dx], wx = kw[dx] * x, wy = kw[dx] * y;
+      sx += wx;
+      sy += wy;
+      sxx += wx * x;
+      sxy += wx * y;
+      syy += wy * y;
+    }
+    hs[0][r][cx] = sx;
+    hs[1][r][cx] = sy;
+    hs[2][r][cx] = sxx;
+    hs[3][r][cx] = sxy;
+    hs[4][r][cx] = syy;
+  }
+  __syncthreads();
   const int lx = threadIdx.x % TILE, ly = threadIdx.x / TILE;
   const int xo = tx0 + lx, yo = ty0 + ly;
   double v = 0.0;
   if (xo < p.w && yo < p.h) {
-    const uint32_t kw[7] = {1, 2, 3, 4, 3, 2, 1};
     SsimStats s = {0, 0, 0, 0, 0, 0};
-    for (int dy = 0; dy < 7; dy++) {
-      const int yy = yo - 3 + dy;
-      if (yy < 0 || yy >= p.h) continue;
-      for (int dx = 0; dx < 7; dx++) {
-        const int xx = xo - 3 + dx;
-        if (xx < 0 || xx >= p.w) continue;
-        const uint32_t wt = kw[dx] * kw[dy];
-        const int li = (ly + dy) * TS + lx + dx;
-        const uint32_t x = ta[li], y = tb[li];
-        s.w += wt;
-        s.xm += wt * x;
-        s.ym += wt * y;
-        s.xxm += wt * x * x;
-        s.xym += wt * x * y;
-        s.yym += wt * y * y;
-      }
+    uint32_t wxs = 0, wys = 0;
+#pragma unroll
+    for (int d = 0; d < 7; d++) {
+      const uint32_t k = kw[d];
+      s.xm += k * hs[0][ly + d][lx];
+      s.ym += k * hs[1][ly + d][lx];
+      s.xxm += k * hs[2][ly + d][lx];
+      s.xym += k * hs[3][ly + d][lx];
+      s.yym += k * hs[4][ly + d][lx];
+      const int xx = xo - 3 + d, yy = yo - 3 + d;
+      wxs += (xx >= 0 && xx < p.w) ? k : 0u;
+      wys += (yy >= 0 && yy < p.h) ? k : 0u;
     }
+    s.w = wxs * wys;
     v = ssim_calc(s, s.w);  // SSIMFromStatsClipped; s.w == 256 for interior windows
   }
   // block reduction (fixed order -> deterministic)
