@@ -372,7 +372,7 @@ __device__ __forceinline__ int quad_bcast32(int v) {
 template <int FIRST, int CTX_TYPE>
 __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int* l0s, int init_ctx, int lam16,
                                             int k, int16_t* q, int* nz) {
-  constexpr int64_t BIG = 1ll << 59, VALID = 1ll << 58;
+  constexpr int64_t BIG = 1ll << 59;
   init_ctx = min(init_ctx, 2);
   const int e = min(k, 2);
   const int psh = e == 0 ? 0 : 1;  // index -> predecessor context shift; also the level-code offset
@@ -430,7 +430,9 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
     // terminal (EOB after this position) of context tctx
     const int64_t tps = tctx == 2 ? ps2 : ps1;
     const int64_t eobs = tps + (n < 15 ? (int64_t)eob_n * lam16 : 0);
-    const bool w = tps < VALID && eobs < best_terminal;
+    // (an invalid state, >= 2^59, never beats best_terminal, which starts at a
+    // valid EOB cost below 2^51 and only decreases: no separate validity test)
+    const bool w = eobs < best_terminal;
     best_terminal = w ? eobs : best_terminal;
     best_n = w ? n : best_n;
     best_h = w ? (tctx == 2 ? h2 : h1) : best_h;
