@@ -38,7 +38,8 @@ __device__ __forceinline__ uint32_t add_pixels(uint32_t a, uint32_t b) {
   const uint32_t rb = (a & 0x00ff00ffu) + (b & 0x00ff00ffu);
   return (ag & 0xff00ff00u) | (rb & 0x00ff00ffu);
 }
-__device__ __forceinline__ uint32_t avg2(uint32_t a, uint32_t b) { return (((a ^ b) & 0xfefefefeu) >> 1) + (a & b); }
+// per-byte floor((a + b) / 2): v_lerp_u8 with no rounding bits
+__device__ __forceinline__ uint32_t avg2(uint32_t a, uint32_t b) { return __builtin_amdgcn_lerp(a, b, 0u); }
 __device__ __forceinline__ int chan(uint32_t v, int s) { return (int)((v >> s) & 0xff); }
 // Select (encode_predictor.go:49-95): sum over channels of |l - tl| minus
 // that of |t - tl|, as two v_sad_u8 (sum of absolute byte differences)
@@ -49,32 +50,29 @@ __device__ __forceinline__ uint32_t select_pred(uint32_t l, uint32_t t, uint32_t
 // The clamped predictors on two 16-bit lanes at a time (bytes 0, 2 and bytes
 // 1, 3 of the pixel); every intermediate fits int16.
 typedef short v2i16 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ v2i16 lanes16(uint32_t x) {
-  v2i16 r;
-  r.x = (short)(x & 0xff);
-  r.y = (short)((x >> 16) & 0xff);
-  return r;
-}
-__device__ __forceinline__ uint32_t pack16(v2i16 v) { return (uint32_t)(uint16_t)v.x | (uint32_t)(uint16_t)v.y << 16; }
+// bytes 0, 2 (lo) / 1, 3 (hi) of a pixel as two 16-bit lanes, and back (v_perm_b32)
+__device__ __forceinline__ v2i16 as_v2(uint32_t x) { return __builtin_bit_cast(v2i16, x); }
+__device__ __forceinline__ uint32_t as_u(v2i16 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ v2i16 lanes_lo(uint32_t x) { return as_v2(__builtin_amdgcn_perm(0u, x, 0x0c020c00u)); }
+__device__ __forceinline__ v2i16 lanes_hi(uint32_t x) { return as_v2(__builtin_amdgcn_perm(0u, x, 0x0c030c01u)); }
+__device__ __forceinline__ uint32_t pack_lanes(v2i16 lo, v2i16 hi) { return __builtin_amdgcn_perm(as_u(hi), as_u(lo), 0x06020400u); }
 __device__ __forceinline__ v2i16 clamp255(v2i16 v) {
   const v2i16 zero = {0, 0}, top = {255, 255};
   return __builtin_elementwise_min(__builtin_elementwise_max(v, zero), top);
 }
 __device__ __forceinline__ uint32_t clamp_add_sub_full(uint32_t a, uint32_t b, uint32_t c) {
-  const v2i16 lo = clamp255(lanes16(a) + lanes16(b) - lanes16(c));                // bytes 0, 2
-  const v2i16 hi = clamp255(lanes16(a >> 8) + lanes16(b >> 8) - lanes16(c >> 8));  // bytes 1, 3
-  return pack16(lo) | pack16(hi) << 8;
+  const v2i16 lo = clamp255(lanes_lo(a) + lanes_lo(b) - lanes_lo(c));  // bytes 0, 2
+  const v2i16 hi = clamp255(lanes_hi(a) + lanes_hi(b) - lanes_hi(c));  // bytes 1, 3
+  return pack_lanes(lo, hi);
 }
 __device__ __forceinline__ v2i16 half_step(v2i16 va, v2i16 vc) {
   const v2i16 d = va - vc;
-  // d / 2 truncating toward zero, as Go's '/': add 1 to negative d before the arithmetic shift
-  const v2i16 neg = {(short)(d.x < 0), (short)(d.y < 0)};
+  // d / 2 truncating toward zero, as Go's '/': add the sign bit to d before the arithmetic shift
+  const v2i16 neg = as_v2(as_u(d) >> 15 & 0x00010001u);
   return clamp255(va + ((d + neg) >> (v2i16){1, 1}));
 }
 __device__ __forceinline__ uint32_t clamp_add_sub_half(uint32_t avg, uint32_t c) {
-  const v2i16 lo = half_step(lanes16(avg), lanes16(c));
-  const v2i16 hi = half_step(lanes16(avg >> 8), lanes16(c >> 8));
-  return pack16(lo) | pack16(hi) << 8;
+  return pack_lanes(half_step(lanes_lo(avg), lanes_lo(c)), half_step(lanes_hi(avg), lanes_hi(c)));
 }
 // predictPixel (encode_predictor.go:148-180); the decoder's switch
 // (decode_transform.go:257-350) computes the same predictors.
@@ -123,6 +121,69 @@ __device__ __forceinline__ uint32_t predict_lanes(int mode, uint32_t l, uint32_t
   else if (mode == 12) p = clamp_add_sub_full(l, t, tl);
   else if (mode == 13) p = clamp_add_sub_half(avg, tl);
   return p;
+}
+
+// The inverse walk's predictor as one branch-free stream: every candidate
+// the modes share is formed once and a per-pixel control word (kPredCtl,
+// staged per chunk) picks among them with bit masks -- no lane-varying switch,
+// no compare-to-mask hazards.  Modes 1-10 and 13's inner average are
+// avg2(P, Q) with P in {L, T, TR, TL, avg2(L, TR), avg2(L, TL)} and Q in
+// {L, T, TR, TL, avg2(T, TR)} (avg2(X, X) = X); 11 / 12 / 13 / black override.
+enum : uint32_t {
+  C_PAVG = 1u << 0,   // P = avg2(L, R1)
+  C_PL = 1u << 1,     // P = L (else Pc)
+  C_PC_TR = 1u << 2,  // Pc = TR (else T)
+  C_PC_TL = 1u << 3,  // Pc = TL
+  C_R1_TL = 1u << 4,  // R1 = TL (else TR)
+  C_QL = 1u << 5,     // Q = L (else Qc)
+  C_Q6 = 1u << 6,     // Qc: 0 T, C_Q6 TR, C_Q7 TL, both avg2(T, TR)
+  C_Q7 = 1u << 7,
+  C_SEL = 1u << 8,    // Select (11)
+  C_CF = 1u << 9,     // ClampAddSubtractFull (12)
+  C_CH = 1u << 10,    // ClampAddSubtractHalf (13) of avg2(L, T)
+  C_BLACK = 1u << 11, // 0, 14, 15
+  C_EDGE = 1u << 12,  // x = width - 1: TR is this row's first pixel
+};
+constexpr uint32_t kPredCtl[16] = {
+    C_BLACK,                          // 0
+    C_PL | C_QL,                      // 1 L
+    0,                                // 2 T
+    C_PC_TR | C_Q6,                   // 3 TR
+    C_PC_TL | C_Q7,                   // 4 TL
+    C_PAVG,                           // 5 avg2(avg2(L, TR), T)
+    C_PL | C_Q7,                      // 6 avg2(L, TL)
+    C_PL,                             // 7 avg2(L, T)
+    C_PC_TL,                          // 8 avg2(TL, T)
+    C_Q6,                             // 9 avg2(T, TR)
+    C_PAVG | C_R1_TL | C_Q6 | C_Q7,   // 10 avg2(avg2(L, TL), avg2(T, TR))
+    C_SEL,                            // 11
+    C_CF,                             // 12
+    C_CH | C_PL,                      // 13 (avg2(L, T) first)
+    C_BLACK, C_BLACK};
+// bit `bit` of c set ? a : b, through a sign-extended bit mask (v_bfe_i32 + v_bfi_b32)
+// (v_bfi_b32 written out: the compiler turns the mask form back into
+// compare + v_cndmask pairs, with VCC hazard nops between them)
+template <int BIT>
+__device__ __forceinline__ uint32_t bsel(uint32_t c, uint32_t a, uint32_t b) {
+  const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)c, BIT, 1);
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t predict_ctl(uint32_t c, uint32_t l, uint32_t t, uint32_t tr, uint32_t tl) {
+  // what does not depend on L (the walk's serial input) first
+  const uint32_t pc = bsel<3>(c, tl, bsel<2>(c, tr, t));
+  const uint32_t r1 = bsel<4>(c, tl, tr);
+  const uint32_t qc = bsel<7>(c, bsel<6>(c, avg2(t, tr), tl), bsel<6>(c, tr, t));
+  const int sad_t = (int)__builtin_amdgcn_sad_u8(t, tl, 0u);
+  const uint32_t q = bsel<5>(c, l, qc);
+  const uint32_t p = bsel<0>(c, avg2(l, r1), bsel<1>(c, l, pc));
+  const uint32_t pavg = avg2(p, q);
+  const int pa = (int)__builtin_amdgcn_sad_u8(l, tl, 0u) - sad_t;
+  uint32_t r = bsel<8>(c, pa <= 0 ? t : l, pavg);
+  r = bsel<9>(c, clamp_add_sub_full(l, t, tl), r);
+  r = bsel<10>(c, clamp_add_sub_half(pavg, tl), r);
+  return bsel<11>(c, ARGB_BLACK, r);
 }
 
 // Go math.Log / math.Log2 (src/math/log.go, log10.go) for counts beyond the
@@ -312,7 +373,9 @@ constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
 
 __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
   __shared__ int sh_band;
+  __shared__ uint32_t ctab[19];  // kPredCtl, then the border rules: 16 x = 0 (T), 17 x = 0 on row 0 (black), 18 row 0 (L)
   const int lane = threadIdx.x;
+  if (lane < 19) ctab[lane] = lane < 16 ? kPredCtl[lane] : (lane == 16 ? kPredCtl[2] : (lane == 17 ? kPredCtl[0] : kPredCtl[1]));
   const int w = a.width;
   const int total = a.bands * a.n_img;
   for (;;) {
@@ -389,7 +452,16 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
     load_chunk(0, rc, mc);
     issue_up(0, ug);
     for (int s0 = 0; s0 < steps; s0 += 16) {
-      uint32_t rn[16], mn[16], ov[16];
+      uint32_t rn[16], mn[16], ov[16], cc[16];
+      // the chunk's control words (the tile modes arrived a chunk ago), with
+      // the reference's border rules: row 0 L (black at x = 0), column 0 T,
+      // TR past the right edge is this row's first pixel
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const int x = s0 + u - 2 * lane;
+        const int idx = x == 0 ? (y == 0 ? 17 : 16) : (y == 0 ? 18 : (int)((mc[u] >> 8) & 0xf));
+        cc[u] = ctab[idx] | (x == w - 1 ? (uint32_t)C_EDGE : 0u);
+      }
       take_up(s0, ug, uc);
       load_chunk(s0 + 16, rn, mn);
 #pragma unroll
@@ -401,12 +473,8 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
         const uint32_t up_x1 = (uint32_t)__builtin_amdgcn_update_dpp((int)uc[u + 2], (int)o1, 0x138, 0xf, 0xf, false);
         const uint32_t up_x = (uint32_t)__builtin_amdgcn_update_dpp((int)uc[u + 1], (int)o2, 0x138, 0xf, 0xf, false);
         const uint32_t up_xm1 = (uint32_t)__builtin_amdgcn_update_dpp((int)uc[u], (int)o3, 0x138, 0xf, 0xf, false);
-        // the reference's border rules as modes: row 0 L (black at x = 0),
-        // column 0 T; TR past the right edge is this row's first pixel
-        int mode = (int)((mc[u] >> 8) & 0xf);
-        mode = x == 0 ? (y == 0 ? 0 : 2) : (y == 0 ? 1 : mode);
-        const uint32_t tr = x < w - 1 ? up_x1 : first;
-        const uint32_t v = add_pixels(rc[u], predict_lanes(mode, o1, up_x, tr, up_xm1));
+        const uint32_t tr = bsel<12>(cc[u], first, up_x1);
+        const uint32_t v = add_pixels(rc[u], predict_ctl(cc[u], o1, up_x, tr, up_xm1));
         const bool valid = live && x >= 0 && x < w;
         if (hands_off && valid) __hip_atomic_store(hand_mine + x, 1ull << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         first = x == 0 ? v : first;
