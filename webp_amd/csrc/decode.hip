@@ -70,6 +70,12 @@ __device__ __forceinline__ void st_sc1_64(uint8_t* p, uint64_t v) {
 __device__ __forceinline__ void st_sc1_32(uint8_t* p, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// one 16-B write-through store (a bottom-row record leaves as 8 x 16 B, one 128-B line)
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_sc1_128(uint8_t* p, uint4 w) {
+  const u32x4_t v = {w.x, w.y, w.z, w.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
 // Coefficients are read exactly once: non-temporal loads, so the stream
 // (2 B / coefficient, the kernel's largest input) does not push the frame's
 // partly written output lines out of L2 before their other pieces arrive.
@@ -96,6 +102,7 @@ struct DecArgs {
   uint8_t* U;
   uint8_t* V;
   uint8_t* top;   // [n_img][mbw][TOP_BYTES]
+  uint8_t* bot;   // [n_img][mbw][BOT_BYTES] (k_decode_split): final rows 12..15 of a band's last row, for the next band
   int* progress;  // [n_img][mbh]: macroblocks completed (reconstructed + filtered + stored)
   int* ctl;       // [0] row dequeue counter, [1] error flag (wait timeout)
   int* diag;      // wg::diag_words + DIAG_DECODE
@@ -936,6 +943,8 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
       uint8_t* const fv = fu + 12 * FC_STRIDE;
       int* prog_above = progress_f + (int64_t)img * mbh + mby - 1;
       int* prog_mine = progress_f + (int64_t)img * mbh + mby;
+      uint8_t* const bot_img = a.bot + (int64_t)img * mbw * BOT_BYTES;
+      const bool hand = !to_lds && mby < mbh - 1;  // a band's last row with a band below
       uint8_t* Yp = a.Y + (int64_t)img * ys * 16 * mbh;
       uint8_t* Up = a.U + (int64_t)img * uvs * 8 * mbh;
       uint8_t* Vp = a.V + (int64_t)img * uvs * 8 * mbh;
@@ -1004,19 +1013,17 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
             const int rr = lane - 44;
             *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = lds64(bt + 96 + 8 * rr);
           }
-        } else if (mby > 0) {
+        } else if (mby > 0) {  // across bands: the record the band above's last row left (same layout as bot_ring)
+          const uint8_t* rec = bot_img + mbx * BOT_BYTES;
           if (lane >= 52 && lane < 60) {
             const int k = lane - 52, rr = k >> 1, half = k & 1;
-            *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) =
-                ld_sc1_64(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half);
+            *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = ld_sc1_64(rec + 16 * rr + 8 * half);
           } else if (lane >= 60) {
             const int rr = lane - 60;
-            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) =
-                ld_sc1_64(Up + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
+            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) = ld_sc1_64(rec + 64 + 8 * rr);
           } else if (lane >= 44 && lane < 48) {
             const int rr = lane - 44;
-            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) =
-                ld_sc1_64(Vp + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
+            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = ld_sc1_64(rec + 96 + 8 * rr);
           }
         }
         const uint32_t w7 = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(info_ring[r][mslot])[7]);
@@ -1055,29 +1062,28 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         }
         STAMP(9);
         lane = opaque_lane() & 63;
-        // ---- stores (as k_decode_bands) ----
-        // A band's last row first stores the rows the next band reads (MB
-        // x - 1's bottom rows, final after this MB's left-edge filter) and
-        // publishes; the other frame rows are outputs only and follow.
-        if (!to_lds) {
-          const int which = lane >> 5, k = lane & 31, x = mbx - 1 + which;
-          if (which == 0 ? mbx > 0 : mbx == mbw - 1) {
+        // ---- stores ----
+        // A band's last row first hands the next band MB x - 1's bottom rows
+        // 12..15 (final after this MB's left-edge filter; at the row's end this
+        // MB's too) as one 128-B write-through record per MB, and publishes.
+        // Every frame byte is then stored once, by the wave that finalises
+        // it, with plain (write-back) stores that L2 merges into whole lines:
+        // rows 13..15 are the next band's to store after its top-edge filter.
+        if (hand) {
+          const int which = lane >> 3, k = lane & 7, x = mbx - 1 + which;
+          if (lane < 16 && (which == 0 ? mbx > 0 : mbx == mbw - 1)) {
+            uint4 w;
             if (k < 4) {
-              const int j = 12 + k;
-              const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
-              uint8_t* dst = Yp + (int64_t)(16 * mby + j) * ys + 16 * x;
-              st_sc1_64(dst, (uint64_t)w.y << 32 | w.x);
-              st_sc1_64(dst + 8, (uint64_t)w.w << 32 | w.z);
-            } else if (k < 12) {
-              const int pl = k >= 8, j = 4 + (k & 3);
-              st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x,
-                        lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
+              w = *reinterpret_cast<const uint4*>(fy + (16 + k) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
+            } else {  // U rows 4,5 | 6,7, V rows 4,5 | 6,7
+              const uint8_t* src = ((k >= 6) ? fv : fu) + (8 + 2 * (k & 1)) * FC_STRIDE + FC_X0 + 8 * (x - mbx);
+              const uint64_t a0 = lds64(src), a1 = lds64(src + FC_STRIDE);
+              w = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
             }
+            st_sc1_128(bot_img + x * BOT_BYTES + 16 * k, w);
           }
-          if (mby < mbh - 1) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows are out before the flag
-            if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record is out before the flag
+          if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         {
           const bool last = mbx == mbw - 1;
@@ -1097,7 +1103,10 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
             c0 = mbx - 4;
             c1 = mbx - 1;
           }
-          const int ylim = to_lds ? 13 : 12, clim = to_lds ? 5 : 4;
+          // rows below ylim / clim are this wave's; the rest the row below
+          // stores (the image's last row stores all; with the simple filter
+          // chroma is never filtered, so its rows are all this wave's)
+          const int ylim = to_lds || hand ? 13 : 16, clim = to_lds || (hand && !luma_only) ? 5 : 8;
           if (lane < 48) {
             const int j = lane & 15, x = y0 + (lane >> 4);
             if (y0 >= 0 && j < ylim && x <= y1) {
@@ -1178,8 +1187,9 @@ extern "C" int wg_debug_phases(unsigned long long* host, int n) {
 
 extern "C" size_t wg_decode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images) {
   if (mbw <= 0 || mbh <= 0 || n_images <= 0) return 0;
-  // top records | ctl[4] | progress (reconstruction) | progress_f (filter, k_decode_split)
-  return (size_t)n_images * mbw * TOP_BYTES + sizeof(int) * (2 * (size_t)n_images * mbh + 4);
+  // top records | ctl[4] | progress (reconstruction) | progress_f (filter, k_decode_split) | bottom records (16-B aligned)
+  const size_t head = (size_t)n_images * mbw * TOP_BYTES + sizeof(int) * (2 * (size_t)n_images * mbh + 4);
+  return ((head + 15) & ~(size_t)15) + (size_t)n_images * mbw * BOT_BYTES;
 }
 
 extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int32_t filter_type, int32_t mbw,
@@ -1200,6 +1210,10 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   a.top = static_cast<uint8_t*>(work);
   a.ctl = reinterpret_cast<int*>(a.top + (size_t)n_images * mbw * TOP_BYTES);
   a.progress = a.ctl + 4;
+  {
+    const size_t head = (size_t)n_images * mbw * TOP_BYTES + sizeof(int) * (2 * (size_t)n_images * mbh + 4);
+    a.bot = static_cast<uint8_t*>(work) + ((head + 15) & ~(size_t)15);
+  }
   a.filter_type = filter_type;
   a.mbw = mbw;
   a.mbh = mbh;
