@@ -33,10 +33,11 @@ __device__ __forceinline__ uint32_t sub_pixels(uint32_t a, uint32_t b) {
   const uint32_t rb = 0xff00ff00u + (a & 0x00ff00ffu) - (b & 0x00ff00ffu);
   return (ag & 0xff00ff00u) | (rb & 0x00ff00ffu);
 }
+// per-byte a + b mod 256: the low 7 bits of each byte add without carrying
+// out of it, and bit 7 is a7 ^ b7 ^ the carry into it (v_xor3 + v_bfi)
 __device__ __forceinline__ uint32_t add_pixels(uint32_t a, uint32_t b) {
-  const uint32_t ag = (a & 0xff00ff00u) + (b & 0xff00ff00u);
-  const uint32_t rb = (a & 0x00ff00ffu) + (b & 0x00ff00ffu);
-  return (ag & 0xff00ff00u) | (rb & 0x00ff00ffu);
+  const uint32_t s = (a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu);
+  return ((a ^ b ^ s) & 0x80808080u) | (s & 0x7f7f7f7fu);
 }
 // per-byte floor((a + b) / 2): v_lerp_u8 with no rounding bits
 __device__ __forceinline__ uint32_t avg2(uint32_t a, uint32_t b) { return __builtin_amdgcn_lerp(a, b, 0u); }
@@ -68,7 +69,8 @@ __device__ __forceinline__ uint32_t clamp_add_sub_full(uint32_t a, uint32_t b, u
 __device__ __forceinline__ v2i16 half_step(v2i16 va, v2i16 vc) {
   const v2i16 d = va - vc;
   // d / 2 truncating toward zero, as Go's '/': add the sign bit to d before the arithmetic shift
-  const v2i16 neg = as_v2(as_u(d) >> 15 & 0x00010001u);
+  typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
+  const v2i16 neg = __builtin_bit_cast(v2i16, __builtin_bit_cast(v2u16, d) >> (v2u16){15, 15});
   return clamp255(va + ((d + neg) >> (v2i16){1, 1}));
 }
 __device__ __forceinline__ uint32_t clamp_add_sub_half(uint32_t avg, uint32_t c) {
@@ -353,22 +355,23 @@ constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
 // last row.  Bands are dequeued in (band, image) order from a counter, so a
 // band only ever waits on a band owned by a running wave.
 //
-// Hand-off between bands: the band's last lane writes every pixel of its row
-// as it makes it, as an 8-B {pixel, tag} granule with one sc1 (write-through)
-// store (MI355X_MICROARCH.md, R2 granules: untorn, no flag, no drain); the
-// band below loads the granules it needs with sc1 loads and re-polls any
-// whose tag is not set yet.  The band below then trails by the diagonal's
-// 128 steps plus a store's flight and its own lookahead (a progress counter
-// published every 32 columns behind a store drain cost it ~90 more steps per
-// band: 6.2 -> 4.x ms at 4096^2).
+// Hand-off between bands: the band's last lane writes its row's pixels as
+// 8-B {pixel, tag} granules, two at a time with one 16-B sc1 (write-through)
+// store (MI355X_MICROARCH.md, R2 granules: untorn, no flag, no drain); lane 0
+// of the band below loads one granule a step, UPD steps before it needs it,
+// and re-polls one whose tag is not set yet.  The band below then trails by
+// the diagonal's 128 steps plus UPD, a step for the pairing and a store's
+// flight (per-chunk loads of 18 granules trailed by ~20 more steps; a
+// progress counter published every 32 columns behind a store drain by ~90).
 //
-// The walk runs in chunks of 16 steps, and everything but the predictor is
-// done per chunk, one chunk ahead: each lane's 16 residuals and tile modes,
-// lane 0's 18 pixels of the row above (the DPP shift leaves lane 0 its own
-// register: update_dpp's `old`, no per-step branch) and the 16 outputs
-// (stored as one 64-B run per lane).
-#ifndef UP_AT
-#define UP_AT 12  // step of the chunk at which the next chunk's row-above loads are issued
+// The walk runs in chunks of 16 steps, and everything but the predictor and
+// the row above is done per chunk: each lane's 16 residuals and tile modes
+// (loaded a chunk ahead, one pair per step) and the 16 outputs (stored as one
+// 64-B run per lane).  The DPP shift leaves lane 0 its own register
+// (update_dpp's `old`, no per-step branch).
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+#ifndef UPD
+#define UPD 6  // steps between a row-above granule's load and its use
 #endif
 
 __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
@@ -389,8 +392,9 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
     const bool live = y < a.height;
     const uint32_t* in = a.in + img * a.pitch;
     uint32_t* out = a.out + img * a.pitch;
-    const uint64_t* hand_above = a.hand + ((int64_t)img * a.bands + band - 1) * w;  // band > 0
-    uint64_t* hand_mine = a.hand + ((int64_t)img * a.bands + band) * w;
+    const int hs = (w + 1) & ~1;  // granules per hand-off row (even: 16-B aligned pairs)
+    const uint64_t* hand_above = a.hand + ((int64_t)img * a.bands + band - 1) * hs;  // band > 0
+    uint64_t* hand_mine = a.hand + ((int64_t)img * a.bands + band) * hs;
     const int last_lane = min(63, a.height - 1 - band * 64);
     const bool hands_off = band + 1 < a.bands && lane == last_lane;
     const uint32_t* mrow =
@@ -399,58 +403,50 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
     uint32_t* orow = out + (int64_t)min(y, a.height - 1) * w;
     uint32_t o1 = 0, o2 = 0, o3 = 0, first = 0;  // this lane's outputs at x-1, x-2, x-3; at x = 0
     const int steps = w + 2 * last_lane;
-    // residuals and modes of pixels s - 2k .. s - 2k + 15 of this lane's row
-    auto load_chunk = [&](int s, uint32_t* r, uint32_t* m) {
-      const int x0 = s - 2 * lane;
-#pragma unroll
-      for (int u = 0; u < 16; u++) {
-        const int x = x0 + u;
-        const bool ok = live && x >= 0 && x < w;
-        r[u] = ok ? inrow[x] : 0u;
-        m[u] = ok ? mrow[x >> a.bits] : 0u;
-      }
+    // lane 0's row above, one granule a step: column c sits in gr[c & 15],
+    // loaded UPD steps before step c - 1 (where it is TR); up_take re-polls it
+    // until its tag is set and returns the pixel
+    // (unconditional loads at clamped addresses: a load inside a branch makes
+    // the compiler drain every load before its use)
+    const uint64_t* up_row = band > 0 ? hand_above : hand_mine;  // band 0: any valid row, values unused
+    auto up_load = [&](int c) -> uint64_t {
+      return __hip_atomic_load(up_row + min(c, w - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    // lane 0's row above for the chunk at step s: columns s - 1 .. s + 16 of
-    // the band above's last row as {pixel, tag} granules.  issue_up loads
-    // them (UP_AT steps before the chunk); take_up, at the chunk's start,
-    // re-polls until every tag is set and keeps the pixels.
-    auto issue_up = [&](int s, uint64_t* g) {
-#pragma unroll
-      for (int j = 0; j < 18; j++)  // the same address in every lane: one line per load
-        g[j] = band > 0 && s < w ? __hip_atomic_load(hand_above + min(max(s - 1 + j, 0), w - 1), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)
-                                 : ~0ull;
-    };
-    auto take_up = [&](int s, uint64_t* g, uint32_t* up) {
-      bool ready = true;
-#pragma unroll
-      for (int j = 0; j < 18; j++) ready &= (g[j] >> 32) != 0;
-      if (!__builtin_amdgcn_readfirstlane((int)ready)) {
+    auto up_take = [&](int c, uint64_t g) -> uint32_t {
+      const uint2 gw = __builtin_bit_cast(uint2, g);
+      if (band > 0 && c < w && __builtin_amdgcn_readfirstlane((int)gw.y) == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (uint32_t it = 0;; it++) {
           __builtin_amdgcn_s_sleep(1);
-          issue_up(s, g);
-          ready = true;
-#pragma unroll
-          for (int j = 0; j < 18; j++) ready &= (g[j] >> 32) != 0;
-          if (__builtin_amdgcn_readfirstlane((int)ready)) break;
+          g = up_load(c);
+          if (__builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) != 0) break;
           if ((it & 15) == 15 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
                                   __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
             if (lane == 0) {
               __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              wg::note_timeout(a.diag, s, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0, 0);
+              wg::note_timeout(a.diag, c, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0, 0);
             }
             break;
           }
         }
       }
-#pragma unroll
-      for (int j = 0; j < 18; j++) up[j] = band > 0 ? (uint32_t)g[j] : 0u;
+      return band > 0 ? (uint32_t)g : 0u;
     };
-    uint32_t rc[16], mc[16], uc[18];
-    uint64_t ug[18];
-    load_chunk(0, rc, mc);
-    issue_up(0, ug);
+    // residuals and modes of pixel x of this lane's row (0 outside it)
+    // (only the inputs of pixels inside the row are used, so a clamped
+    // address suffices -- and a select of a load would be sunk into a branch)
+    auto ld_res = [&](int x) -> uint32_t { return inrow[min(max(x, 0), w - 1)]; };
+    auto ld_mode = [&](int x) -> uint32_t { return mrow[min(max(x, 0), w - 1) >> a.bits]; };
+    uint32_t rc[16], mc[16];
+    uint64_t gr[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      rc[u] = ld_res(u - 2 * lane);
+      mc[u] = ld_mode(u - 2 * lane);
+    }
+#pragma unroll
+    for (int c = 0; c <= UPD; c++) gr[c & 15] = up_load(c);
+    uint32_t cT = up_take(0, gr[0]), cTL = cT;  // columns s and s - 1 of the row above at step s (lane 0)
     for (int s0 = 0; s0 < steps; s0 += 16) {
       uint32_t rn[16], mn[16], ov[16], cc[16];
       // the chunk's control words (the tile modes arrived a chunk ago), with
@@ -462,21 +458,33 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
         const int idx = x == 0 ? (y == 0 ? 17 : 16) : (y == 0 ? 18 : (int)((mc[u] >> 8) & 0xf));
         cc[u] = ctab[idx] | (x == w - 1 ? (uint32_t)C_EDGE : 0u);
       }
-      take_up(s0, ug, uc);
-      load_chunk(s0 + 16, rn, mn);
 #pragma unroll
       for (int u = 0; u < 16; u++) {
-        if (u == UP_AT) issue_up(s0 + 16, ug);  // the next chunk's row above, UP_AT steps into this one
         const int x = s0 + u - 2 * lane;  // steps past the end run idle (x >= w on every lane)
+        rn[u] = ld_res(x + 16);  // the next chunk's inputs, a pair a step
+        mn[u] = ld_mode(x + 16);
+        gr[(u + 1 + UPD) & 15] = up_load(s0 + u + 1 + UPD);
+        const uint32_t cTR = up_take(s0 + u + 1, gr[(u + 1) & 15]);
         // row above: lane k-1's outputs at x+1, x, x-1 from its previous step
         // (wave_shr:1); lane 0 keeps its own copy of the band above's row
-        const uint32_t up_x1 = (uint32_t)__builtin_amdgcn_update_dpp((int)uc[u + 2], (int)o1, 0x138, 0xf, 0xf, false);
-        const uint32_t up_x = (uint32_t)__builtin_amdgcn_update_dpp((int)uc[u + 1], (int)o2, 0x138, 0xf, 0xf, false);
-        const uint32_t up_xm1 = (uint32_t)__builtin_amdgcn_update_dpp((int)uc[u], (int)o3, 0x138, 0xf, 0xf, false);
+        const uint32_t up_x1 = (uint32_t)__builtin_amdgcn_update_dpp((int)cTR, (int)o1, 0x138, 0xf, 0xf, false);
+        const uint32_t up_x = (uint32_t)__builtin_amdgcn_update_dpp((int)cT, (int)o2, 0x138, 0xf, 0xf, false);
+        const uint32_t up_xm1 = (uint32_t)__builtin_amdgcn_update_dpp((int)cTL, (int)o3, 0x138, 0xf, 0xf, false);
+        cTL = cT;
+        cT = cTR;
         const uint32_t tr = bsel<12>(cc[u], first, up_x1);
         const uint32_t v = add_pixels(rc[u], predict_ctl(cc[u], o1, up_x, tr, up_xm1));
         const bool valid = live && x >= 0 && x < w;
-        if (hands_off && valid) __hip_atomic_store(hand_mine + x, 1ull << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the hand-off: x has the step's parity (2 * lane is even), so odd
+        // steps store the pair (x - 1, x); an odd width's last pixel goes alone
+        if (u & 1) {
+          if (hands_off && valid) {
+            const u32x4_t g2 = {o1, 1u, v, 1u};
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(hand_mine + x - 1), "v"(g2) : "memory");
+          }
+        } else if (hands_off && x == w - 1) {
+          __hip_atomic_store(hand_mine + x, 1ull << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         first = x == 0 ? v : first;
         o3 = o2;
         o2 = o1;
@@ -577,7 +585,7 @@ extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32
 
 extern "C" size_t wg_vp8l_inverse_work_bytes(int32_t width, int32_t height, int32_t n_images) {
   if (width <= 0 || height <= 0 || n_images <= 0) return 0;
-  return 16 + sizeof(uint64_t) * (size_t)n_images * ((height + 63) / 64) * width;
+  return 16 + sizeof(uint64_t) * (size_t)n_images * ((height + 63) / 64) * ((width + 1) & ~1);
 }
 
 extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, int32_t width, int32_t height,
