@@ -49,8 +49,10 @@ def test_invalid_arguments_are_rejected_without_gpu():
 
 def test_work_size_helpers():
     from webp_amd import _lib
-    # top records | ctl[4] | reconstruction progress | filter progress (k_decode_split)
-    assert _lib.lib.wg_decode_work_bytes(120, 68, 2) == 2 * 120 * 32 + 4 * (2 * 2 * 68 + 4)
+    # top records | ctl[4] | reconstruction progress | filter progress (k_decode_split), 16-B aligned
+    # | one 128-B bottom-rows record per MB column (a band's hand-off to the next band)
+    head = 2 * 120 * 32 + 4 * (2 * 2 * 68 + 4)
+    assert _lib.lib.wg_decode_work_bytes(120, 68, 2) == ((head + 15) & ~15) + 2 * 120 * 128
     assert _lib.lib.wg_decode_work_bytes(0, 68, 2) == 0
     # ctl (16 B) | one {pixel, tag} granule per column of each band's last row
     assert _lib.lib.wg_vp8l_inverse_work_bytes(100, 130, 2) == 16 + 8 * 2 * 3 * 100
