@@ -387,6 +387,9 @@ int wg_upsample_nrgba(const uint8_t* y, int32_t y_stride, int64_t y_pitch, const
  * ssim.go:116-160): out[img] = sum over pixels of the clipped-window SSIM.
  * `work` needs wg_plane_ssim_work_bytes(w, h, n_images) bytes. */
 size_t wg_plane_ssim_work_bytes(int32_t w, int32_t h, int32_t n_images);
+/* Partial sums per 16-row tile row of a w-wide plane (one per 58-column
+ * strip): the layout of wg_plane_ssim_rows' output. */
+int32_t wg_plane_ssim_row_partials(int32_t w);
 int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uint8_t* b, int32_t b_stride,
                   int64_t b_pitch, int32_t w, int32_t h, int32_t n_images, double* out, void* work,
                   void* stream);
@@ -395,7 +398,8 @@ int wg_plane_ssim(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uin
  * shards by row bands with a 3-row halo).  Tile rows [ty_begin, ty_end) of
  * 16 pixel rows each; a and b must hold rows 16*ty_begin - 3 .. 16*ty_end + 2
  * (clipped to the plane) at their full-plane positions.  partial receives
- * ceil(w/16) * (ty_end - ty_begin) doubles per image (image-major).  The
+ * wg_plane_ssim_row_partials(w) * (ty_end - ty_begin) doubles per image
+ * (image-major, tile-row-major).  The
  * bands' partials concatenated in tile-row order and passed to
  * wg_plane_ssim_reduce give exactly wg_plane_ssim's sum. */
 int wg_plane_ssim_rows(const uint8_t* a, int32_t a_stride, int64_t a_pitch, const uint8_t* b, int32_t b_stride,

@@ -87,16 +87,17 @@ def oracle_residual_rows(argb, bits, quality, t0, t1):
 
 
 def ssim_tile_partials(a, b, t0, t1):
-    """Stand-in for wg_plane_ssim_rows: per 16x16 tile the sum of the
-    clipped-window SSIM (SSIMGetClipped, ssim.go:132) of its pixels."""
+    """Stand-in for wg_plane_ssim_rows: per 16-row x 58-column tile the sum
+    of the clipped-window SSIM (SSIMGetClipped, ssim.go:132) of its pixels."""
     a, b = a.numpy(), b.numpy()
     h, w = a.shape
+    sw = shard.SSIM_STRIP
     out = []
     for ty in range(t0, t1):
-        for tx in range((w + 15) // 16):
+        for tx in range(shard.ssim_row_partials(w)):
             s = 0.0
             for y in range(ty * 16, min(ty * 16 + 16, h)):
-                for x in range(tx * 16, min(tx * 16 + 16, w)):
+                for x in range(tx * sw, min(tx * sw + sw, w)):
                     s += O.lib.or_ssim_get_clipped(O.u8(a), w, O.u8(b), w, x, y, w, h)
             out.append(s)
     return torch.tensor(out, dtype=torch.float64)

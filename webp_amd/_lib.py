@@ -74,6 +74,7 @@ SIGNATURES = {
     "wg_analysis_alphas": [_vp, _vp, _vp, _i32, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp],
     "wg_upsample_nrgba": [_vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp],
     "wg_plane_ssim_work_bytes": [_i32, _i32, _i32],
+    "wg_plane_ssim_row_partials": [_i32],
     "wg_plane_ssim_rows": [_vp, _i32, _i64, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp],
     "wg_plane_ssim_reduce": [_vp, _i64, _i32, _vp, _vp],
     "wg_plane_ssim": [_vp, _i32, _i64, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp],

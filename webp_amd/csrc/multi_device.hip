@@ -287,7 +287,7 @@ extern "C" int wg_plane_ssim_devices(const int32_t* devices, int32_t n_devices, 
   WG_REQUIRE(w > 0 && h > 0 && a_stride >= w && b_stride >= w);
   if (int rc = check_devices(devices, n_devices)) return rc;
   constexpr int TILE = 16, HALO = 3;
-  const int tx = (w + TILE - 1) / TILE, ty = (h + TILE - 1) / TILE;
+  const int tx = wg_plane_ssim_row_partials(w), ty = (h + TILE - 1) / TILE;  // partials per tile row, tile rows
   int prev_dev = 0;
   if (hipGetDevice(&prev_dev) != hipSuccess) return wg::check_launch("hipGetDevice");
   std::vector<Band> bands((size_t)n_devices);

@@ -157,7 +157,12 @@ def _device_residual_rows(argb, bits, quality, t0, t1):
     return modes[t0:t1], res[t0 << bits:min(t1 << bits, h)]
 
 
-SSIM_TILE = 16
+SSIM_TILE = 16   # rows per tile row of wg_plane_ssim_rows
+SSIM_STRIP = 58  # columns per partial sum (wg_plane_ssim_row_partials)
+
+
+def ssim_row_partials(w):
+    return (w + SSIM_STRIP - 1) // SSIM_STRIP
 
 
 def plane_ssim_sharded(a, b, world, rank, compute=None, reduce=None):
@@ -167,7 +172,7 @@ def plane_ssim_sharded(a, b, world, rank, compute=None, reduce=None):
     in the single-GPU order.  Rank 0 gets the float64 sum."""
     h, w = a.shape[-2:]
     ty = (h + SSIM_TILE - 1) // SSIM_TILE
-    tx = (w + SSIM_TILE - 1) // SSIM_TILE
+    tx = ssim_row_partials(w)
     t0, t1 = band_of(ty, world, rank)
     compute = compute or _device_ssim_rows
     reduce = reduce or _device_ssim_reduce
@@ -183,7 +188,7 @@ def _device_ssim_rows(a, b, t0, t1):
     from ._lib import call
     from .frames import _stream
     h, w = a.shape[-2:]
-    tx = (w + SSIM_TILE - 1) // SSIM_TILE
+    tx = ssim_row_partials(w)
     out = torch.empty(tx * (t1 - t0), dtype=torch.float64, device=a.device)
     call("wg_plane_ssim_rows", a.data_ptr(), a.shape[-1], a.numel(), b.data_ptr(), b.shape[-1], b.numel(), w, h, t0, t1,
          1, out.data_ptr(), _stream())
