@@ -35,6 +35,7 @@ reconstruction, NRGBA) to rank 0 with grouped RCCL send/recv
 Rank 0 prints one JSON line.
 """
 import argparse
+import contextlib
 import json
 import os
 import socket
@@ -109,7 +110,10 @@ def parse():
     p.add_argument("--batch", type=int, default=64, help="frames per GPU per step (C4: 512 frames / 8 GPUs)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget for the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--slots", type=int, default=3, help="batches in flight (one HIP stream each)")
+    p.add_argument("--slots", type=int, default=3, help="batches in flight (two HIP streams each)")
+    p.add_argument("--split", action="store_true",
+                   help="run each batch's decode side on a second stream beside its encode side (A/B: "
+                        "6,152 / 5,905 vs 6,025 / 6,177 MPix/s without, within run-to-run noise)")
     p.add_argument("--iso-steps", type=int, default=2, help="untimed one-batch passes for the isolated kernel times")
     p.add_argument("--no-gather", action="store_true",
                    help="with N > 1, skip the gather of the last batch's outputs to rank 0 (timed apart from value)")
@@ -165,6 +169,7 @@ class Slot:
 
     def __init__(self, batch, device, frames, lib):
         self.stream = torch.cuda.Stream(device)
+        self.dstream = torch.cuda.Stream(device)  # the decode side (independent of the encode side's data)
         self.Y = torch.empty((batch, 16 * MBH, 16 * MBW), dtype=torch.uint8, device=device)
         self.U = torch.empty((batch, 8 * MBH, 8 * MBW), dtype=torch.uint8, device=device)
         self.V = torch.empty_like(self.U)
@@ -193,10 +198,11 @@ class Pipeline:
     step still runs every stage over its whole batch; the timed region ends
     with a device-wide synchronisation."""
 
-    def __init__(self, rgba, mb, co, batch, device, slots=1):
+    def __init__(self, rgba, mb, co, batch, device, slots=1, split=False):
         from webp_amd import _lib, frames
         self.frames = frames
         self.rgba, self.mb, self.co, self.batch = rgba, mb, co, batch
+        self.split = split  # decode side on the slot's second stream, beside its encode side
         self.cfg = frames.encoder_config(**ENC_CFG)
         self.proba = frames.default_proba(device)
         self.slots = [Slot(batch, device, frames, _lib.lib) for _ in range(slots)]
@@ -210,6 +216,8 @@ class Pipeline:
         for sl in self.slots:
             with torch.cuda.stream(sl.stream):
                 sl.uv_sum.zero_()
+            with torch.cuda.stream(sl.dstream):
+                sl.dY[:1, :1].zero_()
         torch.cuda.synchronize(device)  # inputs made on the default stream are ready for every slot stream
 
     def step(self, record=False, side=None):
@@ -221,14 +229,22 @@ class Pipeline:
             self._stages(sl, record and side is None, side)
 
     def _stages(self, sl, record, side=None):
+        """Encode side on the slot's stream; decode side on its second stream
+        (split) or after the encode side on the same one.  The encode and
+        decode sides share no data, so with `split` a slot's decode runs
+        beside its encode; the step's region still covers both (the timed
+        region ends with a device-wide synchronisation)."""
         f = self.frames
         ev = []
 
-        def mark():
+        def mark(stream=None):
             if record:
                 ev.append(torch.cuda.Event(enable_timing=True))
-                ev[-1].record()  # on the slot's stream (the current stream here)
+                ev[-1].record(stream)  # the slot's stream (current) unless given
 
+        # (the decode side needs no wait: its inputs were ready before the first
+        # step, and a slot's decodes are ordered by its decode stream)
+        dstream = sl.dstream if self.split else None
         mark()
         if side != "decode":
             f.import_rgba(self.rgba, has_alpha=False, out=(sl.Y, sl.U, sl.V))
@@ -242,10 +258,15 @@ class Pipeline:
                          quality=ENC_CFG["quality"], out=sl.enc_out, recon=(sl.rY, sl.rU, sl.rV), work=sl.enc_work)
             mark()
         if side != "encode":
-            f.decode_frames(self.mb, self.co, 2, MBW, MBH, self.batch, out=(sl.dY, sl.dU, sl.dV), work=sl.work)
-            mark()
-            f.build_nrgba(sl.dY, sl.dU, sl.dV, W, H, out=sl.out)
-            mark()
+            ctx = torch.cuda.stream(dstream) if dstream is not None else contextlib.nullcontext()
+            with ctx:
+                if dstream is not None and record:  # decode's own start mark, on its stream
+                    ev.append(torch.cuda.Event(enable_timing=True))
+                    ev[-1].record(dstream)
+                f.decode_frames(self.mb, self.co, 2, MBW, MBH, self.batch, out=(sl.dY, sl.dU, sl.dV), work=sl.work)
+                mark(dstream)
+                f.build_nrgba(sl.dY, sl.dU, sl.dV, W, H, out=sl.out)
+                mark(dstream)
         if record:
             self.events.append(ev)
 
@@ -255,8 +276,13 @@ class Pipeline:
         names = list(BYTES_PER_PX)
         acc = {k: 0.0 for k in names}
         for ev in self.events:
-            for k, name in enumerate(names):
-                acc[name] += ev[k].elapsed_time(ev[k + 1])
+            # consecutive marks; split: the decode side's own start mark sits
+            # between the encode side's last mark and the decode mark
+            pairs = [(k, k + 1) for k in range(len(names))]
+            if len(ev) == len(names) + 2:
+                pairs = pairs[:4] + [(5, 6), (6, 7)]
+            for (a, b), name in zip(pairs, names):
+                acc[name] += ev[a].elapsed_time(ev[b])
         n = max(1, len(self.events))
         self.events = []
         return {k: v / n for k, v in acc.items()}
@@ -269,6 +295,7 @@ class Pipeline:
             if sl.used:
                 with torch.cuda.stream(sl.stream):
                     self.frames.encode_status(sl.enc_work, MBW, self.batch)
+                with torch.cuda.stream(sl.dstream if self.split else sl.stream):
                     self.frames.decode_status(sl.work, MBW, self.batch)
 
 
@@ -368,7 +395,7 @@ def aggregate_mpix_s(world, batch, steps, elapsed):
 def isolated_stage_ms(rgba, mb, co, batch, device, steps):
     """Per-kernel launch time with one batch in flight (no overlap with other
     slots' kernels): the roofline's launch duration."""
-    pipe = Pipeline(rgba, mb, co, batch, device, slots=1)
+    pipe = Pipeline(rgba, mb, co, batch, device, slots=1, split=False)
     pipe.step()
     torch.cuda.synchronize()
     for _ in range(steps):
@@ -499,7 +526,7 @@ def main():
         sys.exit(2)
 
     rgba, mb, co, parsed = make_inputs(args.batch, rank, device)
-    pipe = Pipeline(rgba, mb, co, args.batch, device, slots=args.slots)
+    pipe = Pipeline(rgba, mb, co, args.batch, device, slots=args.slots, split=args.split)
     elapsed = timed_region(pipe.step, args.steps, args.warmup, world, torch.cuda.synchronize, device)
     overlapped = pipe.stage_ms()
     pipe.check_status()  # raises if any launch so far hit an in-kernel wait timeout
@@ -550,7 +577,8 @@ def main():
                                   "ids and per-segment quantisers from assignSegments/setSegmentParams on the GPU "
                                   "(k_segments)",
                        "frames_per_gpu": args.batch, "width": W, "height": H, "parallelism": f"frames sharded x{world}",
-                       "batches_in_flight": args.slots},
+                       "batches_in_flight": args.slots,
+                       "streams_per_batch": 2 if args.split else 1},
             "value_stat": f"mean over the {args.steps} timed steps (the contract's K-step region); medians in `runs`",
             "runs": runs,
             "stage_ms_isolated": {k: round(v, 3) for k, v in iso.items()},

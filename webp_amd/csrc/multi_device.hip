@@ -39,6 +39,23 @@ int fail_hip(hipError_t e, const char* what) {
   return WG_EHIP;
 }
 
+// The caller's host buffers, page-locked for the duration of the call
+// (hipHostRegister, portable to every device), so the per-device uploads and
+// the gather are DMA transfers that overlap across devices instead of
+// copies staged through the runtime's bounce buffers.  A buffer that is
+// already pinned (or cannot be registered) is used as it is.
+struct HostPins {
+  std::vector<void*> mine;
+  void pin(const void* p, size_t n) {
+    if (!p || n == 0) return;
+    if (hipHostRegister(const_cast<void*>(p), n, hipHostRegisterPortable) == hipSuccess) mine.push_back(const_cast<void*>(p));
+    else (void)hipGetLastError();  // not fatal: the copies stay correct, only slower
+  }
+  ~HostPins() {
+    for (void* p : mine) (void)hipHostUnregister(p);
+  }
+};
+
 // A first kernel on a new stream (its hardware queue is created then), issued
 // before any persistent kernel runs: creating a queue while wg_encode_mbs runs
 // on another one stalled it past its dependency-wait bound (webpgpu.h).
@@ -66,6 +83,14 @@ extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_device
   const int64_t rgba_b = (int64_t)w * h * 4, y_b = 256 * n_mb, uv_b = 64 * n_mb, seg_pitch = 4 * sizeof(wg_segment);
   int prev_dev = 0;
   if (hipGetDevice(&prev_dev) != hipSuccess) return wg::check_launch("hipGetDevice");
+  HostPins pins;
+  pins.pin(rgba, (size_t)(rgba_b * n_images));
+  pins.pin(mb_out, (size_t)(n_mb * n_images) * sizeof(wg_mb_enc));
+  pins.pin(ry, (size_t)(y_b * n_images));
+  pins.pin(ru, (size_t)(uv_b * n_images));
+  pins.pin(rv, (size_t)(uv_b * n_images));
+  pins.pin(seg_ids_out, (size_t)(n_mb * n_images));
+  pins.pin(info_out, (size_t)n_images * sizeof(wg_frame_segs));
 
   std::vector<DevJob> jobs((size_t)n_devices);
   for (int i = 0; i < n_images; i++) jobs[(size_t)(i % n_devices)].frames.push_back(i);
@@ -134,19 +159,14 @@ extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_device
                             cfg->quality, j.out, j.ry, j.ru, j.rv, j.work, st)) != WG_OK)
       break;
   }
-  // the gather: each device's frames back to their places in the host buffers
+  // the gather: each device's frames back to their places in the host
+  // buffers, enqueued on every device first (the copies of one device overlap
+  // the others' kernels and copies), then each stream synchronised and its
+  // in-kernel wait status checked (a timed-out launch invalidates the outputs)
   for (auto& j : jobs) {
-    if (!j.mem) continue;
-    if (hipError_t e = hipSetDevice(j.dev); e != hipSuccess) {
-      if (rc == WG_OK) rc = fail_hip(e, "hipSetDevice (gather)");
-      continue;
-    }
-    if (rc == WG_OK) {
-      const int st = wg_encode_status(j.work, mbw, (int)j.frames.size(), j.stream);  // synchronises the stream
-      if (st != WG_OK) rc = st;
-    }
-    hipError_t e = hipSuccess;
-    for (size_t q = 0; q < j.frames.size() && rc == WG_OK && e == hipSuccess; q++) {
+    if (!j.mem || rc != WG_OK) continue;
+    hipError_t e = hipSetDevice(j.dev);
+    for (size_t q = 0; q < j.frames.size() && e == hipSuccess; q++) {
       const int64_t i = j.frames[q];
       const int64_t rec_b = n_mb * (int64_t)sizeof(wg_mb_enc);
       e = hipMemcpyAsync(static_cast<uint8_t*>(mb_out) + i * rec_b, j.out + (int64_t)q * rec_b, (size_t)rec_b,
@@ -159,8 +179,16 @@ extern "C" int wg_encode_frames_devices(const int32_t* devices, int32_t n_device
       if (e == hipSuccess && info_out)
         e = hipMemcpyAsync(info_out + i, j.info + q, sizeof(wg_frame_segs), hipMemcpyDeviceToHost, j.stream);
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(j.stream);
-    if (e != hipSuccess && rc == WG_OK) rc = fail_hip(e, "gather (device to host)");
+    if (e != hipSuccess) rc = fail_hip(e, "gather (device to host)");
+  }
+  for (auto& j : jobs) {
+    if (!j.mem || rc != WG_OK) continue;
+    if (hipError_t e = hipSetDevice(j.dev); e != hipSuccess) {
+      rc = fail_hip(e, "hipSetDevice (gather)");
+      continue;
+    }
+    const int st = wg_encode_status(j.work, mbw, (int)j.frames.size(), j.stream);  // synchronises the stream
+    if (st != WG_OK) rc = st;
   }
   for (auto& j : jobs) {
     if (!j.stream && !j.mem) continue;
@@ -228,6 +256,10 @@ extern "C" int wg_vp8l_residual_image_devices(const int32_t* devices, int32_t n_
   const int64_t px = (int64_t)width * height, row_b = (int64_t)width * 4;
   int prev_dev = 0;
   if (hipGetDevice(&prev_dev) != hipSuccess) return wg::check_launch("hipGetDevice");
+  HostPins pins;
+  pins.pin(argb, (size_t)(px * 4));
+  pins.pin(modes, (size_t)tx * ty * 4);
+  pins.pin(residuals, (size_t)(px * 4));
   std::vector<Band> bands((size_t)n_devices);
   int rc = WG_OK;
   for (int k = 0; k < n_devices && rc == WG_OK; k++) {
@@ -274,6 +306,11 @@ extern "C" int wg_vp8l_residual_image_devices(const int32_t* devices, int32_t n_
     if (e == hipSuccess)
       e = hipMemcpyAsync(residuals + (int64_t)r0 * width, base + in_b + (size_t)(r0 - h0) * row_b,
                          (size_t)((r1 - r0) * row_b), hipMemcpyDeviceToHost, b.stream);
+    if (e != hipSuccess) rc = fail_hip(e, "gather (residual bands)");
+  }
+  for (auto& b : bands) {  // every device's gather is in flight: now wait for each
+    if (!b.mem || rc != WG_OK) continue;
+    hipError_t e = hipSetDevice(b.dev);
     if (e == hipSuccess) e = hipStreamSynchronize(b.stream);
     if (e != hipSuccess) rc = fail_hip(e, "gather (residual bands)");
   }
@@ -292,6 +329,10 @@ extern "C" int wg_plane_ssim_devices(const int32_t* devices, int32_t n_devices, 
   if (hipGetDevice(&prev_dev) != hipSuccess) return wg::check_launch("hipGetDevice");
   std::vector<Band> bands((size_t)n_devices);
   std::vector<double> partial((size_t)tx * ty);
+  HostPins pins;  // (declared after `partial`: unpinned before it is freed)
+  pins.pin(a, (size_t)a_stride * h);
+  pins.pin(b_plane, (size_t)b_stride * h);
+  pins.pin(partial.data(), partial.size() * sizeof(double));
   int rc = WG_OK;
   // each band's buffer: its rows + halo of both planes, then its partial sums
   auto rows_of = [&](const Band& b, int* r0, int* r1) {
@@ -340,6 +381,11 @@ extern "C" int wg_plane_ssim_devices(const int32_t* devices, int32_t n_devices, 
     const size_t a_b = align_up((size_t)(r1 - r0) * a_stride), b_b = align_up((size_t)(r1 - r0) * b_stride);
     hipError_t e = hipMemcpyAsync(partial.data() + (size_t)b.t0 * tx, base + a_b + b_b,
                                   (size_t)tx * (b.t1 - b.t0) * sizeof(double), hipMemcpyDeviceToHost, b.stream);
+    if (e != hipSuccess) rc = fail_hip(e, "gather (ssim bands)");
+  }
+  for (auto& b : bands) {  // every device's partials are in flight: now wait for each
+    if (!b.mem || rc != WG_OK) continue;
+    hipError_t e = hipSetDevice(b.dev);
     if (e == hipSuccess) e = hipStreamSynchronize(b.stream);
     if (e != hipSuccess) rc = fail_hip(e, "gather (ssim bands)");
   }
