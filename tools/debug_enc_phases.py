@@ -11,7 +11,7 @@ from webp_amd import _lib, frames
 from tools import synth
 B, W, H = int(os.environ.get("BATCH", "64")), 1920, 1080
 MBW, MBH = 120, 68
-names = ["wait", "import+ctx", "i16rd", "i4rd", "uvrd", "final", "recon+export", "-", "i4:prescreen", "i4:select", "i4:candidates", "i4:winner", "c:pred+fdct", "c:trellis", "c:recon+disto", "c:rate"]
+names = ["wait", "import+ctx", "i16rd", "i4rd", "uvrd", "final", "recon+export", "c:dp(in trellis)", "i4:prescreen", "i4:select", "i4:candidates", "i4:winner", "c:pred+fdct", "c:trellis", "c:recon+disto", "c:rate"]
 STAMPED = hasattr(_lib.lib, "wg_debug_enc_phases")  # only the stamped build (-DWG_STAMPS) exports it
 if STAMPED:
     _lib.lib.wg_debug_enc_phases.argtypes = [ctypes.c_void_p, ctypes.c_int]

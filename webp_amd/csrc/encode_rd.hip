@@ -333,6 +333,70 @@ __device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, c
   return L0raw > 0;
 }
 
+// trellis_prep for two positions of one block at once, with the table reads
+// in two rounds: everything that depends on the position only (the
+// coefficient, sharpening, quantiser, distortion weight, level-0 token row),
+// then the level costs of L0 and L0 + 1.  The scheduling barriers keep each
+// round's reads issued together (left to itself the compiler waited on each
+// read before issuing the next: eight LDS round trips per lane instead of two).
+// Positions below FIRST (the I16 AC blocks' DC) take a zero coefficient and
+// report no level.
+template <int CTX_TYPE, int FIRST>
+__device__ __forceinline__ bool trellis_prep2(const Tables& t, const int* co, int n0, const SQuant& sq, int lam16,
+                                              TRec out[2], int l0s[2]) {
+  constexpr int64_t BIG = 1ll << 59;
+  int co_z[2], sh[2], quant[2], iquant[2], w4096[2];
+  uint64_t vz[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const int n = n0 + j, zig = zig_of(n), band = band_of(n + 1);
+    co_z[j] = n >= FIRST ? co[zig] : 0;
+    sh[j] = sq.sharpen[zig];
+    quant[j] = n == 0 ? sq.dc_quant : sq.quant;
+    iquant[j] = n == 0 ? sq.dc_iquant : sq.iquant;
+    w4096[j] = t.wtr[zig];
+    vz[j] = t.vcost[CTX_TYPE * 8 + band][0];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  int c0[2], L0raw[2], L0[2], thresh[2], lf0[2], lf1[2];
+  uint64_t v0[2], v1[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    c0[j] = max(abs(co_z[j]) + sh[j], 0);
+    L0raw[j] = (c0[j] * iquant[j]) >> 17;
+    L0[j] = min(L0raw[j], 2047);
+    thresh[j] = min((int)(((uint32_t)c0[j] * (uint32_t)iquant[j] + 65536u) >> 17), 2047);
+    const int band = band_of(n0 + j + 1);
+    lf0[j] = t.lfixed[L0[j]];
+    lf1[j] = t.lfixed[min(L0[j] + 1, 2047)];
+    v0[j] = t.vcost[CTX_TYPE * 8 + band][min(L0[j], 67)];
+    v1[j] = t.vcost[CTX_TYPE * 8 + band][min(L0[j] + 1, 67)];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  bool pnz = false;
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const bool has0 = L0[j] > 0 && L0[j] <= thresh[j];
+    const bool has1 = L0[j] + 1 <= 2047 && L0[j] + 1 <= thresh[j];
+    const int w = w4096[j] * 4096;
+    const int e0 = c0[j] - L0[j] * quant[j], e1 = c0[j] - (L0[j] + 1) * quant[j];
+    const int64_t A0 = (int64_t)lf0[j] * lam16 + (int64_t)w * (e0 * e0 - c0[j] * c0[j]) + (has0 ? 0 : BIG);
+    const int64_t A1 = (int64_t)lf1[j] * lam16 + (int64_t)w * (e1 * e1 - c0[j] * c0[j]) + (has1 ? 0 : BIG);
+    const bool z = L0[j] == 0;
+#pragma unroll
+    for (int pc = 0; pc < 3; pc++) {
+      const int64_t r1 = (int64_t)vc_of(v0[j], pc) * lam16 + A0 + 2 * pc;
+      const int64_t r2 = (int64_t)vc_of(v1[j], pc) * lam16 + A1 + 2 * pc + 1;
+      out[j].x[0][pc] = (int64_t)vc_of(vz[j], pc) * lam16 + pc;
+      out[j].x[1][pc] = z ? r2 : r1;
+      out[j].x[2][pc] = z ? BIG : r2;
+    }
+    l0s[j] = L0[j] << 3 | (co_z[j] < 0 ? 4 : 0) | min(L0[j], 2);
+    pnz |= L0raw[j] > 0 && n0 + j >= FIRST;
+  }
+  return pnz;
+}
+
 // 64-bit value of lane j of this lane's quad (DPP quad_perm broadcast)
 template <int J>
 __device__ __forceinline__ int64_t quad_bcast(int64_t v) {
@@ -910,7 +974,7 @@ constexpr int ORDER_TAG = 0x5e0d0000;  // marks a row schedule in the work buffe
 #ifdef WG_STAMPS
 // Diagnostic build only: cycles per phase summed over macroblocks.
 __device__ unsigned long long g_enc_phase[16];
-#define ESTAMP_DECL unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0, sub_prev = 0, cst_prev = 0
+#define ESTAMP_DECL unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0, sub_prev = 0, cst_prev = 0, dst_prev = 0
 #define ESTAMP(k)                                                                  \
   do {                                                                             \
     __builtin_amdgcn_sched_barrier(0);                                             \
@@ -945,7 +1009,18 @@ __device__ unsigned long long g_enc_phase[16];
     if ((k) >= 0) st_acc[12 + (k)] += ts_ - cst_prev;                             \
     cst_prev = ts_;                                                                \
   } while (0)
+// the I4 trellis DP alone (inside c:trellis): st_acc[7]
+#define DSTAMP(k)                                                                  \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long ts_;                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");   \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    if ((k) >= 0) st_acc[7] += ts_ - dst_prev;                                     \
+    dst_prev = ts_;                                                                \
+  } while (0)
 #else
+#define DSTAMP(k) (void)0
 #define CSTAMP(k) (void)0
 #define SSTAMP(k) (void)0
 #define ESTAMP_DECL int st_unused_ = 0
@@ -1453,12 +1528,20 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
           bool pnz = false;
           if (bvalid && hl < 8 * K) {
             const int c = hl >> 3, n0 = 2 * (hl & 7), sl = half * 3 + c;
+            // both positions into registers first, then stored: their table
+            // reads issue together instead of waiting behind the first one's stores
+            TRec rr[2];
+            int l0[2];
+            pnz = trellis_prep2<3, 0>(t, s.co_buf[sl], n0, sg.y1, lam16, rr, l0);
 #pragma unroll
-            for (int j = 0; j < 2; j++)
-              pnz |= trellis_prep<3>(t, s.co_buf[sl][zig_of(n0 + j)], n0 + j, sg.y1, lam16, s.trec[sl][n0 + j], s.l0s[sl][n0 + j]);
+            for (int j = 0; j < 2; j++) {
+              s.trec[sl][n0 + j] = rr[j];
+              s.l0s[sl][n0 + j] = l0[j];
+            }
           }
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
+          DSTAMP(-1);
           // the trellis DP: one lane quad per candidate (lane 4c + k owns end context k)
           if (bvalid && hl < 4 * K) {
             const int c = hl >> 2, sl = half * 3 + c;
@@ -1475,6 +1558,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
             }
           }
           lds_sync();
+          DSTAMP(0);
           }  // TRELLIS
           // candidates: reconstruction + distortion on the candidate's lane quad
           // (lane 4c + r owns row r; the TDisto column pass reads the row pass
@@ -1703,11 +1787,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
             const int j = lane >> 3, n0 = 2 * (lane & 7), pb = first + j;
             TRec rr[2];
             int l0[2];
-#pragma unroll
-            for (int k = 0; k < 2; k++) {  // position 0 (the DC, coded by the WHT) is not part of this trellis
-              const bool used = n0 + k >= 1;
-              pnz |= trellis_prep<0>(t, used ? s.co_buf[pb][zig_of(n0 + k)] : 0, n0 + k, sg.y1, lam16, rr[k], l0[k]) && used;
-            }
+            // (position 0, the DC coded by the WHT, is not part of this trellis)
+            pnz = trellis_prep2<0, 1>(t, s.co_buf[pb], n0, sg.y1, lam16, rr, l0);
 #pragma unroll
             for (int k = 0; k < 2; k++)
               if (n0 + k >= 1) {
