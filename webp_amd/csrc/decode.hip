@@ -1173,6 +1173,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
 int g_num_cus = 0;
 int g_rows_per_cu = 0;   // resident k_decode_bands workgroups per CU (occupancy)
 int g_split_per_cu = 0;  // resident k_decode_split workgroups per CU
+int g_max_wg = 0;        // grid cap (0: every resident slot; WG_DECODE_MAX_WG)
 int g_use_split = 1;     // WG_DECODE_KERNEL=bands selects k_decode_bands (A/B)
 
 }  // namespace
@@ -1235,12 +1236,14 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
     g_split_per_cu = per_cu_s;
     if (const char* e = getenv("WG_DECODE_WG_PER_CU")) g_rows_per_cu = atoi(e) > 0 ? atoi(e) : per_cu;  // tuning
     if (const char* e = getenv("WG_DECODE_KERNEL")) g_use_split = strcmp(e, "bands") != 0;
+    if (const char* e = getenv("WG_DECODE_MAX_WG")) g_max_wg = atoi(e) > 0 ? atoi(e) : 0;  // tuning: cap the grid
   }
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * (2 * (size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(decode ctl)");
   if (g_use_split) {
     const int bands = n_images * ((mbh + SW - 1) / SW);
-    const int grid = bands < g_split_per_cu * g_num_cus ? bands : g_split_per_cu * g_num_cus;
+    int grid = bands < g_split_per_cu * g_num_cus ? bands : g_split_per_cu * g_num_cus;
+    if (g_max_wg > 0 && grid > g_max_wg) grid = g_max_wg;
     hipLaunchKernelGGL(k_decode_split, dim3((unsigned)grid), dim3(128 * SW), 0, s, a);
     return wg::check_launch("k_decode_split");
   }
