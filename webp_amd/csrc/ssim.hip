@@ -104,8 +104,12 @@ __global__ __launch_bounds__(64) void k_plane_ssim(const SsimArgs p) {
   // column (a plane's offsets fit 31 bits, wg_plane_ssim_rows checks); the
   // mask for rows / columns outside the image is applied at use, so the
   // loads of a block stay in flight while the block before it is processed
+  // (the row loop runs in blocks of 8, so it may ask for up to 7 rows past
+  // y1 + 2: clamped to the rows the band owns with its halo, which a band
+  // buffer of wg_plane_ssim_devices holds; their outputs are not kept)
+  const int r_lo = max(y0 - 3, 0), r_hi = min(y1 + 2, p.h - 1);
   auto load = [&](int r, uint32_t& va, uint32_t& vb) {
-    const int rc = min(max(r, 0), p.h - 1);
+    const int rc = min(max(r, r_lo), r_hi);
     va = A[(uint32_t)(rc * p.a_stride) + xo];
     vb = B[(uint32_t)(rc * p.b_stride) + xo];
   };
