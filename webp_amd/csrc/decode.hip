@@ -134,8 +134,16 @@ __device__ unsigned long long g_phase[16];
 #endif
 
 // wave-level LDS ordering: this wave's LDS accesses retire before what follows
+// (the LDS unit executes one wave's DS instructions in issue order, so a
+// read after a write of the same wave -- or another wave's read after this
+// wave's later flag store -- sees the write without draining the queue; the
+// drain cost C3 3.6%: 4.75 -> 4.58 ms.  WG_DEC_DRAIN restores it, A/B.)
 __device__ __forceinline__ void lds_sync() {
+#ifdef WG_DEC_DRAIN
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+  asm volatile("" ::: "memory");
+#endif
   __builtin_amdgcn_wave_barrier();
 }
 
