@@ -234,6 +234,7 @@ constexpr int SEL_WAVES = 4;
 // 0-3, each walking its channel's bins in order.
 __global__ __launch_bounds__(64 * SEL_WAVES) void k_vp8l_select(SelArgs a) {
   __shared__ uint32_t hist[SEL_WAVES][4 * 256];
+  __shared__ double terms[SEL_WAVES][4 * 256];  // each bin's fastSLog2 term
   __shared__ double chan_cost[SEL_WAVES][4];
   __shared__ double cost[14];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -270,13 +271,22 @@ __global__ __launch_bounds__(64 * SEL_WAVES) void k_vp8l_select(SelArgs a) {
       atomicAdd(&hg[3 * 256 + (res & 0xff)], 1u);
     }
     wave_lds_sync();
+    // the terms fastSLog2(v) of every bin, looked up by all lanes at once
+    // (0.0 for an empty bin: ce - 0.0 == ce, so the sum below equals the
+    // reference's, which skips them); the float64 sum stays serial, in the
+    // reference's order, on one lane per channel
+    double* tm = terms[wave];
+#pragma unroll 4
+    for (int i = lane; i < 4 * 256; i += 64) {
+      const uint32_t v = hg[i];
+      tm[i] = v > 0 ? fast_slog2(a.lut, v) : 0.0;
+    }
+    wave_lds_sync();
     if (lane < 4) {  // estimateEntropy's float64 sum, in the reference's order
-      const uint32_t* hc = hg + lane * 256;
+      const double* tc = tm + lane * 256;
       double ce = fast_slog2(a.lut, count);
-      for (int i = 0; i < 256; i++) {
-        const uint32_t v = hc[i];
-        if (v > 0) ce -= fast_slog2(a.lut, v);
-      }
+#pragma unroll 8
+      for (int i = 0; i < 256; i++) ce -= tc[i];
       chan_cost[wave][lane] = ce;
     }
     wave_lds_sync();
