@@ -82,18 +82,22 @@ __global__ __launch_bounds__(CC_THREADS) void k_cc_select(CcArgs a) {
       m = step ? -128 + 8 * c : best[2] - 7 + c;
     }
     const bool live = (sel_mode == 1 ? (c & 15) < 15 : (sel_mode == 2 && !step ? c < 15 : true)) && m >= -128 && m <= 127;
-    if (live) {
+    // (sel_mode is uniform; within modes 0 / 1 the target channel is a
+    // per-lane shift, not a branch: the lanes of one wave search both the
+    // green->red and the green->blue candidates, and a branch on the channel
+    // ran both bodies for every pixel)
+    if (live && sel_mode != 2) {
+      const int tsh = ch == 0 ? 16 : 0;  // red or blue
+      for (int i = g; i < n; i += ngroups) {
+        const uint32_t p = pixel(i);
+        sum += cc_term(m, (p >> 8) & 0xff, (p >> tsh) & 0xff);
+      }
+    } else if (live) {
       const int g2r = best[0], g2b = best[1];
       for (int i = g; i < n; i += ngroups) {
         const uint32_t p = pixel(i);
         const int gr = (p >> 8) & 0xff, rd = (p >> 16) & 0xff, bl = p & 0xff;
-        if (ch == 0) {
-          sum += cc_term(m, gr, rd);
-        } else if (ch == 1) {
-          sum += cc_term(m, gr, bl);
-        } else {
-          sum += cc_term(m, (rd - cc_delta(g2r, gr)) & 0xff, (bl - cc_delta(g2b, gr)) & 0xff);
-        }
+        sum += cc_term(m, (rd - cc_delta(g2r, gr)) & 0xff, (bl - cc_delta(g2b, gr)) & 0xff);
       }
     }
     part[tid] = live ? sum : 0x7fffffff;
