@@ -712,13 +712,18 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
 constexpr int SW = WG_DEC_SW;          // rows per band (one R and one F wave each)
 constexpr int RING_M = WG_DEC_RING_M;  // R -> F ring depth (R's work buffers of unfiltered MBs)
 
-__device__ __forceinline__ bool needs_top_right(uint32_t is_i4, const uint8_t* imodes) {
-  // blocks 3, 7, 11, 15 read the MB above-right in VE4 / LD4 / VL4 (wg_dsp.h pred4_row)
-  if (!is_i4) return false;
-  bool n = false;
+// The first I4 wavefront step (block b at step bx + 2 by) that reads the MB
+// above-right, or 99: blocks 3, 7, 11, 15 (steps 3, 5, 7, 9) read it in
+// VE4 / LD4 / VL4 (wg_dsp.h pred4_row).
+__device__ __forceinline__ int top_right_step(uint32_t is_i4, const uint8_t* imodes) {
+  if (!is_i4) return 99;
+  int st = 99;
 #pragma unroll
-  for (int b = 3; b < 16; b += 4) n |= imodes[b] == 2 || imodes[b] == 6 || imodes[b] == 7;
-  return n;
+  for (int b = 15; b >= 3; b -= 4) {
+    const int m = imodes[b];
+    if (m == 2 || m == 6 || m == 7) st = 3 + 2 * (b >> 2);
+  }
+  return st;
 }
 
 __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
@@ -788,10 +793,13 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         const uint32_t* iw = reinterpret_cast<const uint32_t*>(stage + 48);  // wg_mb_info words
         const uint32_t w6 = __builtin_amdgcn_readfirstlane(iw[6]);
         const uint8_t* imodes = reinterpret_cast<const uint8_t*>(stage + 48) + 8;
-        const bool tr_needed = mbx + 1 < mbw && needs_top_right(w6 & 0xff, imodes);
+        // the step before which R waits for MB x + 1 above (its bottom row is
+        // the top-right context); 99: never
+        const int tr_step =
+            mby > 0 && mbx + 1 < mbw ? __builtin_amdgcn_readfirstlane(top_right_step(w6 & 0xff, imodes)) : 99;
         // ---- dependency on the row above; ring space below (top ring) and in F's ring ----
         if (mby > 0) {
-          const int need = tr_needed ? mbx + 2 : mbx + 1;
+          const int need = mbx + 1;
           if (seen < need) {
             int v = 0;
             if (lane == 0)
@@ -863,7 +871,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         const uint32_t nz_y = __builtin_amdgcn_readfirstlane(iw[0]), nz_uv = __builtin_amdgcn_readfirstlane(iw[1]);
         const uint32_t im0 = __builtin_amdgcn_readfirstlane(iw[2]);
         const int is_i4 = w6 & 0xff, uv_mode = (w6 >> 8) & 0xff;
-        if (is_i4 && lane < 12) {  // replicate top-right down to rows 3, 7, 11 (:155-160)
+        if (is_i4 && tr_step == 99 && lane < 12) {  // replicate top-right down to rows 3, 7, 11 (:155-160)
           const int rr = 4 * (lane / 4 + 1) - 1, i = lane & 3;
           wb[LY + rr * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
         }
@@ -888,6 +896,28 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
             const int my_step = bx + 2 * by;
             const int mode = imodes[blk];
             for (int st = 0; st < 10; st++) {
+              if (st == tr_step) {
+                // the first block that reads the top-right: only now wait for
+                // MB x + 1 above, then its top context's first 4 px, copied
+                // beside rows 3, 7, 11 as well
+                int v = 0;
+                if (lane == 0) {
+                  v = seen;
+                  if (seen < mbx + 2)
+                    v = from_lds ? wait_progress<false>(&prog_r[r - 1], mbx + 2, &a.ctl[1], mbw, a.diag)
+                                 : wait_progress<true>(prog_above, mbx + 2, &a.ctl[1], mbw, a.diag);
+                  const uint32_t tr = from_lds ? lds32(top_ring[r - 1][(mbx + 1) & (RING - 1)])
+                                               : (uint32_t)ld_sc1_64(top + (mbx + 1) * TOP_BYTES);
+                  *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
+                }
+                seen = __shfl(v, 0, 64);
+                lds_sync();
+                if (lane < 12) {
+                  const int r3 = 4 * (lane / 4 + 1) - 1, i = lane & 3;
+                  wb[LY + r3 * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
+                }
+                lds_sync();
+              }
               if (st == my_step) {
                 int X, T[8], L[4];
                 pred4_ctx(wb, LY + 4 * by * WG_BPS + 4 * bx, X, T, L);
