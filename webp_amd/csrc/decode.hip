@@ -738,6 +738,12 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
   // prog_f: MBs F finished; bot_f: MBs whose final bottom rows are in bot_ring
   // (MB x's once MB x + 1's left-edge filter, in its row pass, has run)
   __shared__ int prog_r[SW], prog_f[SW], cons_f[SW], bot_f[SW];
+  // tprog: 4 x (MBs done) + (blocks of the current MB done) of the luma
+  // bottom row in top_ring: block 12 + k's last row (px 4k..4k+3 of row 15)
+  // is final at I4 step 6 + k.  R(y+1) waits on it for its top-right (block
+  // 12 of MB x + 1 above) instead of on the whole MB.  (Waiting block by
+  // block for the top row as well measured slower: C3 4.19 -> 4.34 ms.)
+  __shared__ int tprog[SW];
   __shared__ int sh_word;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -761,6 +767,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         bot_f[r] = 0;
       } else {
         prog_r[r] = 0;
+        tprog[r] = 0;
       }
     }
     __syncthreads();
@@ -779,6 +786,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
       int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
       int* prog_mine = a.progress + (int64_t)img * mbh + mby;
       int seen = 0;
+      int seen_t = 0;  // lane 0 only: tprog of the row above (in the band)
       const int64_t row_mb0 = ((int64_t)img * mbh + mby) * mbw;
       int4 pf = make_int4(0, 0, 0, 0);
       if (lane < 48) pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384) + lane);
@@ -831,19 +839,17 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         lds_sync();
         STAMP(1);
         // ---- top context (unfiltered) ----
-        if (mby > 0 && from_lds) {
+        if (from_lds) {  // (mby > 0)
           const uint8_t* tc = top_ring[r - 1][slot];
           if (lane >= 48 && lane < 52) {
             const int k = lane - 48;
             uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
             *reinterpret_cast<uint64_t*>(dst) = lds64(tc + 8 * k);
           }
-          if (lane == 0) {
-            uint32_t tr;
-            if (mbx < mbw - 1) tr = lds32(top_ring[r - 1][(mbx + 1) & (RING - 1)]);
-            else tr = 0x01010101u * (uint32_t)tc[15];
-            *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
-          }
+          // the top-right of the row's last MB repeats its top[15] (the
+          // others' comes in the I4 steps, once MB x + 1 above has it)
+          if (lane == 0 && mbx == mbw - 1)
+            *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = 0x01010101u * (uint32_t)tc[15];
         } else if (mby > 0) {
           const uint8_t* tc = top + mbx * TOP_BYTES;
           if (lane >= 48 && lane < 52) {
@@ -885,29 +891,41 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           const int code = (nz_y >> (30 - 2 * blk)) & 3;
           int res[4];
           dec_residual_row(cof + blk * 16, code, rr, res);
+          // the last rows of blocks 12..15 (row 15) are the next row's top
+          // context: in the band each goes to R(y+1) as soon as it is made
+          const bool top_lane = to_lds && by == 3 && rr == 3;
           if (!is_i4) {
             const int mode = check_mode(mbx, mby, im0 & 0xff);
             const int dc = predsq_dc(mode, wb + LY, 16);
             const uint32_t pred = predsq_row4(mode, wb + LY, 4 * bx, 4 * by + rr, dc);
-            *reinterpret_cast<uint32_t*>(wb + off) =
-                pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
-                      clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+            const uint32_t row = pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
+                                       clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+            *reinterpret_cast<uint32_t*>(wb + off) = row;
+            if (top_lane) {
+              *reinterpret_cast<uint32_t*>(top_ring[r][slot] + 4 * bx) = row;
+              asm volatile("" ::: "memory");  // (one wave's DS ops complete in order)
+              if (bx == 3) __hip_atomic_store(&tprog[r], 4 * mbx + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
           } else {
             const int my_step = bx + 2 * by;
             const int mode = imodes[blk];
             for (int st = 0; st < 10; st++) {
               if (st == tr_step) {
                 // the first block that reads the top-right: only now wait for
-                // MB x + 1 above, then its top context's first 4 px, copied
-                // beside rows 3, 7, 11 as well
+                // MB x + 1 above (in the band: its block 12 only), then its
+                // bottom row's first 4 px, copied beside rows 3, 7, 11 as well
                 int v = 0;
                 if (lane == 0) {
-                  v = seen;
-                  if (seen < mbx + 2)
-                    v = from_lds ? wait_progress<false>(&prog_r[r - 1], mbx + 2, &a.ctl[1], mbw, a.diag)
-                                 : wait_progress<true>(prog_above, mbx + 2, &a.ctl[1], mbw, a.diag);
-                  const uint32_t tr = from_lds ? lds32(top_ring[r - 1][(mbx + 1) & (RING - 1)])
-                                               : (uint32_t)ld_sc1_64(top + (mbx + 1) * TOP_BYTES);
+                  uint32_t tr;
+                  if (from_lds) {
+                    const int need = 4 * (mbx + 1) + 1;
+                    if (seen_t < need) seen_t = wait_progress<false>(&tprog[r - 1], need, &a.ctl[1], 4 * mbw + 8, a.diag);
+                    tr = lds32(top_ring[r - 1][(mbx + 1) & (RING - 1)]);
+                    v = seen;
+                  } else {
+                    v = seen < mbx + 2 ? wait_progress<true>(prog_above, mbx + 2, &a.ctl[1], mbw, a.diag) : seen;
+                    tr = (uint32_t)ld_sc1_64(top + (mbx + 1) * TOP_BYTES);
+                  }
                   *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
                 }
                 seen = __shfl(v, 0, 64);
@@ -922,9 +940,14 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                 int X, T[8], L[4];
                 pred4_ctx(wb, LY + 4 * by * WG_BPS + 4 * bx, X, T, L);
                 const uint32_t pred = pred4_row(mode, rr, X, T, L);
-                *reinterpret_cast<uint32_t*>(wb + off) =
-                    pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
-                          clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+                const uint32_t row = pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
+                                           clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+                *reinterpret_cast<uint32_t*>(wb + off) = row;
+                if (top_lane) {  // (blocks 12..15 run at steps 6..9, one a step)
+                  *reinterpret_cast<uint32_t*>(top_ring[r][slot] + 4 * bx) = row;
+                  asm volatile("" ::: "memory");
+                  __hip_atomic_store(&tprog[r], 4 * mbx + bx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
               }
               lds_sync();
             }
@@ -955,7 +978,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         STAMP(4);
         lane = opaque_lane() & 63;
         // ---- hand-offs: unfiltered top context for R(y+1), the MB and its info for F(y) ----
-        if (mby < mbh - 1 && lane >= 32 && lane < 36) {
+        if (mby < mbh - 1 && lane >= (to_lds ? 34 : 32) && lane < 36) {  // (in the band the luma row is out already)
           const int k = lane - 32;
           const uint8_t* src =
               k < 2 ? wb + LY + 15 * WG_BPS + 8 * k : (k == 2 ? wb + LU + 7 * WG_BPS : wb + LV + 7 * WG_BPS);
