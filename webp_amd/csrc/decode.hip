@@ -822,19 +822,17 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         }
         // ---- this MB's work buffer: left context from the previous MB's (:118-126), or the row start (:93-110) ----
         uint8_t* const wb = wb_all[r][mslot];
-        if (mbx == 0) {
-          if (lane < 16) wb[LY - 1 + lane * WG_BPS] = 129;
-          else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = 129;
-          else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = 129;
-          else if (lane < 35) wb[(lane == 32 ? LY : lane == 33 ? LU : LV) - WG_BPS - 1] = mby > 0 ? 129 : 127;
-        } else {
-          const uint8_t* pw = wb_all[r][(mbx - 1) & (RING_M - 1)];
-          if (lane < 16) wb[LY - 1 + lane * WG_BPS] = pw[LY + 15 + lane * WG_BPS];
-          else if (lane < 24) wb[LU - 1 + (lane - 16) * WG_BPS] = pw[LU + 7 + (lane - 16) * WG_BPS];
-          else if (lane < 32) wb[LV - 1 + (lane - 24) * WG_BPS] = pw[LV + 7 + (lane - 24) * WG_BPS];
-          else if (lane == 32) wb[LY - WG_BPS - 1] = pw[LY - WG_BPS + 15];
-          else if (lane == 33) wb[LU - WG_BPS - 1] = pw[LU - WG_BPS + 7];
-          else if (lane == 34) wb[LV - WG_BPS - 1] = pw[LV - WG_BPS + 7];
+        if (lane < 35) {
+          // one byte a lane, addresses by selects (one LDS read + write for
+          // the wave, not one divergent branch per plane): lanes 0-15 / 16-23
+          // / 24-31 the Y / U / V left column, lanes 32-34 the top-left corners
+          const int pl = lane < 16 ? 0 : (lane < 24 ? 1 : (lane < 32 ? 2 : lane - 32));
+          const int row = lane < 16 ? lane : (lane < 24 ? lane - 16 : (lane < 32 ? lane - 24 : -1));
+          const int o = (pl == 0 ? LY : (pl == 1 ? LU : LV)) + row * WG_BPS;
+          uint8_t v;
+          if (mbx == 0) v = row < 0 && mby == 0 ? 127 : 129;
+          else v = wb_all[r][(mbx - 1) & (RING_M - 1)][o + (pl ? 7 : 15)];
+          wb[o - 1] = v;
         }
         lds_sync();
         STAMP(1);
@@ -1054,39 +1052,26 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           }
         }
         // the MB into the tiles (rows 4..) and the filter rows above (rows 0..3)
+        // (every lane group's read first, then the writes: one LDS round trip)
         const uint8_t* ms = wb_all[r][mslot];
-        if (lane < 16) {
-          *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) =
-              *reinterpret_cast<const uint4*>(ms + LY + lane * WG_BPS);
-        } else if (lane < 32) {
-          const int pl = lane >= 24, j = (lane - 16) & 7;
-          *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0) = lds64(ms + (pl ? LV : LU) + j * WG_BPS);
-        }
-        if (mby > 0 && from_lds) {
-          const uint8_t* bt = bot_ring[r - 1][slot];
-          if (lane >= 52 && lane < 60) {
-            const int k = lane - 52, rr = k >> 1, half = k & 1;
-            *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = lds64(bt + 16 * rr + 8 * half);
-          } else if (lane >= 60) {
-            const int rr = lane - 60;
-            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) = lds64(bt + 64 + 8 * rr);
-          } else if (lane >= 44 && lane < 48) {
-            const int rr = lane - 44;
-            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = lds64(bt + 96 + 8 * rr);
-          }
-        } else if (mby > 0) {  // across bands: the record the band above's last row left (same layout as bot_ring)
-          const uint8_t* rec = bot_img + mbx * BOT_BYTES;
-          if (lane >= 52 && lane < 60) {
-            const int k = lane - 52, rr = k >> 1, half = k & 1;
-            *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = ld_sc1_64(rec + 16 * rr + 8 * half);
-          } else if (lane >= 60) {
-            const int rr = lane - 60;
-            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) = ld_sc1_64(rec + 64 + 8 * rr);
-          } else if (lane >= 44 && lane < 48) {
-            const int rr = lane - 44;
-            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = ld_sc1_64(rec + 96 + 8 * rr);
-          }
-        }
+        const bool y_lane = lane < 16, c_lane = lane >= 16 && lane < 32;
+        // the rows above from bot_ring / the cross-band record (same layout):
+        // lanes 52-59 Y rows 0..3 in 8-B halves, 60-63 U, 44-47 V
+        const bool b_lane = mby > 0 && (lane >= 52 || (lane >= 44 && lane < 48));
+        const int bk = lane - 52;
+        const int b_src = lane >= 60 ? 64 + 8 * (lane - 60) : (lane >= 52 ? 16 * (bk >> 1) + 8 * (bk & 1) : 96 + 8 * (lane - 44));
+        uint8_t* const b_dst = lane >= 60 ? fu + (lane - 60) * FC_STRIDE + FC_X0
+                                          : (lane >= 52 ? fy + (bk >> 1) * FY_STRIDE + FY_X0 + 8 * (bk & 1)
+                                                        : fv + (lane - 44) * FC_STRIDE + FC_X0);
+        const int c_pl = lane >= 24, c_j = (lane - 16) & 7;
+        uint4 yv = make_uint4(0, 0, 0, 0);
+        uint64_t cv = 0, bv = 0;
+        if (y_lane) yv = *reinterpret_cast<const uint4*>(ms + LY + lane * WG_BPS);
+        if (c_lane) cv = lds64(ms + (c_pl ? LV : LU) + c_j * WG_BPS);
+        if (b_lane) bv = from_lds ? lds64(bot_ring[r - 1][slot] + b_src) : ld_sc1_64(bot_img + mbx * BOT_BYTES + b_src);
+        if (y_lane) *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) = yv;
+        if (c_lane) *reinterpret_cast<uint64_t*>((c_pl ? fv : fu) + (c_j + 4) * FC_STRIDE + FC_X0) = cv;
+        if (b_lane) *reinterpret_cast<uint64_t*>(b_dst) = bv;
         const uint32_t w7 = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(info_ring[r][mslot])[7]);
         lds_sync();
         if (lane == 0) __hip_atomic_store(&cons_f[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
