@@ -1088,16 +1088,14 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         if (to_lds && mbx > 0) {
           // the left MB's bottom rows are final now (our left-edge filter was
           // the last to touch them): its columns 12..15 into its bot_ring slot
-          if (do_filter && lane >= 16 && lane < 28) {
+          // (lanes 16-19 Y rows 12..15, 20-27 U / V rows 4..7; addresses by
+          // selects: one LDS read + write)
+          if (do_filter && lane >= 16 && lane < (luma_only ? 20 : 28)) {
             uint8_t* bl = bot_ring[r][(mbx - 1) & (RING - 1)];
-            const int k = lane - 16;
-            if (k < 4) {
-              *reinterpret_cast<uint32_t*>(bl + 16 * k + 12) = lds32(fy + (16 + k) * FY_STRIDE + FY_X0 - 4);
-            } else if (!luma_only) {
-              const int pl = k >= 8, rr = k & 3;
-              *reinterpret_cast<uint32_t*>(bl + 64 + 32 * pl + 8 * rr + 4) =
-                  lds32((pl ? fv : fu) + (8 + rr) * FC_STRIDE + FC_X0 - 4);
-            }
+            const int k = lane - 16, pl = k >= 8, rr = k & 3;
+            const int dst = k < 4 ? 16 * k + 12 : 64 + 32 * pl + 8 * rr + 4;
+            const uint8_t* src = k < 4 ? fy + (16 + k) * FY_STRIDE + FY_X0 - 4 : (pl ? fv : fu) + (8 + rr) * FC_STRIDE + FC_X0 - 4;
+            *reinterpret_cast<uint32_t*>(bl + dst) = lds32(src);
           }
           lds_sync();
           if (lane == 0) __hip_atomic_store(&bot_f[r], mbx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1153,53 +1151,53 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           // stores (the image's last row stores all; with the simple filter
           // chroma is never filtered, so its rows are all this wave's)
           const int ylim = to_lds || hand ? 13 : 16, clim = to_lds || (hand && !luma_only) ? 5 : 8;
-          if (lane < 48) {
-            const int j = lane & 15, x = y0 + (lane >> 4);
-            if (y0 >= 0 && j < ylim && x <= y1) {
-              const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
-              *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby + j) * ys + 16 * x) = w;
-            }
-          }
-#pragma unroll
-          for (int h = 0; h < 2; h++) {
-            const int i = lane + 64 * h, pl = (i >> 3) & 1, j = i & 7, x = c0 + (i >> 4);
-            if (c0 >= 0 && i < 80 && j < clim && x <= c1)
-              *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x) =
-                  lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx));
-          }
+          int t0 = -1, t1 = -1, u0 = -1, u1 = -1;
           if (mby > 0) {
-            int t0 = -1, t1 = -1;
             if ((mbx & 1) == 1 || last) {
               t0 = mbx & ~1;
               t1 = mbx;
             }
-            int u0 = -1, u1 = -1;
             if ((mbx & 3) == 3 || last) {
               u0 = mbx & ~3;
               u1 = mbx;
             }
-            if (lane < 6) {
-              const int rr = 1 + (lane >> 1), part = lane & 1, x = t0 + part;
-              if (t0 >= 0 && x <= t1)
-                *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * x) =
-                    *reinterpret_cast<const uint4*>(fy + rr * FY_STRIDE + FY_X0 + 16 * (x - mbx));
-            } else if ((from_lds || !luma_only) && lane >= 8 && lane < 32) {
-              const int k = lane - 8, pl = k >= 12, rr = 1 + (k % 12) / 4, q = k & 3, x = u0 + q;
-              if (u0 >= 0 && x <= u1)
-                *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * x) =
-                    lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0 + 8 * (x - mbx));
-            }
           }
-        }
-        if (to_lds) {
-          uint8_t* bt = bot_ring[r][slot];
-          if (lane < 8) {
-            const int rr = lane >> 1, half = lane & 1;
-            *reinterpret_cast<uint64_t*>(bt + 16 * rr + 8 * half) = lds64(fy + (16 + rr) * FY_STRIDE + FY_X0 + 8 * half);
-          } else if (lane < 16) {
-            const int k = lane - 8, pl = k >= 4, rr = k & 3;
-            *reinterpret_cast<uint64_t*>(bt + 64 + 32 * pl + 8 * rr) = lds64((pl ? fv : fu) + (8 + rr) * FC_STRIDE + FC_X0);
-          }
+          // every piece's LDS read first, then the stores (one LDS round trip):
+          //   ym: Y rows of MBs y0..y1 (lane = 16 MB + row)
+          //   cm0 / cm1: U / V rows of MBs c0..c1 (i = lane, lane + 64)
+          //   yt / ct: the rows above this row's top-edge filter rewrote
+          //     (Y rows 13..15 of MBs t0..t1: lanes 0-5; U / V rows 5..7 of
+          //     MBs u0..u1: lanes 8-31)
+          //   bb: this MB's bottom rows for the row below (bot_ring)
+          const int yj = lane & 15, yx = y0 + (lane >> 4);
+          const bool sy = lane < 48 && y0 >= 0 && yj < ylim && yx <= y1;
+          const int ci0 = lane, ci1 = lane + 64;
+          const int cx0 = c0 + (ci0 >> 4), cx1 = c0 + (ci1 >> 4);
+          const bool sc0 = c0 >= 0 && (ci0 & 7) < clim && cx0 <= c1;
+          const bool sc1 = c0 >= 0 && ci1 < 80 && (ci1 & 7) < clim && cx1 <= c1;
+          const int tr_ = 1 + (lane >> 1), tx = t0 + (lane & 1);
+          const bool syt = lane < 6 && t0 >= 0 && tx <= t1;
+          const int ck = lane - 8, cpl = ck >= 12, crr = 1 + (ck % 12) / 4, cx = u0 + (ck & 3);
+          const bool sct = (from_lds || !luma_only) && lane >= 8 && lane < 32 && u0 >= 0 && cx <= u1;
+          const bool sb = to_lds && lane < 16;
+          const int bpl = lane >= 12, brr = lane & 3;
+          uint4 ym = make_uint4(0, 0, 0, 0), yt = make_uint4(0, 0, 0, 0);
+          uint64_t cm0 = 0, cm1 = 0, ct = 0, bb = 0;
+          if (sy) ym = *reinterpret_cast<const uint4*>(fy + (yj + 4) * FY_STRIDE + FY_X0 + 16 * (yx - mbx));
+          if (sc0) cm0 = lds64(((ci0 >> 3) & 1 ? fv : fu) + ((ci0 & 7) + 4) * FC_STRIDE + FC_X0 + 8 * (cx0 - mbx));
+          if (sc1) cm1 = lds64(((ci1 >> 3) & 1 ? fv : fu) + ((ci1 & 7) + 4) * FC_STRIDE + FC_X0 + 8 * (cx1 - mbx));
+          if (syt) yt = *reinterpret_cast<const uint4*>(fy + tr_ * FY_STRIDE + FY_X0 + 16 * (tx - mbx));
+          if (sct) ct = lds64((cpl ? fv : fu) + crr * FC_STRIDE + FC_X0 + 8 * (cx - mbx));
+          if (sb)
+            bb = lds64(lane < 8 ? fy + (16 + (lane >> 1)) * FY_STRIDE + FY_X0 + 8 * (lane & 1)
+                                : (bpl ? fv : fu) + (8 + brr) * FC_STRIDE + FC_X0);
+          if (sy) *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby + yj) * ys + 16 * yx) = ym;
+          if (sc0) *reinterpret_cast<uint64_t*>(((ci0 >> 3) & 1 ? Vp : Up) + (int64_t)(8 * mby + (ci0 & 7)) * uvs + 8 * cx0) = cm0;
+          if (sc1) *reinterpret_cast<uint64_t*>(((ci1 >> 3) & 1 ? Vp : Up) + (int64_t)(8 * mby + (ci1 & 7)) * uvs + 8 * cx1) = cm1;
+          if (syt) *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby - 4 + tr_) * ys + 16 * tx) = yt;
+          if (sct) *reinterpret_cast<uint64_t*>((cpl ? Vp : Up) + (int64_t)(8 * mby - 4 + crr) * uvs + 8 * cx) = ct;
+          if (sb)
+            *reinterpret_cast<uint64_t*>(bot_ring[r][slot] + (lane < 8 ? 16 * (lane >> 1) + 8 * (lane & 1) : 64 + 32 * bpl + 8 * brr)) = bb;
         }
         lds_sync();
         lane = opaque_lane() & 63;
