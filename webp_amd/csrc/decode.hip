@@ -715,13 +715,14 @@ constexpr int RING_M = WG_DEC_RING_M;  // R -> F ring depth (R's work buffers of
 // The first I4 wavefront step (block b at step bx + 2 by) that reads the MB
 // above-right, or 99: blocks 3, 7, 11, 15 (steps 3, 5, 7, 9) read it in
 // VE4 / LD4 / VL4 (wg_dsp.h pred4_row).
-__device__ __forceinline__ int top_right_step(uint32_t is_i4, const uint8_t* imodes) {
+__device__ __forceinline__ int top_right_step(uint32_t is_i4, uint32_t right_modes) {
+  // right_modes: the modes of blocks 3, 7, 11, 15, one byte each
   if (!is_i4) return 99;
   int st = 99;
 #pragma unroll
-  for (int b = 15; b >= 3; b -= 4) {
-    const int m = imodes[b];
-    if (m == 2 || m == 6 || m == 7) st = 3 + 2 * (b >> 2);
+  for (int k = 3; k >= 0; k--) {
+    const uint32_t m = (right_modes >> (8 * k)) & 0xff;
+    if (m == 2 || m == 6 || m == 7) st = 3 + 2 * k;
   }
   return st;
 }
@@ -797,14 +798,23 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         STAMP(0);
         lane = opaque_lane() & 63;
         if (lane < 50) stage[lane] = pf;
+        // the MB's wg_mb_info words straight from the prefetch registers
+        // (lanes 48, 49), not back from LDS: nz masks, modes, flags
+        const uint32_t nz_y = (uint32_t)__builtin_amdgcn_readlane(pf.x, 48);
+        const uint32_t nz_uv = (uint32_t)__builtin_amdgcn_readlane(pf.y, 48);
+        const uint32_t im0 = (uint32_t)__builtin_amdgcn_readlane(pf.z, 48);
+        const uint32_t im1 = (uint32_t)__builtin_amdgcn_readlane(pf.w, 48);
+        const uint32_t im2 = (uint32_t)__builtin_amdgcn_readlane(pf.x, 49);
+        const uint32_t im3 = (uint32_t)__builtin_amdgcn_readlane(pf.y, 49);
+        const uint32_t w6 = (uint32_t)__builtin_amdgcn_readlane(pf.z, 49);
         lds_sync();
-        const uint32_t* iw = reinterpret_cast<const uint32_t*>(stage + 48);  // wg_mb_info words
-        const uint32_t w6 = __builtin_amdgcn_readfirstlane(iw[6]);
         const uint8_t* imodes = reinterpret_cast<const uint8_t*>(stage + 48) + 8;
         // the step before which R waits for MB x + 1 above (its bottom row is
         // the top-right context); 99: never
         const int tr_step =
-            mby > 0 && mbx + 1 < mbw ? __builtin_amdgcn_readfirstlane(top_right_step(w6 & 0xff, imodes)) : 99;
+            mby > 0 && mbx + 1 < mbw
+                ? top_right_step(w6 & 0xff, (im0 >> 24) | (im1 >> 24) << 8 | (im2 >> 24) << 16 | (im3 >> 24) << 24)
+                : 99;
         // ---- dependency on the row above; ring space below (top ring) and in F's ring ----
         if (mby > 0) {
           const int need = mbx + 1;
@@ -872,8 +882,6 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           if (lane < 48) pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384) + lane);
           else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + mbi + 1)[lane - 48];
         }
-        const uint32_t nz_y = __builtin_amdgcn_readfirstlane(iw[0]), nz_uv = __builtin_amdgcn_readfirstlane(iw[1]);
-        const uint32_t im0 = __builtin_amdgcn_readfirstlane(iw[2]);
         const int is_i4 = w6 & 0xff, uv_mode = (w6 >> 8) & 0xff;
         if (is_i4 && tr_step == 99 && lane < 12) {  // replicate top-right down to rows 3, 7, 11 (:155-160)
           const int rr = 4 * (lane / 4 + 1) - 1, i = lane & 3;
