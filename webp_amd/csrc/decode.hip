@@ -883,7 +883,10 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + mbi + 1)[lane - 48];
         }
         const int is_i4 = w6 & 0xff, uv_mode = (w6 >> 8) & 0xff;
-        if (is_i4 && tr_step == 99 && lane < 12) {  // replicate top-right down to rows 3, 7, 11 (:155-160)
+        // replicate the top-right down to rows 3, 7, 11 (:155-160) where it is
+        // known already: the first row (127) and a row's last MB (its top[15]);
+        // elsewhere it comes at tr_step, or no block reads it
+        if (is_i4 && tr_step == 99 && (mby == 0 || mbx == mbw - 1) && lane < 12) {
           const int rr = 4 * (lane / 4 + 1) - 1, i = lane & 3;
           wb[LY + rr * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
         }
@@ -932,14 +935,10 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                     v = seen < mbx + 2 ? wait_progress<true>(prog_above, mbx + 2, &a.ctl[1], mbw, a.diag) : seen;
                     tr = (uint32_t)ld_sc1_64(top + (mbx + 1) * TOP_BYTES);
                   }
-                  *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
+#pragma unroll
+                  for (int k = 0; k < 4; k++) *reinterpret_cast<uint32_t*>(wb + LY + (4 * k - 1) * WG_BPS + 16) = tr;
                 }
                 seen = __shfl(v, 0, 64);
-                lds_sync();
-                if (lane < 12) {
-                  const int r3 = 4 * (lane / 4 + 1) - 1, i = lane & 3;
-                  wb[LY + r3 * WG_BPS + 16 + i] = wb[LY - WG_BPS + 16 + i];
-                }
                 lds_sync();
               }
               if (st == my_step) {
