@@ -832,33 +832,33 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         }
         // ---- this MB's work buffer: left context from the previous MB's (:118-126), or the row start (:93-110) ----
         uint8_t* const wb = wb_all[r][mslot];
-        if (lane < 35) {
-          // one byte a lane, addresses by selects (one LDS read + write for
-          // the wave, not one divergent branch per plane): lanes 0-15 / 16-23
-          // / 24-31 the Y / U / V left column, lanes 32-34 the top-left corners
-          const int pl = lane < 16 ? 0 : (lane < 24 ? 1 : (lane < 32 ? 2 : lane - 32));
-          const int row = lane < 16 ? lane : (lane < 24 ? lane - 16 : (lane < 32 ? lane - 24 : -1));
-          const int o = (pl == 0 ? LY : (pl == 1 ? LU : LV)) + row * WG_BPS;
-          uint8_t v;
-          if (mbx == 0) v = row < 0 && mby == 0 ? 127 : 129;
-          else v = wb_all[r][(mbx - 1) & (RING_M - 1)][o + (pl ? 7 : 15)];
-          wb[o - 1] = v;
-        }
-        lds_sync();
-        STAMP(1);
-        // ---- top context (unfiltered) ----
-        if (from_lds) {  // (mby > 0)
-          const uint8_t* tc = top_ring[r - 1][slot];
-          if (lane >= 48 && lane < 52) {
-            const int k = lane - 48;
-            uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
-            *reinterpret_cast<uint64_t*>(dst) = lds64(tc + 8 * k);
-          }
+        // (left context and, in the band, top context and F's info record:
+        // every read first, then the writes -- one LDS round trip)
+        const bool l_lane = lane < 35, t_lane = from_lds && lane >= 48 && lane < 52;
+        // left: lanes 0-15 / 16-23 / 24-31 the Y / U / V column, 32-34 the
+        // top-left corners, one byte a lane with select-computed addresses
+        const int l_pl = lane < 16 ? 0 : (lane < 24 ? 1 : (lane < 32 ? 2 : lane - 32));
+        const int l_row = lane < 16 ? lane : (lane < 24 ? lane - 16 : (lane < 32 ? lane - 24 : -1));
+        const int l_o = (l_pl == 0 ? LY : (l_pl == 1 ? LU : LV)) + l_row * WG_BPS;
+        // top (unfiltered): lanes 48-51 Y 0..7 / Y 8..15 / U / V
+        const int t_k = lane - 48;
+        uint8_t* const t_dst = t_k < 2 ? wb + LY - WG_BPS + 8 * t_k : (t_k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
+        uint8_t lv = l_row < 0 && mby == 0 ? 127 : 129;
+        uint64_t tv = 0;
+        if (l_lane && mbx > 0) lv = wb_all[r][(mbx - 1) & (RING_M - 1)][l_o + (l_pl ? 7 : 15)];
+        if (t_lane) tv = lds64(top_ring[r - 1][slot] + 8 * t_k);
+        if (l_lane) wb[l_o - 1] = lv;
+        if (t_lane) *reinterpret_cast<uint64_t*>(t_dst) = tv;
+        if (lane >= 48 && lane < 50) *reinterpret_cast<int4*>(info_ring[r][mslot] + 16 * (lane - 48)) = pf;
+        if (from_lds && mbx == mbw - 1) {
           // the top-right of the row's last MB repeats its top[15] (the
           // others' comes in the I4 steps, once MB x + 1 above has it)
-          if (lane == 0 && mbx == mbw - 1)
-            *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = 0x01010101u * (uint32_t)tc[15];
-        } else if (mby > 0) {
+          const uint32_t t15 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(tv >> 32), 49) >> 24;
+          if (lane == 0) *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = 0x01010101u * t15;
+        }
+        STAMP(1);
+        // ---- top context across bands / on the first row ----
+        if (!from_lds && mby > 0) {
           const uint8_t* tc = top + mbx * TOP_BYTES;
           if (lane >= 48 && lane < 52) {
             const uint64_t w = ld_sc1_64(tc + 8 * (lane - 48));
@@ -872,7 +872,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
             else tr = 0x01010101u * (uint32_t)(ld_sc1_64(tc + 8) >> 56);
             *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
           }
-        } else {
+        } else if (mby == 0) {
           if (lane < 21) wb[LY - WG_BPS + lane - 1] = 127;
           else if (lane < 30) wb[LU - WG_BPS + lane - 22] = 127;
           else if (lane < 39) wb[LV - WG_BPS + lane - 31] = 127;
@@ -975,23 +975,24 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
             if (bits & 0xaa) dec_residual_row(bco, 3, rr, res);
             else if (bco[0] != 0) dec_residual_row(bco, 1, rr, res);
           }
-          *reinterpret_cast<uint32_t*>(wb + base + (4 * cby + rr) * WG_BPS + 4 * cbx) =
-              pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
-                    clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+          const uint32_t crow = pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
+                                      clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
+          *reinterpret_cast<uint32_t*>(wb + base + (4 * cby + rr) * WG_BPS + 4 * cbx) = crow;
+          // the bottom row (row 7) is the next row's top context: in the band
+          // straight into the top ring
+          if (to_lds && cby == 1 && rr == 3) *reinterpret_cast<uint32_t*>(top_ring[r][slot] + 16 + 8 * pl + 4 * cbx) = crow;
         }
         lds_sync();
         STAMP(4);
         lane = opaque_lane() & 63;
         // ---- hand-offs: unfiltered top context for R(y+1), the MB and its info for F(y) ----
-        if (mby < mbh - 1 && lane >= (to_lds ? 34 : 32) && lane < 36) {  // (in the band the luma row is out already)
+        if (!to_lds && mby < mbh - 1 && lane >= 32 && lane < 36) {  // (in the band the rows are out already)
           const int k = lane - 32;
           const uint8_t* src =
               k < 2 ? wb + LY + 15 * WG_BPS + 8 * k : (k == 2 ? wb + LU + 7 * WG_BPS : wb + LV + 7 * WG_BPS);
           if (to_lds) *reinterpret_cast<uint64_t*>(top_ring[r][slot] + 8 * k) = lds64(src);
           else st_sc1_64(top + mbx * TOP_BYTES + 8 * k, lds64(src));
         }
-        if (lane >= 48 && lane < 50)
-          *reinterpret_cast<int4*>(info_ring[r][mslot] + 16 * (lane - 48)) = stage[lane];
         lds_sync();
         STAMP(5);
         // ---- publish: LDS for F(y) and R(y+1) in the band; global for the next band ----
