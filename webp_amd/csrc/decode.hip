@@ -1035,10 +1035,15 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         }
         lds_sync();
         STAMP(7);
-        // rotate the filter tiles: the MBs to the left move one MB further left
-        if (mbx > 0) {
-          uint4 y0 = make_uint4(0, 0, 0, 0);
-          uint64_t c[2] = {0, 0};
+        // rotate the filter tiles (the MBs to the left move one MB further
+        // left), then the MB into the tiles (rows 4..) and the filter rows
+        // above (rows 0..3): every read of both first, then the writes (one
+        // LDS round trip; the rotation reads the columns the copy-in and the
+        // rotation itself overwrite, so all reads precede all writes)
+        const bool rot = mbx > 0;
+        uint4 y0 = make_uint4(0, 0, 0, 0);
+        uint64_t c[2] = {0, 0};
+        if (rot) {
           if (lane < 40) y0 = *reinterpret_cast<const uint4*>(fy + (lane >> 1) * FY_STRIDE + FY_X0 - 16 + 16 * (lane & 1));
 #pragma unroll
           for (int h = 0; h < 2; h++) {
@@ -1048,19 +1053,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
               c[h] = lds64((pl ? fv : fu) + (row - 12 * pl) * FC_STRIDE + FC_X0 - 24 + 8 * (i & 3));
             }
           }
-          lds_sync();
-          if (lane < 40) *reinterpret_cast<uint4*>(fy + (lane >> 1) * FY_STRIDE + FY_X0 - 32 + 16 * (lane & 1)) = y0;
-#pragma unroll
-          for (int h = 0; h < 2; h++) {
-            const int i = lane + 64 * h;
-            if (i < 96) {
-              const int row = i >> 2, pl = row >= 12;
-              *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (row - 12 * pl) * FC_STRIDE + FC_X0 - 32 + 8 * (i & 3)) = c[h];
-            }
-          }
         }
-        // the MB into the tiles (rows 4..) and the filter rows above (rows 0..3)
-        // (every lane group's read first, then the writes: one LDS round trip)
         const uint8_t* ms = wb_all[r][mslot];
         const bool y_lane = lane < 16, c_lane = lane >= 16 && lane < 32;
         // the rows above from bot_ring / the cross-band record (same layout):
@@ -1077,10 +1070,23 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         if (y_lane) yv = *reinterpret_cast<const uint4*>(ms + LY + lane * WG_BPS);
         if (c_lane) cv = lds64(ms + (c_pl ? LV : LU) + c_j * WG_BPS);
         if (b_lane) bv = from_lds ? lds64(bot_ring[r - 1][slot] + b_src) : ld_sc1_64(bot_img + mbx * BOT_BYTES + b_src);
+        const uint32_t w7v = reinterpret_cast<const uint32_t*>(info_ring[r][mslot])[7];
+        asm volatile("" ::: "memory");  // (reads above, writes below)
+        if (rot) {
+          if (lane < 40) *reinterpret_cast<uint4*>(fy + (lane >> 1) * FY_STRIDE + FY_X0 - 32 + 16 * (lane & 1)) = y0;
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const int i = lane + 64 * h;
+            if (i < 96) {
+              const int row = i >> 2, pl = row >= 12;
+              *reinterpret_cast<uint64_t*>((pl ? fv : fu) + (row - 12 * pl) * FC_STRIDE + FC_X0 - 32 + 8 * (i & 3)) = c[h];
+            }
+          }
+        }
         if (y_lane) *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) = yv;
         if (c_lane) *reinterpret_cast<uint64_t*>((c_pl ? fv : fu) + (c_j + 4) * FC_STRIDE + FC_X0) = cv;
         if (b_lane) *reinterpret_cast<uint64_t*>(b_dst) = bv;
-        const uint32_t w7 = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(info_ring[r][mslot])[7]);
+        const uint32_t w7 = __builtin_amdgcn_readfirstlane(w7v);
         lds_sync();
         if (lane == 0) __hip_atomic_store(&cons_f[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int f_limit = w7 & 0xff, ilevel = (w7 >> 8) & 0xff, f_inner = (w7 >> 16) & 0xff, hev_t = w7 >> 24;
