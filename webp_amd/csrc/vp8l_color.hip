@@ -29,9 +29,10 @@ constexpr int CC_LDS_PIXELS = 64 * 64;  // tiles up to bits = 6 are staged in LD
 
 __device__ __forceinline__ int cc_delta(int m, int c) { return (m * (int)(int8_t)c) >> 5; }
 // |t - delta| folded as the reference does: r = uint8(t - delta); r > 128 ? 256 - r : r
+// (= |int8(t - delta)|: r < 128 -> r, r = 128 -> 128, r > 128 -> 256 - r)
 __device__ __forceinline__ int cc_term(int m, int s, int t) {
-  const int r = (t - cc_delta(m, s)) & 0xff;
-  return r > 128 ? 256 - r : r;
+  const int v = (int)(int8_t)(uint8_t)(t - cc_delta(m, s));
+  return v < 0 ? -v : v;
 }
 
 struct CcArgs {
@@ -42,7 +43,7 @@ struct CcArgs {
 };
 
 __global__ __launch_bounds__(CC_THREADS) void k_cc_select(CcArgs a) {
-  __shared__ uint32_t px[CC_LDS_PIXELS];
+  __shared__ __attribute__((aligned(16))) uint32_t px[CC_LDS_PIXELS];
   __shared__ int part[CC_THREADS];
   __shared__ int cost[64];
   __shared__ int best[3];
@@ -86,19 +87,33 @@ __global__ __launch_bounds__(CC_THREADS) void k_cc_select(CcArgs a) {
     // per-lane shift, not a branch: the lanes of one wave search both the
     // green->red and the green->blue candidates, and a branch on the channel
     // ran both bodies for every pixel)
+    // staged: group g sums a contiguous chunk of the tile, 4 pixels an LDS
+    // read (the sums are integers: any order gives the reference's)
+    const int chunk = ((n + ngroups - 1) / ngroups + 3) & ~3;
+    const int i0 = staged ? g * chunk : g, i1 = staged ? min(n, i0 + chunk) : n, di = staged ? 1 : ngroups;
     if (live && sel_mode != 2) {
       const int tsh = ch == 0 ? 16 : 0;  // red or blue
-      for (int i = g; i < n; i += ngroups) {
-        const uint32_t p = pixel(i);
-        sum += cc_term(m, (p >> 8) & 0xff, (p >> tsh) & 0xff);
-      }
+      auto term = [&](uint32_t p) { return cc_term(m, (p >> 8) & 0xff, (p >> tsh) & 0xff); };
+      int i = i0;
+      if (staged)
+        for (; i + 4 <= i1; i += 4) {
+          const uint4 q = *reinterpret_cast<const uint4*>(&px[i]);
+          sum += term(q.x) + term(q.y) + term(q.z) + term(q.w);
+        }
+      for (; i < i1; i += di) sum += term(pixel(i));
     } else if (live) {
       const int g2r = best[0], g2b = best[1];
-      for (int i = g; i < n; i += ngroups) {
-        const uint32_t p = pixel(i);
+      auto term = [&](uint32_t p) {
         const int gr = (p >> 8) & 0xff, rd = (p >> 16) & 0xff, bl = p & 0xff;
-        sum += cc_term(m, (rd - cc_delta(g2r, gr)) & 0xff, (bl - cc_delta(g2b, gr)) & 0xff);
-      }
+        return cc_term(m, (rd - cc_delta(g2r, gr)) & 0xff, (bl - cc_delta(g2b, gr)) & 0xff);
+      };
+      int i = i0;
+      if (staged)
+        for (; i + 4 <= i1; i += 4) {
+          const uint4 q = *reinterpret_cast<const uint4*>(&px[i]);
+          sum += term(q.x) + term(q.y) + term(q.z) + term(q.w);
+        }
+      for (; i < i1; i += di) sum += term(pixel(i));
     }
     part[tid] = live ? sum : 0x7fffffff;
     __syncthreads();
