@@ -480,9 +480,25 @@ def launch_ranks(argv, n):
     return subprocess.run(cmd, env=env).returncode
 
 
+def gather_check_tensors(rank, batch=2, w=64, h=48):
+    """Stand-ins for a slot's outputs (wg_mb_enc records, reconstruction, NRGBA)
+    in the bench's dtypes and layouts, filled with a rank-specific pattern."""
+    mbw, mbh = (w + 15) // 16, (h + 15) // 16
+    shapes = [((batch * mbw * mbh, 864), torch.uint8), ((batch, 16 * mbh, 16 * mbw), torch.uint8),
+              ((batch, 8 * mbh, 8 * mbw), torch.uint8), ((batch, 8 * mbh, 8 * mbw), torch.uint8),
+              ((batch, h, w, 4), torch.uint8)]
+    out = []
+    for j, (shape, dt) in enumerate(shapes):
+        n = int(np.prod(shape))
+        out.append(((torch.arange(n, dtype=torch.int64) * (7 + j) + 31 * rank + j) % 251).to(dt).reshape(shape))
+    return out
+
+
 def launcher_check(args, world, rank):
     """--launcher-check: the launch / join / timing path on gloo with an empty
-    step (no GPU, nothing measured); rank 0 prints the ranks that joined."""
+    step (no GPU, nothing measured), then the N > 1 gather of main()
+    (shard.timed_gather_to_root) over stand-in outputs; rank 0 prints the
+    ranks that joined and whether it received every rank's tensors intact."""
     dev = torch.device("cpu")
     if world > 1:
         torch.distributed.init_process_group("gloo")
@@ -490,10 +506,18 @@ def launcher_check(args, world, rank):
     if world > 1:
         torch.distributed.all_reduce(joined)
     elapsed = timed_region(lambda record=False: None, args.steps, args.warmup, world, lambda: None, dev)
+    gather = None
+    if world > 1 and not args.no_gather:
+        from webp_amd import shard
+        gather, parts = shard.timed_gather_to_root(gather_check_tensors(rank), world, rank, dev, keep=True)
+        if rank == 0:
+            gather["ok"] = len(parts) == world and all(
+                len(parts[r]) == 5 and all(torch.equal(a, b) for a, b in zip(parts[r], gather_check_tensors(r)))
+                for r in range(world))
     if rank == 0:
         print(json.dumps({"metric": "launcher check (no GPU work; not a measurement)", "value": None,
                           "n_gpus": world, "ranks_joined": int(joined.item()), "steps": args.steps,
-                          "warmup": args.warmup, "elapsed_s": elapsed}), flush=True)
+                          "warmup": args.warmup, "elapsed_s": elapsed, "gather": gather}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

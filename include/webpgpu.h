@@ -23,7 +23,11 @@
  *    running them concurrently with other streams: the first kernel on a new
  *    stream makes the runtime create a hardware queue, which on MI355X
  *    stalled a persistent kernel already running on another queue past that
- *    bound.
+ *    bound.  A timeout is reported once, by the first *_status call of that
+ *    kernel family on the device after it; later clean launches report WG_OK.
+ *  - Device state (timeout records, the encoder's constant tables) belongs
+ *    to the device of `stream`; the frame entry points require it to be the
+ *    calling thread's current device.
  *
  * The Go-side binding a maintainer adds (cgo) is shown in INTEGRATION.md.
  */
@@ -54,6 +58,11 @@ const char* wg_last_error(void);
 int wg_version(void);
 /* Checks that the current device is gfx950 and the kernels are loadable. */
 int wg_device_check(void);
+/* Diagnostics: records one timed-out dependency wait in the device's record
+ * of kernel family `family` (0 encode, 16 decode, 32 VP8L inverse, 48 alpha)
+ * as a persistent kernel's timed-out wait would, so tests can check how the
+ * *_status entry points report and recover.  Not used by the product path. */
+int wg_debug_inject_timeout(int32_t family, void* stream);
 
 /* ===================================================================== *
  * 1. Block-level layer: the internal/dsp function variables, batched.
@@ -120,6 +129,23 @@ int wg_upsample_line_pairs(int32_t format, const uint8_t* top_y, const uint8_t* 
                            int64_t uv_step, uint8_t* top_dst, uint8_t* bot_dst, int64_t dst_step,
                            const uint8_t* alpha_top, const uint8_t* alpha_bot, int64_t alpha_step, int32_t width,
                            int32_t n, void* stream);
+
+/* PointSampleRow(y, u, v, dst, width) (internal/dsp/upsample.go:238-245) over
+ * n rows: y + i*y_step, u/v + i*uv_step (chroma sample x>>1 per pixel), RGB
+ * (3 B/px) to dst + i*dst_step.  n <= 65535. */
+int wg_point_sample_rows(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t y_step, int64_t uv_step,
+                         uint8_t* dst, int64_t dst_step, int32_t width, int32_t n, void* stream);
+
+/* ConvertARGBToY(argb, y, width) (internal/dsp/yuv.go:270-278) over n rows:
+ * packed 0xAARRGGBB words at argb + i*argb_pitch (elements), Y bytes at
+ * y + i*y_pitch.  n <= 65535. */
+int wg_convert_argb_to_y(const uint32_t* argb, int64_t argb_pitch, uint8_t* y, int64_t y_pitch, int32_t width,
+                         int32_t n, void* stream);
+/* ConvertARGBToUV(argb, u, v, srcWidth, doStore) (yuv.go:291-330) over n
+ * rows: (src_width + 1) / 2 U and V samples at u/v + i*uv_pitch; do_store 0
+ * averages each into the sample already there, as the Go call does. */
+int wg_convert_argb_to_uv(const uint32_t* argb, int64_t argb_pitch, uint8_t* u, uint8_t* v, int64_t uv_pitch,
+                          int32_t src_width, int32_t do_store, int32_t n, void* stream);
 
 /* AccumulateRGBA(r, g, b, a, stride, dst, width) (internal/dsp/yuv.go:486-547)
  * over n row pairs: planar channel rows at r/g/b/a + i*in_pitch (second row

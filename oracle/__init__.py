@@ -80,6 +80,9 @@ _SIGS = {
     "or_linear_to_gamma": (_i, [ctypes.c_uint32, _i]),
     "or_accumulate_rgba": (None, [_u8p, _u8p, _u8p, _u8p, _i, _u16p, _i]),
     "or_convert_rgba32_to_uv": (None, [_u16p, _u8p, _u8p, _i]),
+    "or_convert_argb_to_y": (None, [ctypes.c_void_p, _u8p, _i]),
+    "or_convert_argb_to_uv": (None, [ctypes.c_void_p, _u8p, _u8p, _i, _i]),
+    "or_point_sample_row": (None, [_u8p, _u8p, _u8p, _u8p, _i]),
     "or_upsample_line_pair_nrgba": (None, [_u8p] * 10 + [_i]),
     "or_upsample_line_pair_rgb": (None, [_u8p] * 8 + [_i]),
     "or_build_nrgba": (None, [_i, _i, _u8p, _i, _u8p, _u8p, _i, _u8p, _u8p]),
@@ -668,6 +671,34 @@ def convert_rgba32_to_uv(rgb, width, state=None):
     else:
         lib.or_convert_rgba32_to_uv_dithered(rgb.ctypes.data_as(_u16p), u8(u), u8(v), width, state.ctypes.data)
     return u, v
+
+
+def convert_argb_to_y(argb, width):
+    """ConvertARGBToY (yuv.go:270): packed uint32 0xAARRGGBB row -> Y bytes."""
+    argb = np.ascontiguousarray(argb, np.uint32)
+    assert argb.size >= width
+    y = np.zeros(width, np.uint8)
+    lib.or_convert_argb_to_y(argb.ctypes.data, u8(y), width)
+    return y
+
+
+def convert_argb_to_uv(argb, src_width, do_store, u=None, v=None):
+    """ConvertARGBToUV (yuv.go:291): returns (u, v) of (src_width + 1) // 2
+    samples; with do_store False the samples are averaged into copies of u, v."""
+    argb = np.ascontiguousarray(argb, np.uint32)
+    assert argb.size >= src_width
+    n = (src_width + 1) // 2
+    u = np.zeros(n, np.uint8) if u is None else np.array(u[:n], np.uint8)
+    v = np.zeros(n, np.uint8) if v is None else np.array(v[:n], np.uint8)
+    lib.or_convert_argb_to_uv(argb.ctypes.data, u8(u), u8(v), src_width, int(bool(do_store)))
+    return u, v
+
+
+def point_sample_row(y, u, v, width):
+    """PointSampleRow (upsample.go:240): RGB row, 3 bytes per pixel."""
+    dst = np.zeros(3 * width, np.uint8)
+    lib.or_point_sample_row(u8(y), u8(u), u8(v), u8(dst), width)
+    return dst
 
 
 def upsample_line_pair(ty, by, tu, tv, bu, bv, width, nrgba, at=None, ab=None):

@@ -115,6 +115,44 @@ void or_convert_rgba32_to_uv(const uint16_t* rgb, uint8_t* u, uint8_t* v, int wi
   }
 }
 
+/* ConvertARGBToY (yuv.go:270-278): packed 0xAARRGGBB -> RGBToY per pixel */
+void or_convert_argb_to_y(const uint32_t* argb, uint8_t* y, int width) {
+  for (int i = 0; i < width; i++) {
+    const uint32_t p = argb[i];
+    y[i] = (uint8_t)or_rgb_to_y((int)((p >> 16) & 0xff), (int)((p >> 8) & 0xff), (int)(p & 0xff));
+  }
+}
+
+/* ConvertARGBToUV (yuv.go:291-330): a pixel pair per U/V sample, its
+ * channels doubled into the sum-of-4 scale (the odd last pixel x4); do_store
+ * writes the sample, else averages it into u/v ((old + new + 1) >> 1) */
+void or_convert_argb_to_uv(const uint32_t* argb, uint8_t* u, uint8_t* v, int src_width, int do_store) {
+  const int uv_width = src_width >> 1, rnd = (1 << 15) << 2;
+  for (int i = 0; i <= uv_width; i++) {
+    int r, g, b;
+    if (i < uv_width) {
+      const uint32_t v0 = argb[2 * i], v1 = argb[2 * i + 1];
+      r = (int)((v0 >> 15) & 0x1fe) + (int)((v1 >> 15) & 0x1fe);
+      g = (int)((v0 >> 7) & 0x1fe) + (int)((v1 >> 7) & 0x1fe);
+      b = (int)((v0 << 1) & 0x1fe) + (int)((v1 << 1) & 0x1fe);
+    } else {
+      if (!(src_width & 1)) break;
+      const uint32_t v0 = argb[2 * uv_width];
+      r = (int)((v0 >> 14) & 0x3fc);
+      g = (int)((v0 >> 6) & 0x3fc);
+      b = (int)((v0 << 2) & 0x3fc);
+    }
+    const int tu = or_rgb_to_u(r, g, b, rnd), tv = or_rgb_to_v(r, g, b, rnd);
+    if (do_store) {
+      u[i] = (uint8_t)tu;
+      v[i] = (uint8_t)tv;
+    } else {
+      u[i] = (uint8_t)((u[i] + tu + 1) >> 1);
+      v[i] = (uint8_t)((v[i] + tv + 1) >> 1);
+    }
+  }
+}
+
 /* ---------------- VP8Random, random.go ---------------- */
 void or_convert_rgba32_to_uv_dithered(const uint16_t* rgb, uint8_t* u, uint8_t* v, int width, or_random* rg) { /* :568 */
   for (int i = 0; i < width; i++) {
@@ -211,6 +249,11 @@ void or_upsample_line_pair_nrgba(const uint8_t* ty, const uint8_t* by, const uin
                                  const uint8_t* bu, const uint8_t* bv, uint8_t* td, uint8_t* bd,
                                  const uint8_t* at, const uint8_t* ab, int width) {
   upsample_pair(ty, by, tu, tv, bu, bv, td, bd, at, ab, width, emit_nrgba);
+}
+
+/* PointSampleRow (upsample.go:238-245): nearest chroma sample, RGB 3 B/px */
+void or_point_sample_row(const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* dst, int width) {
+  for (int x = 0; x < width; x++) or_yuv_to_rgb(y[x], u[x >> 1], v[x >> 1], dst + 3 * x);
 }
 
 /* buildNRGBA webp.go:379-450 */

@@ -75,6 +75,9 @@ int or_linear_to_gamma(uint32_t base, int shift);               /* :236 */
 void or_accumulate_rgba(const uint8_t* r, const uint8_t* g, const uint8_t* b, const uint8_t* a,
                         int stride, uint16_t* dst, int width);   /* :486 */
 void or_convert_rgba32_to_uv(const uint16_t* rgb, uint8_t* u, uint8_t* v, int width); /* :553 */
+void or_convert_argb_to_y(const uint32_t* argb, uint8_t* y, int width);           /* :270 */
+void or_convert_argb_to_uv(const uint32_t* argb, uint8_t* u, uint8_t* v, int src_width,
+                           int do_store);                                         /* :291 */
 
 /* ---- VP8Random (internal/dsp/random.go) ---- */
 typedef struct { int index1, index2; uint32_t tab[55]; int amp; } or_random;
@@ -96,6 +99,8 @@ void or_upsample_line_pair_rgb(const uint8_t* top_y, const uint8_t* bot_y,
                                const uint8_t* top_u, const uint8_t* top_v,
                                const uint8_t* bot_u, const uint8_t* bot_v,
                                uint8_t* top_dst, uint8_t* bot_dst, int width); /* :45 */
+void or_point_sample_row(const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* dst,
+                         int width); /* PointSampleRow :240 */
 /* buildNRGBA (webp.go:379-450): alpha may be NULL (then A=255); out stride = 4*w */
 void or_build_nrgba(int w, int h, const uint8_t* y, int y_stride, const uint8_t* u, const uint8_t* v,
                     int uv_stride, const uint8_t* alpha, uint8_t* out);

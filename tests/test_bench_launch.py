@@ -1,4 +1,5 @@
-"""CPU: `python bench.py --gpus N` starts N ranks itself.
+"""CPU: `python bench.py --gpus N` starts N ranks itself,
+and its N > 1 gather to rank 0 delivers every rank's outputs.
 
 The launcher path is bench.py's own: with --gpus 2 and no WORLD_SIZE in the
 environment, bench.py runs torch.distributed.run in a child process (the
@@ -35,6 +36,11 @@ def test_gpus_flag_launches_ranks(n):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == n and rec["ranks_joined"] == n
     assert rec["steps"] == 3 and rec["warmup"] == 1 and rec["value"] is None
+    if n > 1:  # main()'s N > 1 gather (shard.timed_gather_to_root): every rank's outputs reach rank 0 intact
+        g = rec["gather"]
+        assert g["ok"] and g["bytes_to_root"] == g["bytes_per_rank"] * (n - 1) and g["bytes_per_rank"] > 0
+    else:
+        assert rec["gather"] is None
 
 
 @pytest.mark.timeout(120)

@@ -53,6 +53,10 @@ SIGNATURES = {
     "wg_filter": [_i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp],
     "wg_upsample_line_pairs": [_i32, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32,
                                _i32, _vp],
+    "wg_debug_inject_timeout": [_i32, _vp],
+    "wg_point_sample_rows": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i32, _i32, _vp],
+    "wg_convert_argb_to_y": [_vp, _i64, _vp, _i64, _i32, _i32, _vp],
+    "wg_convert_argb_to_uv": [_vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _vp],
     "wg_accumulate_rgba": [_vp, _vp, _vp, _vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp],
     "wg_convert_rgba32_to_uv": [_vp, _i64, _vp, _vp, _i64, _i32, _i32, _vp],
     "wg_random_init_host": [_vp, ctypes.c_float],

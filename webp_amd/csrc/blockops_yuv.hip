@@ -6,6 +6,8 @@
 //
 //   UpsampleLinePair / UpsampleLinePairNRGBA   upsample.go:45-236,
 //                                              upsample_direct_amd64.go:10-134
+//   PointSampleRow                             upsample.go:238-245
+//   ConvertARGBToY / ConvertARGBToUV           yuv.go:270-330
 //   AccumulateRGBA                             yuv.go:486-547
 //   ConvertRGBA32ToUV / ...Dithered + VP8Random  yuv.go:553-576, random.go:17-79
 //   SSE / PSNRFromSSE                          ssim.go:163-181
@@ -82,6 +84,77 @@ __global__ void __launch_bounds__(TPB) k_line_pairs(const LpArgs a) {
     const int ab = a.alpha_bot ? a.alpha_bot[i * a.alpha_step + x] : 255;
     put_px(a.bot_dst + i * a.dst_step, x, a.nrgba, yuv_to_rgba(a.bot_y[i * a.y_step + x], bu, bv, ab));
   }
+}
+
+// ---- PointSampleRow: one thread per (instance, pair of output pixels) ----
+// A pixel pair shares its chroma sample; its 6 RGB bytes leave as three 2-B
+// stores where the rows are 2-byte aligned, else as byte stores.
+__global__ void __launch_bounds__(TPB) k_point_sample(const uint8_t* y, const uint8_t* u, const uint8_t* v,
+                                                      int64_t y_step, int64_t uv_step, uint8_t* dst, int64_t dst_step,
+                                                      int width, int wide) {
+  const int c = blockIdx.x * TPB + threadIdx.x;  // chroma column = pixels 2c, 2c + 1
+  const int64_t i = blockIdx.y;
+  if (2 * c >= width) return;
+  const uint8_t* yr = y + i * y_step;
+  const int cu = u[i * uv_step + c], cv = v[i * uv_step + c];
+  const uint32_t p0 = yuv_to_rgba(yr[2 * c], cu, cv, 0);
+  uint8_t* d = dst + i * dst_step + 6 * (int64_t)c;
+  if (2 * c + 1 < width) {
+    const uint32_t p1 = yuv_to_rgba(yr[2 * c + 1], cu, cv, 0);
+    if (wide) {  // r0 g0 | b0 r1 | g1 b1
+      uint16_t* h = reinterpret_cast<uint16_t*>(d);
+      h[0] = (uint16_t)(p0 & 0xffff);
+      h[1] = (uint16_t)(((p0 >> 16) & 0xff) | (p1 & 0xff) << 8);
+      h[2] = (uint16_t)((p1 >> 8) & 0xffff);
+    } else {
+      d[0] = byte_of(p0, 0), d[1] = byte_of(p0, 1), d[2] = byte_of(p0, 2);
+      d[3] = byte_of(p1, 0), d[4] = byte_of(p1, 1), d[5] = byte_of(p1, 2);
+    }
+  } else {
+    d[0] = byte_of(p0, 0), d[1] = byte_of(p0, 1), d[2] = byte_of(p0, 2);
+  }
+}
+
+// ---- ConvertARGBToY: one thread per (instance, pixel) ----
+__global__ void __launch_bounds__(TPB) k_argb_to_y(const uint32_t* argb, int64_t argb_pitch, uint8_t* y,
+                                                   int64_t y_pitch, int width) {
+  const int x = blockIdx.x * TPB + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (x >= width) return;
+  const uint32_t p = argb[i * argb_pitch + x];
+  y[i * y_pitch + x] = (uint8_t)rgb_to_y((int)byte_of(p, 2), (int)byte_of(p, 1), (int)byte_of(p, 0));
+}
+
+// ---- ConvertARGBToUV: one thread per (instance, U/V sample) ----
+// A pair's channels are doubled into the sum-of-4 scale (the odd last pixel
+// x4); do_store writes the sample, else rounds it into the existing one.
+__global__ void __launch_bounds__(TPB) k_argb_to_uv(const uint32_t* argb, int64_t argb_pitch, uint8_t* u, uint8_t* v,
+                                                    int64_t uv_pitch, int src_width, int do_store) {
+  const int k = blockIdx.x * TPB + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (k >= (src_width + 1) >> 1) return;
+  const uint32_t* p = argb + i * argb_pitch + 2 * (int64_t)k;
+  int r, g, b;
+  if (2 * k + 1 < src_width) {
+    const uint32_t v0 = p[0], v1 = p[1];
+    r = 2 * ((int)byte_of(v0, 2) + (int)byte_of(v1, 2));
+    g = 2 * ((int)byte_of(v0, 1) + (int)byte_of(v1, 1));
+    b = 2 * ((int)byte_of(v0, 0) + (int)byte_of(v1, 0));
+  } else {
+    const uint32_t v0 = p[0];
+    r = 4 * (int)byte_of(v0, 2);
+    g = 4 * (int)byte_of(v0, 1);
+    b = 4 * (int)byte_of(v0, 0);
+  }
+  int tu = clip_uv(-9719 * r - 19081 * g + 28800 * b), tv = clip_uv(28800 * r - 24116 * g - 4684 * b);
+  uint8_t* uo = u + i * uv_pitch + k;
+  uint8_t* vo = v + i * uv_pitch + k;
+  if (!do_store) {
+    tu = (*uo + tu + 1) >> 1;
+    tv = (*vo + tv + 1) >> 1;
+  }
+  *uo = (uint8_t)tu;
+  *vo = (uint8_t)tv;
 }
 
 // ---- AccumulateRGBA: one thread per (instance, 2x2 quad) ----
@@ -315,6 +388,34 @@ int wg_upsample_line_pairs(int32_t format, const uint8_t* top_y, const uint8_t* 
               y_step, uv_step, dst_step, alpha_step, width, format};
   hipLaunchKernelGGL(k_line_pairs, dim3(blocks_for(width, TPB), (unsigned)n), dim3(TPB), 0, as_stream(stream), a);
   return check_launch("k_line_pairs");
+}
+
+int wg_point_sample_rows(const uint8_t* y, const uint8_t* u, const uint8_t* v, int64_t y_step, int64_t uv_step,
+                         uint8_t* dst, int64_t dst_step, int32_t width, int32_t n, void* stream) {
+  WG_REQUIRE(y && u && v && dst && width >= 0 && n >= 0 && n <= 65535);
+  if (width == 0 || n == 0) return WG_OK;
+  const int wide = ((reinterpret_cast<uintptr_t>(dst) | (uintptr_t)dst_step) & 1) == 0;
+  hipLaunchKernelGGL(k_point_sample, dim3(blocks_for((width + 1) >> 1, TPB), (unsigned)n), dim3(TPB), 0,
+                     as_stream(stream), y, u, v, y_step, uv_step, dst, dst_step, width, wide);
+  return check_launch("k_point_sample");
+}
+
+int wg_convert_argb_to_y(const uint32_t* argb, int64_t argb_pitch, uint8_t* y, int64_t y_pitch, int32_t width,
+                         int32_t n, void* stream) {
+  WG_REQUIRE(argb && y && width >= 0 && n >= 0 && n <= 65535);
+  if (width == 0 || n == 0) return WG_OK;
+  hipLaunchKernelGGL(k_argb_to_y, dim3(blocks_for(width, TPB), (unsigned)n), dim3(TPB), 0, as_stream(stream), argb,
+                     argb_pitch, y, y_pitch, width);
+  return check_launch("k_argb_to_y");
+}
+
+int wg_convert_argb_to_uv(const uint32_t* argb, int64_t argb_pitch, uint8_t* u, uint8_t* v, int64_t uv_pitch,
+                          int32_t src_width, int32_t do_store, int32_t n, void* stream) {
+  WG_REQUIRE(argb && u && v && src_width >= 0 && n >= 0 && n <= 65535);
+  if (src_width == 0 || n == 0) return WG_OK;
+  hipLaunchKernelGGL(k_argb_to_uv, dim3(blocks_for((src_width + 1) >> 1, TPB), (unsigned)n), dim3(TPB), 0,
+                     as_stream(stream), argb, argb_pitch, u, v, uv_pitch, src_width, do_store ? 1 : 0);
+  return check_launch("k_argb_to_uv");
 }
 
 int wg_accumulate_rgba(const uint8_t* r, const uint8_t* g, const uint8_t* b, const uint8_t* a, int32_t stride,

@@ -26,6 +26,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <mutex>
+
 #include "wg_common.h"
 #include "wg_dsp.h"
 
@@ -233,7 +235,7 @@ __device__ __forceinline__ int wait_progress(const int* p, int need, int* err_fl
   for (uint32_t it = 0;; it++) {
     int v;
     if (GLOBAL) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else v = __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);  // pairs with the tprog release
     if (v >= need) return v;
     // never hang the GPU: after SPIN_TICKS (or once any wait has timed out)
     // flag the error and carry on with whatever is in memory
@@ -913,7 +915,10 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
             if (top_lane) {
               *reinterpret_cast<uint32_t*>(top_ring[r][slot] + 4 * bx) = row;
               asm volatile("" ::: "memory");  // (one wave's DS ops complete in order)
-              if (bx == 3) __hip_atomic_store(&tprog[r], 4 * mbx + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              // (a workgroup-scope release: the top-ring row is visible to R(y+1)
+              // before the count that announces it, by the memory model, not
+              // only by the LDS unit's in-order execution)
+              if (bx == 3) __hip_atomic_store(&tprog[r], 4 * mbx + 4, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
           } else {
             const int my_step = bx + 2 * by;
@@ -951,7 +956,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                 if (top_lane) {  // (blocks 12..15 run at steps 6..9, one a step)
                   *reinterpret_cast<uint32_t*>(top_ring[r][slot] + 4 * bx) = row;
                   asm volatile("" ::: "memory");
-                  __hip_atomic_store(&tprog[r], 4 * mbx + bx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                  __hip_atomic_store(&tprog[r], 4 * mbx + bx + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
               }
               lds_sync();
@@ -1228,11 +1233,39 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
   STAMP_FLUSH();
 }
 
-int g_num_cus = 0;
-int g_rows_per_cu = 0;   // resident k_decode_bands workgroups per CU (occupancy)
-int g_split_per_cu = 0;  // resident k_decode_split workgroups per CU
-int g_max_wg = 0;        // grid cap (0: every resident slot; WG_DECODE_MAX_WG)
-int g_use_split = 1;     // WG_DECODE_KERNEL=bands selects k_decode_bands (A/B)
+// launch configuration, read once per process (under the mutex: host
+// threads may call wg_decode_frames concurrently)
+struct DecConfig {
+  int num_cus = 0;
+  int rows_per_cu = 0;   // resident k_decode_bands workgroups per CU (occupancy)
+  int split_per_cu = 0;  // resident k_decode_split workgroups per CU
+  int max_wg = 0;        // grid cap (0: every resident slot; WG_DECODE_MAX_WG)
+  int use_split = 1;     // WG_DECODE_KERNEL=bands selects k_decode_bands (A/B)
+};
+std::mutex g_dec_cfg_mu;
+DecConfig g_dec_cfg;
+
+int dec_config(DecConfig* out) {
+  std::lock_guard<std::mutex> lock(g_dec_cfg_mu);
+  DecConfig& c = g_dec_cfg;
+  if (c.num_cus == 0) {
+    int dev = 0, cus = 0, per_cu = 0, per_cu_s = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0 ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_bands, 64 * DW, 0) != hipSuccess || per_cu <= 0 ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, k_decode_split, 128 * SW, 0) != hipSuccess ||
+        per_cu_s <= 0)
+      return wg::check_launch("decode occupancy query");
+    c.rows_per_cu = per_cu;
+    c.split_per_cu = per_cu_s;
+    if (const char* e = getenv("WG_DECODE_WG_PER_CU")) c.rows_per_cu = atoi(e) > 0 ? atoi(e) : per_cu;  // tuning
+    if (const char* e = getenv("WG_DECODE_KERNEL")) c.use_split = strcmp(e, "bands") != 0;
+    if (const char* e = getenv("WG_DECODE_MAX_WG")) c.max_wg = atoi(e) > 0 ? atoi(e) : 0;  // tuning: cap the grid
+    c.num_cus = cus;
+  }
+  *out = c;
+  return WG_OK;
+}
 
 }  // namespace
 
@@ -1281,32 +1314,19 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   a.diag = wg::diag_words(s);
   if (!a.diag) return WG_EHIP;
   a.diag += wg::DIAG_DECODE;
-  if (g_num_cus == 0) {
-    int dev = 0, cus = 0, per_cu = 0, per_cu_s = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0 ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_bands, 64 * DW, 0) != hipSuccess || per_cu <= 0 ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, k_decode_split, 128 * SW, 0) != hipSuccess ||
-        per_cu_s <= 0)
-      return wg::check_launch("decode occupancy query");
-    g_num_cus = cus;
-    g_rows_per_cu = per_cu;
-    g_split_per_cu = per_cu_s;
-    if (const char* e = getenv("WG_DECODE_WG_PER_CU")) g_rows_per_cu = atoi(e) > 0 ? atoi(e) : per_cu;  // tuning
-    if (const char* e = getenv("WG_DECODE_KERNEL")) g_use_split = strcmp(e, "bands") != 0;
-    if (const char* e = getenv("WG_DECODE_MAX_WG")) g_max_wg = atoi(e) > 0 ? atoi(e) : 0;  // tuning: cap the grid
-  }
+  DecConfig cfg;
+  if (const int e = dec_config(&cfg)) return e;
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * (2 * (size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(decode ctl)");
-  if (g_use_split) {
+  if (cfg.use_split) {
     const int bands = n_images * ((mbh + SW - 1) / SW);
-    int grid = bands < g_split_per_cu * g_num_cus ? bands : g_split_per_cu * g_num_cus;
-    if (g_max_wg > 0 && grid > g_max_wg) grid = g_max_wg;
+    int grid = bands < cfg.split_per_cu * cfg.num_cus ? bands : cfg.split_per_cu * cfg.num_cus;
+    if (cfg.max_wg > 0 && grid > cfg.max_wg) grid = cfg.max_wg;
     hipLaunchKernelGGL(k_decode_split, dim3((unsigned)grid), dim3(128 * SW), 0, s, a);
     return wg::check_launch("k_decode_split");
   }
   const int bands = n_images * ((mbh + DW - 1) / DW);
-  const int grid = bands < g_rows_per_cu * g_num_cus ? bands : g_rows_per_cu * g_num_cus;
+  const int grid = bands < cfg.rows_per_cu * cfg.num_cus ? bands : cfg.rows_per_cu * cfg.num_cus;
   hipLaunchKernelGGL(k_decode_bands, dim3((unsigned)grid), dim3(64 * DW), 0, s, a);
   return wg::check_launch("k_decode_bands");
 }

@@ -2266,9 +2266,13 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   WG_REQUIRE(y_pitch >= (int64_t)256 * mbw * mbh && uv_pitch >= (int64_t)64 * mbw * mbh && (y_pitch & 15) == 0 &&
              (uv_pitch & 7) == 0);
   hipStream_t s = wg::as_stream(stream);
-  int dev = 0;
+  int dev = 0, sdev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return wg::check_launch("hipGetDevice");
+  if (wg::stream_device(s, &sdev) != WG_OK) return WG_EHIP;
   WG_REQUIRE(dev >= 0 && dev < 64);
+  // the constant tables are uploaded to, and the occupancy read from, the
+  // current device: the stream must be on it (webpgpu.h conventions)
+  if (sdev != dev) return wg::invalid("wg_encode_mbs: the stream's device is not the current device");
   {
     std::lock_guard<std::mutex> lock(g_tables_mu);
     if (!(g_tables_ready_mask >> dev & 1)) {  // constant tables: level codes, fixed I4 mode costs, scan orders

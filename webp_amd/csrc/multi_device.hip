@@ -14,6 +14,8 @@
 // host buffers in frame order, which is where the reference's Phase B
 // (recordAllTokens, encode_parallel.go:1497) and the bitstream writer run.
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "vp8_tables.h"
@@ -42,17 +44,55 @@ int fail_hip(hipError_t e, const char* what) {
 // The caller's host buffers, page-locked for the duration of the call
 // (hipHostRegister, portable to every device), so the per-device uploads and
 // the gather are DMA transfers that overlap across devices instead of
-// copies staged through the runtime's bounce buffers.  A buffer that is
-// already pinned (or cannot be registered) is used as it is.
+// copies staged through the runtime's bounce buffers.
+//
+// Registrations are reference-counted across the process: concurrent calls
+// (host threads) may pass the same or overlapping host buffers, and a range
+// is unregistered only when the last call holding it returns -- never under
+// another call's in-flight DMA.  A range that lies inside one this library
+// registered takes a reference on it; one that cannot be registered (pinned
+// by the caller, or overlapping a registered range) holds references on every
+// registered range it overlaps and is copied as it is.
+struct PinRange {
+  size_t n;
+  int refs;
+};
+std::mutex g_pin_mu;
+std::map<uintptr_t, PinRange> g_pins;  // by start address
+
 struct HostPins {
-  std::vector<void*> mine;
+  std::vector<uintptr_t> held;  // starts of the g_pins ranges this call holds a reference on
   void pin(const void* p, size_t n) {
     if (!p || n == 0) return;
-    if (hipHostRegister(const_cast<void*>(p), n, hipHostRegisterPortable) == hipSuccess) mine.push_back(const_cast<void*>(p));
-    else (void)hipGetLastError();  // not fatal: the copies stay correct, only slower
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p), e = a + n;
+    std::lock_guard<std::mutex> lock(g_pin_mu);
+    // registered ranges overlapping [a, e)
+    std::vector<uintptr_t> over;
+    auto it = g_pins.upper_bound(a);
+    if (it != g_pins.begin()) --it;
+    for (; it != g_pins.end() && it->first < e; ++it)
+      if (it->first + it->second.n > a) over.push_back(it->first);
+    if (over.empty() && hipHostRegister(const_cast<void*>(p), n, hipHostRegisterPortable) == hipSuccess) {
+      g_pins[a] = PinRange{n, 1};
+      held.push_back(a);
+      return;
+    }
+    (void)hipGetLastError();  // not fatal: the copies stay correct
+    for (uintptr_t k : over) {
+      g_pins[k].refs++;
+      held.push_back(k);
+    }
   }
   ~HostPins() {
-    for (void* p : mine) (void)hipHostUnregister(p);
+    std::lock_guard<std::mutex> lock(g_pin_mu);
+    for (uintptr_t k : held) {
+      auto it = g_pins.find(k);
+      if (it == g_pins.end()) continue;
+      if (--it->second.refs == 0) {
+        (void)hipHostUnregister(reinterpret_cast<void*>(k));
+        g_pins.erase(it);
+      }
+    }
   }
 };
 

@@ -29,13 +29,20 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 inline unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
-// Timed-out dependency waits of the persistent kernels, per device: a
-// zeroed, never-reset block of 16 ints per kernel family (DIAG_ENCODE ...):
-// [0] timed-out waits of every launch since the library loaded, [1] set once
-// the first one is recorded, [2..7] its coordinates (kernel-specific).
-// Returns nullptr (error set) if the block cannot be made.
+// The device a stream belongs to (the current device for the null stream).
+int stream_device(hipStream_t s, int* dev);
+
+// Timed-out dependency waits of the persistent kernels, per device (the
+// device of stream s): a zeroed, never-reset block of 16 ints per kernel
+// family (DIAG_ENCODE ...): [0] timed-out waits of every launch since the
+// library loaded, [1] set once the first one is recorded, [2..7] its
+// coordinates (kernel-specific).  Returns nullptr (error set) if the block
+// cannot be made.
 enum { DIAG_ENCODE = 0, DIAG_DECODE = 16, DIAG_VP8L_INVERSE = 32, DIAG_ALPHA = 48 };
 int* diag_words(hipStream_t s);
+// Of the cumulative count `total` of a family on s's device, how many no
+// status call has reported yet; marks them reported.
+int take_new_timeouts(hipStream_t s, int family, int total);
 
 // lane-0 call on a timed-out wait: counts it and records the first one
 __device__ inline void note_timeout(int* diag, int c2, int c3, int c4, int c5, int c6, int c7) {
@@ -51,9 +58,12 @@ __device__ inline void note_timeout(int* diag, int c2, int c3, int c4, int c5, i
 
 // The status entry points of the persistent kernels: `flag` is the launch's
 // own timeout word in its work buffer (cleared by each launch), `diag` the
-// device's never-reset record of timed-out waits of every launch of that
-// kernel family (diag_words), so a timeout in any launch -- not only the last
-// one on `work` -- is reported.  `fields` names diag[2..7].  Synchronises `s`.
+// device's cumulative record of timed-out waits of every launch of that
+// kernel family (diag_words).  A timeout in any launch -- not only the last
+// one on `work` -- is reported by the first status call after it, and only
+// by that one: once reported, later clean launches return WG_OK again (a
+// long-lived host survives one transient stall).  `fields` names diag[2..7].
+// Synchronises `s`.
 inline int wait_status(const int* flag, int family, hipStream_t s, const char* what, const char* fields) {
   int* diag = diag_words(s);
   if (!diag) return WG_EHIP;
@@ -62,9 +72,11 @@ inline int wait_status(const int* flag, int family, hipStream_t s, const char* w
       hipMemcpyAsync(d, diag + family, sizeof(d), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return check_launch(what);
-  if (f || d[0]) {
+  const int fresh = take_new_timeouts(s, family, d[0]);
+  if (f || fresh) {
     std::string m = std::string(what) + ": a dependency wait timed out (output invalid)" +
-                    (f ? "" : " in an earlier launch") + "; " + std::to_string(d[0]) + " timed-out waits so far";
+                    (f ? "" : " in an earlier launch") + "; " + std::to_string(fresh) + " new timed-out waits (" +
+                    std::to_string(d[0]) + " since the library loaded)";
     if (d[1]) {
       m += ", the first at (" + std::string(fields) + ") =";
       for (int k = 2; k < 8; k++) m += " " + std::to_string(d[k]);

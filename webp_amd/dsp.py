@@ -222,19 +222,34 @@ def filter_edge(name, p, base, stride, thresh, ithresh=None, hev=None, uv_delta=
 
 # ---- line-pair upsampler (upsample.go:45-236, upsample_direct_amd64.go:10) ----
 
-def _rows(t, n=None):
-    _dev(t, torch.uint8)
-    assert t.dim() == 2 and (n is None or t.shape[0] == n)
+def _rows(t, n=None, need=0, dtype=torch.uint8):
+    """A (n, L) batch of rows; each row must hold the `need` elements the call reads."""
+    _dev(t, dtype)
+    if t.dim() != 2 or (n is not None and t.shape[0] != n):
+        raise ValueError(f"expected (n, L) rows{'' if n is None else f' with n = {n}'}, got {tuple(t.shape)}")
+    if t.shape[1] < need:
+        raise ValueError(f"rows of {t.shape[1]} elements, the call reads {need}")
     return t
 
 
+def _plane_need(width, height, stride):
+    """elements a (width x height, stride) block spans: (height - 1) * stride + width"""
+    if stride < width:
+        raise ValueError("stride < width")
+    return 0 if width <= 0 or height <= 0 else (height - 1) * stride + width
+
+
 def _line_pairs(fmt, top_y, bot_y, top_u, top_v, bot_u, bot_v, width, alpha_top=None, alpha_bot=None):
-    n = _rows(top_y).shape[0]
+    cw = (width + 1) // 2
+    n = _rows(top_y, None, width).shape[0]
     for t in (top_u, top_v, bot_u, bot_v):
-        _rows(t, n)
+        _rows(t, n, cw)
         assert t.stride(0) == top_u.stride(0)
     if bot_y is not None:
-        assert _rows(bot_y, n).stride(0) == top_y.stride(0)
+        assert _rows(bot_y, n, width).stride(0) == top_y.stride(0)
+    for t in (alpha_top, alpha_bot):
+        if t is not None:
+            _rows(t, n, width)
     bpp = 4 if fmt else 3
     top_dst = torch.empty((n, bpp * width), dtype=torch.uint8, device=top_y.device)
     bot_dst = torch.empty_like(top_dst) if bot_y is not None else None
@@ -262,15 +277,66 @@ def UpsampleLinePairNRGBA(top_y, bot_y, top_u, top_v, bot_u, bot_v, width, alpha
     return _line_pairs(1, top_y, bot_y, top_u, top_v, bot_u, bot_v, width, alpha_top, alpha_bot)
 
 
+def PointSampleRow(y, u, v, width):
+    """PointSampleRow(y, u, v, dst, width) (upsample.go:240) for n rows: y
+    (n, >= width), u / v (n, >= (width + 1) // 2) uint8; returns dst (n, 3*width) RGB."""
+    n = _rows(y, None, width).shape[0]
+    _rows(u, n, (width + 1) // 2)
+    assert _rows(v, n, (width + 1) // 2).stride(0) == u.stride(0)
+    dst = torch.empty((n, 3 * width), dtype=torch.uint8, device=y.device)
+    call("wg_point_sample_rows", y.data_ptr(), u.data_ptr(), v.data_ptr(), y.stride(0), u.stride(0), dst.data_ptr(),
+         dst.stride(0), width, n, _stream())
+    return dst
+
+
+# ---- packed ARGB -> YUV rows (yuv.go:255-330) ----
+
+def _argb_rows(argb, width):
+    if argb.dtype == torch.int32:  # torch has no uint32 arithmetic; the bits are what count
+        argb = argb.view(torch.uint32)
+    return _rows(argb, None, width, torch.uint32)
+
+
+def ConvertARGBToY(argb, width):
+    """ConvertARGBToY(argb, y, width) (yuv.go:270): argb (n, >= width) packed
+    0xAARRGGBB uint32 (or int32 bits); returns y (n, width) uint8."""
+    argb = _argb_rows(argb, width)
+    n = argb.shape[0]
+    y = torch.empty((n, width), dtype=torch.uint8, device=argb.device)
+    call("wg_convert_argb_to_y", argb.data_ptr(), argb.stride(0), y.data_ptr(), y.stride(0), width, n, _stream())
+    return y
+
+
+def ConvertARGBToUV(argb, src_width, do_store, u=None, v=None):
+    """ConvertARGBToUV(argb, u, v, srcWidth, doStore) (yuv.go:291) for n rows:
+    returns (u, v) (n, (src_width + 1) // 2); with do_store False the samples
+    are averaged into u / v (given, updated in place), as the Go call does."""
+    argb = _argb_rows(argb, src_width)
+    n, cw = argb.shape[0], (src_width + 1) // 2
+    if u is None or v is None:
+        if not do_store:
+            raise ValueError("doStore false averages into existing u, v rows")
+        u = torch.empty((n, cw), dtype=torch.uint8, device=argb.device)
+        v = torch.empty_like(u)
+    _rows(u, n, cw)
+    assert _rows(v, n, cw).stride(0) == u.stride(0)
+    call("wg_convert_argb_to_uv", argb.data_ptr(), argb.stride(0), u.data_ptr(), v.data_ptr(), u.stride(0), src_width,
+         int(bool(do_store)), n, _stream())
+    return u, v
+
+
 # ---- RGBA -> YUV420 chroma helpers (yuv.go:486-576, random.go) ----
 
 def AccumulateRGBA(r, g, b, a, stride, width):
     """AccumulateRGBA(r, g, b, a, stride, dst, width) (yuv.go:486) for n row
     pairs: r/g/b/a are (n, L) uint8 planar rows (second row at +stride);
     returns dst as (n, 4 * ceil(width / 2)) uint16."""
-    n = _rows(r).shape[0]
+    need = stride + width if width > 0 else 0  # the second row at +stride
+    if stride < width:
+        raise ValueError("stride < width")
+    n = _rows(r, None, need).shape[0]
     for t in (g, b, a):
-        assert _rows(t, n).stride(0) == r.stride(0)
+        assert _rows(t, n, need).stride(0) == r.stride(0)
     dst = torch.empty((n, 4 * ((width + 1) // 2)), dtype=torch.uint16, device=r.device)
     call("wg_accumulate_rgba", r.data_ptr(), g.data_ptr(), b.data_ptr(), a.data_ptr(), stride, r.stride(0),
          dst.data_ptr(), dst.stride(0), width, n, _stream())
@@ -279,7 +345,7 @@ def AccumulateRGBA(r, g, b, a, stride, width):
 
 def ConvertRGBA32ToUV(rgb, width):
     """ConvertRGBA32ToUV(rgb, u, v, width) (yuv.go:553): rgb (n, >= 4*width) uint16; returns (u, v) (n, width)."""
-    _dev(rgb, torch.uint16)
+    _rows(rgb, None, 4 * width, torch.uint16)
     n = rgb.shape[0]
     u = torch.empty((n, width), dtype=torch.uint8, device=rgb.device)
     v = torch.empty_like(u)
@@ -305,7 +371,7 @@ def InitRandom(dithering, n=1, device="cuda"):
 def ConvertRGBA32ToUVDithered(rgb, width, states):
     """ConvertRGBA32ToUVDithered(rgb, u, v, width, rg) (yuv.go:568): row i
     draws from states[i] (InitRandom), which advance in place."""
-    _dev(rgb, torch.uint16)
+    _rows(rgb, None, 4 * width, torch.uint16)
     _dev(states, torch.uint8)
     n = rgb.shape[0]
     assert states.shape == (n, RANDOM_BYTES)
@@ -321,8 +387,8 @@ def ConvertRGBA32ToUVDithered(rgb, width, states):
 def SSE(pix, ref, width, height, pix_stride, ref_stride):
     """SSE(pix, ref, width, height, pixStride, refStride) (ssim.go:172) per
     buffer pair: pix / ref (n, L) uint8; returns (n,) int64 (uint64 bits)."""
-    n = _rows(pix).shape[0]
-    _rows(ref, n)
+    n = _rows(pix, None, _plane_need(width, height, pix_stride)).shape[0]
+    _rows(ref, n, _plane_need(width, height, ref_stride))
     out = torch.empty(n, dtype=torch.int64, device=pix.device)
     call("wg_sse_planes", pix.data_ptr(), ref.data_ptr(), width, height, pix_stride, ref_stride, pix.stride(0),
          ref.stride(0), out.data_ptr(), n, _stream())
@@ -341,8 +407,8 @@ def PSNRFromSSE(sse, count):
 def DistoStatsOfBlocks(pix, ref, width, height, pix_stride, ref_stride):
     """The DistoStats that SSIMFromBlocks (ssim.go:103) accumulates, per block
     pair: (n, 6) int32 holding the uint32 fields (W, Xm, Ym, Xxm, Xym, Yym)."""
-    n = _rows(pix).shape[0]
-    _rows(ref, n)
+    n = _rows(pix, None, _plane_need(width, height, pix_stride)).shape[0]
+    _rows(ref, n, _plane_need(width, height, ref_stride))
     out = torch.empty((n, 6), dtype=torch.int32, device=pix.device)
     call("wg_disto_stats_blocks", pix.data_ptr(), ref.data_ptr(), width, height, pix_stride, ref_stride,
          pix.stride(0), ref.stride(0), out.data_ptr(), n, _stream())

@@ -205,10 +205,11 @@ def _device_ssim_reduce(partials):
 
 # ---------------- bench helper ----------------
 
-def timed_gather_to_root(tensors, world, rank, device):
+def timed_gather_to_root(tensors, world, rank, device, keep=False):
     """Gather every rank's batch outputs (same shapes on every rank) to rank 0,
     bracketed by barriers and device syncs; returns the timing record rank 0
-    reports (bytes all ranks sent, wall time, aggregate GB/s into rank 0)."""
+    reports (bytes all ranks sent, wall time, aggregate GB/s into rank 0), and
+    with keep=True also what rank 0 received (None on the other ranks)."""
     sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
     sync()
     dist.barrier()
@@ -222,10 +223,13 @@ def timed_gather_to_root(tensors, world, rank, device):
     el = float(t.item())
     per_rank = int(sum(x.numel() * x.element_size() for x in tensors))
     moved = per_rank * (world - 1)
+    rec = {"what": "per-rank wg_mb_enc records + reconstruction + NRGBA of the last batch -> rank 0",
+           "collective": "grouped send/recv (batch_isend_irecv)", "bytes_per_rank": per_rank,
+           "bytes_to_root": moved, "ms": round(el * 1e3, 3), "GB/s_into_root": round(moved / max(el, 1e-9) / 1e9, 2)}
+    if keep:
+        return rec, parts
     del parts
-    return {"what": "per-rank wg_mb_enc records + reconstruction + NRGBA of the last batch -> rank 0",
-            "collective": "grouped send/recv (batch_isend_irecv)", "bytes_per_rank": per_rank,
-            "bytes_to_root": moved, "ms": round(el * 1e3, 3), "GB/s_into_root": round(moved / el / 1e9, 2)}
+    return rec
 
 
 def assemble_frames_numpy(parts, n, world):
