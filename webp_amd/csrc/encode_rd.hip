@@ -972,6 +972,7 @@ struct EncArgs {
   int* ctl;       // [0] dequeue, [1] error
   int* diag;      // wg::diag_words + DIAG_ENCODE
   const int* order;  // the work buffer's row schedule (wg_encode_row_order): dequeue index -> row * n_img + image
+  const int* border; // the same schedule over bands of WAVES rows: dequeue index -> band * n_img + image
   const int* order_tag;  // {ORDER_TAG ^ n_img, ~(ORDER_TAG ^ mbh)} when the schedule was built for this batch shape, else (row, image) order
   int64_t y_pitch, uv_pitch;
   int width, height, mbw, mbh, n_img, quality;
@@ -1036,6 +1037,13 @@ __device__ unsigned long long g_enc_phase[16];
 #define ESTAMP_DECL int st_unused_ = 0
 #define ESTAMP(k) (void)st_unused_
 #define ESTAMP_FLUSH() (void)st_unused_
+#endif
+
+#ifdef WG_ROWTIMES
+// Diagnostic build only: per dequeued row, {ro, start, end, block} in
+// s_memrealtime ticks (100 MHz) -- the launch's row timeline
+// (tools/enc_timeline.py).
+__device__ unsigned long long g_row_times[16384][4];
 #endif
 
 #ifndef WG_ENC_OCC
@@ -1108,21 +1116,41 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
   ESTAMP_DECL;
 
   const bool use_order = a.order_tag[0] == (ORDER_TAG ^ a.n_img) && a.order_tag[1] == ~(ORDER_TAG ^ mbh);
+  const int n_bands = (mbh + WAVES - 1) / WAVES;
   for (;;) {
-    int row;
+    // PAIR: the workgroup's wave pair dequeues a row; otherwise the
+    // workgroup dequeues a BAND of WAVES consecutive rows of one image and
+    // wave w walks row WAVES * band + w.  The band's rows start staggered (each
+    // trails the one above by about two macroblocks) and finish together, so
+    // the workgroup leaves as soon as its band is done: with one row per wave
+    // dequeued independently, a workgroup with one row left held all four
+    // wave slots and its LDS through the launch's tail, and the next batch's
+    // launch could not start there (tools/enc_timeline.py).  One barrier after
+    // the dequeue (the next write of word is after the band's closing barrier).
+    int row, mby, img, ro;
     if constexpr (PAIR) {  // the pair dequeues together (the next write of word is two barriers on)
       if (tid == 0) s_waves[0].word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
       row = __builtin_amdgcn_readfirstlane(s_waves[0].word);
+      if (row >= total_rows) break;
+      ro = use_order ? __builtin_amdgcn_readfirstlane(a.order[row]) : row;
+      mby = ro / a.n_img;
+      img = ro % a.n_img;
     } else {
-      if (lane == 0) s.word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lds_sync();
-      row = __builtin_amdgcn_readfirstlane(s.word);
-      lds_sync();
+      if (tid == 0) s_waves[0].word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int band = __builtin_amdgcn_readfirstlane(s_waves[0].word);
+      if (band >= a.n_img * n_bands) break;
+      const int bo = use_order ? __builtin_amdgcn_readfirstlane(a.border[band]) : band;  // band y * n_img + image
+      img = bo % a.n_img;
+      mby = WAVES * (bo / a.n_img) + wave;
+      ro = mby * a.n_img + img;
+      row = WAVES * band + wave;
     }
-    if (row >= total_rows) break;
-    const int ro = use_order ? __builtin_amdgcn_readfirstlane(a.order[row]) : row;
-    const int mby = ro / a.n_img, img = ro % a.n_img;
+    const bool live = mby < mbh;  // (the last band of an image may have fewer rows)
+#ifdef WG_ROWTIMES
+    const unsigned long long row_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint8_t* Y = a.y + img * a.y_pitch;
     const uint8_t* U = a.u + img * a.uv_pitch;
     const uint8_t* V = a.v + img * a.uv_pitch;
@@ -1132,7 +1160,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
     uint8_t* top = a.top + (int64_t)img * mbw * REC;
     int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
     int* prog_mine = a.progress + (int64_t)img * mbh + mby;
-    {  // this image's four segments (4 x 224 B = 56 x 16 B)
+    if (live) {  // this image's four segments (4 x 224 B = 56 x 16 B)
       const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.segs) + img * a.segs_pitch);
       if (lane < 56) reinterpret_cast<uint4*>(s.seg)[lane] = src[lane];
     }
@@ -1150,7 +1178,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
     uint4 stg0 = make_uint4(0, 0, 0, 0), stg1 = stg0, rst0 = stg0;
     uint2 rst1 = make_uint2(0, 0);
 
-    for (int mbx = 0; mbx < mbw; mbx++) {
+    for (int mbx = 0; live && mbx < mbw; mbx++) {
       Shared& s = launder(s_waves[wave]);
       Shared& c = launder(s_waves[PAIR ? 0 : wave]);  // the MB's pixels and context (A's)
       Tables& t = launder(t_lds);
@@ -2119,6 +2147,17 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
       }  // isA
       ESTAMP(7);
     }
+#ifdef WG_ROWTIMES
+    if (live && (tid == 0 || (!PAIR && lane == 0))) {
+      if (row < 16384) {
+        g_row_times[row][0] = (unsigned long long)ro;
+        g_row_times[row][1] = row_t0;
+        g_row_times[row][2] = __builtin_amdgcn_s_memrealtime();
+        g_row_times[row][3] = (unsigned long long)blockIdx.x << 8 | (unsigned long long)wave;
+      }
+    }
+#endif
+    if constexpr (!PAIR) __syncthreads();  // the band is done: the workgroup dequeues the next one together
   }
   ESTAMP_FLUSH();
 }
@@ -2170,13 +2209,22 @@ extern "C" int wg_debug_enc_phases(unsigned long long* host, int n) {
 }
 #endif
 
+#ifdef WG_ROWTIMES
+extern "C" int wg_debug_enc_rows(unsigned long long* host, int n_rows) {
+  if (n_rows > 16384) n_rows = 16384;
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_row_times), sizeof(unsigned long long) * 4 * n_rows);
+  return 0;
+}
+#endif
+
 // work: hand-off records [n][mbw][REC] | ctl[4] | progress[n*mbh] (cleared by
-// every wg_encode_mbs) | tag[4] | row schedule order[n*mbh] | slack[n]
-// (wg_encode_row_order; kept across calls)
+// every wg_encode_mbs) | tag[4] | row schedule order[n*mbh] | slack[n] |
+// band schedule border[n*ceil(mbh/4)] (wg_encode_row_order; kept across calls)
 extern "C" size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images) {
   if (mbw <= 0 || mbh <= 0 || n_images <= 0) return 0;
+  const size_t bands = (size_t)n_images * ((mbh + WAVES - 1) / WAVES);
   return (size_t)n_images * mbw * REC + sizeof(int) * ((size_t)n_images * mbh + 4) +
-         sizeof(int) * (4 + (size_t)n_images * mbh + (size_t)n_images);
+         sizeof(int) * (4 + (size_t)n_images * mbh + (size_t)n_images + bands);
 }
 
 #ifndef WG_ENC_SLACK_DIV
@@ -2224,6 +2272,24 @@ __global__ __launch_bounds__(256) void k_row_order(const int* slack, int n_img, 
   }
   order[pos] = k;
 }
+// The same schedule over bands of WAVES rows (the 4-wave launches dequeue a
+// band per workgroup): band b of frame i takes the key of its first row,
+// (WAVES b - slack_i, b, i), and is placed among the bands by it.  Keys grow
+// with b within a frame, so a band is dequeued after the band above.
+__global__ __launch_bounds__(256) void k_band_order(const int* slack, int n_img, int mbh, int* border) {
+  const int nb = (mbh + WAVES - 1) / WAVES;
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n_img * nb) return;
+  const int b = k / n_img, i = k % n_img, di = slack[i], r = WAVES * b - di;
+  int pos = 0;  // bands with a smaller key (WAVES b' - d_j, b', j)
+  for (int j = 0; j < n_img; j++) {
+    const int dj = slack[j], v = r + dj;  // band b' of frame j precedes when WAVES b' < v (ties below)
+    const int lt = v <= 0 ? 0 : min((v + WAVES - 1) / WAVES, nb);
+    const bool tie = v >= 0 && v % WAVES == 0 && v / WAVES < nb && (dj < di || (dj == di && j < i));
+    pos += lt + (tie ? 1 : 0);
+  }
+  border[pos] = b * n_img + i;
+}
 
 }  // namespace
 
@@ -2236,9 +2302,12 @@ extern "C" int wg_encode_row_order(const int32_t* alphas, int32_t mbw, int32_t m
   int* tag = progress + rows;
   int* order = tag + 4;
   int* slack = order + rows;
+  int* border = slack + n_images;
+  const int bands = n_images * ((mbh + WAVES - 1) / WAVES);
   hipStream_t s = wg::as_stream(stream);
   hipLaunchKernelGGL(k_row_slack, dim3((unsigned)n_images), dim3(256), 0, s, alphas, mbw * mbh, mbh, tag, slack);
   hipLaunchKernelGGL(k_row_order, dim3(wg::blocks_for(rows, 256)), dim3(256), 0, s, slack, n_images, mbh, order);
+  hipLaunchKernelGGL(k_band_order, dim3(wg::blocks_for(bands, 256)), dim3(256), 0, s, slack, n_images, mbh, border);
   return wg::check_launch("k_row_order");
 }
 
@@ -2308,8 +2377,9 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   a.mbh = mbh;
   a.n_img = n_images;
   a.quality = quality;
-  a.order = a.progress + (size_t)n_images * mbh + 4;  // work: ... | progress | tag[4] | order | slack
+  a.order = a.progress + (size_t)n_images * mbh + 4;  // work: ... | progress | tag[4] | order | slack | border
   a.order_tag = a.order - 4;
+  a.border = a.order + (size_t)n_images * mbh + n_images;
   a.diag = wg::diag_words(s);
   if (!a.diag) return WG_EHIP;
   a.diag += wg::DIAG_ENCODE;
@@ -2336,7 +2406,7 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
     else
       hipLaunchKernelGGL((k_encode_rows<false, true>), dim3((unsigned)grid), dim3(128), 0, s, a);
   } else {
-    const int wgs = (rows + WAVES - 1) / WAVES;  // each wave dequeues rows on its own
+    const int wgs = n_images * ((mbh + WAVES - 1) / WAVES);  // each workgroup dequeues bands of WAVES rows
     const int grid = wgs < per_cu * cus ? wgs : per_cu * cus;
     if (method >= 4)
       hipLaunchKernelGGL((k_encode_rows<true, false>), dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
