@@ -110,14 +110,16 @@ struct alignas(8) TRec {
   // x[row][pc]: the transition from predecessor context pc, as a key
   // (score x16 + order idx) to add to that predecessor's state, with the
   // rows routed by the end context they reach:
-  //   R0  level 0 (end context 0): zero-token cost * lam16 + idx pc
   //   R1  level 1 or L0 >= 2: (nz token + level cost) * lam16 + distortion,
   //       idx 2pc for level L0, 2pc + 1 for level L0 + 1 (= 1 when L0 = 0)
   //   R2  level L0 + 1 >= 2 (idx 2pc + 1), all BIG when L0 = 0
-  // + BIG when that level is not a candidate
-  int64_t x[3][3];
+  // + BIG when that level is not a candidate.  The level-0 row R0 (end
+  // context 0: zero-token cost * lam16 + idx pc) depends only on the position
+  // and the segment's lambda: one table per macroblock and phase
+  // (Shared::r0, trellis_r0), not a row of every record.
+  int64_t x[2][3];
 };
-static_assert(sizeof(TRec) == 72, "TRec layout");
+static_assert(sizeof(TRec) == 48, "TRec layout");
 
 __constant__ uint16_t c_level_codes[134];
 __constant__ uint16_t c_fixed_i4[1000];
@@ -183,6 +185,7 @@ struct Shared {
   int mode_rate[4], mode_disto[4], uv_rate[4], uv_disto[4];
   int co_buf[16][16];      // transform coefficients handed to the trellis prep lanes
   TRec trec[6][16];        // trellis position records: I4 (half, candidate) / final I16 (diagonal slot)
+  int64_t r0[16][3];       // the phase's level-0 trellis row (trellis_r0)
   int l0s[6][16];          // per position: L0 << 3 | negative << 2 | min(L0, 2)
   alignas(16) int16_t cand_q[6][16];  // I4 candidates' levels for the lane-parallel token cost
   int cand_nz[6], cand_rate[6];
@@ -195,7 +198,15 @@ struct Shared {
   int s16_flag, post_best16, post_best_uv, post_nz_dc;
   uint64_t s16v, post_s16;
 };
-constexpr int WAVES = 4;  // waves (macroblock rows in flight) per workgroup
+constexpr int WAVES = 4;  // rows per band: the waves of a group (one wave a row)
+// Groups (bands in flight) per workgroup.  3 = 12-wave workgroups, one per
+// CU, three waves per SIMD (149 VGPRs, 161 KB of LDS): measured slower in the
+// bench than two 4-wave workgroups per CU ("Three waves per SIMD"),
+// so 1 is the default.
+#ifndef WG_ENC_GROUPS
+#define WG_ENC_GROUPS 1
+#endif
+constexpr int GROUPS = WG_ENC_GROUPS;
 
 __device__ __forceinline__ int ecost(const Tables& t, int p) { return t.ecost[p]; }
 __device__ __forceinline__ int bit_cost(const Tables& t, int bit, int p) { return t.ecost[bit ? 255 - p : p]; }
@@ -296,46 +307,24 @@ __device__ __forceinline__ int token_cost(const Tables& t, const QT& q, int nz_c
 // (level candidates, distortion deltas, token + level costs per predecessor
 // context) is computed by one lane per position into a TRec; the lane that
 // runs the serial DP then does only the 3 x 3 transitions per position.
-// Returns whether the position has a non-zero level under the neutral bias
-// (the reference's all-zero pre-scan).
+// R0, the level-0 row, is the same for every block of a phase
+// (trellis_r0).
+//
+// The R0 table of a phase: position n, predecessor context pc -> the
+// zero-token cost of band(n + 1) * lam16 + idx pc; lane 3n + pc writes it.
 template <int CTX_TYPE>
-__device__ __forceinline__ bool trellis_prep(const Tables& t, int co_z, int n, const SQuant& sq, int lam16, TRec& out,
-                                             int& l0s) {
-  constexpr int64_t BIG = 1ll << 59;
-  const int zig = zig_of(n), band = band_of(n + 1);
-  const int c0 = max(abs(co_z) + sq.sharpen[zig], 0);
-  const int quant = n == 0 ? sq.dc_quant : sq.quant;
-  const int iquant = n == 0 ? sq.dc_iquant : sq.iquant;
-  const int L0raw = (c0 * iquant) >> 17;
-  const int L0 = min(L0raw, 2047);
-  const int thresh = min((int)(((uint32_t)c0 * (uint32_t)iquant + 65536u) >> 17), 2047);
-  const bool has0 = L0 > 0 && L0 <= thresh;
-  const bool has1 = L0 + 1 <= 2047 && L0 + 1 <= thresh;
-  const int w4096 = t.wtr[zig] * 4096;
-  const int e0 = c0 - L0 * quant, e1 = c0 - (L0 + 1) * quant;
-  const int64_t A0 = (int64_t)t.lfixed[L0] * lam16 + (int64_t)w4096 * (e0 * e0 - c0 * c0) + (has0 ? 0 : BIG);
-  const int64_t A1 = (int64_t)t.lfixed[min(L0 + 1, 2047)] * lam16 + (int64_t)w4096 * (e1 * e1 - c0 * c0) + (has1 ? 0 : BIG);
-  const uint64_t vz = t.vcost[CTX_TYPE * 8 + band][0];
-  const uint64_t v0 = t.vcost[CTX_TYPE * 8 + band][min(L0, 67)], v1 = t.vcost[CTX_TYPE * 8 + band][min(L0 + 1, 67)];
-  // rows by end context: L0 = 0 sends level 1 (= L0 + 1) to context 1 and
-  // nothing to context 2; otherwise L0 -> R1, L0 + 1 -> R2 (trellis_dp4
-  // merges R1 into context 2 when L0 >= 2)
-  const bool z = L0 == 0;
-#pragma unroll
-  for (int pc = 0; pc < 3; pc++) {
-    const int64_t r1 = (int64_t)vc_of(v0, pc) * lam16 + A0 + 2 * pc;
-    const int64_t r2 = (int64_t)vc_of(v1, pc) * lam16 + A1 + 2 * pc + 1;
-    out.x[0][pc] = (int64_t)vc_of(vz, pc) * lam16 + pc;
-    out.x[1][pc] = z ? r2 : r1;
-    out.x[2][pc] = z ? BIG : r2;
+__device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16, int64_t (*r0)[3]) {
+  if (lane < 48) {
+    const int n = lane / 3, pc = lane - 3 * n;
+    r0[n][pc] = (int64_t)vc_of(t.vcost[CTX_TYPE * 8 + band_of(n + 1)][0], pc) * lam16 + pc;
   }
-  l0s = L0 << 3 | (co_z < 0 ? 4 : 0) | min(L0, 2);
-  return L0raw > 0;
 }
 
-// trellis_prep for two positions of one block at once, with the table reads
+// The level candidates, distortion deltas and token + level costs of two
+// positions of one block at once (returns whether either has a non-zero
+// level under the neutral bias: the reference's all-zero pre-scan), with the table reads
 // in two rounds: everything that depends on the position only (the
-// coefficient, sharpening, quantiser, distortion weight, level-0 token row),
+// coefficient, sharpening, quantiser, distortion weight),
 // then the level costs of L0 and L0 + 1.  The scheduling barriers keep each
 // round's reads issued together (left to itself the compiler waited on each
 // read before issuing the next: eight LDS round trips per lane instead of two).
@@ -346,16 +335,14 @@ __device__ __forceinline__ bool trellis_prep2(const Tables& t, const int* co, in
                                               TRec out[2], int l0s[2]) {
   constexpr int64_t BIG = 1ll << 59;
   int co_z[2], sh[2], quant[2], iquant[2], w4096[2];
-  uint64_t vz[2];
 #pragma unroll
   for (int j = 0; j < 2; j++) {
-    const int n = n0 + j, zig = zig_of(n), band = band_of(n + 1);
+    const int n = n0 + j, zig = zig_of(n);
     co_z[j] = n >= FIRST ? co[zig] : 0;
     sh[j] = sq.sharpen[zig];
     quant[j] = n == 0 ? sq.dc_quant : sq.quant;
     iquant[j] = n == 0 ? sq.dc_iquant : sq.iquant;
     w4096[j] = t.wtr[zig];
-    vz[j] = t.vcost[CTX_TYPE * 8 + band][0];
   }
   __builtin_amdgcn_sched_barrier(0);
   int c0[2], L0raw[2], L0[2], thresh[2], lf0[2], lf1[2];
@@ -387,9 +374,8 @@ __device__ __forceinline__ bool trellis_prep2(const Tables& t, const int* co, in
     for (int pc = 0; pc < 3; pc++) {
       const int64_t r1 = (int64_t)vc_of(v0[j], pc) * lam16 + A0 + 2 * pc;
       const int64_t r2 = (int64_t)vc_of(v1[j], pc) * lam16 + A1 + 2 * pc + 1;
-      out[j].x[0][pc] = (int64_t)vc_of(vz[j], pc) * lam16 + pc;
-      out[j].x[1][pc] = z ? r2 : r1;
-      out[j].x[2][pc] = z ? BIG : r2;
+      out[j].x[0][pc] = z ? r2 : r1;
+      out[j].x[1][pc] = z ? BIG : r2;
     }
     l0s[j] = L0[j] << 3 | (co_z[j] < 0 ? 4 : 0) | min(L0[j], 2);
     pnz |= L0raw[j] > 0 && n0 + j >= FIRST;
@@ -434,8 +420,8 @@ __device__ __forceinline__ int quad_bcast32(int v) {
 // chain: the quad's lane r writes positions 4r..4r+3 (raster) to q, and lane
 // 0 writes the zigzag nz count to *nz.
 template <int FIRST, int CTX_TYPE>
-__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int* l0s, int init_ctx, int lam16,
-                                            int k, int16_t* q, int* nz) {
+__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[3], const int* l0s,
+                                            int init_ctx, int lam16, int k, int16_t* q, int* nz) {
   constexpr int64_t BIG = 1ll << 59;
   init_ctx = min(init_ctx, 2);
   const int e = min(k, 2);
@@ -448,9 +434,12 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   int64_t best_terminal = (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16;
   int best_n = -1;
   uint32_t best_h = 0;
-  const int64_t* mine = &rec[0].x[e][0];
+  // this lane's row: R0 from the phase's table (3 words a position), R1 / R2
+  // from the block's records (6 words a position)
+  const int64_t* mine = e == 0 ? &r0[0][0] : &rec[0].x[e - 1][0];
+  const int STRIDE = e == 0 ? 3 : (int)(sizeof(TRec) / sizeof(int64_t));
   const uint16_t* eobp = &t.tok[CTX_TYPE * 8].eob[0] + tctx;
-  constexpr int STRIDE = sizeof(TRec) / sizeof(int64_t), TSTR = sizeof(TokRow) / 2;
+  constexpr int TSTR = sizeof(TokRow) / 2;
   // Position n's row, class and EOB cost are loaded during position n - 1
   // and pinned by the asm below, so no LDS round trip sits on the chain.
   int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
@@ -1047,8 +1036,21 @@ __device__ unsigned long long g_row_times[16384][4];
 #endif
 
 #ifndef WG_ENC_OCC
-#define WG_ENC_OCC 2  // waves per SIMD (VGPR budget 512 / occupancy)
+#define WG_ENC_OCC (WG_ENC_GROUPS == 3 ? 3 : 2)  // waves per SIMD (VGPR budget 512 / occupancy)
 #endif
+
+// The barrier of one group of WAVES waves inside a larger workgroup: each
+// wave's lane 0 counts itself in at *cnt (release) and waits until the whole
+// group has (acquire).  *gen is the wave's running target; every wave of the
+// group passes the same barriers.
+__device__ __forceinline__ void group_barrier(int* cnt, int& gen, int lane) {
+  gen += WAVES;
+  if (lane == 0) {
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gen) __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
 // TRELLIS: method >= 4 (trellis quantisation in the I4 RD and the final I16
 // residuals, encode_parallel.go:793, :1202); method 3 quantises plainly
 // (pickBestI4ModeRDParallel :842-929, QuantizeCoeffs at :1215).
@@ -1064,10 +1066,13 @@ __device__ unsigned long long g_row_times[16384][4];
 // roughly halves a macroblock's latency for launches whose rows fit the
 // wave slots twice over (one frame, C2); a full batch keeps one wave a row.
 template <bool TRELLIS, bool PAIR>
-__global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_rows(EncArgs a) {
-  constexpr int NW = PAIR ? 2 : WAVES;
+__global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC_OCC) void k_encode_rows(EncArgs a) {
+  constexpr int NW = PAIR ? 2 : WAVES * GROUPS;
   __shared__ Tables t_lds;
   __shared__ Shared s_waves[NW];
+  __shared__ int s_gbar[GROUPS];  // the groups' barrier counters (group_barrier)
+  static_assert(PAIR || sizeof(Tables) + NW * sizeof(Shared) + sizeof(s_gbar) <= 160 * 1024,
+                "the workgroup's LDS must fit one CU");
   Tables& t = t_lds;
   const int tid = threadIdx.x;
   constexpr int NT = 64 * NW;
@@ -1076,6 +1081,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
   for (int i = tid; i < 2048; i += NT) t.lfixed[i] = vp8_level_fixed_costs[i];
   for (int i = tid; i < 1000; i += NT) t.fixed_i4[i] = c_fixed_i4[i];
   if (tid < 16) t.wtr[tid] = c_wtrellis[tid];
+  if (tid < GROUPS) s_gbar[tid] = 0;
   for (int i = tid; i < 160; i += NT) t.pcode[i >> 4][i & 15] = kPred4Code[i >> 4][i & 15];
   __syncthreads();
   for (int i = tid; i < 4 * 8 * 68; i += NT) {
@@ -1117,16 +1123,21 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
 
   const bool use_order = a.order_tag[0] == (ORDER_TAG ^ a.n_img) && a.order_tag[1] == ~(ORDER_TAG ^ mbh);
   const int n_bands = (mbh + WAVES - 1) / WAVES;
+  // (not PAIR) this wave's group and its place in it
+  const int grp = wave / WAVES, gw = wave - WAVES * grp;
+  int gen = 0;
   for (;;) {
-    // PAIR: the workgroup's wave pair dequeues a row; otherwise the
-    // workgroup dequeues a BAND of WAVES consecutive rows of one image and
-    // wave w walks row WAVES * band + w.  The band's rows start staggered (each
-    // trails the one above by about two macroblocks) and finish together, so
-    // the workgroup leaves as soon as its band is done: with one row per wave
-    // dequeued independently, a workgroup with one row left held all four
-    // wave slots and its LDS through the launch's tail, and the next batch's
-    // launch could not start there (tools/enc_timeline.py).  One barrier after
-    // the dequeue (the next write of word is after the band's closing barrier).
+    // PAIR: the workgroup's wave pair dequeues a row; otherwise each group
+    // of WAVES waves dequeues a BAND of WAVES consecutive rows of one image
+    // and its wave w walks row WAVES * band + w.  The band's rows start
+    // staggered (each trails the one above by about two macroblocks) and
+    // finish together, so the group takes its next band as soon as this one
+    // is done, and the workgroup leaves when its groups find no band left:
+    // with one row per wave dequeued independently, a workgroup with one row
+    // left held all its wave slots and its LDS through the launch's tail, and
+    // the next batch's launch could not start there (tools/enc_timeline.py).
+    // A group barrier after the dequeue (the next write of word is after the
+    // band's closing barrier).
     int row, mby, img, ro;
     if constexpr (PAIR) {  // the pair dequeues together (the next write of word is two barriers on)
       if (tid == 0) s_waves[0].word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1137,15 +1148,17 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
       mby = ro / a.n_img;
       img = ro % a.n_img;
     } else {
-      if (tid == 0) s_waves[0].word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const int band = __builtin_amdgcn_readfirstlane(s_waves[0].word);
+      int& word = s_waves[WAVES * grp].word;
+      if (gw == 0 && lane == 0) word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (GROUPS == 1) __syncthreads();
+      else group_barrier(&s_gbar[grp], gen, lane);
+      const int band = __builtin_amdgcn_readfirstlane(word);
       if (band >= a.n_img * n_bands) break;
       const int bo = use_order ? __builtin_amdgcn_readfirstlane(a.border[band]) : band;  // band y * n_img + image
       img = bo % a.n_img;
-      mby = WAVES * (bo / a.n_img) + wave;
+      mby = WAVES * (bo / a.n_img) + gw;
       ro = mby * a.n_img + img;
-      row = WAVES * band + wave;
+      row = WAVES * band + gw;
     }
     const bool live = mby < mbh;  // (the last band of an image may have fewer rows)
 #ifdef WG_ROWTIMES
@@ -1322,9 +1335,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
       uint64_t s16 = ~0ull;
       if (isB) {
       // ================= I16 RD (pickBestI16ModeRDParallel :624-737) =================
-      // and UV RD (pickBestUVModeRDParallel :1030-1114) in one pass: the two
-      // are independent, and as one straight-line stream their dependency
-      // chains interleave instead of running back to back
+      // then UV RD (pickBestUVModeRDParallel :1030-1114)
       bool src_flat;
       {
         // isFlatSource16 (encode_analysis.go:358)
@@ -1352,44 +1363,16 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
         co[0] = 0;
         nz16 = quantize(co, q16, sg.y1, 1);
       }
-      // UV lane = (mode, plane, block) over lanes 0..31; lanes 32..63 repeat
-      // them (discarded) so that no branch splits the stream
-      const int ul = lane & 31, um = ul >> 3, uk = ul & 7, upl = uk >> 2, uub = uk & 3, uubx = uub & 1, uuby = uub >> 1;
-      P4 usrc, upred;
-      Q16 uq;
-      int unz;
-      {
-        const int base = upl ? VOFF : UOFF;
-        usrc = ld4(c.yin + base + 4 * uuby * BPS + 4 * uubx);
-        upred = predsq_p(check_mode(mbx, mby, um), c.yout + base, 8, 4 * uubx, 4 * uuby);
-        int co[16];
-        fdct_p(usrc, upred, co);
-        unz = quantize(co, uq, sg.uv, 0);
-      }
-      // left / top block of the same plane (only read when ubx / uby > 0): DPP row shifts
-      const int unzl = __builtin_amdgcn_update_dpp(0, unz, 0x111, 0xf, 0xf, false);  // row_shr:1
-      const int unzt = __builtin_amdgcn_update_dpp(0, unz, 0x112, 0xf, 0xf, false);  // row_shr:2
       // contexts from the neighbours' nz within the same mode
       // left / top neighbour within the mode's 16-lane row (only read when bx / by > 0): DPP row shifts
-      const int nz_left = __builtin_amdgcn_update_dpp(0, nz16, 0x111, 0xf, 0xf, false);  // row_shr:1
-      const int nz_top = __builtin_amdgcn_update_dpp(0, nz16, 0x114, 0xf, 0xf, false);   // row_shr:4
       {
+        const int nz_left = __builtin_amdgcn_update_dpp(0, nz16, 0x111, 0xf, 0xf, false);  // row_shr:1
+        const int nz_top = __builtin_amdgcn_update_dpp(0, nz16, 0x114, 0xf, 0xf, false);   // row_shr:4
         const int l = bx > 0 ? (nz_left > 0) : (int)((left_nz >> by) & 1);
         const int tp = by > 0 ? (nz_top > 0) : (int)((top_nz >> bx) & 1);
         const int ctx = min(l + tp, 2);
         int rate = token_cost(t, q16, nz16, 0, ctx, 1);
         rate = mvalid ? rate : 0;
-        int urate, usse, uacn = 0;
-        {
-          const int ul_ = uubx > 0 ? (unzl > 0) : (int)((left_nz >> (4 + 2 * upl + uuby)) & 1);
-          const int ut_ = uuby > 0 ? (unzt > 0) : (int)((top_nz >> (4 + 2 * upl + uubx)) & 1);
-          urate = token_cost(t, uq, unz, 2, min(ul_ + ut_, 2), 0);
-          int dq[16];
-          dequant(uq, dq, sg.uv);
-          usse = sse_p(usrc, recon_p(upred, dq));
-#pragma unroll
-          for (int i = 1; i < 16; i++) uacn += uq.get(i) != 0;
-        }
         bool acnz = false;
 #pragma unroll
         for (int i = 1; i < 16; i++) acnz |= q16.get(i) != 0;
@@ -1404,7 +1387,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
         const int td = sg.tlambda_sd > 0 ? tdisto_p(src16, rec16) : 0;
         const int rsum = group_sum_first<16>(rate), ssum = group_sum_first<16>(sse), tsum = group_sum_first<16>(td);  // used by lane b == 0
         const unsigned long long acmask = __ballot(acnz);
-        const int ursum = group_sum_first<8>(urate), ussum = group_sum_first<8>(usse), uasum = group_sum_first<8>(uacn);  // lane uk == 0
         if (b == 0 && mvalid) {
           const int total_rate = vp8_mode_fixed_cost16[m] + dccost + rsum;
           int disto = ssum;
@@ -1413,14 +1395,46 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
           s.mode_rate[m] = total_rate;
           s.mode_disto[m] = disto;
         }
+      }
+      // The UV RD after the I16 one, not interleaved with it: as one stream
+      // the two held 184 VGPRs at once (the kernel's peak), apart they fit the
+      // budget of three waves per SIMD.
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        // UV lane = (mode, plane, block) over lanes 0..31; lanes 32..63 repeat
+        // them (discarded) so that no branch splits the stream
+        const int ul = lane & 31, um = ul >> 3, uk = ul & 7, upl = uk >> 2, uub = uk & 3, uubx = uub & 1, uuby = uub >> 1;
+        const int base = upl ? VOFF : UOFF;
+        const P4 usrc = ld4(c.yin + base + 4 * uuby * BPS + 4 * uubx);
+        const P4 upred = predsq_p(check_mode(mbx, mby, um), c.yout + base, 8, 4 * uubx, 4 * uuby);
+        Q16 uq;
+        int unz;
+        {
+          int co[16];
+          fdct_p(usrc, upred, co);
+          unz = quantize(co, uq, sg.uv, 0);
+        }
+        // left / top block of the same plane (only read when ubx / uby > 0): DPP row shifts
+        const int unzl = __builtin_amdgcn_update_dpp(0, unz, 0x111, 0xf, 0xf, false);  // row_shr:1
+        const int unzt = __builtin_amdgcn_update_dpp(0, unz, 0x112, 0xf, 0xf, false);  // row_shr:2
+        const int ul_ = uubx > 0 ? (unzl > 0) : (int)((left_nz >> (4 + 2 * upl + uuby)) & 1);
+        const int ut_ = uuby > 0 ? (unzt > 0) : (int)((top_nz >> (4 + 2 * upl + uubx)) & 1);
+        const int urate = token_cost(t, uq, unz, 2, min(ul_ + ut_, 2), 0);
+        int dq[16];
+        dequant(uq, dq, sg.uv);
+        const int usse = sse_p(usrc, recon_p(upred, dq));
+        int uacn = 0;
+#pragma unroll
+        for (int i = 1; i < 16; i++) uacn += uq.get(i) != 0;
+        const int ursum = group_sum_first<8>(urate), ussum = group_sum_first<8>(usse), uasum = group_sum_first<8>(uacn);  // lane uk == 0
         if (lane < 32 && uk == 0) {
           int total = vp8_mode_fixed_cost_uv[um] + ursum;
           if (um > 0 && uasum <= 2) total += 140 * 8;
           s.uv_rate[um] = total;
           s.uv_disto[um] = ussum;
         }
-        lds_sync();
       }
+      lds_sync();
       {
         uint64_t best = ~0ull;
         for (int mm = 0; mm < 4; mm++) {
@@ -1475,6 +1489,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
           if (i < YUV / 4) reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
         }
       }
+      if constexpr (TRELLIS) trellis_r0<3>(t, lane, sg.tlambda_i4 * 16, s.r0);
       lds_sync();
       {
         // running totals over the finished blocks: rate, distortion and header
@@ -1587,7 +1602,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
               // the DP is the step's serial chain: let it win issue arbitration
               // against the SIMD's other wave while it runs
               __builtin_amdgcn_s_setprio(3);
-              trellis_dp4<0, 3>(t, s.trec[sl], s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
+              trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
               __builtin_amdgcn_s_setprio(2);
             } else if ((hl & 3) == 0) {
 #pragma unroll
@@ -1814,6 +1829,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
         // followed by the reference's raster-order resolution of the actual
         // contexts.  (Walking the 7 block diagonals took 7 prep + DP rounds.)
         const int lam16 = sg.tlambda_i16 * 16;
+        trellis_r0<0>(t, lane, lam16, s.r0);  // (read after the first round's lds_sync)
         int16_t* res_q = reinterpret_cast<int16_t*>(s.yout2);  // [16 tasks][16] levels (yout2 is free for I16 MBs)
         int* res_nz = reinterpret_cast<int*>(s.yout2 + 512);   // [16]
         for (int r = 0; r < 3; r++) {
@@ -1854,7 +1870,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
             if (tj >= 0) {
               if ((pnz_mask >> (8 * tj)) & 0xff) {
                 int nzv = 0;
-                trellis_dp4<1, 0>(t, s.trec[tj], s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
+                trellis_dp4<1, 0>(t, s.trec[tj], s.r0, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
                 if ((lane & 3) == 0) res_nz[q] = nzv;
               } else if ((lane & 3) == 0) {
 #pragma unroll
@@ -2157,7 +2173,11 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES), WG_ENC_OCC) void k_encode_
       }
     }
 #endif
-    if constexpr (!PAIR) __syncthreads();  // the band is done: the workgroup dequeues the next one together
+    // the band is done: the group dequeues the next one together
+    if constexpr (!PAIR) {
+      if constexpr (GROUPS == 1) __syncthreads();
+      else group_barrier(&s_gbar[grp], gen, lane);
+    }
   }
   ESTAMP_FLUSH();
 }
@@ -2387,7 +2407,7 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
     return wg::check_launch("hipMemsetAsync(encode ctl)");
   int cus = 0, per_cu = 0, per_cu_pair = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows<true, false>, 64 * WAVES, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows<true, false>, 64 * WAVES * GROUPS, 0) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pair, k_encode_rows<true, true>, 128, 0) != hipSuccess ||
       per_cu <= 0 || per_cu_pair <= 0)
     return wg::check_launch("encode occupancy query");
@@ -2406,12 +2426,13 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
     else
       hipLaunchKernelGGL((k_encode_rows<false, true>), dim3((unsigned)grid), dim3(128), 0, s, a);
   } else {
-    const int wgs = n_images * ((mbh + WAVES - 1) / WAVES);  // each workgroup dequeues bands of WAVES rows
+    // each group of a workgroup dequeues bands of WAVES rows
+    const int wgs = (n_images * ((mbh + WAVES - 1) / WAVES) + GROUPS - 1) / GROUPS;
     const int grid = wgs < per_cu * cus ? wgs : per_cu * cus;
     if (method >= 4)
-      hipLaunchKernelGGL((k_encode_rows<true, false>), dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
+      hipLaunchKernelGGL((k_encode_rows<true, false>), dim3((unsigned)grid), dim3(64 * WAVES * GROUPS), 0, s, a);
     else
-      hipLaunchKernelGGL((k_encode_rows<false, false>), dim3((unsigned)grid), dim3(64 * WAVES), 0, s, a);
+      hipLaunchKernelGGL((k_encode_rows<false, false>), dim3((unsigned)grid), dim3(64 * WAVES * GROUPS), 0, s, a);
   }
   return wg::check_launch("k_encode_rows");
 }
