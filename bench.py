@@ -68,6 +68,11 @@ CONTENTS = ("grad", "noise", "blobs")
 BITSTREAMS = os.path.join(ROOT, "tests", "golden", "q75_1080p.npz")
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 VALU_FILE = os.path.join(ROOT, "profiles", "pmc_valu.json")
+# SQ passes over one 64 x 1080p k_encode_rows launch (tools/gpu_enc_pmc.sh): wave
+# cycles, instruction mix, waits, LDS array cycles
+ENC_SQ_FILE = os.path.join(ROOT, "profiles", "enc_sq.json")
+CLOCK_HZ = 2.4e9  # MI355X_MICROARCH.md: shader clock
+SIMDS = 256 * 4
 # VALU issue peak: 256 CUs x 4 SIMDs, one 64-lane VALU instruction per SIMD
 # every 2 cycles (MI355X_MICROARCH.md), at the 2.4 GHz peak clock.
 VALU_PEAK_WINST_S = 256 * 4 * 0.5 * 2.4e9
@@ -100,6 +105,50 @@ def pmc_valu(kernel, launch_ms, step_ms):
             "peak": round(VALU_PEAK_WINST_S / 1e12, 4), "unit": "T wave-instr/s",
             "frac": round(rate / VALU_PEAK_WINST_S, 4), "source": os.path.relpath(VALU_FILE, ROOT),
             "frac_per_step": round(insts / (step_ms / 1e3) / VALU_PEAK_WINST_S, 4)}
+
+
+def slot_model(launch_ms, batch, enc_waves_per_simd=2):
+    """The encoder launch as wave-slot time: the wave cycles
+    one launch spends per macroblock (SQ_WAVE_CYCLES of the committed SQ pass,
+    quad-cycles x 4, waits included) x the macroblocks / the resident wave
+    slots / the clock, beside the measured launch; plus where a wave's cycles
+    go (issuing, waiting on LDS / memory, waiting for issue) and how busy the
+    HBM, VALU and LDS are.  None without the pass."""
+    try:
+        rec = json.load(open(ENC_SQ_FILE))["k_encode_rows"]
+    except (OSError, KeyError, ValueError):
+        return None
+    mbs = batch * MBW * MBH
+    wave_cyc = rec["SQ_WAVE_CYCLES"] * 4
+    slots = SIMDS * enc_waves_per_simd
+    launch_cyc = launch_ms / 1e3 * CLOCK_HZ
+    pred_ms = wave_cyc / slots / CLOCK_HZ * 1e3
+    return {
+        "source": os.path.relpath(ENC_SQ_FILE, ROOT),
+        "wave_cycles_per_mb": int(wave_cyc / mbs), "mbs_per_launch": mbs, "resident_wave_slots": slots,
+        "predicted_full_slots_ms": round(pred_ms, 3), "measured_launch_ms": round(launch_ms, 3),
+        "slot_fill": round(pred_ms / launch_ms, 3),
+        "wave_time": {"issuing": round(rec["SQ_ACTIVE_INST_ANY"] / rec["SQ_WAVE_CYCLES"], 3),
+                      "waiting_on_results": round(rec["SQ_WAIT_ANY"] / rec["SQ_WAVE_CYCLES"], 3),
+                      "waiting_for_issue": round(rec["SQ_WAIT_INST_ANY"] / rec["SQ_WAVE_CYCLES"], 3)},
+        "valu_busy": round(rec["SQ_INSTS_VALU"] * 2 / (SIMDS * launch_cyc), 3),
+        "lds_array_busy": round(rec["SQ_LDS_IDX_ACTIVE"] / (SIMDS / 4 * launch_cyc), 3),
+        "lds_bank_conflict_share": round(rec["SQ_LDS_BANK_CONFLICT"] / rec["SQ_LDS_IDX_ACTIVE"], 3),
+        "note": "slot_fill < 1 is the launch's ramp and tail (fewer rows than slots); per-wave time is issue + "
+                "LDS round trips of an in-order wave: a third wave per SIMD (tools/gpu_ab.sh, WG_ENC_GROUPS=3 / "
+                "WG_ENC_OCC=3) did not raise throughput",
+    }
+
+
+def bound_of(hbm_frac, model):
+    """roofline.bound from the measurements: 'hbm' when the kernel moves at
+    least half of HBM peak, else what the slot model says a wave is doing."""
+    if hbm_frac >= 0.5:
+        return "hbm"
+    if model is None:
+        return "latency"
+    return "issue+lds-latency (in-order waves; HBM %.3f, VALU %.2f, LDS array %.2f busy)" % (
+        hbm_frac, model["valu_busy"], model["lds_array_busy"])
 
 
 def parse():
@@ -579,6 +628,7 @@ def main():
         alg = BYTES_PER_PX[dominant] * px_rank_step
         achieved = alg / (iso[dominant] / 1e3) / 1e9
         traffic, traffic_src = pmc_traffic(kernel)
+        model = slot_model(iso[dominant], args.batch) if kernel == "k_encode_rows" else None
         rec = {
             "metric": "MPixels/s encode+decode DSP path (1920x1080 q75)",
             "value": round(value, 1),
@@ -607,7 +657,8 @@ def main():
             "runs": runs,
             "stage_ms_isolated": {k: round(v, 3) for k, v in iso.items()},
             "stage_ms_overlapped": {k: round(v, 3) for k, v in overlapped.items()},
-            "roofline": {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "roofline": {"kernel": kernel, "bound": bound_of(achieved / HBM_PEAK_GBS, model), "peak_kind": "hbm",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src, "bytes_per_px": BYTES_PER_PX[dominant],
                          "algorithmic_bytes_per_launch": int(alg),
@@ -621,8 +672,9 @@ def main():
                          "launches_in_flight": args.slots,
                          "isolated_vs_step": "the isolated launch is longer than ms_per_step because consecutive "
                                              "batches' launches overlap on their own streams",
-                         "limiter": "critical path of the macroblock wavefront (latency), not HBM: see critical_path "
-                                    "and valu"},
+                         "limiter": "wave-slot time per macroblock (instruction issue + LDS round trips of in-order "
+                                    "waves), not HBM: see slot_model, critical_path and valu",
+                         "slot_model": model},
             "stage_roofline": {k: {"kernel": KERNELS[k],
                                    "GB/s": round(BYTES_PER_PX[k] * px_rank_step / (v / 1e3) / 1e9, 1),
                                    "frac": round(BYTES_PER_PX[k] * px_rank_step / (v / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}

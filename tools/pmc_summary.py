@@ -51,8 +51,23 @@ def valu_json(out, paths):
     print(json.dumps(rec, indent=1))
 
 
+def any_json(out, paths):
+    """Per-kernel per-launch averages of every counter in the files."""
+    agg = load(paths)
+    rec = {}
+    for name, ctrs in agg.items():
+        if not name.startswith("k_"):
+            continue
+        rec[name] = {c: sum(v) / len(v) for c, v in ctrs.items()}
+        rec[name]["launches"] = max(len(v) for v in ctrs.values())
+    json.dump(rec, open(out, "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
 def main(argv):
     out = None
+    if argv and argv[0] == "--any-json":
+        return any_json(argv[1], argv[2:])
     if argv and argv[0] == "--valu-json":
         return valu_json(argv[1], argv[2:])
     if argv and argv[0] == "--json":

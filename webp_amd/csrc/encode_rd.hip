@@ -121,6 +121,13 @@ struct alignas(8) TRec {
 };
 static_assert(sizeof(TRec) == 48, "TRec layout");
 
+// two int16 values in one word (low = a)
+__device__ __forceinline__ uint32_t pack16(int a, int b) { return (uint32_t)(a & 0xffff) | (uint32_t)b << 16; }
+// four coefficients (each fits int16) into an 8-B aligned int16 row piece
+__device__ __forceinline__ void st_co4(int16_t* d, const int* c) {
+  *reinterpret_cast<uint2*>(d) = make_uint2(pack16(c[0], c[1]), pack16(c[2], c[3]));
+}
+
 __constant__ uint16_t c_level_codes[134];
 __constant__ uint16_t c_fixed_i4[1000];
 __constant__ int32_t c_wtrellis[16];
@@ -175,7 +182,6 @@ struct Tables {
 };
 // Per-wave state: each wave of the workgroup encodes its own macroblock row
 struct Shared {
-  Segment seg[4];  // the quantisers of the row's image (per-image segment tables)
   uint8_t yin[YUV], yout[YUV], yout2[YUV];
   alignas(16) int16_t coeffs[400];
   uint8_t mbtail[64];  // wg_mb_enc bytes 800..863, staged so the record leaves in one 16-B-per-lane store
@@ -183,10 +189,10 @@ struct Shared {
   uint8_t modes4[16];
   uint8_t nzy[16], nzuv[8];
   int mode_rate[4], mode_disto[4], uv_rate[4], uv_disto[4];
-  int co_buf[16][16];      // transform coefficients handed to the trellis prep lanes
+  alignas(16) int16_t co_buf[16][16];  // transform coefficients handed to the trellis prep lanes (|c| < 2^12)
   TRec trec[6][16];        // trellis position records: I4 (half, candidate) / final I16 (diagonal slot)
   int64_t r0[16][3];       // the phase's level-0 trellis row (trellis_r0)
-  int l0s[6][16];          // per position: L0 << 3 | negative << 2 | min(L0, 2)
+  int16_t l0s[6][16];      // per position: L0 << 3 | negative << 2 | min(L0, 2) (< 2^14)
   alignas(16) int16_t cand_q[6][16];  // I4 candidates' levels for the lane-parallel token cost
   int cand_nz[6], cand_rate[6];
   alignas(16) uint8_t pv[2][64];  // per half-wave: the I4 block's prediction value table
@@ -331,7 +337,7 @@ __device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16,
 // Positions below FIRST (the I16 AC blocks' DC) take a zero coefficient and
 // report no level.
 template <int CTX_TYPE, int FIRST>
-__device__ __forceinline__ bool trellis_prep2(const Tables& t, const int* co, int n0, const SQuant& sq, int lam16,
+__device__ __forceinline__ bool trellis_prep2(const Tables& t, const int16_t* co, int n0, const SQuant& sq, int lam16,
                                               TRec out[2], int l0s[2]) {
   constexpr int64_t BIG = 1ll << 59;
   int co_z[2], sh[2], quant[2], iquant[2], w4096[2];
@@ -420,7 +426,7 @@ __device__ __forceinline__ int quad_bcast32(int v) {
 // chain: the quad's lane r writes positions 4r..4r+3 (raster) to q, and lane
 // 0 writes the zigzag nz count to *nz.
 template <int FIRST, int CTX_TYPE>
-__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[3], const int* l0s,
+__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[3], const int16_t* l0s,
                                             int init_ctx, int lam16, int k, int16_t* q, int* nz) {
   constexpr int64_t BIG = 1ll << 59;
   init_ctx = min(init_ctx, 2);
@@ -1039,6 +1045,12 @@ __device__ unsigned long long g_row_times[16384][4];
 #define WG_ENC_OCC (WG_ENC_GROUPS == 3 ? 3 : 2)  // waves per SIMD (VGPR budget 512 / occupancy)
 #endif
 
+// An image's four segment tables (4 x 224 B = 56 x 16 B) into LDS
+__device__ __forceinline__ void load_segments(const EncArgs& a, int img, Segment* dst, int lane) {
+  const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.segs) + img * a.segs_pitch);
+  if (lane < 56) reinterpret_cast<uint4*>(dst)[lane] = src[lane];
+}
+
 // The barrier of one group of WAVES waves inside a larger workgroup: each
 // wave's lane 0 counts itself in at *cnt (release) and waits until the whole
 // group has (acquire).  *gen is the wave's running target; every wave of the
@@ -1071,7 +1083,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
   __shared__ Tables t_lds;
   __shared__ Shared s_waves[NW];
   __shared__ int s_gbar[GROUPS];  // the groups' barrier counters (group_barrier)
-  static_assert(PAIR || sizeof(Tables) + NW * sizeof(Shared) + sizeof(s_gbar) <= 160 * 1024,
+  // the quantisers of the image a group's band (PAIR: the pair's row) belongs to
+  __shared__ Segment s_seg[PAIR ? 1 : GROUPS][4];
+  static_assert(PAIR || sizeof(Tables) + NW * sizeof(Shared) + sizeof(s_gbar) + sizeof(s_seg) <= 160 * 1024,
                 "the workgroup's LDS must fit one CU");
   Tables& t = t_lds;
   const int tid = threadIdx.x;
@@ -1149,7 +1163,15 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       img = ro % a.n_img;
     } else {
       int& word = s_waves[WAVES * grp].word;
-      if (gw == 0 && lane == 0) word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (gw == 0) {  // the group's leader dequeues and fetches the band's image's segments
+        if (lane == 0) word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lds_sync();
+        const int band = __builtin_amdgcn_readfirstlane(word);
+        if (band < a.n_img * n_bands) {
+          const int bo = use_order ? __builtin_amdgcn_readfirstlane(a.border[band]) : band;
+          load_segments(a, bo % a.n_img, s_seg[grp], lane);
+        }
+      }
       if constexpr (GROUPS == 1) __syncthreads();
       else group_barrier(&s_gbar[grp], gen, lane);
       const int band = __builtin_amdgcn_readfirstlane(word);
@@ -1173,10 +1195,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
     uint8_t* top = a.top + (int64_t)img * mbw * REC;
     int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
     int* prog_mine = a.progress + (int64_t)img * mbh + mby;
-    if (live) {  // this image's four segments (4 x 224 B = 56 x 16 B)
-      const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.segs) + img * a.segs_pitch);
-      if (lane < 56) reinterpret_cast<uint4*>(s.seg)[lane] = src[lane];
-    }
+    if (PAIR && isA) load_segments(a, img, s_seg[0], lane);  // (B reads them after the MB's first join barrier)
     // left context (encodeRow :257-282)
     if (lane < 16) s.yout[YOFF - 1 + lane * BPS] = 129;
     else if (lane < 24) s.yout[UOFF - 1 + (lane - 16) * BPS] = 129;
@@ -1231,7 +1250,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       if (isA) wait_above(mbx + 1);
       ESTAMP(1);
       const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
-      const Segment& sg = s.seg[segid];
+      const Segment& sg = s_seg[PAIR ? 0 : grp][segid];
       uint32_t top_nz = 0, top_modes = 0;
       int top_nz_dc = 0;
       if (isA) {
@@ -1565,7 +1584,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             fdct(src, pred, co);
             if constexpr (TRELLIS) {
 #pragma unroll
-              for (int i = 0; i < 16; i++) s.co_buf[slot][i] = co[i];
+              for (int i = 0; i < 4; i++) st_co4(&s.co_buf[slot][4 * i], co + 4 * i);
             } else {  // method 3: QuantizeCoeffs (pickBestI4ModeRDParallel :890)
               int16_t q[16];
               s.cand_nz[slot] = quantize(co, q, sg.y1, 0);
@@ -1649,7 +1668,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             }
             rec_row = pack4(rr[0], rr[1], rr[2], rr[3]);
             // tTransform row pass (ssim.go:266-304) of the reconstruction and the source
-            int* th = &s.co_buf[2 * qsl][0] + 8 * qr;  // co_buf is free again after the trellis prep
+            int16_t* th = &s.co_buf[2 * qsl][0] + 8 * qr;  // co_buf is free again after the trellis prep
             int4 tr, ts;
             {
               const int a0 = rr[0] + rr[2], a1 = rr[1] + rr[3], a2 = rr[1] - rr[3], a3 = rr[0] - rr[2];
@@ -1660,8 +1679,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               ts = make_int4(a0 + a1, a3 + a2, a3 - a2, a0 - a1);
             }
             if (qact) {
-              reinterpret_cast<int4*>(th)[0] = tr;
-              reinterpret_cast<int4*>(th)[1] = ts;
+              reinterpret_cast<uint2*>(th)[0] = make_uint2(pack16(tr.x, tr.y), pack16(tr.z, tr.w));  // |values| <= 1020
+              reinterpret_cast<uint2*>(th)[1] = make_uint2(pack16(ts.x, ts.y), pack16(ts.z, ts.w));
             }
 #pragma unroll
             for (int i = 1; i < 16; i++) cnt += qv[i] != 0;
@@ -1669,7 +1688,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           lds_sync();
           int wrec = 0, wsrc = 0;  // weighted column sums of column qr
           {
-            const int* tx = &s.co_buf[2 * qsl][0];
+            const int16_t* tx = &s.co_buf[2 * qsl][0];
             int cr[4], cs[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -1805,7 +1824,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           fdct(src, pred, co);
           if constexpr (TRELLIS) {
 #pragma unroll
-            for (int i = 1; i < 16; i++) s.co_buf[lane][i] = co[i];
+            for (int i = 0; i < 4; i++) st_co4(&s.co_buf[lane][4 * i], co + 4 * i);  // ([0], the DC, is not read)
           } else {  // method 3: the AC levels by QuantizeCoeffs (encodeI16ResidualsParallel :1215)
             int16_t q[16];
             s.nzy[lane] = (uint8_t)quantize(co, q, sg.y1, 1);
