@@ -160,9 +160,12 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget for the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--slots", type=int, default=3, help="batches in flight (two HIP streams each)")
-    p.add_argument("--split", action="store_true",
-                   help="run each batch's decode side on a second stream beside its encode side (A/B: "
-                        "6,152 / 5,905 vs 6,025 / 6,177 MPix/s without, within run-to-run noise)")
+    p.add_argument("--no-split", dest="split", action="store_false",
+                   help="run each batch's decode side after its encode side on the batch's one stream instead of "
+                        "on a second stream beside it (round 4, tools/gpu_bench_cfg.sh, 3 alternations: split "
+                        "6,470-6,697 mean / 6,387-6,446 median MPix/s, one stream 6,374-6,389 / 6,208-6,401: with one "
+                        "stream a batch's next encode waits behind its own decode, which runs slowly beside the "
+                        "other batches' encodes, and the GPU idles at the ends of the decodes)")
     p.add_argument("--iso-steps", type=int, default=2, help="untimed one-batch passes for the isolated kernel times")
     p.add_argument("--no-gather", action="store_true",
                    help="with N > 1, skip the gather of the last batch's outputs to rank 0 (timed apart from value)")
