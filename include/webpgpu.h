@@ -522,9 +522,10 @@ int wg_alpha_filter(int32_t filter, const uint8_t* in, uint8_t* out, int32_t wid
                     int32_t n_images, void* stream);
 
 /* alphaUnfilterHorizontal / Vertical / Gradient (alpha.go:128-203), in place.
- * work: wg_alpha_unfilter_work_bytes(height, n_images) device bytes (gradient
- * only: band dequeue + progress counters; zeroed by the call). */
-size_t wg_alpha_unfilter_work_bytes(int32_t height, int32_t n_images);
+ * work: wg_alpha_unfilter_work_bytes(width, height, n_images) device bytes,
+ * 16-B aligned (gradient only: band dequeue, progress counters and the bands'
+ * hand-off rows; zeroed by the call). */
+size_t wg_alpha_unfilter_work_bytes(int32_t width, int32_t height, int32_t n_images);
 int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, int32_t height, int64_t pitch, int32_t n_images,
                       void* work, void* stream);
 /* synchronises `stream`; WG_EHIP if a gradient band wait timed out */

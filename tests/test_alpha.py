@@ -394,9 +394,31 @@ def test_gpu_unfilter_fast_path_bands(cuda):
     segmented vertical scan: several chunks and bands, ragged last band."""
     from webp_amd import alpha as A
     for f in (2, 3):
-        for i, (h, w) in enumerate([(64 * 5 + 2, 320), (129, 256), (2, 64), (700, 4096 // 8), (18, 16)]):
+        for i, (h, w) in enumerate([(64 * 5 + 2, 320), (129, 256), (2, 64), (700, 4096 // 8), (18, 16), (66, 64),
+                                    (64 * 3 + 1, 80), (1025, 1024), (2, 4096), (200, 4096 + 16)]):
             r = np.stack([plane(h, w, 300 + 5 * i + k) for k in range(3)])
             want = np.stack([O.alpha_unfilter(f, x) for x in r])
             d = _t(r, cuda)
             A.alpha_unfilter(f, d, check=True)
             assert (d.cpu().numpy() == want).all(), (f, h, w)
+
+
+@pytest.mark.gpu
+def test_gpu_gradient_unfilter_both_walks(cuda, monkeypatch):
+    """The register-resident diagonal walk (k_alpha_gdiag, 16-B widths >= 64)
+    and the LDS-staged one it replaced (k_alpha_gbands, forced by
+    WG_ALPHA_GBANDS) give the oracle's planes; every 16-step chunk offset,
+    ragged last bands, a 1-row last band, and 4096-wide rows."""
+    from webp_amd import alpha as A
+    shapes = [(66, 64), (130, 96), (64 * 4 + 1, 4096), (64 + 17, 2048 + 48)]
+    for use_old in (False, True):
+        if use_old:
+            monkeypatch.setenv("WG_ALPHA_GBANDS", "1")
+        else:
+            monkeypatch.delenv("WG_ALPHA_GBANDS", raising=False)
+        for i, (h, w) in enumerate(shapes):
+            r = np.stack([plane(h, w, 700 + 3 * i + k) for k in range(2)])
+            want = np.stack([O.alpha_unfilter(3, x) for x in r])
+            d = _t(r, cuda)
+            A.alpha_unfilter(3, d, check=True)
+            assert (d.cpu().numpy() == want).all(), (use_old, h, w, np.argwhere(d.cpu().numpy() != want)[:4])

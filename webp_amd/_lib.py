@@ -93,7 +93,7 @@ SIGNATURES = {
     "wg_vp8l_color_space_inverse": [_vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _vp],
     "wg_vp8l_color_index_inverse": [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp],
     "wg_alpha_filter": [_i32, _vp, _vp, _i32, _i32, _i64, _i32, _vp],
-    "wg_alpha_unfilter_work_bytes": [_i32, _i32],
+    "wg_alpha_unfilter_work_bytes": [_i32, _i32, _i32],
     "wg_alpha_unfilter": [_i32, _vp, _i32, _i32, _i64, _i32, _vp, _vp],
     "wg_alpha_unfilter_status": [_vp, _vp],
     "wg_alpha_estimate_work_bytes": [_i32],

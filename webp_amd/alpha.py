@@ -46,7 +46,7 @@ def alpha_unfilter(filter_, planes, check=False):
     """In place; check=True synchronises and raises if a gradient band wait timed out."""
     p = _planes(planes)
     n, h, w = p.shape
-    work = torch.empty(max(lib.wg_alpha_unfilter_work_bytes(h, n), 16), dtype=torch.uint8, device=p.device)
+    work = torch.empty(max(lib.wg_alpha_unfilter_work_bytes(w, h, n), 16), dtype=torch.uint8, device=p.device)
     call("wg_alpha_unfilter", filter_, p.data_ptr(), w, h, h * w, n, work.data_ptr(), _stream())
     if check and filter_ == GRADIENT and h > 1:
         call("wg_alpha_unfilter_status", work.data_ptr(), _stream())

@@ -376,6 +376,180 @@ __global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
   }
 }
 
+// Gradient unfilter below row 0, fast path (w % 16 == 0, w >= 64, 16-B
+// aligned rows and images).  The same band / diagonal walk as
+// k_alpha_gbands (lane k owns row 1 + 64b + k at x = s - k; the row above by
+// a whole-wave DPP shift), with the per-step work in registers:
+//  - each lane's residual bytes come in 16-step chunks as one 32-B aligned
+//    load pair, two chunks ahead, and are cut to the lane's 16-byte window
+//    (offset (-k) & 15, fixed per lane) with selects + v_alignbyte, so a step
+//    reads no memory;
+//  - lane 0's row above (the band above's last row) arrives as 4-pixel
+//    granules {pixels, tag} that the band above's last lane stores with one
+//    8-B write-through store each, as soon as it has made them (no progress
+//    counter, no store drain); lane 0 loads a chunk's five granules two
+//    chunks ahead and re-polls only if a tag is still clear;
+//  - outputs go to the LDS ring (one byte store a step, off the chain) and
+//    back to the frame 64 columns at a time, as in k_alpha_gbands.
+// Band 0's row above is row 0 (already unfiltered by k_alpha_scan_edge).
+constexpr int GD_CH = 16;  // steps per chunk
+
+struct GdArgs {
+  uint8_t* data;
+  int* ctl;        // [0] band dequeue, [1] error
+  int* diag;       // wg::diag_words + DIAG_ALPHA
+  uint64_t* hand;  // [n_img][bands][w / 4] granules {4 pixels, tag}
+  int64_t pitch;
+  int w, h, bands, n_img;
+};
+
+__device__ __forceinline__ int byte_at(uint32_t v, int i) { return (int)((v >> (8 * i)) & 0xff); }
+
+__global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[64 * GB_STRIDE];
+  __shared__ int sh_band;
+  const int lane = threadIdx.x;
+  const int w = a.w, gw = w >> 2;
+  const int total = a.bands * a.n_img;
+  uint8_t* my_ring = ring + lane * GB_STRIDE;
+  // the lane's window within a 16-B aligned 32-B load: chunk starts are
+  // multiples of 16, so (s0 - k) & 15 = (-k) & 15
+  const int o = (-lane) & 15, q = o >> 2, rsh = o & 3;
+  for (;;) {
+    if (lane == 0) sh_band = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int idx = __builtin_amdgcn_readfirstlane(sh_band);
+    __syncthreads();
+    if (idx >= total) break;
+    const int band = idx / a.n_img, img = idx % a.n_img;
+    const int y = 1 + band * 64 + lane;
+    const bool live = y < a.h;
+    uint8_t* d = a.data + img * a.pitch;
+    uint8_t* my_row = d + (int64_t)min(y, a.h - 1) * w;
+    const int last_lane = min(63, a.h - 2 - band * 64);
+    const uint64_t* hand_above = a.hand + ((int64_t)img * a.bands + band - 1) * gw;  // band > 0
+    uint64_t* hand_mine = a.hand + ((int64_t)img * a.bands + band) * gw;
+    const bool hands_off = band + 1 < a.bands;
+    const int nch = (w + last_lane + GD_CH - 1) / GD_CH;
+    // residual bytes of chunk s0: the 32 aligned bytes holding x = s0 - k ..
+    // s0 - k + 15 (rows >= 1, w >= 64: the start is inside the image; the
+    // end is clamped, and only x >= w can read the clamped bytes)
+    auto ld_res = [&](int s0, uint4& lo, uint4& hi) {
+      const int a16 = s0 - lane - o;
+      lo = *reinterpret_cast<const uint4*>(my_row + min(a16, w - 16));
+      hi = *reinterpret_cast<const uint4*>(my_row + min(a16 + 16, w - 16));
+    };
+    auto window = [&](const uint4& lo, const uint4& hi, uint32_t R[4]) {
+      const uint32_t D[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      uint32_t S[5];
+#pragma unroll
+      for (int i = 0; i < 5; i++) S[i] = q == 0 ? D[i] : (q == 1 ? D[i + 1] : (q == 2 ? D[i + 2] : D[i + 3]));
+#pragma unroll
+      for (int j = 0; j < 4; j++) R[j] = __builtin_amdgcn_alignbyte(S[j + 1], S[j], rsh);
+    };
+    // lane 0's row above for chunk s0: columns s0 - 4 .. s0 + 15, five granules
+    auto ld_up = [&](int s0, uint64_t U[5]) {
+#pragma unroll
+      for (int t = 0; t < 5; t++) {
+        const int g = min(max((s0 >> 2) - 1 + t, 0), gw - 1);
+        U[t] = band > 0 ? __hip_atomic_load(hand_above + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : (1ull << 32 | *reinterpret_cast<const uint32_t*>(d + 4 * g));
+      }
+    };
+    uint4 lo1, hi1, lo2, hi2;
+    uint32_t R[4];
+    {
+      uint4 lo0, hi0;
+      ld_res(0, lo0, hi0);
+      window(lo0, hi0, R);
+    }
+    ld_res(GD_CH, lo1, hi1);
+    ld_res(2 * GD_CH, lo2, hi2);
+    uint64_t U0[5], U1[5], U2[5];
+    ld_up(0, U0);
+    ld_up(GD_CH, U1);
+    ld_up(2 * GD_CH, U2);
+    int o1 = 0, o2 = 0;  // this lane's outputs at x - 1, x - 2
+    int pub = 0;         // granules of the band's last row published
+    for (int m = 0; m < nch; m++) {
+      const int s0 = m * GD_CH;
+      if ((s0 & 63) == 0 && s0 >= 128 && live) gb_chunk_io(my_ring, my_row, s0 - 128, w, true, true);  // every lane is past it
+      if (band > 0) {  // the row above: re-poll the granules whose tag is still clear
+        bool ready = true;
+#pragma unroll
+        for (int t = 0; t < 5; t++) ready &= __builtin_amdgcn_readfirstlane((int)(U0[t] >> 32)) != 0;
+        if (!ready) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          for (uint32_t it = 0;; it++) {
+            __builtin_amdgcn_s_sleep(1);
+            ld_up(s0, U0);
+            ready = true;
+#pragma unroll
+            for (int t = 0; t < 5; t++) ready &= __builtin_amdgcn_readfirstlane((int)(U0[t] >> 32)) != 0;
+            if (ready) break;
+            if ((it & 15) == 15 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+                                    __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+              if (lane == 0) {
+                __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                wg::note_timeout(a.diag, s0, band, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0);
+              }
+              break;
+            }
+          }
+        }
+      }
+      uint32_t UP[5];
+#pragma unroll
+      for (int t = 0; t < 5; t++) UP[t] = (uint32_t)U0[t];
+#pragma unroll
+      for (int u = 0; u < GD_CH; u++) {
+        const int x = s0 + u - lane;
+        const int res = byte_at(R[u >> 2], u & 3);
+        // row above at x and x - 1: lane k - 1's newest and previous outputs
+        // (wave_shr:1); lane 0 keeps the band above's row (update_dpp's old)
+        int top = __builtin_amdgcn_update_dpp(byte_at(UP[1 + (u >> 2)], u & 3), o1, 0x138, 0xf, 0xf, false);
+        int tl = __builtin_amdgcn_update_dpp(byte_at(UP[(u + 3) >> 2], (u + 3) & 3), o2, 0x138, 0xf, 0xf, false);
+        // x == 0: left = top_left = top (alpha.go:177-181)
+        const int left = x == 0 ? top : o1;
+        tl = x == 0 ? top : tl;
+        const int v = (res + clip255(left + top - tl)) & 0xff;
+        const bool valid = live && (unsigned)x < (unsigned)w;
+        o2 = o1;
+        o1 = valid ? v : 0;
+        if (valid) my_ring[x & 127] = (uint8_t)v;
+      }
+      // the band's last row, 4 pixels at a time, for the band below
+      if (hands_off) {
+        const int done = min(max((s0 + GD_CH - last_lane) >> 2, 0), gw);
+        for (int g = pub; g < done; g++) {
+          if (lane == last_lane) {
+            const uint32_t px = *reinterpret_cast<const uint32_t*>(my_ring + ((4 * g) & 127));
+            __hip_atomic_store(hand_mine + g, 1ull << 32 | px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        pub = max(pub, done);
+      }
+      // next chunk's inputs; prefetch two ahead
+      window(lo1, hi1, R);
+      lo1 = lo2;
+      hi1 = hi2;
+      ld_res(s0 + 3 * GD_CH, lo2, hi2);
+#pragma unroll
+      for (int t = 0; t < 5; t++) {
+        U0[t] = U1[t];
+        U1[t] = U2[t];
+      }
+      ld_up(s0 + 3 * GD_CH, U2);
+    }
+    // the last two 64-column blocks (or one) have not been stored yet
+    const int chunks = (w + 63) >> 6;
+    if (live)
+      for (int m = max(0, chunks - 2); m < chunks; m++) gb_chunk_io(my_ring, my_row, m * 64, w, true, true);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // the ring is reused by the next band this wave dequeues
+  }
+}
+
 // -------------------------------------------------------------- estimate
 // estimateBestFilter's bins split by dependence: the "none" bin follows a
 // running mean along each sampled row (serial per row: one lane per row,
@@ -656,10 +830,16 @@ extern "C" int wg_alpha_filter(int32_t filter, const uint8_t* in, uint8_t* out, 
   return wg::check_launch("k_alpha_filter");
 }
 
-extern "C" size_t wg_alpha_unfilter_work_bytes(int32_t height, int32_t n_images) {
-  if (height <= 0 || n_images <= 0) return 0;
+// work: ctl[4] | progress[n_img * bands] (k_alpha_gbands) | hand-off granules
+// [n_img][bands][width / 4] (k_alpha_gdiag), 16-B aligned
+static size_t gd_hand_offset(int32_t height, int32_t n_images) {
   const int bands = (height - 1 + 63) / 64;
-  return sizeof(int) * (4 + (size_t)n_images * (bands > 0 ? bands : 1));
+  return (sizeof(int) * (4 + (size_t)n_images * (bands > 0 ? bands : 1)) + 15) & ~(size_t)15;
+}
+extern "C" size_t wg_alpha_unfilter_work_bytes(int32_t width, int32_t height, int32_t n_images) {
+  if (width <= 0 || height <= 0 || n_images <= 0) return 0;
+  const int bands = (height - 1 + 63) / 64;
+  return gd_hand_offset(height, n_images) + sizeof(uint64_t) * (size_t)n_images * (bands > 0 ? bands : 1) * ((width + 3) / 4);
 }
 
 extern "C" int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, int32_t height, int64_t pitch,
@@ -693,6 +873,32 @@ extern "C" int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, i
     return wg::check_launch("k_alpha_vcols");
   }
   WG_REQUIRE(work);
+  WG_REQUIRE((reinterpret_cast<uintptr_t>(work) & 15) == 0);
+  if (hipMemsetAsync(work, 0, wg_alpha_unfilter_work_bytes(width, height, n_images), s) != hipSuccess)
+    return wg::check_launch("hipMemsetAsync(alpha work)");
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return wg::check_launch("device query");
+  const int bands = (height - 1 + 63) / 64;
+  const int total = bands * n_images;
+  const int grid = total < 4 * cus ? total : 4 * cus;
+  if ((width & 15) == 0 && width >= 64 && (pitch & 15) == 0 && (reinterpret_cast<uintptr_t>(data) & 15) == 0 &&
+      !getenv("WG_ALPHA_GBANDS")) {
+    GdArgs g;
+    g.data = data;
+    g.ctl = static_cast<int*>(work);
+    g.diag = wg::diag_words(s);
+    if (!g.diag) return WG_EHIP;
+    g.diag += wg::DIAG_ALPHA;
+    g.hand = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(work) + gd_hand_offset(height, n_images));
+    g.pitch = pitch;
+    g.w = width;
+    g.h = height;
+    g.bands = bands;
+    g.n_img = n_images;
+    hipLaunchKernelGGL(k_alpha_gdiag, dim3(grid), dim3(64), 0, s, g);
+    return wg::check_launch("k_alpha_gdiag");
+  }
   GArgs a;
   a.data = data;
   a.ctl = static_cast<int*>(work);
@@ -703,15 +909,8 @@ extern "C" int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, i
   a.pitch = pitch;
   a.w = width;
   a.h = height;
-  a.bands = (height - 1 + 63) / 64;
+  a.bands = bands;
   a.n_img = n_images;
-  if (hipMemsetAsync(work, 0, wg_alpha_unfilter_work_bytes(height, n_images), s) != hipSuccess)
-    return wg::check_launch("hipMemsetAsync(alpha work)");
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return wg::check_launch("device query");
-  const int total = a.bands * n_images;
-  const int grid = total < 4 * cus ? total : 4 * cus;
   hipLaunchKernelGGL(k_alpha_gbands, dim3(grid), dim3(64), 0, s, a);
   return wg::check_launch("k_alpha_gbands");
 }
