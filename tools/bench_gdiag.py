@@ -11,7 +11,7 @@ import torch  # noqa: E402
 from webp_amd import alpha as A  # noqa: E402
 
 W = int(os.environ.get("W", "4096"))
-for h in (65, 129, 257, 513, 1025, 2049, 4096):
+for h in [int(v) for v in os.environ.get("HS", "65,129,257,513,1025,2049,4096").split(",")]:
     r = torch.randint(0, 256, (1, h, W), dtype=torch.uint8, device="cuda")
     work = r.clone()
     ts = []

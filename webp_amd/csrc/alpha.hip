@@ -439,13 +439,23 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
       lo = *reinterpret_cast<const uint4*>(my_row + min(a16, w - 16));
       hi = *reinterpret_cast<const uint4*>(my_row + min(a16 + 16, w - 16));
     };
-    auto window = [&](const uint4& lo, const uint4& hi, uint32_t R[4]) {
+    // (x < 0 residuals read as 0: every output left of column 0 is then 0,
+    // which makes x == 0's left = top_left = top rule hold with no select)
+    auto window = [&](int s0, const uint4& lo, const uint4& hi, uint32_t R[4]) {
       const uint32_t D[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       uint32_t S[5];
 #pragma unroll
       for (int i = 0; i < 5; i++) S[i] = q == 0 ? D[i] : (q == 1 ? D[i + 1] : (q == 2 ? D[i + 2] : D[i + 3]));
 #pragma unroll
       for (int j = 0; j < 4; j++) R[j] = __builtin_amdgcn_alignbyte(S[j + 1], S[j], rsh);
+      if (s0 < 64) {  // bytes u with s0 + u - k < 0 (the band's first chunks)
+        const int t = lane - s0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int sh = t - 4 * j;  // the first kept byte of dword j
+          R[j] = sh <= 0 ? R[j] : (sh >= 4 ? 0u : R[j] & (0xffffffffu << (8 * sh)));
+        }
+      }
     };
     // lane 0's row above for chunk s0: columns s0 - 4 .. s0 + 15, five granules
     auto ld_up = [&](int s0, uint64_t U[5]) {
@@ -461,7 +471,7 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
     {
       uint4 lo0, hi0;
       ld_res(0, lo0, hi0);
-      window(lo0, hi0, R);
+      window(0, lo0, hi0, R);
     }
     ld_res(GD_CH, lo1, hi1);
     ld_res(2 * GD_CH, lo2, hi2);
@@ -501,22 +511,35 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
       uint32_t UP[5];
 #pragma unroll
       for (int t = 0; t < 5; t++) UP[t] = (uint32_t)U0[t];
+      if (s0 == 0) UP[0] = 0;  // column -1 (x == 0's top_left is its top: 0 - 0 cancels)
+      // x == 0: left = top_left = top (alpha.go:177-181).  Outputs left of
+      // column 0 are 0 (zero residuals, zero row above: see window), so there
+      // left - top_left = 0 and the plain formula gives top.
+      const int xb = s0 - lane;
+      if (s0 + GD_CH <= w) {  // every lane's x < w: the ring takes every byte (x < 0 ones are rewritten later)
 #pragma unroll
-      for (int u = 0; u < GD_CH; u++) {
-        const int x = s0 + u - lane;
-        const int res = byte_at(R[u >> 2], u & 3);
-        // row above at x and x - 1: lane k - 1's newest and previous outputs
-        // (wave_shr:1); lane 0 keeps the band above's row (update_dpp's old)
-        int top = __builtin_amdgcn_update_dpp(byte_at(UP[1 + (u >> 2)], u & 3), o1, 0x138, 0xf, 0xf, false);
-        int tl = __builtin_amdgcn_update_dpp(byte_at(UP[(u + 3) >> 2], (u + 3) & 3), o2, 0x138, 0xf, 0xf, false);
-        // x == 0: left = top_left = top (alpha.go:177-181)
-        const int left = x == 0 ? top : o1;
-        tl = x == 0 ? top : tl;
-        const int v = (res + clip255(left + top - tl)) & 0xff;
-        const bool valid = live && (unsigned)x < (unsigned)w;
-        o2 = o1;
-        o1 = valid ? v : 0;
-        if (valid) my_ring[x & 127] = (uint8_t)v;
+        for (int u = 0; u < GD_CH; u++) {
+          const int res = byte_at(R[u >> 2], u & 3);
+          // row above at x and x - 1: lane k - 1's newest and previous outputs
+          // (wave_shr:1); lane 0 keeps the band above's row (update_dpp's old)
+          const int top = __builtin_amdgcn_update_dpp(byte_at(UP[1 + (u >> 2)], u & 3), o1, 0x138, 0xf, 0xf, false);
+          const int tl = __builtin_amdgcn_update_dpp(byte_at(UP[(u + 3) >> 2], (u + 3) & 3), o2, 0x138, 0xf, 0xf, false);
+          const int v = (res + clip255(o1 + top - tl)) & 0xff;
+          o2 = o1;
+          o1 = v;
+          my_ring[(xb + u) & 127] = (uint8_t)v;
+        }
+      } else {  // the band's last chunks: bytes past the row end go to the pad byte
+#pragma unroll
+        for (int u = 0; u < GD_CH; u++) {
+          const int res = byte_at(R[u >> 2], u & 3);
+          const int top = __builtin_amdgcn_update_dpp(byte_at(UP[1 + (u >> 2)], u & 3), o1, 0x138, 0xf, 0xf, false);
+          const int tl = __builtin_amdgcn_update_dpp(byte_at(UP[(u + 3) >> 2], (u + 3) & 3), o2, 0x138, 0xf, 0xf, false);
+          const int v = (res + clip255(o1 + top - tl)) & 0xff;
+          o2 = o1;
+          o1 = v;
+          my_ring[xb + u < w ? (xb + u) & 127 : 128] = (uint8_t)v;
+        }
       }
       // the band's last row, 4 pixels at a time, for the band below
       if (hands_off) {
@@ -530,7 +553,7 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
         pub = max(pub, done);
       }
       // next chunk's inputs; prefetch two ahead
-      window(lo1, hi1, R);
+      window(s0 + GD_CH, lo1, hi1, R);
       lo1 = lo2;
       hi1 = hi2;
       ld_res(s0 + 3 * GD_CH, lo2, hi2);
