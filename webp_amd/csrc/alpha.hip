@@ -398,12 +398,33 @@ struct GdArgs {
   uint8_t* data;
   int* ctl;        // [0] band dequeue, [1] error
   int* diag;       // wg::diag_words + DIAG_ALPHA
-  uint64_t* hand;  // [n_img][bands][w / 4] granules {4 pixels, tag}
+  uint64_t* hand;  // [n_img][bands + 1][w / 4] granules {4 pixels, tag}: row 0, then each band's last row
   int64_t pitch;
   int w, h, bands, n_img;
 };
 
 __device__ __forceinline__ int byte_at(uint32_t v, int i) { return (int)((v >> (8 * i)) & 0xff); }
+// 64 columns of a lane's ring back to its row, as 16-B pieces (w % 16 == 0:
+// a piece is either inside the row or past its end); no loop with a
+// run-time count, so the compiler keeps its load-wait bookkeeping exact
+__device__ __forceinline__ void gd_store_block(const uint8_t* ring_row, uint8_t* row, int c0, int w) {
+  const uint32_t* l = reinterpret_cast<const uint32_t*>(ring_row + (c0 & 127));
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    if (c0 + 16 * q < w)
+      *reinterpret_cast<uint4*>(row + c0 + 16 * q) = make_uint4(l[4 * q], l[4 * q + 1], l[4 * q + 2], l[4 * q + 3]);
+}
+
+// row 0 (already unfiltered) as band 0's row above: granule g = {pixels
+// 4g .. 4g + 3, tag 1}
+__global__ __launch_bounds__(256) void k_alpha_row0_granules(GdArgs a) {
+  const int gw = a.w >> 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)gw * a.n_img) return;
+  const int img = (int)(i / gw), g = (int)(i % gw);
+  const uint32_t px = *reinterpret_cast<const uint32_t*>(a.data + img * a.pitch + 4 * g);
+  a.hand[(int64_t)img * (a.bands + 1) * gw + g] = 1ull << 32 | px;
+}
 
 __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[64 * GB_STRIDE];
@@ -415,6 +436,12 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
   // the lane's window within a 16-B aligned 32-B load: chunk starts are
   // multiples of 16, so (s0 - k) & 15 = (-k) & 15
   const int o = (-lane) & 15, q = o >> 2, rsh = o & 3;
+  const uint32_t mq1 = (q & 1) ? ~0u : 0u, mq2 = (q & 2) ? ~0u : 0u;
+  auto bfi = [](uint32_t m, uint32_t a1, uint32_t a0) {  // m ? a1 : a0, bitwise
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a1), "v"(a0));
+    return r;
+  };
   for (;;) {
     if (lane == 0) sh_band = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -427,8 +454,8 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
     uint8_t* d = a.data + img * a.pitch;
     uint8_t* my_row = d + (int64_t)min(y, a.h - 1) * w;
     const int last_lane = min(63, a.h - 2 - band * 64);
-    const uint64_t* hand_above = a.hand + ((int64_t)img * a.bands + band - 1) * gw;  // band > 0
-    uint64_t* hand_mine = a.hand + ((int64_t)img * a.bands + band) * gw;
+    const uint64_t* hand_above = a.hand + ((int64_t)img * (a.bands + 1) + band) * gw;  // (band 0: row 0)
+    uint64_t* hand_mine = a.hand + ((int64_t)img * (a.bands + 1) + band + 1) * gw;
     const bool hands_off = band + 1 < a.bands;
     const int nch = (w + last_lane + GD_CH - 1) / GD_CH;
     // residual bytes of chunk s0: the 32 aligned bytes holding x = s0 - k ..
@@ -443,9 +470,11 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
     // which makes x == 0's left = top_left = top rule hold with no select)
     auto window = [&](int s0, const uint4& lo, const uint4& hi, uint32_t R[4]) {
       const uint32_t D[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      // S[i] = D[i + q] by bit-field inserts on per-lane masks (a ternary on
+      // the lane-varying q compiled to exec-masked branches)
       uint32_t S[5];
 #pragma unroll
-      for (int i = 0; i < 5; i++) S[i] = q == 0 ? D[i] : (q == 1 ? D[i + 1] : (q == 2 ? D[i + 2] : D[i + 3]));
+      for (int i = 0; i < 5; i++) S[i] = bfi(mq2, bfi(mq1, D[i + 3], D[i + 2]), bfi(mq1, D[i + 1], D[i]));
 #pragma unroll
       for (int j = 0; j < 4; j++) R[j] = __builtin_amdgcn_alignbyte(S[j + 1], S[j], rsh);
       if (s0 < 64) {  // bytes u with s0 + u - k < 0 (the band's first chunks)
@@ -457,48 +486,57 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
         }
       }
     };
-    // lane 0's row above for chunk s0: columns s0 - 4 .. s0 + 15, five granules
+    // lane 0's row above for chunk s0: columns s0 - 4 .. s0 + 15, five
+    // granules (one load form for every band: row 0's granules are written
+    // before the launch, k_alpha_row0_granules)
     auto ld_up = [&](int s0, uint64_t U[5]) {
 #pragma unroll
-      for (int t = 0; t < 5; t++) {
-        const int g = min(max((s0 >> 2) - 1 + t, 0), gw - 1);
-        U[t] = band > 0 ? __hip_atomic_load(hand_above + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : (1ull << 32 | *reinterpret_cast<const uint32_t*>(d + 4 * g));
-      }
+      for (int t = 0; t < 5; t++)
+        U[t] = __hip_atomic_load(hand_above + min(max((s0 >> 2) - 1 + t, 0), gw - 1), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
     };
-    uint4 lo1, hi1, lo2, hi2;
+    // Prefetch three chunks ahead in three register sets that the unrolled
+    // chunk loop rotates by role, never by copying (a copy of a register a
+    // load is still filling makes the compiler wait for the load there).
     uint32_t R[4];
     {
       uint4 lo0, hi0;
       ld_res(0, lo0, hi0);
       window(0, lo0, hi0, R);
     }
-    ld_res(GD_CH, lo1, hi1);
-    ld_res(2 * GD_CH, lo2, hi2);
-    uint64_t U0[5], U1[5], U2[5];
-    ld_up(0, U0);
-    ld_up(GD_CH, U1);
-    ld_up(2 * GD_CH, U2);
+    uint4 rX[2], rY[2], rZ[2];  // raw residuals of chunks m + 1, m + 2, m + 3
+    ld_res(GD_CH, rX[0], rX[1]);
+    ld_res(2 * GD_CH, rY[0], rY[1]);
+    ld_res(3 * GD_CH, rZ[0], rZ[1]);
+    uint64_t UA[5], UB[5], UC[5];  // the row above for chunks m, m + 1, m + 2
+    ld_up(0, UA);
+    ld_up(GD_CH, UB);
+    ld_up(2 * GD_CH, UC);
     int o1 = 0, o2 = 0;  // this lane's outputs at x - 1, x - 2
     int pub = 0;         // granules of the band's last row published
-    for (int m = 0; m < nch; m++) {
+    // chunk m: consumes R and Uc (its row above), then windows raw (chunk
+    // m + 1) into R and refills raw with chunk m + 4 and Uc with chunk m + 3
+    auto chunk = [&](int m, uint64_t (&Uc)[5], uint4 (&raw)[2]) {
       const int s0 = m * GD_CH;
-      if ((s0 & 63) == 0 && s0 >= 128 && live) gb_chunk_io(my_ring, my_row, s0 - 128, w, true, true);  // every lane is past it
-      if (band > 0) {  // the row above: re-poll the granules whose tag is still clear
+      if ((s0 & 63) == 0 && s0 >= 128 && live) gd_store_block(my_ring, my_row, s0 - 128, w);  // every lane is past it
+      {  // the row above: re-poll the granules whose tag is still clear
         bool ready = true;
 #pragma unroll
-        for (int t = 0; t < 5; t++) ready &= __builtin_amdgcn_readfirstlane((int)(U0[t] >> 32)) != 0;
-        if (!ready) {
+        for (int t = 0; t < 5; t++) ready &= __builtin_amdgcn_readfirstlane((int)(Uc[t] >> 32)) != 0;
+        if (!ready) {  // (re-polled into other registers: a load into Uc here would make every
+                       // chunk's first use of its Uc wait for all loads in flight)
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          uint64_t T[5];
           for (uint32_t it = 0;; it++) {
             __builtin_amdgcn_s_sleep(1);
-            ld_up(s0, U0);
+            ld_up(s0, T);
             ready = true;
 #pragma unroll
-            for (int t = 0; t < 5; t++) ready &= __builtin_amdgcn_readfirstlane((int)(U0[t] >> 32)) != 0;
+            for (int t = 0; t < 5; t++) ready &= __builtin_amdgcn_readfirstlane((int)(T[t] >> 32)) != 0;
             if (ready) break;
-            if ((it & 15) == 15 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
-                                    __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            // (the timeout alone ends the wait: a vector load of the error flag
+            // here made the compiler treat the chunk buffers as just loaded)
+            if ((it & 15) == 15 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
               if (lane == 0) {
                 __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 wg::note_timeout(a.diag, s0, band, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0);
@@ -506,11 +544,13 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
               break;
             }
           }
+#pragma unroll
+          for (int t = 0; t < 5; t++) Uc[t] = T[t];
         }
       }
       uint32_t UP[5];
 #pragma unroll
-      for (int t = 0; t < 5; t++) UP[t] = (uint32_t)U0[t];
+      for (int t = 0; t < 5; t++) UP[t] = (uint32_t)Uc[t];
       if (s0 == 0) UP[0] = 0;  // column -1 (x == 0's top_left is its top: 0 - 0 cancels)
       // x == 0: left = top_left = top (alpha.go:177-181).  Outputs left of
       // column 0 are 0 (zero residuals, zero row above: see window), so there
@@ -542,32 +582,39 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
         }
       }
       // the band's last row, 4 pixels at a time, for the band below
+      // (a chunk moves the last lane on by 16 columns: at most 4 granules)
       if (hands_off) {
         const int done = min(max((s0 + GD_CH - last_lane) >> 2, 0), gw);
-        for (int g = pub; g < done; g++) {
-          if (lane == last_lane) {
+#pragma unroll
+        for (int j = 0; j < GD_CH / 4; j++) {
+          const int g = pub + j;
+          if (g < done && lane == last_lane) {
             const uint32_t px = *reinterpret_cast<const uint32_t*>(my_ring + ((4 * g) & 127));
             __hip_atomic_store(hand_mine + g, 1ull << 32 | px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
         pub = max(pub, done);
       }
-      // next chunk's inputs; prefetch two ahead
-      window(s0 + GD_CH, lo1, hi1, R);
-      lo1 = lo2;
-      hi1 = hi2;
-      ld_res(s0 + 3 * GD_CH, lo2, hi2);
-#pragma unroll
-      for (int t = 0; t < 5; t++) {
-        U0[t] = U1[t];
-        U1[t] = U2[t];
-      }
-      ld_up(s0 + 3 * GD_CH, U2);
+      window(s0 + GD_CH, raw[0], raw[1], R);
+      ld_res(s0 + 4 * GD_CH, raw[0], raw[1]);
+      ld_up(s0 + 3 * GD_CH, Uc);
+      // (the loads stay here, three chunks ahead of their use: sunk to the
+      // loop latch they would be the newest in flight at the next use)
+      asm volatile("" ::: "memory");
+    };
+    for (int m = 0; m < nch; m += 3) {
+      chunk(m, UA, rX);
+      if (m + 1 >= nch) break;
+      chunk(m + 1, UB, rY);
+      if (m + 2 >= nch) break;
+      chunk(m + 2, UC, rZ);
     }
     // the last two 64-column blocks (or one) have not been stored yet
     const int chunks = (w + 63) >> 6;
-    if (live)
-      for (int m = max(0, chunks - 2); m < chunks; m++) gb_chunk_io(my_ring, my_row, m * 64, w, true, true);
+    if (live) {
+      if (chunks >= 2) gd_store_block(my_ring, my_row, (chunks - 2) * 64, w);
+      gd_store_block(my_ring, my_row, (chunks - 1) * 64, w);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // the ring is reused by the next band this wave dequeues
   }
@@ -854,7 +901,8 @@ extern "C" int wg_alpha_filter(int32_t filter, const uint8_t* in, uint8_t* out, 
 }
 
 // work: ctl[4] | progress[n_img * bands] (k_alpha_gbands) | hand-off granules
-// [n_img][bands][width / 4] (k_alpha_gdiag), 16-B aligned
+// [n_img][bands + 1][width / 4] (k_alpha_gdiag: row 0, then each band's last
+// row), 16-B aligned
 static size_t gd_hand_offset(int32_t height, int32_t n_images) {
   const int bands = (height - 1 + 63) / 64;
   return (sizeof(int) * (4 + (size_t)n_images * (bands > 0 ? bands : 1)) + 15) & ~(size_t)15;
@@ -862,7 +910,7 @@ static size_t gd_hand_offset(int32_t height, int32_t n_images) {
 extern "C" size_t wg_alpha_unfilter_work_bytes(int32_t width, int32_t height, int32_t n_images) {
   if (width <= 0 || height <= 0 || n_images <= 0) return 0;
   const int bands = (height - 1 + 63) / 64;
-  return gd_hand_offset(height, n_images) + sizeof(uint64_t) * (size_t)n_images * (bands > 0 ? bands : 1) * ((width + 3) / 4);
+  return gd_hand_offset(height, n_images) + sizeof(uint64_t) * (size_t)n_images * (bands + 1) * ((width + 3) / 4);
 }
 
 extern "C" int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, int32_t height, int64_t pitch,
@@ -919,6 +967,8 @@ extern "C" int wg_alpha_unfilter(int32_t filter, uint8_t* data, int32_t width, i
     g.h = height;
     g.bands = bands;
     g.n_img = n_images;
+    hipLaunchKernelGGL(k_alpha_row0_granules, dim3(wg::blocks_for((int64_t)(width / 4) * n_images, 256)), dim3(256), 0, s, g);
+    if ((rc = wg::check_launch("k_alpha_row0_granules")) != WG_OK) return rc;
     hipLaunchKernelGGL(k_alpha_gdiag, dim3(grid), dim3(64), 0, s, g);
     return wg::check_launch("k_alpha_gdiag");
   }
