@@ -55,7 +55,7 @@ def test_work_size_helpers():
     assert _lib.lib.wg_decode_work_bytes(120, 68, 2) == ((head + 15) & ~15) + 2 * 120 * 128
     assert _lib.lib.wg_decode_work_bytes(0, 68, 2) == 0
     # ctl (16 B) | one {pixel, tag} granule per column of each band's last row
-    assert _lib.lib.wg_vp8l_inverse_work_bytes(100, 130, 2) == 16 + 8 * 2 * 3 * 100
+    assert _lib.lib.wg_vp8l_inverse_work_bytes(100, 130, 2) == 16 + 8 * 2 * 5 * 100  # 32-row bands
     assert _lib.lib.wg_vp8l_inverse_work_bytes(100, 0, 2) == 0
     assert _lib.lib.wg_plane_ssim_work_bytes(33, 17, 1) == 8 * 1 * 2  # one 58-column strip, two tile rows
     assert _lib.lib.wg_plane_ssim_row_partials(59) == 2 and _lib.lib.wg_plane_ssim_row_partials(58) == 1

@@ -179,15 +179,50 @@ __device__ __forceinline__ void st_sc1_16(void* p, uint16_t v) {
 constexpr int WB_OWN = 32, WB_HALO = 16, WB_PUB = 16;
 static_assert(WB_OWN + 2 * WB_HALO == 64 && WB_HALO % WB_PUB == 0, "wave band layout");
 
-__device__ __forceinline__ int dpp_from_left(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false); }   // wave_shr:1: lane i <- i - 1
-__device__ __forceinline__ int dpp_from_right(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false); }  // wave_shl:1: lane i <- i + 1
+// (bound_ctrl: the wave's end lanes, always halo lanes, read 0 -- no register to initialise)
+__device__ __forceinline__ int dpp_from_left(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); }   // wave_shr:1: lane i <- i - 1
+__device__ __forceinline__ int dpp_from_right(int v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true); }  // wave_shl:1: lane i <- i + 1
 
+// the gray value of linear RGB (gray() for inputs in [0, 65535] -- sRGB's
+// linear values and every gamma value: the weights sum to 65536, so the sum
+// fits 32 bits unsigned)
+// a * b + c on the 24-bit multiplier (full rate, where v_mul_lo_u32 is
+// quarter rate): a, b < 2^24 and the result < 2^32 at every call
+__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t gray_u32(uint32_t r, uint32_t g, uint32_t b) {
+  return mad_u24(r, 13933u, mad_u24(g, 46871u, mad_u24(b, 4732u, 32768u))) >> 16;
+}
+// from_lin for the walk: fromLinearSrgb's interpolation on the 24-bit
+// multiplier (the table is non-decreasing, so v1 - v0 >= 0, and
+// (v1 - v0) * x + 64 < 2^17)
 template <bool LUT>
-__global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
-  __shared__ SharpTabs t;
-  const int blk = blockIdx.x, band = blk % nb, it = (blk / nb) & 3, img = blk / (4 * nb);
-  if (img >= a.n_img) return;  // uniform over the block
-  load_tabs(t, a.tabs);
+__device__ __forceinline__ int from_lin_w(const uint32_t* l2g, const uint16_t* lut, int n, uint32_t v) {
+  if (LUT) return lut[min(v, (uint32_t)(n - 1))];
+  const uint32_t pos = v >> 7, x = v & 127u;
+  const uint32_t v0 = l2g[pos] >> 6, v1 = l2g[pos + 1] >> 6;
+  return (int)(v0 + (mad_u24(v1 - v0, x, 64u) >> 7));
+}
+// a 32-bit word at a wave-uniform base + uniform byte offset + this lane's
+// byte offset: the uniform part stays in SGPRs (global_load saddr + a 32-bit
+// VGPR offset) instead of a 64-bit address per lane and load
+template <typename T>
+__device__ __forceinline__ const uint32_t* at(const T* base, int64_t ubytes, uint32_t lbytes) {
+  return reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(base) + ubytes + lbytes);
+}
+// (the lane offsets are laundered once a step: hoisted out of the walk, base
+// + lane offset would become a 64-bit per-lane pointer and every load a 64-bit add)
+__device__ __forceinline__ void launder_v(uint32_t& v) { asm volatile("" : "+v"(v)); }
+
+// One band of one iteration.  EDGE: the band's lanes include column 0 or
+// column uvw - 1 (the reference's filter2 at the plane's edges); the other
+// bands run without those selects.
+template <bool LUT, bool EDGE>
+__device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpTabs& t, int nb, int band, int it,
+                                                int img) {
   const int lane = threadIdx.x;
   const int uvw = a.uvw, uvh = a.uvh, w = a.w, rs = a.uv_rs;
   const int c = band * WB_OWN - WB_HALO + lane;  // this lane's UV column
@@ -203,6 +238,7 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
   int* prog_img = a.prog + (int64_t)img * 4 * nb;  // [iteration][band]: row pairs finished
   int* prog_out = prog_img + it * nb + band;
   bool timed_out = false;  // wave-uniform
+  const int64_t uv_row_bytes = 2 * (int64_t)rs, y_row_bytes = 2 * (int64_t)w;
 
   // wait (the whole wave, on one wave-uniform address) until band bb of
   // iteration ii has finished `need` row pairs; the progress seen (uvh for a band that does not exist)
@@ -228,7 +264,7 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
       seen_in = m;
     }
   };
-  // a chroma row of 3 int16 channels at this lane's column, from a state row.
+  // A chroma row of 3 int16 channels at this lane's column, from a state row.
   // The loads are unconditional (clamped columns / rows) and keep the raw
   // zero-extended halves: a load inside a branch, or one whose value is
   // sign-extended right away, makes the compiler wait for it there, which
@@ -236,19 +272,27 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
   // 16-bit values travel as the aligned 32-bit word holding them (a 16-bit
   // load's result gets masked right away, which again forces the wait):
   // element e of a 4-byte-aligned state base is in word e >> 1, half e & 1.
-  // Rows are 16-byte aligned, so a channel's half depends only on the
-  // column and the channel (hs[ch]).  The other half may be a neighbour's
-  // value being stored concurrently: it is never used.
+  // Rows are 16-byte aligned, so a channel's word and half depend only on
+  // the column and the channel: the lane's byte offsets lo_uv / half shifts
+  // hs, fixed for the walk.  The other half may be a neighbour's value being
+  // stored concurrently: it is never used.
   int hs[3];
-  for (int ch = 0; ch < 3; ch++) hs[ch] = 16 * ((ch * uvw + cl) & 1);
-  auto word = [](const int16_t* base, int64_t e) { return reinterpret_cast<const uint32_t*>(base) + (e >> 1); };
+  uint32_t lo_uv[3], st_uv[3];
+#pragma unroll
+  for (int ch = 0; ch < 3; ch++) {
+    hs[ch] = 16 * ((ch * uvw + cl) & 1);
+    lo_uv[ch] = 4u * (uint32_t)((ch * uvw + cl) >> 1);
+    st_uv[ch] = 2u * (uint32_t)(ch * uvw + cl);
+  }
+  uint32_t lo_y = 4u * (uint32_t)cl;  // the luma pair at x = 2cl, 2cl + 1 of a row
   struct Row {
     uint32_t v[3];
   };
   auto load_row = [&](int row) {
     Row r;
-    const int64_t e0 = (int64_t)min(row, uvh - 1) * rs + cl;  // clamped: the last row pair's next is its cur
-    for (int ch = 0; ch < 3; ch++) r.v[ch] = ld_sc1(word(in_uv, e0 + ch * uvw));
+    const int64_t ub = (int64_t)min(row, uvh - 1) * uv_row_bytes;  // clamped: the last row pair's next is its cur
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) r.v[ch] = ld_sc1(at(in_uv, ub, lo_uv[ch]));
     return r;
   };
   struct In {
@@ -257,18 +301,20 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
   auto load_in = [&](int jp) {
     In r;
     const int jc = min(jp, uvh - 1);
-    const int64_t yo = (int64_t)(2 * jc) * w + 2 * cl;
-    r.y[0] = ld_sc1(in_y + yo);
-    r.y[1] = ld_sc1(in_y + yo + w);
-    r.ty[0] = *reinterpret_cast<const uint32_t*>(ty + yo);
-    r.ty[1] = *reinterpret_cast<const uint32_t*>(ty + yo + w);
-    for (int ch = 0; ch < 3; ch++) r.tuv[ch] = *word(tuv, (int64_t)jc * rs + ch * uvw + cl);
+    const int64_t yb = (int64_t)(2 * jc) * y_row_bytes;
+    r.y[0] = ld_sc1(at(in_y, yb, lo_y));
+    r.y[1] = ld_sc1(at(in_y, yb + y_row_bytes, lo_y));
+    r.ty[0] = *at(ty, yb, lo_y);
+    r.ty[1] = *at(ty, yb + y_row_bytes, lo_y);
+    const int64_t ub = (int64_t)jc * uv_row_bytes;
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) r.tuv[ch] = *at(tuv, ub, lo_uv[ch]);
     return r;
   };
   // the signed 16-bit value of this column's channel ch in a loaded word
-  auto sx16 = [&](uint32_t v, int ch) { return (int)(int16_t)(uint16_t)(v >> hs[ch]); };
+  auto sx16 = [&](uint32_t v, int ch) { return __builtin_amdgcn_sbfe((int)v, hs[ch], 16); };
 
-  uint64_t my_sum = 0;
+  uint32_t my_sum = 0;  // |dY| over this lane's pixels: < 4 * 1023 per row pair, uvh <= 2^13
   // rings of four row pairs, indexed by ju % 4 (compile-time after the
   // unrolled loop below, so no register moves): the input state's chroma row
   // and luma / target pair of row pairs ju .. ju + 3, prefetched three ahead
@@ -287,10 +333,19 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
     if (ju > 0 && ju % WB_HALO == 0) {  // the halo lanes' prev: the neighbours' row ju - 1 of this iteration
       wait_for(it, band - 1, ju);
       wait_for(it, band + 1, ju);
-      if (act && !own)
-        for (int ch = 0; ch < 3; ch++) P.v[ch] = ld_sc1(word(out_uv, (int64_t)(ju - 1) * rs + ch * uvw + cl));
+      if (act && !own) {
+        const int64_t ub = (int64_t)(ju - 1) * uv_row_bytes;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) P.v[ch] = ld_sc1(at(out_uv, ub, lo_uv[ch]));
+      }
     }
     const int j = 2 * ju;
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+      launder_v(lo_uv[ch]);
+      launder_v(st_uv[ch]);
+    }
+    launder_v(lo_y);
     pf_row = load_row(ju + 3);
     pf_in = load_in(ju + 3);
     int upd[3] = {0, 0, 0};
@@ -306,14 +361,14 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
         const int a0 = dpp_from_left(a1), b0 = dpp_from_left(b1), n0 = dpp_from_left(n1);
         const int a2 = dpp_from_right(a1), b2 = dpp_from_right(b1), n2 = dpp_from_right(n1);
         int e0, e1, f0, f1;  // x = 2c: row j / j+1
-        if (c == 0) {
+        if (EDGE && c == 0) {
           e0 = (a1 * 3 + b1 + 2) >> 2;  // filter2(cur[0], prev[0])
           f0 = (a1 * 3 + n1 + 2) >> 2;
         } else {
           e0 = (a1 * 9 + a0 * 3 + b1 * 3 + b0 + 8) >> 4;
           f0 = (a1 * 9 + a0 * 3 + n1 * 3 + n0 + 8) >> 4;
         }
-        if (c == uvw - 1) {  // x = w-1: filter2(cur[uvw-1], prev[uvw-1])
+        if (EDGE && c == uvw - 1) {  // x = w-1: filter2(cur[uvw-1], prev[uvw-1])
           e1 = (a1 * 3 + b1 + 2) >> 2;
           f1 = (a1 * 3 + n1 + 2) >> 2;
         } else {
@@ -334,7 +389,10 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
         for (int cc = 0; cc < 2; cc++) {
 #pragma unroll
           for (int ch = 0; ch < 3; ch++) lin[r][cc][ch] = to_linear(t.g2l, iv[r][cc][ch]);
-          yv[r][cc] = from_lin<LUT>(t.l2g, a.lut, a.lut_n, (uint32_t)gray(lin[r][cc][0], lin[r][cc][1], lin[r][cc][2]));
+          // (the other transfer functions' linear values reach ~72k: 64-bit gray)
+          const uint32_t g = LUT ? (uint32_t)gray(lin[r][cc][0], lin[r][cc][1], lin[r][cc][2])
+                                 : gray_u32(lin[r][cc][0], lin[r][cc][1], lin[r][cc][2]);
+          yv[r][cc] = from_lin_w<LUT>(t.l2g, a.lut, a.lut_n, g);
         }
       const int byv[2][2] = {{by00, by01}, {by10, by11}};
       int ny[2][2];
@@ -344,7 +402,7 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
         for (int cc = 0; cc < 2; cc++) {
           const int d = (int)((in_cur.ty[r] >> (16 * cc)) & 0xffff) - yv[r][cc];
           ny[r][cc] = clip_bd(byv[r][cc] + d);
-          if (own) my_sum += (uint64_t)(d < 0 ? -d : d);
+          my_sum += (uint32_t)abs(d);
         }
       ynew[0] = (uint32_t)ny[0][0] | (uint32_t)ny[0][1] << 16;
       ynew[1] = (uint32_t)ny[1][0] | (uint32_t)ny[1][1] << 16;
@@ -352,8 +410,8 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
       int rgbv[3];
 #pragma unroll
       for (int ch = 0; ch < 3; ch++)
-        rgbv[ch] = from_lin<LUT>(t.l2g, a.lut, a.lut_n, (lin[0][0][ch] + lin[0][1][ch] + lin[1][0][ch] + lin[1][1][ch] + 2) >> 2);
-      const int gv = gray(rgbv[0], rgbv[1], rgbv[2]);
+        rgbv[ch] = from_lin_w<LUT>(t.l2g, a.lut, a.lut_n, (lin[0][0][ch] + lin[0][1][ch] + lin[1][0][ch] + lin[1][1][ch] + 2) >> 2);
+      const int gv = (int)gray_u32(rgbv[0], rgbv[1], rgbv[2]);
 #pragma unroll
       for (int ch = 0; ch < 3; ch++) {
         const int16_t srcv = (int16_t)(rgbv[ch] - gv);
@@ -363,9 +421,12 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
     }
     // publish this band's own columns of the updated UV row ju and luma pair (write-through)
     if (own) {
-      for (int ch = 0; ch < 3; ch++) st_sc1_16(out_uv + (int64_t)ju * rs + ch * uvw + c, (uint16_t)upd[ch]);
-      st_sc1(out_y + (int64_t)j * w + 2 * c, ynew[0]);
-      st_sc1(out_y + (int64_t)(j + 1) * w + 2 * c, ynew[1]);
+      uint8_t* ob = reinterpret_cast<uint8_t*>(out_uv) + (int64_t)ju * uv_row_bytes;
+#pragma unroll
+      for (int ch = 0; ch < 3; ch++) st_sc1_16(ob + st_uv[ch], (uint16_t)upd[ch]);
+      uint8_t* oy = reinterpret_cast<uint8_t*>(out_y) + (int64_t)j * y_row_bytes;
+      st_sc1(oy + lo_y, ynew[0]);
+      st_sc1(oy + y_row_bytes + lo_y, ynew[1]);
     }
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) P.v[ch] = (uint32_t)(uint16_t)upd[ch] << hs[ch];  // prev <- the updated cur (in its half)
@@ -383,13 +444,26 @@ __global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
       step(j0 + k, R[k], R[(k + 1) & 3], R[(k + 3) & 3], I[k], I[(k + 3) & 3]);
     }
   }
-  // the band's share of the iteration's |dY| sum (:254-263); k_sharp_final applies the exit rule
-  unsigned long long sm = my_sum;
+  // the band's share of the iteration's |dY| sum over its own columns
+  // (:254-263); k_sharp_final applies the exit rule
+  unsigned long long sm = own ? my_sum : 0u;
   for (int off = 32; off > 0; off >>= 1) sm += __shfl_down(sm, off, 64);
   if (lane == 0) {
     atomicAdd(reinterpret_cast<unsigned long long*>(a.sums + img * 4 + it), sm);
     if (timed_out) a.iters[img] = -1;
   }
+}
+
+template <bool LUT>
+__global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
+  __shared__ SharpTabs t;
+  const int blk = blockIdx.x, band = blk % nb, it = (blk / nb) & 3, img = blk / (4 * nb);
+  if (img >= a.n_img) return;  // uniform over the block
+  load_tabs(t, a.tabs);
+  // the band's lanes cover columns band * WB_OWN - WB_HALO .. + 63
+  const int c0 = band * WB_OWN - WB_HALO;
+  if (c0 <= 0 || c0 + 63 >= a.uvw - 1) sharp_wave_band<LUT, true>(a, t, nb, band, it, img);
+  else sharp_wave_band<LUT, false>(a, t, nb, band, it, img);
 }
 
 // The iterations the reference runs (:224-264): 0 and 1 always; after

@@ -358,39 +358,116 @@ struct InvArgs {
 constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
 
 // predictorInverseTransform.  Rows depend on the row above (T, TL, TR) and on
-// their own left neighbour.  A wave takes a band of 64 rows and walks it as a
-// diagonal: at step s lane k reconstructs pixel x = s - 2k of row
-// band*64 + k.  The row above comes from the previous lane's last three
-// outputs (a whole-wave DPP shift); lane 0's row above is the band above's
-// last row.  Bands are dequeued in (band, image) order from a counter, so a
-// band only ever waits on a band owned by a running wave.
+// their own left neighbour.  A wave takes a band of 32 rows and walks it as a
+// diagonal: at step s the lane pair (2k, 2k + 1) reconstructs pixel
+// x = s - 2k of row band*32 + k, lane 2k its blue and red channels and lane
+// 2k + 1 its green and alpha ones, each as bytes 0 and 2 of a word (bytes 1
+// and 3 zero: the "c2" form).  Per channel the predictors are byte averages
+// (v_lerp_u8), 16-bit clamps with no unpacking, and a masked add; only
+// Select sums over all four channels, one DPP add with the pair's other
+// lane.  (A whole pixel per lane took ~130 instructions a step, most of them
+// unpacking and repacking the clamped predictors' 16-bit lanes; the walk is
+// issue-bound, one wave alone on its SIMD, so halving the band and the work
+// per lane nearly halves the step.)  The row above comes from the lane pair
+// before's last three outputs (two whole-wave DPP shifts); the first pair's
+// row above is the band above's last row.  Bands are dequeued in (band,
+// image) order from a counter, so a band only ever waits on a band owned by
+// a running wave.
 //
-// Hand-off between bands: the band's last lane writes its row's pixels as
-// 8-B {pixel, tag} granules, two at a time with one 16-B sc1 (write-through)
-// store (MI355X_MICROARCH.md, R2 granules: untorn, no flag, no drain); lane 0
-// of the band below loads one granule a step, UPD steps before it needs it,
-// and re-polls one whose tag is not set yet.  The band below then trails by
-// the diagonal's 128 steps plus UPD, a step for the pairing and a store's
-// flight (per-chunk loads of 18 granules trailed by ~20 more steps; a
-// progress counter published every 32 columns behind a store drain by ~90).
+// Hand-off between bands: the band's last row writes its pixels as 8-B
+// {pixel, tag} granules, two at a time with one 16-B sc1 (write-through)
+// store (MI355X_MICROARCH.md, R2 granules: untorn, no flag, no drain); the
+// band below loads one granule a step, UPD steps before it needs it, and
+// re-polls one whose tag is not set yet.  The band below then trails by the
+// diagonal's 64 steps plus UPD, a step for the pairing and a store's flight.
 //
 // The walk runs in chunks of 16 steps, and everything but the predictor and
 // the row above is done per chunk: each lane's 16 residuals and tile modes
-// (loaded a chunk ahead, one pair per step) and the 16 outputs (stored as one
-// 64-B run per lane).  The DPP shift leaves lane 0 its own register
-// (update_dpp's `old`, no per-step branch).
+// (loaded a chunk ahead, one pair per step) and the 16 outputs (the even
+// lane of each pair stores the whole pixels as one 64-B run).
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4a4_t __attribute__((ext_vector_type(4), aligned(4)));  // a row's pixels: 4-B aligned
 #ifndef UPD
 #define UPD 6  // steps between a row-above granule's load and its use
 #endif
+constexpr int INV_ROWS = 32;  // rows per band (a lane pair per row)
+constexpr uint32_t C2_EVEN = 0x0c020c00u, C2_ODD = 0x0c030c01u;  // v_perm selectors: a pixel's c2 halves
 
+__device__ __forceinline__ uint32_t c2_of(uint32_t p, uint32_t sel) { return __builtin_amdgcn_perm(0u, p, sel); }
+__device__ __forceinline__ uint32_t c2_add(uint32_t a, uint32_t b) { return (a + b) & 0x00ff00ffu; }  // mod 256 per channel
+__device__ __forceinline__ uint32_t c2_clamp_full(uint32_t a, uint32_t b, uint32_t c) {
+  return as_u(clamp255(as_v2(a) + as_v2(b) - as_v2(c)));
+}
+__device__ __forceinline__ uint32_t c2_clamp_half(uint32_t avg, uint32_t c) { return as_u(half_step(as_v2(avg), as_v2(c))); }
+// predict_ctl on half pixels (c2 form), with the control word's select
+// masks m[b] = (bit b set ? ~0 : 0) read from LDS; `black` is this lane's
+// half of ARGB_BLACK
+__device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+struct SelMasks {
+  uint32_t m[13];
+};
+__device__ __forceinline__ uint32_t predict_c2(const SelMasks& k, uint32_t l, uint32_t t, uint32_t tr, uint32_t tl,
+                                               uint32_t black) {
+  const uint32_t* m = k.m;
+  const uint32_t pc = msel(m[3], tl, msel(m[2], tr, t));
+  const uint32_t r1 = msel(m[4], tl, tr);
+  const uint32_t qc = msel(m[7], msel(m[6], avg2(t, tr), tl), msel(m[6], tr, t));
+  const int sad_t = (int)__builtin_amdgcn_sad_u8(t, tl, 0u);
+  const uint32_t q = msel(m[5], l, qc);
+  const uint32_t p = msel(m[0], avg2(l, r1), msel(m[1], l, pc));
+  const uint32_t pavg = avg2(p, q);
+  // Select: the channel sums of |L - TL| - |T - TL|, this lane's two plus the pair's other two (quad_perm 1,0,3,2)
+  const int pa_half = (int)__builtin_amdgcn_sad_u8(l, tl, 0u) - sad_t;
+  const int pa = pa_half + __builtin_amdgcn_update_dpp(0, pa_half, 0xb1, 0xf, 0xf, false);
+  uint32_t r = msel(m[8], pa <= 0 ? t : l, pavg);
+  r = msel(m[9], c2_clamp_full(l, t, tl), r);
+  r = msel(m[10], c2_clamp_half(pavg, tl), r);
+  return msel(m[11], black, r);
+}
+// the value of the lane pair before (lane i <- i - 2, two wave_shr:1); the
+// first pair gets the band above's c2 halves (lane 0 `even`, lane 1 `odd`)
+__device__ __forceinline__ uint32_t from_pair_above(uint32_t v, uint32_t even, uint32_t odd) {
+  const uint32_t s1 = (uint32_t)__builtin_amdgcn_update_dpp((int)odd, (int)v, 0x138, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)even, (int)s1, 0x138, 0xf, 0xf, false);
+}
+
+template <bool TILE16>
 __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
   __shared__ int sh_band;
-  __shared__ uint32_t ctab[19];  // kPredCtl, then the border rules: 16 x = 0 (T), 17 x = 0 on row 0 (black), 18 row 0 (L)
+  // The control words' select masks, 64 B a row: rows 0-15 kPredCtl[mode],
+  // then the border rules 16 x = 0 (T), 17 x = 0 on row 0 (black), 18 row 0
+  // (L); rows 19-37 the same with C_EDGE (x = w - 1).  A step reads its row
+  // with three 16-B reads and one 4-B read, a step ahead, instead of
+  // extracting 13 bit masks on the VALU.
+  constexpr int MROWS = 38;
+  __shared__ uint32_t mtab[MROWS][16];
   const int lane = threadIdx.x;
-  if (lane < 19) ctab[lane] = lane < 16 ? kPredCtl[lane] : (lane == 16 ? kPredCtl[2] : (lane == 17 ? kPredCtl[0] : kPredCtl[1]));
+  for (int i = lane; i < MROWS * 16; i += 64) {
+    const int row = i >> 4, b = i & 15, id = row % 19;
+    const uint32_t ctl = (id < 16 ? kPredCtl[id] : (id == 16 ? kPredCtl[2] : (id == 17 ? kPredCtl[0] : kPredCtl[1]))) |
+                         (row >= 19 ? (uint32_t)C_EDGE : 0u);
+    mtab[row][b] = b < 13 && ((ctl >> b) & 1) ? ~0u : 0u;
+  }
+  __syncthreads();
+  auto ld_masks = [&](uint32_t row) {
+    SelMasks k;
+    const uint4 a0 = *reinterpret_cast<const uint4*>(&mtab[row][0]), a1 = *reinterpret_cast<const uint4*>(&mtab[row][4]);
+    const uint4 a2 = *reinterpret_cast<const uint4*>(&mtab[row][8]);
+    k.m[0] = a0.x, k.m[1] = a0.y, k.m[2] = a0.z, k.m[3] = a0.w;
+    k.m[4] = a1.x, k.m[5] = a1.y, k.m[6] = a1.z, k.m[7] = a1.w;
+    k.m[8] = a2.x, k.m[9] = a2.y, k.m[10] = a2.z, k.m[11] = a2.w;
+    k.m[12] = mtab[row][12];
+    return k;
+  };
   const int w = a.width;
   const int total = a.bands * a.n_img;
+  const int k = lane >> 1;  // the lane pair's row in the band
+  const uint32_t sel = (lane & 1) ? C2_ODD : C2_EVEN;
+  const uint32_t black = (lane & 1) ? 0x00ff0000u : 0u;  // ARGB_BLACK's channels (alpha 255)
   for (;;) {
     if (lane == 0) sh_band = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -398,22 +475,22 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
     __syncthreads();
     if (idx >= total) break;
     const int band = idx / a.n_img, img = idx % a.n_img;
-    const int y = band * 64 + lane;
+    const int y = band * INV_ROWS + k;
     const bool live = y < a.height;
     const uint32_t* in = a.in + img * a.pitch;
     uint32_t* out = a.out + img * a.pitch;
     const int hs = (w + 1) & ~1;  // granules per hand-off row (even: 16-B aligned pairs)
     const uint64_t* hand_above = a.hand + ((int64_t)img * a.bands + band - 1) * hs;  // band > 0
     uint64_t* hand_mine = a.hand + ((int64_t)img * a.bands + band) * hs;
-    const int last_lane = min(63, a.height - 1 - band * 64);
-    const bool hands_off = band + 1 < a.bands && lane == last_lane;
+    const int last_row = min(INV_ROWS - 1, a.height - 1 - band * INV_ROWS);
+    const bool hands_off = band + 1 < a.bands && lane == 2 * last_row;  // the last row's even lane
     const uint32_t* mrow =
         a.modes + (int64_t)img * a.tiles_x * a.tiles_y + (int64_t)(min(y, a.height - 1) >> a.bits) * a.tiles_x;
     const uint32_t* inrow = in + (int64_t)min(y, a.height - 1) * w;
     uint32_t* orow = out + (int64_t)min(y, a.height - 1) * w;
-    uint32_t o1 = 0, o2 = 0, o3 = 0, first = 0;  // this lane's outputs at x-1, x-2, x-3; at x = 0
-    const int steps = w + 2 * last_lane;
-    // lane 0's row above, one granule a step: column c sits in gr[c & 15],
+    uint32_t o1 = 0, first = 0;  // this lane's output (c2) at x - 1; at x = 0
+    const int steps = w + 2 * last_row;
+    // the band above's row, one granule a step: column c sits in gr[c & 15],
     // loaded UPD steps before step c - 1 (where it is TR); up_take re-polls it
     // until its tag is set and returns the pixel
     // (unconditional loads at clamped addresses: a load inside a branch makes
@@ -442,83 +519,137 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
       }
       return band > 0 ? (uint32_t)g : 0u;
     };
-    // residuals and modes of pixel x of this lane's row (0 outside it)
-    // (only the inputs of pixels inside the row are used, so a clamped
-    // address suffices -- and a select of a load would be sunk into a branch)
-    auto ld_res = [&](int x) -> uint32_t { return inrow[min(max(x, 0), w - 1)]; };
-    auto ld_mode = [&](int x) -> uint32_t { return mrow[min(max(x, 0), w - 1) >> a.bits]; };
-    uint32_t rc[16], mc[16];
-    uint64_t gr[16];
+    // A chunk's inputs: the residuals of pixels x0 .. x0 + 15 of the lane's
+    // row -- four 16-B loads where the chunk lies inside the row, else
+    // single loads at clamped addresses (the walk's first and last chunks;
+    // only pixels inside the row are used) -- and their tiles' modes: with
+    // tiles of >= 16 pixels (TILE16) a chunk touches at most two tiles, t0
+    // for u < ub and the next one past it.
+    auto ld_res = [&](int x0, uint32_t* r) {
+      if (x0 >= 0 && x0 + 15 < w) {
+        const u32x4a4_t* p = reinterpret_cast<const u32x4a4_t*>(inrow + x0);
 #pragma unroll
-    for (int u = 0; u < 16; u++) {
-      rc[u] = ld_res(u - 2 * lane);
-      mc[u] = ld_mode(u - 2 * lane);
-    }
+        for (int j = 0; j < 4; j++) {
+          const u32x4a4_t v = p[j];
+          r[4 * j] = v.x;
+          r[4 * j + 1] = v.y;
+          r[4 * j + 2] = v.z;
+          r[4 * j + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 16; u++) r[u] = inrow[min(max(x0 + u, 0), w - 1)];
+      }
+    };
+    struct Modes {
+      uint32_t m[TILE16 ? 2 : 16];
+      int ub;
+    };
+    auto ld_modes = [&](int x0, Modes& m) {
+      if constexpr (TILE16) {
+        const int t0 = min(max(x0, 0), w - 1) >> a.bits;
+        m.m[0] = mrow[t0];
+        m.m[1] = mrow[min(t0 + 1, a.tiles_x - 1)];
+        m.ub = ((t0 + 1) << a.bits) - x0;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 16; u++) m.m[u] = mrow[min(max(x0 + u, 0), w - 1) >> a.bits];
+        m.ub = 0;
+      }
+    };
+    uint32_t rc[16];
+    Modes mc;
+    uint64_t gr[16];
+    ld_res(-2 * k, rc);
+    ld_modes(-2 * k, mc);
 #pragma unroll
     for (int c = 0; c <= UPD; c++) gr[c & 15] = up_load(c);
-    uint32_t cT = up_take(0, gr[0]), cTL = cT;  // columns s and s - 1 of the row above at step s (lane 0)
+    // the row above at x and x - 1 (T and TL) of the step, as c2 halves: TR
+    // and T of the step before
+    const uint32_t cT = up_take(0, gr[0]);
+    uint32_t t = c2_of(cT, sel), tl = t;
     for (int s0 = 0; s0 < steps; s0 += 16) {
-      uint32_t rn[16], mn[16], ov[16], cc[16];
+      const int x0 = s0 - 2 * k;  // this chunk's first pixel in the lane's row
+      uint32_t rn[16], ov[16], cc[16];  // cc: the pixels' mask rows
+      Modes mn;
       // the chunk's control words (the tile modes arrived a chunk ago), with
       // the reference's border rules: row 0 L (black at x = 0), column 0 T,
-      // TR past the right edge is this row's first pixel
+      // TR past the right edge is this row's first pixel.  Those apply in the
+      // walk's first and last chunks only (x0 <= 0 or x0 + 15 >= w - 1 on
+      // some lane of the wave).
+      if constexpr (TILE16) {
+        const uint32_t k0 = y == 0 ? 18u : (mc.m[0] >> 8) & 0xf, k1 = y == 0 ? 18u : (mc.m[1] >> 8) & 0xf;
 #pragma unroll
-      for (int u = 0; u < 16; u++) {
-        const int x = s0 + u - 2 * lane;
-        const int idx = x == 0 ? (y == 0 ? 17 : 16) : (y == 0 ? 18 : (int)((mc[u] >> 8) & 0xf));
-        cc[u] = ctab[idx] | (x == w - 1 ? (uint32_t)C_EDGE : 0u);
+        for (int u = 0; u < 16; u++) cc[u] = u < mc.ub ? k0 : k1;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 16; u++) cc[u] = y == 0 ? 18u : (mc.m[u] >> 8) & 0xf;
       }
-#pragma unroll
-      for (int u = 0; u < 16; u++) {
-        const int x = s0 + u - 2 * lane;  // steps past the end run idle (x >= w on every lane)
-        rn[u] = ld_res(x + 16);  // the next chunk's inputs, a pair a step
-        mn[u] = ld_mode(x + 16);
-        gr[(u + 1 + UPD) & 15] = up_load(s0 + u + 1 + UPD);
-        const uint32_t cTR = up_take(s0 + u + 1, gr[(u + 1) & 15]);
-        // row above: lane k-1's outputs at x+1, x, x-1 from its previous step
-        // (wave_shr:1); lane 0 keeps its own copy of the band above's row
-        const uint32_t up_x1 = (uint32_t)__builtin_amdgcn_update_dpp((int)cTR, (int)o1, 0x138, 0xf, 0xf, false);
-        const uint32_t up_x = (uint32_t)__builtin_amdgcn_update_dpp((int)cT, (int)o2, 0x138, 0xf, 0xf, false);
-        const uint32_t up_xm1 = (uint32_t)__builtin_amdgcn_update_dpp((int)cTL, (int)o3, 0x138, 0xf, 0xf, false);
-        cTL = cT;
-        cT = cTR;
-        const uint32_t tr = bsel<12>(cc[u], first, up_x1);
-        const uint32_t v = add_pixels(rc[u], predict_ctl(cc[u], o1, up_x, tr, up_xm1));
-        const bool valid = live && x >= 0 && x < w;
-        // the hand-off: x has the step's parity (2 * lane is even), so odd
-        // steps store the pair (x - 1, x); an odd width's last pixel goes alone
-        if (u & 1) {
-          if (hands_off && valid) {
-            const u32x4_t g2 = {o1, 1u, v, 1u};
-            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(hand_mine + x - 1), "v"(g2) : "memory");
-          }
-        } else if (hands_off && x == w - 1) {
-          __hip_atomic_store(hand_mine + x, 1ull << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        first = x == 0 ? v : first;
-        o3 = o2;
-        o2 = o1;
-        o1 = valid ? v : 0u;
-        ov[u] = v;
-      }
-      // this chunk's outputs: pixels x0 .. x0 + 15 of the lane's row (8-B aligned)
-      const int x0 = s0 - 2 * lane;
-      if (live && x0 >= 0 && x0 + 15 < w) {
-        uint64_t* d = reinterpret_cast<uint64_t*>(orow + x0);
-#pragma unroll
-        for (int j = 0; j < 8; j++) d[j] = (uint64_t)ov[2 * j + 1] << 32 | ov[2 * j];
-      } else if (live) {
+      // (a chunk where x = 0 on some lane: the walk's first ones)
+      const bool starts = __builtin_amdgcn_readfirstlane(s0 <= 2 * (INV_ROWS - 1));
+      if (starts || __builtin_amdgcn_readfirstlane(s0 + 15 >= w - 1)) {
+        const uint32_t kx0 = y == 0 ? 17u : 16u;
 #pragma unroll
         for (int u = 0; u < 16; u++) {
           const int x = x0 + u;
-          if (x >= 0 && x < w) orow[x] = ov[u];
+          cc[u] = (x == 0 ? kx0 : cc[u]) + (x == w - 1 ? 19u : 0u);
+        }
+      }
+      SelMasks km = ld_masks(cc[0]);
+      ld_res(x0 + 16, rn);  // the next chunk's inputs
+      ld_modes(x0 + 16, mn);
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const int x = x0 + u;  // steps past the end run idle (x >= w on every lane)
+        gr[(u + 1 + UPD) & 15] = up_load(s0 + u + 1 + UPD);
+        const uint32_t cTR = up_take(s0 + u + 1, gr[(u + 1) & 15]);
+        // row above at x + 1: the pair before's output from its previous
+        // step; at x and x - 1 the last two steps' TR
+        const uint32_t up_x1 = from_pair_above(o1, c2_of(cTR, C2_EVEN), c2_of(cTR, C2_ODD));
+        const SelMasks kn = ld_masks(cc[(u + 1) & 15]);  // the next step's (u = 15: unused)
+        const uint32_t tr = msel(km.m[12], first, up_x1);
+        const uint32_t v = c2_add(c2_of(rc[u], sel), predict_c2(km, o1, t, tr, tl, black));
+        km = kn;
+        tl = t;
+        t = up_x1;
+        // the whole pixel on the pair's even lane (quad_perm 1,1,3,3: the odd lane's half)
+        const uint32_t vodd = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xf5, 0xf, 0xf, false);
+        const uint32_t full = v | vodd << 8;
+        // the hand-off: x has the step's parity (2k is even), so odd steps
+        // store the pair (x - 1, x); an odd width's last pixel goes alone
+        // (the hand-off lane's row is live)
+        if (u & 1) {
+          if (hands_off && (uint32_t)x < (uint32_t)w) {
+            const u32x4_t g2 = {ov[u - 1], 1u, full, 1u};
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(hand_mine + x - 1), "v"(g2) : "memory");
+          }
+        } else if (hands_off && x == w - 1) {
+          __hip_atomic_store(hand_mine + x, 1ull << 32 | full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (starts) first = x == 0 ? v : first;
+        // (outputs at x outside the row are never read: at x = 0 the row
+        // above's TL and the left neighbour are unused, and the pair below
+        // reads x = w as TR only where C_EDGE takes `first` instead)
+        o1 = v;
+        ov[u] = full;
+      }
+      // this chunk's outputs: pixels x0 .. x0 + 15 of the row, from the even lane
+      if ((lane & 1) == 0 && live) {
+        if (x0 >= 0 && x0 + 15 < w) {
+          uint64_t* d = reinterpret_cast<uint64_t*>(orow + x0);
+#pragma unroll
+          for (int j = 0; j < 8; j++) d[j] = (uint64_t)ov[2 * j + 1] << 32 | ov[2 * j];
+        } else {
+#pragma unroll
+          for (int u = 0; u < 16; u++) {
+            const int x = x0 + u;
+            if (x >= 0 && x < w) orow[x] = ov[u];
+          }
         }
       }
 #pragma unroll
-      for (int u = 0; u < 16; u++) {
-        rc[u] = rn[u];
-        mc[u] = mn[u];
-      }
+      for (int u = 0; u < 16; u++) rc[u] = rn[u];
+      mc = mn;
     }
   }
 }
@@ -595,7 +726,7 @@ extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32
 
 extern "C" size_t wg_vp8l_inverse_work_bytes(int32_t width, int32_t height, int32_t n_images) {
   if (width <= 0 || height <= 0 || n_images <= 0) return 0;
-  return 16 + sizeof(uint64_t) * (size_t)n_images * ((height + 63) / 64) * ((width + 1) & ~1);
+  return 16 + sizeof(uint64_t) * (size_t)n_images * ((height + INV_ROWS - 1) / INV_ROWS) * ((width + 1) & ~1);
 }
 
 extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, int32_t width, int32_t height,
@@ -609,7 +740,7 @@ extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, in
   a.modes = modes;
   a.in = residuals;
   a.out = out;
-  a.bands = (height + 63) / 64;
+  a.bands = (height + INV_ROWS - 1) / INV_ROWS;
   a.n_img = n_images;
   a.ctl = static_cast<int*>(work);
   a.diag = wg::diag_words(s);
@@ -627,7 +758,10 @@ extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, in
     return wg::check_launch("hipMemsetAsync(vp8l work)");
   const int total = a.bands * n_images;
   const int grid = total < 2048 ? total : 2048;
-  hipLaunchKernelGGL(k_vp8l_inverse, dim3((unsigned)grid), dim3(64), 0, s, a);
+  if (bits >= 4)
+    hipLaunchKernelGGL(k_vp8l_inverse<true>, dim3((unsigned)grid), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_vp8l_inverse<false>, dim3((unsigned)grid), dim3(64), 0, s, a);
   return wg::check_launch("k_vp8l_inverse");
 }
 
