@@ -210,7 +210,7 @@ __device__ __forceinline__ int from_lin_w(const uint32_t* l2g, const uint16_t* l
 // byte offset: the uniform part stays in SGPRs (global_load saddr + a 32-bit
 // VGPR offset) instead of a 64-bit address per lane and load
 template <typename T>
-__device__ __forceinline__ const uint32_t* at(const T* base, int64_t ubytes, uint32_t lbytes) {
+__device__ __forceinline__ const uint32_t* at(const T* base, uint32_t ubytes, uint32_t lbytes) {
   return reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(base) + ubytes + lbytes);
 }
 // (the lane offsets are laundered once a step: hoisted out of the walk, base
@@ -238,7 +238,9 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
   int* prog_img = a.prog + (int64_t)img * 4 * nb;  // [iteration][band]: row pairs finished
   int* prog_out = prog_img + it * nb + band;
   bool timed_out = false;  // wave-uniform
-  const int64_t uv_row_bytes = 2 * (int64_t)rs, y_row_bytes = 2 * (int64_t)w;
+  // byte offsets inside one state plane fit 32 bits (a 16383^2 image's Y
+  // state is 537 MB): 32-bit scalar row offsets, not 64-bit products
+  const uint32_t uv_row_bytes = 2u * (uint32_t)rs, y_row_bytes = 2u * (uint32_t)w;
 
   // wait (the whole wave, on one wave-uniform address) until band bb of
   // iteration ii has finished `need` row pairs; the progress seen (uvh for a band that does not exist)
@@ -290,7 +292,7 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
   };
   auto load_row = [&](int row) {
     Row r;
-    const int64_t ub = (int64_t)min(row, uvh - 1) * uv_row_bytes;  // clamped: the last row pair's next is its cur
+    const uint32_t ub = (uint32_t)min(row, uvh - 1) * uv_row_bytes;  // clamped: the last row pair's next is its cur
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) r.v[ch] = ld_sc1(at(in_uv, ub, lo_uv[ch]));
     return r;
@@ -301,12 +303,12 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
   auto load_in = [&](int jp) {
     In r;
     const int jc = min(jp, uvh - 1);
-    const int64_t yb = (int64_t)(2 * jc) * y_row_bytes;
+    const uint32_t yb = (uint32_t)(2 * jc) * y_row_bytes;
     r.y[0] = ld_sc1(at(in_y, yb, lo_y));
     r.y[1] = ld_sc1(at(in_y, yb + y_row_bytes, lo_y));
     r.ty[0] = *at(ty, yb, lo_y);
     r.ty[1] = *at(ty, yb + y_row_bytes, lo_y);
-    const int64_t ub = (int64_t)jc * uv_row_bytes;
+    const uint32_t ub = (uint32_t)jc * uv_row_bytes;
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) r.tuv[ch] = *at(tuv, ub, lo_uv[ch]);
     return r;
@@ -334,7 +336,7 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
       wait_for(it, band - 1, ju);
       wait_for(it, band + 1, ju);
       if (act && !own) {
-        const int64_t ub = (int64_t)(ju - 1) * uv_row_bytes;
+        const uint32_t ub = (uint32_t)(ju - 1) * uv_row_bytes;
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) P.v[ch] = ld_sc1(at(out_uv, ub, lo_uv[ch]));
       }
@@ -421,10 +423,10 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     }
     // publish this band's own columns of the updated UV row ju and luma pair (write-through)
     if (own) {
-      uint8_t* ob = reinterpret_cast<uint8_t*>(out_uv) + (int64_t)ju * uv_row_bytes;
+      uint8_t* ob = reinterpret_cast<uint8_t*>(out_uv) + (uint32_t)ju * uv_row_bytes;
 #pragma unroll
       for (int ch = 0; ch < 3; ch++) st_sc1_16(ob + st_uv[ch], (uint16_t)upd[ch]);
-      uint8_t* oy = reinterpret_cast<uint8_t*>(out_y) + (int64_t)j * y_row_bytes;
+      uint8_t* oy = reinterpret_cast<uint8_t*>(out_y) + (uint32_t)j * y_row_bytes;
       st_sc1(oy + lo_y, ynew[0]);
       st_sc1(oy + y_row_bytes + lo_y, ynew[1]);
     }
@@ -603,6 +605,8 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
                                       int64_t y_pitch, uint8_t* u, uint8_t* v, int32_t uv_stride, int64_t uv_pitch,
                                       void* work, void* stream) {
   WG_REQUIRE(rgb && matrix_host && y && u && v && width > 0 && height > 0 && n_images > 0);
+  // (the walk's in-plane byte offsets are 32-bit: 2 B a pixel, < 2^31)
+  WG_REQUIRE((int64_t)((width + 1) & ~1) * ((height + 1) & ~1) < (1ll << 30));
   WG_REQUIRE(rgb_stride >= 3 * width && y_stride >= width && uv_stride >= (width + 1) / 2);
   hipStream_t s = wg::as_stream(stream);
   if (!sharp_enabled) {  // convertStandard (sharpyuv.go:68-115)
