@@ -176,7 +176,10 @@ __device__ __forceinline__ void st_sc1_16(void* p, uint16_t v) {
 // prev, the only row this iteration produces itself; cur / next / luma come
 // from the previous state in memory every step), so every WB_HALO row pairs
 // the halo lanes reload prev from the neighbour bands' published output.
-constexpr int WB_OWN = 32, WB_HALO = 16, WB_PUB = 16;
+#ifndef WG_SHARP_OWN
+#define WG_SHARP_OWN 32
+#endif
+constexpr int WB_OWN = WG_SHARP_OWN, WB_HALO = (64 - WB_OWN) / 2, WB_PUB = WB_HALO;
 static_assert(WB_OWN + 2 * WB_HALO == 64 && WB_HALO % WB_PUB == 0, "wave band layout");
 
 // (bound_ctrl: the wave's end lanes, always halo lanes, read 0 -- no register to initialise)
@@ -217,13 +220,36 @@ __device__ __forceinline__ const uint32_t* at(const T* base, uint32_t ubytes, ui
 // + lane offset would become a 64-bit per-lane pointer and every load a 64-bit add)
 __device__ __forceinline__ void launder_v(uint32_t& v) { asm volatile("" : "+v"(v)); }
 
-// One band of one iteration.  EDGE: the band's lanes include column 0 or
-// column uvw - 1 (the reference's filter2 at the plane's edges); the other
-// bands run without those selects.
-template <bool LUT, bool EDGE>
-__device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpTabs& t, int nb, int band, int it,
-                                                int img) {
-  const int lane = threadIdx.x;
+// The band walk is split between the workgroup's two waves (round 4): wave A
+// (ROLE 0) makes row j of each row pair -- the Gauss-Seidel chain: it reads
+// prev, the row pair above's updated chroma -- and the chroma update; wave B
+// (ROLE 1) makes row j + 1, which reads only the input state (cur and next),
+// so it runs ahead of A and hands A, per row pair and column, its two
+// pixels' linear RGB sums through an LDS ring (XD row pairs deep).  A's
+// step is then half the interpolation, half the gamma lookups and half the
+// luma update of the one-wave walk: the walk was issue-bound (one wave alone
+// on its SIMD, ~650 instructions a row pair).
+constexpr int XD = WB_PUB <= 16 ? 16 : 32;  // exchange ring depth, in row pairs (>= WB_PUB: see the drain hand-shake)
+struct SharpX {
+  uint4 sum[XD][64];  // B's row j + 1: the sums of its two pixels' linear R, G, B per column lane
+  int prog_b;         // row pairs B has put into sum[]
+  int prog_a;         // row pairs A has taken out of sum[]
+  int drained_b;      // row pairs whose luma stores B has drained (for A's progress publication)
+};
+__device__ __forceinline__ int lds_acquire(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// One band of one iteration, one row of each row pair (ROLE).  EDGE: the
+// band's lanes include column 0 or column uvw - 1 (the reference's filter2
+// at the plane's edges); the other bands run without those selects.
+template <bool LUT, bool EDGE, int ROLE>
+__device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpTabs& t, SharpX& x, int nb, int band,
+                                                int it, int img) {
+  const int lane = threadIdx.x & 63;
   const int uvw = a.uvw, uvh = a.uvh, w = a.w, rs = a.uv_rs;
   const int c = band * WB_OWN - WB_HALO + lane;  // this lane's UV column
   const bool act = c >= 0 && c < uvw;
@@ -256,6 +282,19 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
         return uvh;
       }
       __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  // the same for the other wave's LDS progress word
+  auto wait_lds = [&](const int* p, int need) {
+    if (timed_out || __builtin_amdgcn_readfirstlane(lds_acquire(p)) >= need) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t k = 0;; k++) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_readfirstlane(lds_acquire(p)) >= need) return;
+      if ((k & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+        timed_out = true;
+        return;
+      }
     }
   };
   int seen_in = it == 0 ? uvh : 0;  // input state rows known ready (iteration it-1, bands band-1..band+1)
@@ -297,29 +336,32 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     for (int ch = 0; ch < 3; ch++) r.v[ch] = ld_sc1(at(in_uv, ub, lo_uv[ch]));
     return r;
   };
+  // this role's luma row of a row pair: the input state's and the target's
+  // pixel pair, and (A) the chroma targets
   struct In {
-    uint32_t y[2], ty[2], tuv[3];
+    uint32_t y, ty, tuv[ROLE == 0 ? 3 : 1];
   };
   auto load_in = [&](int jp) {
     In r;
     const int jc = min(jp, uvh - 1);
-    const uint32_t yb = (uint32_t)(2 * jc) * y_row_bytes;
-    r.y[0] = ld_sc1(at(in_y, yb, lo_y));
-    r.y[1] = ld_sc1(at(in_y, yb + y_row_bytes, lo_y));
-    r.ty[0] = *at(ty, yb, lo_y);
-    r.ty[1] = *at(ty, yb + y_row_bytes, lo_y);
-    const uint32_t ub = (uint32_t)jc * uv_row_bytes;
+    const uint32_t yb = (uint32_t)(2 * jc + ROLE) * y_row_bytes;
+    r.y = ld_sc1(at(in_y, yb, lo_y));
+    r.ty = *at(ty, yb, lo_y);
+    if constexpr (ROLE == 0) {
+      const uint32_t ub = (uint32_t)jc * uv_row_bytes;
 #pragma unroll
-    for (int ch = 0; ch < 3; ch++) r.tuv[ch] = *at(tuv, ub, lo_uv[ch]);
+      for (int ch = 0; ch < 3; ch++) r.tuv[ch] = *at(tuv, ub, lo_uv[ch]);
+    }
     return r;
   };
   // the signed 16-bit value of this column's channel ch in a loaded word
   auto sx16 = [&](uint32_t v, int ch) { return __builtin_amdgcn_sbfe((int)v, hs[ch], 16); };
 
-  uint32_t my_sum = 0;  // |dY| over this lane's pixels: < 4 * 1023 per row pair, uvh <= 2^13
+  uint32_t my_sum = 0;  // |dY| over this lane's pixels: < 2 * 1023 per row pair, uvh <= 2^13
   // rings of four row pairs, indexed by ju % 4 (compile-time after the
   // unrolled loop below, so no register moves): the input state's chroma row
-  // and luma / target pair of row pairs ju .. ju + 3, prefetched three ahead
+  // and this role's luma / target row of row pairs ju .. ju + 3, prefetched
+  // three ahead
   Row R[4];
   In I[4];
   wait_input(min(4, uvh));
@@ -329,17 +371,21 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
   I[0] = load_in(0);
   I[1] = load_in(1);
   I[2] = load_in(2);
-  Row P = R[0];  // prev(row 0) = cur(row 0)
+  Row P = R[0];  // (A) prev(row 0) = cur(row 0)
   auto step = [&](int ju, const Row& C, const Row& N, Row& pf_row, const In& in_cur, In& pf_in) {
     wait_input(min(ju + 4, uvh));  // UV row ju + 3 and luma pair ju + 3 of the input state
-    if (ju > 0 && ju % WB_HALO == 0) {  // the halo lanes' prev: the neighbours' row ju - 1 of this iteration
-      wait_for(it, band - 1, ju);
-      wait_for(it, band + 1, ju);
-      if (act && !own) {
-        const uint32_t ub = (uint32_t)(ju - 1) * uv_row_bytes;
+    if constexpr (ROLE == 0) {
+      if (ju > 0 && ju % WB_HALO == 0) {  // the halo lanes' prev: the neighbours' row ju - 1 of this iteration
+        wait_for(it, band - 1, ju);
+        wait_for(it, band + 1, ju);
+        if (act && !own) {
+          const uint32_t ub = (uint32_t)(ju - 1) * uv_row_bytes;
 #pragma unroll
-        for (int ch = 0; ch < 3; ch++) P.v[ch] = ld_sc1(at(out_uv, ub, lo_uv[ch]));
+          for (int ch = 0; ch < 3; ch++) P.v[ch] = ld_sc1(at(out_uv, ub, lo_uv[ch]));
+        }
       }
+    } else {
+      wait_lds(&x.prog_a, ju - XD + 1);  // A has taken ring slot ju % XD's previous row pair
     }
     const int j = 2 * ju;
 #pragma unroll
@@ -350,93 +396,85 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     launder_v(lo_y);
     pf_row = load_row(ju + 3);
     pf_in = load_in(ju + 3);
-    int upd[3] = {0, 0, 0};
-    uint32_t ynew[2] = {0, 0};
-    {
-      // interpolateTwoRows (:322-359) for pixels x = 2c, 2c+1 of rows j, j+1
-      int iv[2][2][3];
-      const uint32_t r0 = in_cur.y[0], r1 = in_cur.y[1];
-      const int by00 = r0 & 0xffff, by01 = r0 >> 16, by10 = r1 & 0xffff, by11 = r1 >> 16;
+    // interpolateTwoRows (:322-359) for pixels x = 2c, 2c + 1 of row j (A:
+    // from cur and prev) or j + 1 (B: from cur and next)
+    const Row& O = ROLE == 0 ? P : N;
+    int iv[2][3];
+    const int by0 = in_cur.y & 0xffff, by1 = in_cur.y >> 16;
 #pragma unroll
-      for (int ch = 0; ch < 3; ch++) {
-        const int a1 = sx16(C.v[ch], ch), b1 = sx16(P.v[ch], ch), n1 = sx16(N.v[ch], ch);
-        const int a0 = dpp_from_left(a1), b0 = dpp_from_left(b1), n0 = dpp_from_left(n1);
-        const int a2 = dpp_from_right(a1), b2 = dpp_from_right(b1), n2 = dpp_from_right(n1);
-        int e0, e1, f0, f1;  // x = 2c: row j / j+1
-        if (EDGE && c == 0) {
-          e0 = (a1 * 3 + b1 + 2) >> 2;  // filter2(cur[0], prev[0])
-          f0 = (a1 * 3 + n1 + 2) >> 2;
-        } else {
-          e0 = (a1 * 9 + a0 * 3 + b1 * 3 + b0 + 8) >> 4;
-          f0 = (a1 * 9 + a0 * 3 + n1 * 3 + n0 + 8) >> 4;
-        }
-        if (EDGE && c == uvw - 1) {  // x = w-1: filter2(cur[uvw-1], prev[uvw-1])
-          e1 = (a1 * 3 + b1 + 2) >> 2;
-          f1 = (a1 * 3 + n1 + 2) >> 2;
-        } else {
-          e1 = (a1 * 9 + a2 * 3 + b1 * 3 + b2 + 8) >> 4;
-          f1 = (a1 * 9 + a2 * 3 + n1 * 3 + n2 + 8) >> 4;
-        }
-        iv[0][0][ch] = clip_bd(by00 + e0);
-        iv[0][1][ch] = clip_bd(by01 + e1);
-        iv[1][0][ch] = clip_bd(by10 + f0);
-        iv[1][1][ch] = clip_bd(by11 + f1);
+    for (int ch = 0; ch < 3; ch++) {
+      const int a1 = sx16(C.v[ch], ch), b1 = sx16(O.v[ch], ch);
+      const int a0 = dpp_from_left(a1), b0 = dpp_from_left(b1);
+      const int a2 = dpp_from_right(a1), b2 = dpp_from_right(b1);
+      int e0, e1;
+      if (EDGE && c == 0) e0 = (a1 * 3 + b1 + 2) >> 2;  // filter2(cur[0], prev / next[0])
+      else e0 = (a1 * 9 + a0 * 3 + b1 * 3 + b0 + 8) >> 4;
+      if (EDGE && c == uvw - 1) e1 = (a1 * 3 + b1 + 2) >> 2;  // x = w-1: filter2(cur[uvw-1], prev / next[uvw-1])
+      else e1 = (a1 * 9 + a2 * 3 + b1 * 3 + b2 + 8) >> 4;
+      iv[0][ch] = clip_bd(by0 + e0);
+      iv[1][ch] = clip_bd(by1 + e1);
+    }
+    // updateW -> bestRGBY, sharpYUVUpdateY (:361-381)
+    uint32_t lin[2][3];
+    int ny[2];
+#pragma unroll
+    for (int cc = 0; cc < 2; cc++) {
+#pragma unroll
+      for (int ch = 0; ch < 3; ch++) lin[cc][ch] = to_linear(t.g2l, iv[cc][ch]);
+      // (the other transfer functions' linear values reach ~72k: 64-bit gray)
+      const uint32_t g = LUT ? (uint32_t)gray(lin[cc][0], lin[cc][1], lin[cc][2]) : gray_u32(lin[cc][0], lin[cc][1], lin[cc][2]);
+      const int yv = from_lin_w<LUT>(t.l2g, a.lut, a.lut_n, g);
+      const int d = (int)((in_cur.ty >> (16 * cc)) & 0xffff) - yv;
+      ny[cc] = clip_bd((cc ? by1 : by0) + d);
+      my_sum += (uint32_t)abs(d);
+    }
+    const uint32_t ynew = (uint32_t)ny[0] | (uint32_t)ny[1] << 16;
+    uint8_t* oy = reinterpret_cast<uint8_t*>(out_y) + (uint32_t)(j + ROLE) * y_row_bytes;
+    if constexpr (ROLE == 1) {
+      // hand A this row pair's linear sums, then store the luma row
+      x.sum[ju % XD][lane] = make_uint4(lin[0][0] + lin[1][0], lin[0][1] + lin[1][1], lin[0][2] + lin[1][2], 0u);
+      if (lane == 0) lds_release(&x.prog_b, ju + 1);
+      if (own) st_sc1(oy + lo_y, ynew);
+      if ((ju + 1) % WB_PUB == 0 || ju + 1 == uvh) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) lds_release(&x.drained_b, ju + 1);
       }
-      // updateW -> bestRGBY, sharpYUVUpdateY (:361-381)
-      uint32_t lin[2][2][3];
-      int yv[2][2];
-#pragma unroll
-      for (int r = 0; r < 2; r++)
-#pragma unroll
-        for (int cc = 0; cc < 2; cc++) {
-#pragma unroll
-          for (int ch = 0; ch < 3; ch++) lin[r][cc][ch] = to_linear(t.g2l, iv[r][cc][ch]);
-          // (the other transfer functions' linear values reach ~72k: 64-bit gray)
-          const uint32_t g = LUT ? (uint32_t)gray(lin[r][cc][0], lin[r][cc][1], lin[r][cc][2])
-                                 : gray_u32(lin[r][cc][0], lin[r][cc][1], lin[r][cc][2]);
-          yv[r][cc] = from_lin_w<LUT>(t.l2g, a.lut, a.lut_n, g);
-        }
-      const int byv[2][2] = {{by00, by01}, {by10, by11}};
-      int ny[2][2];
-#pragma unroll
-      for (int r = 0; r < 2; r++)
-#pragma unroll
-        for (int cc = 0; cc < 2; cc++) {
-          const int d = (int)((in_cur.ty[r] >> (16 * cc)) & 0xffff) - yv[r][cc];
-          ny[r][cc] = clip_bd(byv[r][cc] + d);
-          my_sum += (uint32_t)abs(d);
-        }
-      ynew[0] = (uint32_t)ny[0][0] | (uint32_t)ny[0][1] << 16;
-      ynew[1] = (uint32_t)ny[1][0] | (uint32_t)ny[1][1] << 16;
-      // updateChroma -> bestRGBUV, sharpYUVUpdateRGB (:383-388)
+    } else {
+      // updateChroma -> bestRGBUV, sharpYUVUpdateRGB (:383-388), with B's
+      // sums of row j + 1
+      wait_lds(&x.prog_b, ju + 1);
+      const uint4 sb = x.sum[ju % XD][lane];
+      if (lane == 0) lds_release(&x.prog_a, ju + 1);  // (the sums are in registers: the slot is free)
+      const uint32_t bs[3] = {sb.x, sb.y, sb.z};
       int rgbv[3];
 #pragma unroll
       for (int ch = 0; ch < 3; ch++)
-        rgbv[ch] = from_lin_w<LUT>(t.l2g, a.lut, a.lut_n, (lin[0][0][ch] + lin[0][1][ch] + lin[1][0][ch] + lin[1][1][ch] + 2) >> 2);
+        rgbv[ch] = from_lin_w<LUT>(t.l2g, a.lut, a.lut_n, (lin[0][ch] + lin[1][ch] + bs[ch] + 2) >> 2);
       const int gv = (int)gray_u32(rgbv[0], rgbv[1], rgbv[2]);
+      int upd[3];
 #pragma unroll
       for (int ch = 0; ch < 3; ch++) {
         const int16_t srcv = (int16_t)(rgbv[ch] - gv);
         const int16_t d = (int16_t)(sx16(in_cur.tuv[ch], ch) - srcv);
         upd[ch] = (int16_t)(sx16(C.v[ch], ch) + d);
       }
-    }
-    // publish this band's own columns of the updated UV row ju and luma pair (write-through)
-    if (own) {
-      uint8_t* ob = reinterpret_cast<uint8_t*>(out_uv) + (uint32_t)ju * uv_row_bytes;
+      // publish this band's own columns of the updated UV row ju and luma row j (write-through)
+      if (own) {
+        uint8_t* ob = reinterpret_cast<uint8_t*>(out_uv) + (uint32_t)ju * uv_row_bytes;
 #pragma unroll
-      for (int ch = 0; ch < 3; ch++) st_sc1_16(ob + st_uv[ch], (uint16_t)upd[ch]);
-      uint8_t* oy = reinterpret_cast<uint8_t*>(out_y) + (uint32_t)j * y_row_bytes;
-      st_sc1(oy + lo_y, ynew[0]);
-      st_sc1(oy + y_row_bytes + lo_y, ynew[1]);
-    }
+        for (int ch = 0; ch < 3; ch++) st_sc1_16(ob + st_uv[ch], (uint16_t)upd[ch]);
+        st_sc1(oy + lo_y, ynew);
+      }
 #pragma unroll
-    for (int ch = 0; ch < 3; ch++) P.v[ch] = (uint32_t)(uint16_t)upd[ch] << hs[ch];  // prev <- the updated cur (in its half)
-    if ((ju + 1) % WB_PUB == 0 || ju + 1 == uvh) {
-      // publish row pairs <= ju once this wave's stores of them are done (a
-      // drain also waits for the loads in flight, so only every WB_PUB steps)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) st_sc1(prog_out, (uint32_t)(ju + 1));
+      for (int ch = 0; ch < 3; ch++) P.v[ch] = (uint32_t)(uint16_t)upd[ch] << hs[ch];  // prev <- the updated cur (in its half)
+      if ((ju + 1) % WB_PUB == 0 || ju + 1 == uvh) {
+        // publish row pairs <= ju once this wave's stores of them are done,
+        // and B's (a drain also waits for the loads in flight, so only every
+        // WB_PUB steps)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wait_lds(&x.drained_b, ju + 1);
+        if (lane == 0) st_sc1(prog_out, (uint32_t)(ju + 1));
+      }
     }
   };
   for (int j0 = 0; j0 < uvh; j0 += 4) {
@@ -457,15 +495,24 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
 }
 
 template <bool LUT>
-__global__ __launch_bounds__(64) void k_sharp_wave(SharpArgs a, int nb) {
+__global__ __launch_bounds__(128) void k_sharp_wave(SharpArgs a, int nb) {
   __shared__ SharpTabs t;
+  __shared__ SharpX x;
   const int blk = blockIdx.x, band = blk % nb, it = (blk / nb) & 3, img = blk / (4 * nb);
   if (img >= a.n_img) return;  // uniform over the block
-  load_tabs(t, a.tabs);
+  if (threadIdx.x == 0) x.prog_b = x.prog_a = x.drained_b = 0;
+  load_tabs(t, a.tabs);  // (its barrier also orders the counters' initialisation)
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // the band's lanes cover columns band * WB_OWN - WB_HALO .. + 63
   const int c0 = band * WB_OWN - WB_HALO;
-  if (c0 <= 0 || c0 + 63 >= a.uvw - 1) sharp_wave_band<LUT, true>(a, t, nb, band, it, img);
-  else sharp_wave_band<LUT, false>(a, t, nb, band, it, img);
+  const bool edge = c0 <= 0 || c0 + 63 >= a.uvw - 1;
+  if (role == 0) {
+    if (edge) sharp_wave_band<LUT, true, 0>(a, t, x, nb, band, it, img);
+    else sharp_wave_band<LUT, false, 0>(a, t, x, nb, band, it, img);
+  } else {
+    if (edge) sharp_wave_band<LUT, true, 1>(a, t, x, nb, band, it, img);
+    else sharp_wave_band<LUT, false, 1>(a, t, x, nb, band, it, img);
+  }
 }
 
 // The iterations the reference runs (:224-264): 0 and 1 always; after
@@ -685,7 +732,7 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
   // images as the device holds at once (4 iterations x nb bands each)
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sharp_wave<false>, 64, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sharp_wave<false>, 128, 0) != hipSuccess ||
       per_cu <= 0)
     return wg::check_launch("sharpyuv occupancy");
   const int chunk = std::max(1, per_cu * cus / (4 * nb));  // images per launch
@@ -702,9 +749,9 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
     c.iters += i0;
     const unsigned grid = (unsigned)(c.n_img * 4 * nb);
     if (lut)
-      hipLaunchKernelGGL(k_sharp_wave<true>, dim3(grid), dim3(64), 0, s, c, nb);
+      hipLaunchKernelGGL(k_sharp_wave<true>, dim3(grid), dim3(128), 0, s, c, nb);
     else
-      hipLaunchKernelGGL(k_sharp_wave<false>, dim3(grid), dim3(64), 0, s, c, nb);
+      hipLaunchKernelGGL(k_sharp_wave<false>, dim3(grid), dim3(128), 0, s, c, nb);
     rc = wg::check_launch("k_sharp_wave");
     if (rc != WG_OK) return rc;
   }
