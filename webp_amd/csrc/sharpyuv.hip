@@ -396,6 +396,18 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     launder_v(lo_y);
     pf_row = load_row(ju + 3);
     pf_in = load_in(ju + 3);
+    // (A) B's sums of this row pair, read now and used after A's own half:
+    // B's progress word first, then the slot, with no wait between (the LDS
+    // unit performs one wave's reads in issue order, and B wrote the slot
+    // before its release of the word), so a B that is ahead -- the usual
+    // case -- costs no round trip on A's chain
+    uint4 sb = make_uint4(0, 0, 0, 0);
+    int pb = 0;
+    if constexpr (ROLE == 0) {
+      pb = __hip_atomic_load(&x.prog_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      asm volatile("" ::: "memory");
+      sb = x.sum[ju % XD][lane];
+    }
     // interpolateTwoRows (:322-359) for pixels x = 2c, 2c + 1 of row j (A:
     // from cur and prev) or j + 1 (B: from cur and next)
     const Row& O = ROLE == 0 ? P : N;
@@ -442,8 +454,10 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     } else {
       // updateChroma -> bestRGBUV, sharpYUVUpdateRGB (:383-388), with B's
       // sums of row j + 1
-      wait_lds(&x.prog_b, ju + 1);
-      const uint4 sb = x.sum[ju % XD][lane];
+      if (__builtin_amdgcn_readfirstlane(pb) < ju + 1) {  // B was not ahead: wait, then read the slot again
+        wait_lds(&x.prog_b, ju + 1);
+        sb = x.sum[ju % XD][lane];
+      }
       if (lane == 0) lds_release(&x.prog_a, ju + 1);  // (the sums are in registers: the slot is free)
       const uint32_t bs[3] = {sb.x, sb.y, sb.z};
       int rgbv[3];
