@@ -1240,7 +1240,7 @@ struct DecConfig {
   int rows_per_cu = 0;   // resident k_decode_bands workgroups per CU (occupancy)
   int split_per_cu = 0;  // resident k_decode_split workgroups per CU
   int max_wg = 0;        // grid cap (0: every resident slot; WG_DECODE_MAX_WG)
-  int use_split = 1;     // WG_DECODE_KERNEL=bands selects k_decode_bands (A/B)
+  int force = 0;         // WG_DECODE_KERNEL=split / bands forces one kernel (A/B); 0: by batch size
 };
 std::mutex g_dec_cfg_mu;
 DecConfig g_dec_cfg;
@@ -1259,7 +1259,7 @@ int dec_config(DecConfig* out) {
     c.rows_per_cu = per_cu;
     c.split_per_cu = per_cu_s;
     if (const char* e = getenv("WG_DECODE_WG_PER_CU")) c.rows_per_cu = atoi(e) > 0 ? atoi(e) : per_cu;  // tuning
-    if (const char* e = getenv("WG_DECODE_KERNEL")) c.use_split = strcmp(e, "bands") != 0;
+    if (const char* e = getenv("WG_DECODE_KERNEL")) c.force = strcmp(e, "bands") == 0 ? 2 : (strcmp(e, "split") == 0 ? 1 : 0);
     if (const char* e = getenv("WG_DECODE_MAX_WG")) c.max_wg = atoi(e) > 0 ? atoi(e) : 0;  // tuning: cap the grid
     c.num_cus = cus;
   }
@@ -1318,7 +1318,16 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   if (const int e = dec_config(&cfg)) return e;
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * (2 * (size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(decode ctl)");
-  if (cfg.use_split) {
+  // k_decode_split (two waves a row: reconstruction and loop filter apart)
+  // shortens a row's macroblock time, which is what bounds a batch whose rows
+  // all fit the chip at once (C3's one 4096^2 image: 3.8 ms against 5.1 ms
+  // with one wave a row).  A batch with more rows than that holds twice the
+  // wave slots per row for the same throughput, and beside the encoder (the
+  // bench's pipeline) those slots are the encoder's: k_decode_bands there
+  // (64 x 1080p: whole-path median 6,495 -> 7,065 MPix/s, decode side alone
+  // 77.4k -> 76.1k).
+  const bool use_split = cfg.force ? cfg.force == 1 : (int64_t)n_images * mbh <= (int64_t)cfg.split_per_cu * cfg.num_cus * SW;
+  if (use_split) {
     const int bands = n_images * ((mbh + SW - 1) / SW);
     int grid = bands < cfg.split_per_cu * cfg.num_cus ? bands : cfg.split_per_cu * cfg.num_cus;
     if (cfg.max_wg > 0 && grid > cfg.max_wg) grid = cfg.max_wg;
