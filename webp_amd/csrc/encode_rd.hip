@@ -1084,7 +1084,13 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
   __shared__ Shared s_waves[NW];
   __shared__ int s_gbar[GROUPS];  // the groups' barrier counters (group_barrier)
   // the quantisers of the image a group's band (PAIR: the pair's row) belongs to
-  __shared__ Segment s_seg[PAIR ? 1 : GROUPS][4];
+  // (one group: two tables, by band sequence parity -- the group's waves
+  // move on to their next band one by one, see the dequeue below)
+  constexpr bool LOOSE = !PAIR && GROUPS == 1;
+  __shared__ Segment s_seg[PAIR ? 1 : (LOOSE ? 2 : GROUPS)][4];
+  // LOOSE: the band of each sequence parity, its publication (sequence + 1)
+  // and the count of waves done with it (monotonic over the parity's uses)
+  __shared__ int s_band[2], s_ready[2], s_done[2];
   static_assert(PAIR || sizeof(Tables) + NW * sizeof(Shared) + sizeof(s_gbar) + sizeof(s_seg) <= 160 * 1024,
                 "the workgroup's LDS must fit one CU");
   Tables& t = t_lds;
@@ -1096,6 +1102,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
   for (int i = tid; i < 1000; i += NT) t.fixed_i4[i] = c_fixed_i4[i];
   if (tid < 16) t.wtr[tid] = c_wtrellis[tid];
   if (tid < GROUPS) s_gbar[tid] = 0;
+  if (tid < 2) s_ready[tid] = s_done[tid] = 0;
   for (int i = tid; i < 160; i += NT) t.pcode[i >> 4][i & 15] = kPred4Code[i >> 4][i & 15];
   __syncthreads();
   for (int i = tid; i < 4 * 8 * 68; i += NT) {
@@ -1140,6 +1147,23 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
   // (not PAIR) this wave's group and its place in it
   const int grp = wave / WAVES, gw = wave - WAVES * grp;
   int gen = 0;
+  int q = 0;  // LOOSE: this wave's band sequence number in the workgroup
+  // LOOSE: bounded LDS spin of the whole wave until *p >= need (acquire)
+  auto wait_lds = [&](const int* p, int need) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t it = 0;; it++) {
+      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >= need)
+        return;
+      if ((it & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+        if (lane == 0) {
+          __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          wg::note_timeout(a.diag, -1, q, need, 0, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x);
+        }
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
   for (;;) {
     // PAIR: the workgroup's wave pair dequeues a row; otherwise each group
     // of WAVES waves dequeues a BAND of WAVES consecutive rows of one image
@@ -1161,6 +1185,39 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       ro = use_order ? __builtin_amdgcn_readfirstlane(a.order[row]) : row;
       mby = ro / a.n_img;
       img = ro % a.n_img;
+    } else if constexpr (LOOSE) {
+      // The group's waves do not meet between bands: a band's rows start
+      // staggered (each trails the row above by a little more than one
+      // macroblock) and end staggered the same way, so a barrier there held
+      // the leading waves idle for the trailing rows' lag twice a band
+      // (~14 macroblock times of four waves in 480).  Wave 0 dequeues band
+      // sequence q as soon as it finishes q - 1 (and every wave has finished
+      // q - 2, whose table slot it reuses); each wave picks it up when it is
+      // done with its own row of q - 1.  Every wait is still on a row
+      // dequeued earlier.
+      const int p = q & 1;
+      if (gw == 0) {
+        if (q >= 2) wait_lds(&s_done[p], WAVES * (q / 2));
+        int b = 0;
+        if (lane == 0) b = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        b = __shfl(b, 0, 64);
+        if (b < a.n_img * n_bands) {
+          const int bo = use_order ? __builtin_amdgcn_readfirstlane(a.border[b]) : b;
+          load_segments(a, bo % a.n_img, s_seg[p], lane);
+        }
+        if (lane == 0) {
+          s_band[p] = b;
+          __hip_atomic_store(&s_ready[p], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      wait_lds(&s_ready[p], q + 1);
+      const int band = __builtin_amdgcn_readfirstlane(s_band[p]);
+      if (band >= a.n_img * n_bands) break;
+      const int bo = use_order ? __builtin_amdgcn_readfirstlane(a.border[band]) : band;  // band y * n_img + image
+      img = bo % a.n_img;
+      mby = WAVES * (bo / a.n_img) + gw;
+      ro = mby * a.n_img + img;
+      row = WAVES * band + gw;
     } else {
       int& word = s_waves[WAVES * grp].word;
       if (gw == 0) {  // the group's leader dequeues and fetches the band's image's segments
@@ -1250,7 +1307,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       if (isA) wait_above(mbx + 1);
       ESTAMP(1);
       const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
-      const Segment& sg = s_seg[PAIR ? 0 : grp][segid];
+      const Segment& sg = s_seg[PAIR ? 0 : (LOOSE ? (q & 1) : grp)][segid];
       uint32_t top_nz = 0, top_modes = 0;
       int top_nz_dc = 0;
       if (isA) {
@@ -2192,10 +2249,13 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       }
     }
 #endif
-    // the band is done: the group dequeues the next one together
-    if constexpr (!PAIR) {
-      if constexpr (GROUPS == 1) __syncthreads();
-      else group_barrier(&s_gbar[grp], gen, lane);
+    // the band is done: LOOSE, count this wave out of it; else the group
+    // dequeues the next one together
+    if constexpr (LOOSE) {
+      if (lane == 0) __hip_atomic_fetch_add(&s_done[q & 1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      q++;
+    } else if constexpr (!PAIR) {
+      group_barrier(&s_gbar[grp], gen, lane);
     }
   }
   ESTAMP_FLUSH();
