@@ -1319,14 +1319,16 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * (2 * (size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(decode ctl)");
   // k_decode_split (two waves a row: reconstruction and loop filter apart)
-  // shortens a row's macroblock time, which is what bounds a batch whose rows
-  // all fit the chip at once (C3's one 4096^2 image: 3.8 ms against 5.1 ms
-  // with one wave a row).  A batch with more rows than that holds twice the
-  // wave slots per row for the same throughput, and beside the encoder (the
-  // bench's pipeline) those slots are the encoder's: k_decode_bands there
-  // (64 x 1080p: whole-path median 6,495 -> 7,065 MPix/s, decode side alone
-  // 77.4k -> 76.1k).
-  const bool use_split = cfg.force ? cfg.force == 1 : (int64_t)n_images * mbh <= (int64_t)cfg.split_per_cu * cfg.num_cus * SW;
+  // shortens a row's macroblock time, which is what bounds a batch of few
+  // long rows (C3's one 4096^2 image: 3.8 ms against 5.1 ms with one wave a
+  // row; 16 x 4096^2: 5.0 against 8.2 ms).  A batch with many more rows than
+  // the chip holds at once is bound by throughput instead, and there the
+  // split kernel's second wave per row only holds wave slots -- beside the
+  // encoder (the bench's pipeline), the encoder's: k_decode_bands (64 x
+  // 1080p: whole-path median 6,495 -> 7,065 MPix/s, decode side alone 77.4k
+  // -> 76.1k).  The switch is at twice the rows of the resident
+  // split workgroups (a heuristic between those two measured points).
+  const bool use_split = cfg.force ? cfg.force == 1 : (int64_t)n_images * mbh <= (int64_t)2 * cfg.split_per_cu * cfg.num_cus * SW;
   if (use_split) {
     const int bands = n_images * ((mbh + SW - 1) / SW);
     int grid = bands < cfg.split_per_cu * cfg.num_cus ? bands : cfg.split_per_cu * cfg.num_cus;
