@@ -6,7 +6,8 @@ frames, all inputs resident in HBM before timing starts:
                -> segment analysis (k_segments: assignSegments k-means,
                   setSegmentParams, setupSegment at the reference's q75 defaults)
                -> macroblock RD loop, Phase A of encodeFrameParallel (k_encode_rows)
-  decode side  reconstruct + loop filter (k_decode_split) of libwebp q75
+  decode side  reconstruct + loop filter (k_decode_bands at the bench batch;
+               wg_decode_kernel names the one launched) of libwebp q75
                bitstreams of the same three contents, parsed once on the host by
                wg_vp8_parse (tests/golden/q75_1080p.npz), -> fancy upsample to
                NRGBA (k_upsample)
@@ -63,7 +64,7 @@ BYTES_PER_PX = {
     "upsample": 1.5 + 4.0,            # YUV in, NRGBA out
 }
 KERNELS = {"import": "k_import", "analysis": "k_analysis", "segments": "k_segments", "encode": "k_encode_rows",
-           "decode": "k_decode_split", "upsample": "k_upsample"}
+           "decode": "k_decode_split", "upsample": "k_upsample"}  # decode: set from wg_decode_kernel at report time
 CONTENTS = ("grad", "noise", "blobs")
 BITSTREAMS = os.path.join(ROOT, "tests", "golden", "q75_1080p.npz")
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -627,6 +628,9 @@ def main():
         step_ms = elapsed / args.steps * 1e3
         dominant = max(iso, key=iso.get)
         px_rank_step = args.batch * W * H
+        from webp_amd import _lib
+        dk = _lib.lib.wg_decode_kernel(MBH, args.batch)  # the decode kernel this batch launches
+        KERNELS["decode"] = {1: "k_decode_split", 2: "k_decode_bands"}.get(dk, KERNELS["decode"])
         kernel = KERNELS[dominant]
         alg = BYTES_PER_PX[dominant] * px_rank_step
         achieved = alg / (iso[dominant] / 1e3) / 1e9

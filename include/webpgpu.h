@@ -221,6 +221,12 @@ typedef struct wg_mb_info {
 size_t wg_decode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images);
 int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int32_t filter_type, int32_t mbw, int32_t mbh,
                      int32_t n_images, uint8_t* y, uint8_t* u, uint8_t* v, void* work, void* stream);
+/* Which kernel wg_decode_frames launches for a batch of n_images frames of
+ * mbh macroblock rows on the current device: 1 = k_decode_split (two waves a
+ * row; few rows), 2 = k_decode_bands (one wave a row; batches past twice the
+ * resident split rows), or a negative error code.  No reference counterpart:
+ * a query for reports (bench.py labels its decode roofline with it). */
+int wg_decode_kernel(int32_t mbh, int32_t n_images);
 
 /* VP8 bitstream parse (HOST memory in and out; no device work): the CPU
  * half of the reference's decoder as a parse-all-rows-first pass that feeds

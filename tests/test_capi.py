@@ -45,6 +45,7 @@ def test_invalid_arguments_are_rejected_without_gpu():
     assert lib.wg_encode_row_order(None, 120, 68, 1, None, None) == -1
     assert lib.wg_encode_frames_devices(None, 1, None, 64, 64, 1, 0, None, None, None, None, None, None, None) == -1
     assert lib.wg_plane_ssim_devices(None, 1, None, 8, None, 8, 8, 8, None) == -1
+    assert lib.wg_decode_kernel(0, 1) == -1 and lib.wg_decode_kernel(68, 0) == -1
 
 
 def test_work_size_helpers():

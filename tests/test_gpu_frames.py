@@ -70,6 +70,20 @@ def test_decode_1080p_batch(cuda):
     run_decode(120, 68, 2, 2, seed=2024, levels=(20, 32))
 
 
+def test_decode_kernel_switch(cuda):
+    """wg_decode_frames launches k_decode_split for few rows and k_decode_bands
+    past twice the resident split rows (decode.hip use_split); both bit-exact.
+    Narrow frames keep the oracle quick at the batch that crosses over."""
+    from webp_amd import _lib
+    mbh = 68
+    assert _lib.lib.wg_decode_kernel(mbh, 1) == 1
+    n = 1
+    while _lib.lib.wg_decode_kernel(mbh, n) == 1:
+        n *= 2
+    assert _lib.lib.wg_decode_kernel(mbh, n) == 2 and n <= 1024
+    run_decode(3, mbh, n, 2, seed=n, levels=(20, 40))
+
+
 def test_decode_4096_square(cuda):
     """C3 frame shape: 4096x4096 -> 256x256 macroblocks."""
     run_decode(256, 256, 1, 2, seed=4096, levels=(20,))

@@ -69,6 +69,7 @@ SIGNATURES = {
     "wg_decode_frames": [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
     "wg_vp8_parse": [_vp, ctypes.c_size_t, _vp, _vp, _vp, _i64],
     "wg_decode_status": [_vp, _i32, _i32, _vp],
+    "wg_decode_kernel": [_i32, _i32],
     "wg_import_rgba": [_vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "wg_dither_amp": [ctypes.c_float, _i32],
     "wg_dither_plan_bytes": [_i32, _i32],

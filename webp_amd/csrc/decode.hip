@@ -1267,6 +1267,11 @@ int dec_config(DecConfig* out) {
   return WG_OK;
 }
 
+// the switch between the two kernels (see wg_decode_frames)
+bool use_split(const DecConfig& cfg, int32_t mbh, int32_t n_images) {
+  return cfg.force ? cfg.force == 1 : (int64_t)n_images * mbh <= (int64_t)2 * cfg.split_per_cu * cfg.num_cus * SW;
+}
+
 }  // namespace
 
 #ifdef WG_STAMPS
@@ -1328,8 +1333,7 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   // 1080p: whole-path median 6,495 -> 7,065 MPix/s, decode side alone 77.4k
   // -> 76.1k).  The switch is at twice the rows of the resident
   // split workgroups (a heuristic between those two measured points).
-  const bool use_split = cfg.force ? cfg.force == 1 : (int64_t)n_images * mbh <= (int64_t)2 * cfg.split_per_cu * cfg.num_cus * SW;
-  if (use_split) {
+  if (use_split(cfg, mbh, n_images)) {
     const int bands = n_images * ((mbh + SW - 1) / SW);
     int grid = bands < cfg.split_per_cu * cfg.num_cus ? bands : cfg.split_per_cu * cfg.num_cus;
     if (cfg.max_wg > 0 && grid > cfg.max_wg) grid = cfg.max_wg;
@@ -1340,6 +1344,13 @@ extern "C" int wg_decode_frames(const wg_mb_info* mb, const int16_t* coeffs, int
   const int grid = bands < cfg.rows_per_cu * cfg.num_cus ? bands : cfg.rows_per_cu * cfg.num_cus;
   hipLaunchKernelGGL(k_decode_bands, dim3((unsigned)grid), dim3(64 * DW), 0, s, a);
   return wg::check_launch("k_decode_bands");
+}
+
+extern "C" int wg_decode_kernel(int32_t mbh, int32_t n_images) {
+  WG_REQUIRE(mbh > 0 && n_images > 0);
+  DecConfig cfg;
+  if (const int e = dec_config(&cfg)) return e;
+  return use_split(cfg, mbh, n_images) ? 1 : 2;
 }
 
 extern "C" int wg_decode_status(const void* work, int32_t mbw, int32_t n_images, void* stream) {
