@@ -75,6 +75,8 @@ def test_decode_kernel_switch(cuda):
     past twice the resident split rows (decode.hip use_split); both bit-exact.
     Narrow frames keep the oracle quick at the batch that crosses over."""
     from webp_amd import _lib
+    if os.environ.get("WG_DECODE_KERNEL"):
+        pytest.skip("WG_DECODE_KERNEL forces one kernel")
     mbh = 68
     assert _lib.lib.wg_decode_kernel(mbh, 1) == 1
     n = 1

@@ -250,6 +250,33 @@ __device__ __forceinline__ int wait_progress(const int* p, int need, int* err_fl
   }
 }
 
+// The I4 blocks' steps inside one macroblock (decode_frame.go:148-170's raster
+// order, run as a wavefront).  Block (bx, by) reads the finished pixels of
+// its left and top neighbours (and, through them, the top-left one), and
+// the top-right neighbour's bottom row only in the modes that read T[4..7]:
+// VE4, LD4, VL4 (wg_dsp.h pred4_row; the right column's top-right comes
+// from the MB above-right instead, see top_right_step).  Each block runs at
+// the first step after its dependencies: bx + by steps when no mode reads
+// an in-MB top-right, up to the static bx + 2 by.  Returns the 16 steps as
+// 4-bit fields (block b at bits 4b..4b+3); modes are uniform, so this is
+// scalar work.
+__device__ __forceinline__ uint64_t i4_schedule(uint32_t im0, uint32_t im1, uint32_t im2, uint32_t im3) {
+  const uint32_t im[4] = {im0, im1, im2, im3};
+  int st[16];
+  uint64_t packed = 0;
+#pragma unroll
+  for (int b = 0; b < 16; b++) {
+    const int bx = b & 3, by = b >> 2;
+    const uint32_t m = (im[by] >> (8 * bx)) & 0xff;
+    int v = bx > 0 ? st[b - 1] + 1 : 0;
+    if (by > 0) v = max(v, st[b - 4] + 1);
+    if (by > 0 && bx < 3 && (m == 2 || m == 6 || m == 7)) v = max(v, st[b - 3] + 1);
+    st[b] = v;
+    packed |= (uint64_t)v << (4 * b);
+  }
+  return packed;
+}
+
 // Band schedule: a workgroup of DW waves dequeues a band of DW consecutive
 // macroblock rows of one image (ordered counter over (band, image)); wave r
 // walks row DW*band + r.  Wave 0 depends on the previous band's last row
@@ -258,12 +285,12 @@ __device__ __forceinline__ int wait_progress(const int* p, int need, int* err_fl
 // wave of the unfiltered top context (32 B) and the final bottom rows 12..15
 // (128 B) of each finished MB, and an LDS progress word.  The bottom rows of
 // an MB are final once the MB to its right has run its left-edge filter, so,
-// as across bands, the consumer waits for MB x+1 of the row above.  Writes
-// to the frame never overlap between the waves of a band: a producer whose
-// consumer is in the band leaves its rows 13..15 (Y) / 5..7 (U, V) to the
-// consumer, which stores them after its top-edge filter (changed or not).
-// Across bands the original protocol stands (the producer stores everything
-// and drains before publishing; the consumer stores what it modified).
+// as across bands, the consumer waits for MB x+1 of the row above.  Across
+// bands the same rows travel as one 128-B write-through record per MB column
+// (a.bot, as in k_decode_split), drained before the progress flag.  Writes
+// to the frame never overlap: a producer leaves its rows 13..15 (Y) / 5..7
+// (U, V) to the row below, which stores them after its top-edge filter
+// (changed or not), so every frame byte is written once.
 __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t wb_all[DW][WB_SIZE];
   // prefetch landing zone: coefficients (48 x 16 B) then the wg_mb_info (2 x 16 B)
@@ -311,6 +338,10 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
       uint8_t* Yp = a.Y + (int64_t)img * ys * 16 * mbh;
       uint8_t* Up = a.U + (int64_t)img * uvs * 8 * mbh;
       uint8_t* Vp = a.V + (int64_t)img * uvs * 8 * mbh;
+      // a band's last row hands the next band each MB's final rows 12..15 as
+      // one 128-B record (Y 4 x 16 B, U 4 x 8, V 4 x 8; bot_ring's layout)
+      uint8_t* const bot_img = a.bot + (int64_t)img * mbw * BOT_BYTES;
+      const bool hand = !to_lds && mby < mbh - 1;
 
       // row start: left border 129, top-left 129 (127 on the first row) -- decode_frame.go:93-110
       if (lane < 16) wb[LY - 1 + lane * WG_BPS] = 129;
@@ -405,18 +436,16 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
             const int k = lane - 48;
             uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
             *reinterpret_cast<uint64_t*>(dst) = w;
-          } else if (lane >= 52 && lane < 60) {  // filtered frame rows 16y-4..16y-1 (Y)
+          } else if (lane >= 52 && lane < 60) {  // the previous band's record: Y rows 16y-4..16y-1
             const int k = lane - 52, rr = k >> 1, half = k & 1;
-            const uint64_t w = ld_sc1_64(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * mbx + 8 * half);
+            const uint64_t w = ld_sc1_64(bot_img + mbx * BOT_BYTES + 16 * rr + 8 * half);
             *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = w;
           } else if (lane >= 60) {  // U rows 8y-4..8y-1
             const int rr = lane - 60;
-            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) =
-                ld_sc1_64(Up + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
+            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) = ld_sc1_64(bot_img + mbx * BOT_BYTES + 64 + 8 * rr);
           } else if (lane >= 44) {  // V rows (lanes 44..47)
             const int rr = lane - 44;
-            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) =
-                ld_sc1_64(Vp + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * mbx);
+            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = ld_sc1_64(bot_img + mbx * BOT_BYTES + 96 + 8 * rr);
           }
           if (lane == 0) {  // top-right: next MB's top context, or replicate top[15] at the right edge
             uint32_t tr;
@@ -464,9 +493,13 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
                 pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
                       clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
           } else {
-            const int my_step = bx + 2 * by;  // in-MB dependency wavefront
+            const uint64_t sched = i4_schedule(im0, __builtin_amdgcn_readfirstlane(iw[3]),
+                                               __builtin_amdgcn_readfirstlane(iw[4]),
+                                               __builtin_amdgcn_readfirstlane(iw[5]));
+            const int my_step = (int)(sched >> (4 * blk)) & 15;  // in-MB dependency wavefront
+            const int n_steps = (int)(sched >> 60) + 1;           // block 15 is last
             const int mode = imodes[blk];
-            for (int s = 0; s < 10; s++) {
+            for (int s = 0; s < n_steps; s++) {
               if (s == my_step) {
                 int X, T[8], L[4];
                 pred4_ctx(wb, LY + 4 * by * WG_BPS + 4 * bx, X, T, L);
@@ -540,13 +573,25 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
         // row below finishes with its top-edge filter.  Rows leave in 32-B
         // pieces (two Y MBs, four U / V MBs) once every MB of the piece is
         // final, and the rest at the row's end: every frame byte is written
-        // once (but rows 13..15 / 5..7 of a band's last row, see below), and
-        // as whole 32-B sectors.  Only what another workgroup reads while
-        // this launch runs is written through (sc1), per MB: rows 12..15 /
-        // 4..7 of a band's last row, which the next band's first row loads as
-        // its filter context (and rewrites after its top-edge filter).  Rows
-        // 13..15 / 5..7 are left to the row below when it is in this band,
-        // which stores them in 32-B pieces too.
+        // once, by the wave that finalises it, as whole 32-B sectors; rows
+        // 13..15 / 5..7 are the row below's to store, in this band or the
+        // next.  Only the next band's filter context is written through
+        // (sc1): a band's last row hands it MB x - 1's final rows 12..15 (at
+        // the row's end this MB's too) as one 128-B record per MB.
+        if (hand) {
+          const int which = lane >> 3, k = lane & 7, x = mbx - 1 + which;
+          if (lane < 16 && (which == 0 ? mbx > 0 : mbx == mbw - 1)) {
+            uint4 w;
+            if (k < 4) {
+              w = *reinterpret_cast<const uint4*>(fy + (16 + k) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
+            } else {  // U rows 4,5 | 6,7, V rows 4,5 | 6,7
+              const uint8_t* src = ((k >= 6) ? fv : fu) + (8 + 2 * (k & 1)) * FC_STRIDE + FC_X0 + 8 * (x - mbx);
+              const uint64_t a0 = lds64(src), a1 = lds64(src + FC_STRIDE);
+              w = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
+            }
+            st_sc1_128(bot_img + x * BOT_BYTES + 16 * k, w);
+          }
+        }
         {
           const bool last = mbx == mbw - 1;
           // Y: MBs [y0, y1] leave now (tile column of MB m: 16 (m - mbx)).
@@ -568,7 +613,10 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
             c0 = mbx - 4;
             c1 = mbx - 1;
           }
-          const int ylim = to_lds ? 13 : 12, clim = to_lds ? 5 : 4;  // rows below these: batched
+          // rows below ylim / clim are this wave's; the rest the row below
+          // stores (the image's last row stores all; with the simple filter
+          // chroma is never filtered, so its rows are all this wave's)
+          const int ylim = to_lds || hand ? 13 : 16, clim = to_lds || (hand && !luma_only) ? 5 : 8;
           if (lane < 48) {  // Y: row lane & 15, MB y0 + (lane >> 4)
             const int j = lane & 15, x = y0 + (lane >> 4);
             if (y0 >= 0 && j < ylim && x <= y1) {
@@ -582,22 +630,6 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
             if (c0 >= 0 && i < 80 && j < clim && x <= c1)
               *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x) =
                   lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx));
-          }
-          if (!to_lds) {  // a band's last row: rows 12..15 / 4..7 of the left MB (and of this one at the row's end)
-            const int which = lane >> 5, k = lane & 31, x = mbx - 1 + which;
-            if (which == 0 ? mbx > 0 : last) {
-              if (k < 4) {
-                const int j = 12 + k;
-                const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
-                uint8_t* dst = Yp + (int64_t)(16 * mby + j) * ys + 16 * x;
-                st_sc1_64(dst, (uint64_t)w.y << 32 | w.x);
-                st_sc1_64(dst + 8, (uint64_t)w.w << 32 | w.z);
-              } else if (k < 12) {
-                const int pl = k >= 8, j = 4 + (k & 3);
-                st_sc1_64((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x,
-                          lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
-              }
-            }
           }
           if (mby > 0) {
             // rows 13..15 / 5..7 of the MBs above, final after our top-edge
@@ -714,17 +746,16 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
 constexpr int SW = WG_DEC_SW;          // rows per band (one R and one F wave each)
 constexpr int RING_M = WG_DEC_RING_M;  // R -> F ring depth (R's work buffers of unfiltered MBs)
 
-// The first I4 wavefront step (block b at step bx + 2 by) that reads the MB
-// above-right, or 99: blocks 3, 7, 11, 15 (steps 3, 5, 7, 9) read it in
-// VE4 / LD4 / VL4 (wg_dsp.h pred4_row).
-__device__ __forceinline__ int top_right_step(uint32_t is_i4, uint32_t right_modes) {
+// The first I4 wavefront step (i4_schedule) that reads the MB above-right,
+// or 99: blocks 3, 7, 11, 15 read it in VE4 / LD4 / VL4 (wg_dsp.h pred4_row).
+__device__ __forceinline__ int top_right_step(uint32_t is_i4, uint32_t right_modes, uint64_t sched) {
   // right_modes: the modes of blocks 3, 7, 11, 15, one byte each
   if (!is_i4) return 99;
   int st = 99;
 #pragma unroll
   for (int k = 3; k >= 0; k--) {
     const uint32_t m = (right_modes >> (8 * k)) & 0xff;
-    if (m == 2 || m == 6 || m == 7) st = 3 + 2 * k;
+    if (m == 2 || m == 6 || m == 7) st = (int)(sched >> (4 * (3 + 4 * k))) & 15;
   }
   return st;
 }
@@ -743,7 +774,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
   __shared__ int prog_r[SW], prog_f[SW], cons_f[SW], bot_f[SW];
   // tprog: 4 x (MBs done) + (blocks of the current MB done) of the luma
   // bottom row in top_ring: block 12 + k's last row (px 4k..4k+3 of row 15)
-  // is final at I4 step 6 + k.  R(y+1) waits on it for its top-right (block
+  // is final at block 12 + k's I4 step (i4_schedule).  R(y+1) waits on it for its top-right (block
   // 12 of MB x + 1 above) instead of on the whole MB.  (Waiting block by
   // block for the top row as well measured slower: C3 4.19 -> 4.34 ms.)
   __shared__ int tprog[SW];
@@ -810,21 +841,43 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         const uint32_t im3 = (uint32_t)__builtin_amdgcn_readlane(pf.y, 49);
         const uint32_t w6 = (uint32_t)__builtin_amdgcn_readlane(pf.z, 49);
         lds_sync();
+        // the residuals need this MB's coefficients only: made here, before
+        // the waits for the row above, off the wavefront's chain
+        int lres[4], cres[4] = {0, 0, 0, 0};
+        {
+          const int blk = lane >> 2, rr = lane & 3;
+          dec_residual_row(cof + blk * 16, (nz_y >> (30 - 2 * blk)) & 3, rr, lres);
+          if (lane < 32) {
+            const int pl = lane >> 4, cblk = (lane >> 2) & 3;
+            const uint32_t bits = nz_uv >> (8 * pl);
+            const int16_t* bco = cof + (16 + 4 * pl + cblk) * 16;
+            if (bits & 0xff) {
+              if (bits & 0xaa) dec_residual_row(bco, 3, rr, cres);
+              else if (bco[0] != 0) dec_residual_row(bco, 1, rr, cres);
+            }
+          }
+        }
         const uint8_t* imodes = reinterpret_cast<const uint8_t*>(stage + 48) + 8;
         // the step before which R waits for MB x + 1 above (its bottom row is
         // the top-right context); 99: never
+        const uint64_t sched = i4_schedule(im0, im1, im2, im3);
         const int tr_step =
             mby > 0 && mbx + 1 < mbw
-                ? top_right_step(w6 & 0xff, (im0 >> 24) | (im1 >> 24) << 8 | (im2 >> 24) << 16 | (im3 >> 24) << 24)
+                ? top_right_step(w6 & 0xff, (im0 >> 24) | (im1 >> 24) << 8 | (im2 >> 24) << 16 | (im3 >> 24) << 24,
+                                 sched)
                 : 99;
         // ---- dependency on the row above; ring space below (top ring) and in F's ring ----
-        if (mby > 0) {
+        // In the band the luma waits only for the luma of MB x above (its
+        // bottom row, tprog), the chroma for the rest of it (prog_r, before
+        // the chroma phase); across bands for the whole MB (its top record).
+        if (from_lds) {
+          if (lane == 0 && seen_t < 4 * mbx + 4)
+            seen_t = wait_progress<false>(&tprog[r - 1], 4 * mbx + 4, &a.ctl[1], 4 * mbw + 8, a.diag);
+        } else if (mby > 0) {
           const int need = mbx + 1;
           if (seen < need) {
             int v = 0;
-            if (lane == 0)
-              v = from_lds ? wait_progress<false>(&prog_r[r - 1], need, &a.ctl[1], mbw, a.diag)
-                           : wait_progress<true>(prog_above, need, &a.ctl[1], mbw, a.diag);
+            if (lane == 0) v = wait_progress<true>(prog_above, need, &a.ctl[1], mbw, a.diag);
             seen = __shfl(v, 0, 64);
           }
         }
@@ -836,7 +889,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         uint8_t* const wb = wb_all[r][mslot];
         // (left context and, in the band, top context and F's info record:
         // every read first, then the writes -- one LDS round trip)
-        const bool l_lane = lane < 35, t_lane = from_lds && lane >= 48 && lane < 52;
+        const bool l_lane = lane < 35, t_lane = from_lds && lane >= 48 && lane < 50;  // (U, V: before the chroma)
         // left: lanes 0-15 / 16-23 / 24-31 the Y / U / V column, 32-34 the
         // top-left corners, one byte a lane with select-computed addresses
         const int l_pl = lane < 16 ? 0 : (lane < 24 ? 1 : (lane < 32 ? 2 : lane - 32));
@@ -899,9 +952,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         {
           const int blk = lane >> 2, rr = lane & 3, bx = blk & 3, by = blk >> 2;
           const int off = LY + (4 * by + rr) * WG_BPS + 4 * bx;
-          const int code = (nz_y >> (30 - 2 * blk)) & 3;
-          int res[4];
-          dec_residual_row(cof + blk * 16, code, rr, res);
+          const int* const res = lres;
           // the last rows of blocks 12..15 (row 15) are the next row's top
           // context: in the band each goes to R(y+1) as soon as it is made
           const bool top_lane = to_lds && by == 3 && rr == 3;
@@ -921,9 +972,10 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
               if (bx == 3) __hip_atomic_store(&tprog[r], 4 * mbx + 4, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
           } else {
-            const int my_step = bx + 2 * by;
+            const int my_step = (int)(sched >> (4 * blk)) & 15;
+            const int n_steps = (int)(sched >> 60) + 1;  // block 15 is last
             const int mode = imodes[blk];
-            for (int st = 0; st < 10; st++) {
+            for (int st = 0; st < n_steps; st++) {
               if (st == tr_step) {
                 // the first block that reads the top-right: only now wait for
                 // MB x + 1 above (in the band: its block 12 only), then its
@@ -935,7 +987,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                     const int need = 4 * (mbx + 1) + 1;
                     if (seen_t < need) seen_t = wait_progress<false>(&tprog[r - 1], need, &a.ctl[1], 4 * mbw + 8, a.diag);
                     tr = lds32(top_ring[r - 1][(mbx + 1) & (RING - 1)]);
-                    v = seen;
+                    v = seen;  // (unused in the band)
                   } else {
                     v = seen < mbx + 2 ? wait_progress<true>(prog_above, mbx + 2, &a.ctl[1], mbw, a.diag) : seen;
                     tr = (uint32_t)ld_sc1_64(top + (mbx + 1) * TOP_BYTES);
@@ -953,7 +1005,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                 const uint32_t row = pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
                                            clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
                 *reinterpret_cast<uint32_t*>(wb + off) = row;
-                if (top_lane) {  // (blocks 12..15 run at steps 6..9, one a step)
+                if (top_lane) {  // (blocks 12..15 run in order, one a step or more apart)
                   *reinterpret_cast<uint32_t*>(top_ring[r][slot] + 4 * bx) = row;
                   asm volatile("" ::: "memory");
                   __hip_atomic_store(&tprog[r], 4 * mbx + bx + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -966,6 +1018,13 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         STAMP(3);
         lane = opaque_lane() & 63;
         // ---- chroma prediction + residual (doUVTransform :47-68) ----
+        if (from_lds) {  // the chroma top context: once MB x above is whole
+          if (lane == 0 && seen < mbx + 1) seen = wait_progress<false>(&prog_r[r - 1], mbx + 1, &a.ctl[1], mbw, a.diag);
+          if (lane == 50 || lane == 51)
+            *reinterpret_cast<uint64_t*>(lane == 50 ? wb + LU - WG_BPS : wb + LV - WG_BPS) =
+                lds64(top_ring[r - 1][slot] + 8 * (lane - 48));
+          lds_sync();
+        }
         if (lane < 32) {
           const int pl = lane >> 4, cblk = (lane >> 2) & 3, rr = lane & 3;
           const int cbx = cblk & 1, cby = cblk >> 1;
@@ -973,13 +1032,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           const int mode = check_mode(mbx, mby, uv_mode);
           const int dc = predsq_dc(mode, wb + base, 8);
           const uint32_t pred = predsq_row4(mode, wb + base, 4 * cbx, 4 * cby + rr, dc);
-          const uint32_t bits = nz_uv >> (8 * pl);
-          const int16_t* bco = cof + (16 + 4 * pl + cblk) * 16;
-          int res[4] = {0, 0, 0, 0};
-          if (bits & 0xff) {
-            if (bits & 0xaa) dec_residual_row(bco, 3, rr, res);
-            else if (bco[0] != 0) dec_residual_row(bco, 1, rr, res);
-          }
+          const int* const res = cres;
           const uint32_t crow = pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
                                       clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
           *reinterpret_cast<uint32_t*>(wb + base + (4 * cby + rr) * WG_BPS + 4 * cbx) = crow;
