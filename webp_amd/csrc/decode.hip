@@ -870,14 +870,13 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         // In the band the luma waits only for the luma of MB x above (its
         // bottom row, tprog), the chroma for the rest of it (prog_r, before
         // the chroma phase); across bands for the whole MB (its top record).
-        if (from_lds) {
-          if (lane == 0 && seen_t < 4 * mbx + 4)
-            seen_t = wait_progress<false>(&tprog[r - 1], 4 * mbx + 4, &a.ctl[1], 4 * mbw + 8, a.diag);
-        } else if (mby > 0) {
+        if (mby > 0) {
           const int need = mbx + 1;
           if (seen < need) {
             int v = 0;
-            if (lane == 0) v = wait_progress<true>(prog_above, need, &a.ctl[1], mbw, a.diag);
+            if (lane == 0)
+              v = from_lds ? wait_progress<false>(&prog_r[r - 1], need, &a.ctl[1], mbw, a.diag)
+                           : wait_progress<true>(prog_above, need, &a.ctl[1], mbw, a.diag);
             seen = __shfl(v, 0, 64);
           }
         }
@@ -889,7 +888,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         uint8_t* const wb = wb_all[r][mslot];
         // (left context and, in the band, top context and F's info record:
         // every read first, then the writes -- one LDS round trip)
-        const bool l_lane = lane < 35, t_lane = from_lds && lane >= 48 && lane < 50;  // (U, V: before the chroma)
+        const bool l_lane = lane < 35, t_lane = from_lds && lane >= 48 && lane < 52;  // (U, V: before the chroma)
         // left: lanes 0-15 / 16-23 / 24-31 the Y / U / V column, 32-34 the
         // top-left corners, one byte a lane with select-computed addresses
         const int l_pl = lane < 16 ? 0 : (lane < 24 ? 1 : (lane < 32 ? 2 : lane - 32));
@@ -1018,13 +1017,6 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         STAMP(3);
         lane = opaque_lane() & 63;
         // ---- chroma prediction + residual (doUVTransform :47-68) ----
-        if (from_lds) {  // the chroma top context: once MB x above is whole
-          if (lane == 0 && seen < mbx + 1) seen = wait_progress<false>(&prog_r[r - 1], mbx + 1, &a.ctl[1], mbw, a.diag);
-          if (lane == 50 || lane == 51)
-            *reinterpret_cast<uint64_t*>(lane == 50 ? wb + LU - WG_BPS : wb + LV - WG_BPS) =
-                lds64(top_ring[r - 1][slot] + 8 * (lane - 48));
-          lds_sync();
-        }
         if (lane < 32) {
           const int pl = lane >> 4, cblk = (lane >> 2) & 3, rr = lane & 3;
           const int cbx = cblk & 1, cby = cblk >> 1;
