@@ -542,8 +542,18 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
           const int k = lane - 32;
           const uint8_t* src =
               k < 2 ? wb + LY + 15 * WG_BPS + 8 * k : (k == 2 ? wb + LU + 7 * WG_BPS : wb + LV + 7 * WG_BPS);
-          if (to_lds) *reinterpret_cast<uint64_t*>(top_ring[wave][slot] + 8 * k) = lds64(src);
-          else st_sc1_64(top + mbx * TOP_BYTES + 8 * k, lds64(src));
+          if (to_lds) {
+            *reinterpret_cast<uint64_t*>(top_ring[wave][slot] + 8 * k) = lds64(src);
+          } else if (k < 2) {  // the record as two 16-B write-through stores (Y | U V): one 32-B write
+            uint4 w;
+            if (k == 0) {
+              w = *reinterpret_cast<const uint4*>(wb + LY + 15 * WG_BPS);
+            } else {
+              const uint64_t u = lds64(wb + LU + 7 * WG_BPS), v = lds64(wb + LV + 7 * WG_BPS);
+              w = make_uint4((uint32_t)u, (uint32_t)(u >> 32), (uint32_t)v, (uint32_t)(v >> 32));
+            }
+            st_sc1_128(top + mbx * TOP_BYTES + 16 * k, w);
+          }
         }
         if (lane < 16) {
           *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) =
@@ -1040,8 +1050,18 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           const int k = lane - 32;
           const uint8_t* src =
               k < 2 ? wb + LY + 15 * WG_BPS + 8 * k : (k == 2 ? wb + LU + 7 * WG_BPS : wb + LV + 7 * WG_BPS);
-          if (to_lds) *reinterpret_cast<uint64_t*>(top_ring[r][slot] + 8 * k) = lds64(src);
-          else st_sc1_64(top + mbx * TOP_BYTES + 8 * k, lds64(src));
+          if (to_lds) {
+            *reinterpret_cast<uint64_t*>(top_ring[r][slot] + 8 * k) = lds64(src);
+          } else if (k < 2) {  // the record as two 16-B write-through stores (Y | U V): one 32-B write
+            uint4 w;
+            if (k == 0) {
+              w = *reinterpret_cast<const uint4*>(wb + LY + 15 * WG_BPS);
+            } else {
+              const uint64_t u = lds64(wb + LU + 7 * WG_BPS), v = lds64(wb + LV + 7 * WG_BPS);
+              w = make_uint4((uint32_t)u, (uint32_t)(u >> 32), (uint32_t)v, (uint32_t)(v >> 32));
+            }
+            st_sc1_128(top + mbx * TOP_BYTES + 16 * k, w);
+          }
         }
         lds_sync();
         STAMP(5);

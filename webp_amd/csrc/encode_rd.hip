@@ -1908,6 +1908,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         trellis_r0<0>(t, lane, lam16, s.r0);  // (read after the first round's lds_sync)
         int16_t* res_q = reinterpret_cast<int16_t*>(s.yout2);  // [16 tasks][16] levels (yout2 is free for I16 MBs)
         int* res_nz = reinterpret_cast<int*>(s.yout2 + 512);   // [16]
+        uint32_t nzbits = 0;  // the resolved blocks' nz flags (bit = block), a scalar across the rounds
         for (int r = 0; r < 3; r++) {
           Shared& s = launder(s_waves[wave]);
           Tables& t = launder(t_lds);
@@ -1929,6 +1930,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
           // quad q runs task q: walk the round's blocks to find its (block, context)
+          int tnz = 0;  // this quad's task: nz of its levels
           {
             const int q = lane >> 2;
             int acc = 0, tj = -1, tctx = 0;
@@ -1948,6 +1950,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
                 int nzv = 0;
                 trellis_dp4<1, 0>(t, s.trec[tj], s.r0, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
                 if ((lane & 3) == 0) res_nz[q] = nzv;
+                tnz = nzv;
               } else if ((lane & 3) == 0) {
 #pragma unroll
                 for (int i = 0; i < 16; i++) res_q[q * 16 + i] = 0;
@@ -1955,27 +1958,31 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               }
             }
           }
+          // bit 4 q: task q's levels are nonzero (a ballot, not an LDS round trip)
+          const uint64_t tmask = __ballot((lane & 3) == 0 && tnz > 0);
           lds_sync();
-          // the reference's raster order: each block's actual context picks its task
-          if (lane == 0) {
+          // the reference's raster order: each block's actual context picks its
+          // task -- on scalars (the task of the round's block j in bits 4j..4j+3)
+          uint32_t tasks = 0;
+          {
             int acc = 0;
             for (int j = 0; j < m; j++) {
               const int qb = first + j, qbx = qb & 3, qby = qb >> 2;
               const int nfix = (qbx == 0) + (qby == 0);
               const int fixed = (qbx == 0 ? (int)((left_nz >> qby) & 1) : 0) + (qby == 0 ? (int)((top_nz >> qbx) & 1) : 0);
-              const int l = qbx > 0 ? (s.nzy[qb - 1] > 0) : (int)((left_nz >> qby) & 1);
-              const int tp = qby > 0 ? (s.nzy[qb - 4] > 0) : (int)((top_nz >> qbx) & 1);
+              const int l = qbx > 0 ? (int)((nzbits >> (qb - 1)) & 1) : (int)((left_nz >> qby) & 1);
+              const int tp = qby > 0 ? (int)((nzbits >> (qb - 4)) & 1) : (int)((top_nz >> qbx) & 1);
               const int task = acc + min(l + tp, 2) - fixed;
-              s.nzy[qb] = (uint8_t)res_nz[task];
-              s.modes4[qb] = (uint8_t)task;  // scratch: the task each block takes (modes4 is I4-only)
+              nzbits |= (uint32_t)((tmask >> (4 * task)) & 1) << qb;
+              tasks |= (uint32_t)task << (4 * j);
               acc += 3 - nfix;
             }
           }
-          lds_sync();
-          if (lane < 8 * m) {  // copy the chosen levels, two per lane
-            const int j = lane >> 3, qb = first + j, task = s.modes4[qb];
+          if (lane < 8 * m) {  // copy the chosen levels, two per lane, and the block's nz
+            const int j = lane >> 3, qb = first + j, task = (int)(tasks >> (4 * j)) & 15;
             reinterpret_cast<uint32_t*>(s.coeffs + qb * 16)[lane & 7] =
                 reinterpret_cast<const uint32_t*>(res_q + task * 16)[lane & 7];
+            if ((lane & 7) == 0) s.nzy[qb] = (uint8_t)res_nz[task];
           }
           lds_sync();
         }
