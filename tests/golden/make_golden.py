@@ -67,6 +67,7 @@ def main():
     make_sharpyuv_fixtures(img)
     make_reference_testdata()
     make_c3_bitstream()
+    make_encode_compare_fixtures()
     print("wrote", os.path.join(HERE, "libwebp_fixtures.npz"), sum(v.nbytes for v in out.values()), "bytes raw")
 
 
@@ -196,5 +197,30 @@ def make_reference_testdata():
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
+def make_encode_compare_fixtures():
+    """TestEncodeCompare's C side (internal/lossy/encode_compare_test.go:86-117):
+    `cwebp -q Q -segments 1 -m 4` of colorPatternImage at 64x64 / 256x256 /
+    768x576, decoded with `dwebp -yuv`.  Here: libwebp 1.6.0 WebPEncode with
+    WebPConfigInit(Q) + segments 1 + method 4 (cwebp's other defaults are the
+    config's), WebPDecodeYUV of the result.  Keys cwebp_<w>x<h>_q<Q>_{y,u,v}
+    (decoded planes, h x w and h/2 x w/2) and _webp (the bitstream)."""
+    import encode_quality as EQ
+    out = {}
+    for w, h in EQ.COLOR_SIZES:
+        rgba = EQ.color_pattern(w, h)
+        for q in (75, 50):
+            data = L.encode_lossy_cfg(rgba, float(q), segments=1, method=4)
+            Y, U, V = L.decode_yuv(data)
+            key = "cwebp_%dx%d_q%d" % (w, h, q)
+            out[key + "_webp"] = np.frombuffer(data, np.uint8).copy()
+            out[key + "_y"], out[key + "_u"], out[key + "_v"] = Y, U[:h // 2, :w // 2], V[:h // 2, :w // 2]
+    path = os.path.join(HERE, "cwebp_compare.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["encode_compare"]:
+        make_encode_compare_fixtures()
+    else:
+        main()
