@@ -55,6 +55,9 @@ extern "C" {
 #define WG_VOFF (WG_UOFF + 16)
 
 const char* wg_last_error(void);
+/* ABI version of this header; WG_ABI_VERSION when the library matches it.
+ * 2: wg_alpha_unfilter_work_bytes(width, height, n) (was (height, n)). */
+#define WG_ABI_VERSION 2
 int wg_version(void);
 /* Checks that the current device is gfx950 and the kernels are loadable. */
 int wg_device_check(void);

@@ -16,6 +16,15 @@
  *       wg_decode_status); writes ITransform's ref / coefficients / output and
  *       the decoded Y, U, V planes to out.bin for the test to check against
  *       the oracle.
+ *   capi_consumer encode <frame.bin> <out.bin>   (built with -DWG_WITH_HIP)
+ *       INTEGRATION.md's encodeFramePhaseAHIP over the whole device encode
+ *       path, as encode_hip.go calls it for one frame: wg_encoder_config ->
+ *       wg_import_rgba -> wg_analysis_alphas -> wg_segment_analysis ->
+ *       wg_encode_row_order -> wg_encode_mbs -> wg_encode_status.  frame.bin:
+ *       int32 w, h, quality, method, then w*h*4 RGBA bytes, then the 1056
+ *       token probabilities (enc.proba.Bands).  out.bin: the wg_mb_enc
+ *       records, the reconstruction (Y, U, V), the segment ids and the
+ *       wg_frame_segs record, for the test to compare with the oracle.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -68,7 +77,7 @@ static int parse(const uint8_t* data, size_t n, int32_t dims[5], wg_mb_info** mb
 }
 
 static int run_cpu(const uint8_t* data, size_t n) {
-  CHECK(wg_version() == 1);
+  CHECK(wg_version() == WG_ABI_VERSION);
   /* invalid arguments are rejected before any device work */
   CHECK(wg_decode_frames(NULL, NULL, 2, 1, 1, 1, NULL, NULL, NULL, NULL, NULL) == WG_EINVAL);
   CHECK(strstr(wg_last_error(), "invalid argument") != NULL);
@@ -159,11 +168,85 @@ static int run_gpu(const uint8_t* data, size_t n, const char* out_path) {
   fclose(out);
   return fails;
 }
+
+static int run_encode(const uint8_t* in, size_t n, const char* out_path) {
+  CHECK(wg_device_check() == WG_OK);
+  if (fails || n < 16) return fails + 1;
+  int32_t hdr[4];
+  memcpy(hdr, in, sizeof(hdr));
+  const int32_t w = hdr[0], h = hdr[1], quality = hdr[2], method = hdr[3];
+  const size_t rgba_bytes = (size_t)w * h * 4;
+  if (n != 16 + rgba_bytes + 1056) return fails + 1;
+  const uint8_t* rgba = in + 16;
+  const uint8_t* proba = in + 16 + rgba_bytes;
+  const int32_t mbw = (w + 15) / 16, mbh = (h + 15) / 16, nmb = mbw * mbh;
+  const size_t ysz = (size_t)256 * nmb, uvsz = (size_t)64 * nmb;
+  /* EncodeConfig: DefaultConfig(quality) with the method asked for (encode.go:66-86) */
+  wg_enc_config cfg;
+  CHECK(wg_encoder_config(quality, method, 50, 60, 0, 1, 4, 0, &cfg) == WG_OK);
+  void *d_rgba = NULL, *d_y = NULL, *d_u = NULL, *d_v = NULL, *d_alpha = NULL, *d_uvsum = NULL, *d_ids = NULL,
+       *d_segs = NULL, *d_info = NULL, *d_proba = NULL, *d_out = NULL, *d_work = NULL;
+  const size_t work = wg_encode_work_bytes(mbw, mbh, 1);
+  CHECK(hipMalloc(&d_rgba, rgba_bytes) == hipSuccess && hipMalloc(&d_y, ysz) == hipSuccess &&
+        hipMalloc(&d_u, uvsz) == hipSuccess && hipMalloc(&d_v, uvsz) == hipSuccess &&
+        hipMalloc(&d_alpha, 4 * (size_t)nmb) == hipSuccess && hipMalloc(&d_uvsum, 4) == hipSuccess &&
+        hipMalloc(&d_ids, (size_t)nmb) == hipSuccess && hipMalloc(&d_segs, 4 * sizeof(wg_segment)) == hipSuccess &&
+        hipMalloc(&d_info, sizeof(wg_frame_segs)) == hipSuccess && hipMalloc(&d_proba, 1056) == hipSuccess &&
+        hipMalloc(&d_out, sizeof(wg_mb_enc) * (size_t)nmb) == hipSuccess && hipMalloc(&d_work, work) == hipSuccess);
+  if (fails) return fails;
+  CHECK(hipMemcpy(d_rgba, rgba, rgba_bytes, hipMemcpyHostToDevice) == hipSuccess);
+  CHECK(hipMemcpy(d_proba, proba, 1056, hipMemcpyHostToDevice) == hipSuccess);
+  /* importImage (encode.go:671-943), no alpha */
+  int rc = wg_import_rgba((const uint8_t*)d_rgba, w, h, 4 * w, (int64_t)rgba_bytes, 0, (uint8_t*)d_y,
+                          (uint8_t*)d_u, (uint8_t*)d_v, (int64_t)ysz, (int64_t)uvsz, 1, NULL);
+  CHECK(rc == WG_OK);
+  /* computeAlphas -> analysis() -> setSegmentParams / setupSegment, on the device */
+  if (rc == WG_OK)
+    rc = wg_analysis_alphas((const uint8_t*)d_y, (const uint8_t*)d_u, (const uint8_t*)d_v, w, h, (int64_t)ysz,
+                            (int64_t)uvsz, 1, (int32_t*)d_alpha, NULL, NULL, (int32_t*)d_uvsum, NULL);
+  CHECK(rc == WG_OK);
+  if (rc == WG_OK)
+    rc = wg_segment_analysis(&cfg, (const int32_t*)d_alpha, (const int32_t*)d_uvsum, mbw, mbh, 1, (uint8_t*)d_ids,
+                             d_segs, 4 * sizeof(wg_segment), (wg_frame_segs*)d_info, NULL);
+  CHECK(rc == WG_OK);
+  if (rc == WG_OK) rc = wg_encode_row_order((const int32_t*)d_alpha, mbw, mbh, 1, d_work, NULL);
+  CHECK(rc == WG_OK);
+  /* encodeFrameParallel Phase A; the reconstruction goes to separate planes */
+  void *d_ry = NULL, *d_ru = NULL, *d_rv = NULL;
+  CHECK(hipMalloc(&d_ry, ysz) == hipSuccess && hipMalloc(&d_ru, uvsz) == hipSuccess &&
+        hipMalloc(&d_rv, uvsz) == hipSuccess);
+  if (rc == WG_OK)
+    rc = wg_encode_mbs((const uint8_t*)d_y, (const uint8_t*)d_u, (const uint8_t*)d_v, (int64_t)ysz, (int64_t)uvsz, w,
+                       h, 1, (const uint8_t*)d_ids, d_segs, 0, (const uint8_t*)d_proba, cfg.method, cfg.quality,
+                       d_out, (uint8_t*)d_ry, (uint8_t*)d_ru, (uint8_t*)d_rv, d_work, NULL);
+  if (rc == WG_OK) rc = wg_encode_status(d_work, mbw, 1, NULL);
+  CHECK(rc == WG_OK);
+  FILE* out = fopen(out_path, "wb");
+  if (!out) return fails + 1;
+  const size_t host_bytes = sizeof(wg_mb_enc) * (size_t)nmb + ysz + 2 * uvsz + (size_t)nmb + sizeof(wg_frame_segs);
+  uint8_t* host = (uint8_t*)malloc(host_bytes);
+  uint8_t* p = host;
+  CHECK(hipMemcpy(p, d_out, sizeof(wg_mb_enc) * (size_t)nmb, hipMemcpyDeviceToHost) == hipSuccess);
+  p += sizeof(wg_mb_enc) * (size_t)nmb;
+  CHECK(hipMemcpy(p, d_ry, ysz, hipMemcpyDeviceToHost) == hipSuccess);
+  CHECK(hipMemcpy(p + ysz, d_ru, uvsz, hipMemcpyDeviceToHost) == hipSuccess);
+  CHECK(hipMemcpy(p + ysz + uvsz, d_rv, uvsz, hipMemcpyDeviceToHost) == hipSuccess);
+  p += ysz + 2 * uvsz;
+  CHECK(hipMemcpy(p, d_ids, (size_t)nmb, hipMemcpyDeviceToHost) == hipSuccess);
+  CHECK(hipMemcpy(p + nmb, d_info, sizeof(wg_frame_segs), hipMemcpyDeviceToHost) == hipSuccess);
+  fwrite(host, 1, host_bytes, out);
+  fclose(out);
+  free(host);
+  void* ps[15] = {d_rgba, d_y, d_u, d_v, d_alpha, d_uvsum, d_ids, d_segs, d_info, d_proba, d_out, d_work,
+                  d_ry, d_ru, d_rv};
+  for (int i = 0; i < 15; i++) (void)hipFree(ps[i]);
+  return fails;
+}
 #endif
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s cpu|gpu file.webp [out.bin]\n", argv[0]);
+    fprintf(stderr, "usage: %s cpu|gpu file.webp [out.bin] | encode frame.bin out.bin\n", argv[0]);
     return 2;
   }
   size_t n = 0;
@@ -172,6 +255,13 @@ int main(int argc, char** argv) {
   int rc;
   if (strcmp(argv[1], "cpu") == 0) {
     rc = run_cpu(data, n);
+  } else if (strcmp(argv[1], "encode") == 0) {
+#ifdef WG_WITH_HIP
+    rc = argc > 3 ? run_encode(data, n, argv[3]) : 2;
+#else
+    fprintf(stderr, "built without -DWG_WITH_HIP\n");
+    rc = 2;
+#endif
   } else {
 #ifdef WG_WITH_HIP
     rc = argc > 3 ? run_gpu(data, n, argv[3]) : 2;

@@ -92,3 +92,48 @@ def test_c_consumer_gpu_sequences(cuda, tmp_path, name):
     eY, eU, eV = O.decode_frame(mb, co, dims["filter_type"], mbw, mbh)
     assert (Y == eY).all() and (U == eU).all() and (V == eV).all()
     assert hashlib.sha256(Y.tobytes()).hexdigest() == hashlib.sha256(eY.tobytes()).hexdigest()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,kind,q,method", [(96, 80, "noise", 75, 4), (200, 72, "blobs", 40, 6),
+                                               (64, 64, "grad", 90, 3)])
+def test_c_consumer_encode_sequence(cuda, tmp_path, w, h, kind, q, method):
+    """INTEGRATION.md's encodeFramePhaseAHIP over the whole device encode path
+    (wg_encoder_config -> wg_import_rgba -> wg_analysis_alphas ->
+    wg_segment_analysis -> wg_encode_row_order -> wg_encode_mbs ->
+    wg_encode_status), driven from C through hipMalloc'd buffers as cgo would:
+    every wg_mb_enc field, the reconstruction, the segment ids and the frame
+    record equal the oracle's EncodeFrame up to Phase A."""
+    from tools import synth
+    from webp_amd import frames
+    exe = build(tmp_path, gpu=True)
+    gen = {"noise": lambda: synth.noise_rgba(w, h, seed=w), "blobs": lambda: synth.blobs_rgba(w, h, seed=h),
+           "grad": lambda: synth.gradient_rgba(w, h)}[kind]
+    rgba = np.ascontiguousarray(gen()[..., :4]).copy()
+    rgba[..., 3] = 255
+    proba = O.default_proba()
+    frame = tmp_path / "frame.bin"
+    frame.write_bytes(np.array([w, h, q, method], "<i4").tobytes() + rgba.tobytes() + proba.tobytes())
+    out = tmp_path / "enc.bin"
+    p = subprocess.run([exe, "encode", str(frame), str(out)], capture_output=True, text=True, timeout=100)
+    assert p.returncode == 0, (p.stdout, p.stderr)
+    mbw, mbh = (w + 15) // 16, (h + 15) // 16
+    nmb = mbw * mbh
+    raw = np.frombuffer(out.read_bytes(), np.uint8)
+    k = nmb * frames.MB_ENC_DTYPE.itemsize
+    got = raw[:k].view(frames.MB_ENC_DTYPE)
+    ysz, uvsz = 256 * nmb, 64 * nmb
+    ry = raw[k:k + ysz].reshape(16 * mbh, 16 * mbw)
+    ru = raw[k + ysz:k + ysz + uvsz].reshape(8 * mbh, 8 * mbw)
+    rv = raw[k + ysz + uvsz:k + ysz + 2 * uvsz].reshape(8 * mbh, 8 * mbw)
+    ids = raw[k + ysz + 2 * uvsz:k + ysz + 2 * uvsz + nmb]
+    info = raw[k + ysz + 2 * uvsz + nmb:].view(frames.FRAME_SEGS_DTYPE)[0]
+    Y, U, V = O.import_rgba(rgba, has_alpha=False)
+    enc, (ey, eu, ev), e_ids, e_info = O.encode_frame(Y, U, V, w, h, O.encoder_config(quality=q, method=method))
+    assert (ids == e_ids).all()
+    for f in ("num_segments", "base_quant", "filter_level", "quant", "fstrength", "update_map"):
+        assert (info[f] == e_info[f]).all(), f
+    for f in frames.MB_ENC_DTYPE.names:
+        if f != "pad":
+            assert (got[f] == enc[f]).all(), f
+    assert (ry == ey).all() and (ru == eu).all() and (rv == ev).all()

@@ -211,3 +211,44 @@ def test_filters(cuda, name):
     got = host(d)
     assert (got == exp).all()
     assert (exp != bufs).any()  # the inputs actually exercised the filter
+
+
+# ---------------- argument validation: footprints outside the buffer ----------------
+
+def test_block_wrappers_reject_out_of_buffer_footprints(cuda):
+    """A block origin whose footprint leaves its buffer is refused with
+    WG_EINVAL before any device work (the reference panics on the Go bounds
+    check); the same call in bounds runs."""
+    bufs = torch.zeros((4, O.YUV_SIZE), dtype=torch.uint8, device=cuda)
+    co = torch.zeros((4, 64), dtype=torch.int16, device=cuda)
+    bad = [
+        lambda: dsp.PredLuma16(0, bufs, O.YOFF - O.BPS),               # top-left corner at -1
+        lambda: dsp.PredLuma4(0, bufs, torch.tensor([O.YOFF, O.YUV_SIZE - 8])),  # one instance past the end
+        lambda: dsp.PredChroma8(0, bufs, O.YUV_SIZE - 4 * O.BPS),
+        lambda: dsp.Transform(co, bufs, True, O.YUV_SIZE - 2 * O.BPS),
+        lambda: dsp.TransformUV(co[:, :16], bufs, O.UOFF),             # 16 coefficients for 4 blocks
+        lambda: dsp.ITransform(bufs, co[:, :32], bufs, True, O.YUV_SIZE - 8, 0),
+        lambda: dsp.SSE16x16(bufs, bufs, O.YUV_SIZE - 15 * O.BPS, 0),
+        lambda: dsp.filter_edge("VFilter16", bufs, O.YOFF, O.BPS, 20, 10, 1),       # 4 rows above row 0 of Y
+        lambda: dsp.filter_edge("HFilter8i", bufs, O.UOFF, O.BPS, 20, 10, 1, uv_delta=O.YUV_SIZE),
+        lambda: dsp.SSIMGet(bufs, bufs, 120),
+    ]
+    for f in bad:
+        with pytest.raises(dsp.InvalidArgument) as e:
+            f()
+        assert e.value.status == dsp.WG_EINVAL
+    dsp.PredLuma16(0, bufs, O.YOFF)
+    dsp.filter_edge("VFilter16", bufs, O.YOFF + 4 * O.BPS, O.BPS, 20, 10, 1)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("name,lo,hi", [
+    ("SimpleVFilter16", 100 - 64, 100 + 32 + 16), ("SimpleHFilter16", 98, 100 + 15 * 32 + 2),
+    ("SimpleVFilter16i", 100 + 2 * 32, 100 + 13 * 32 + 16), ("VFilter16", 100 - 128, 100 + 96 + 16),
+    ("HFilter16i", 100, 100 + 12 + 3 + 15 * 32 + 1), ("VFilter8", 100 - 128, 100 + 7 + 96 + 1 + 12),
+    ("VFilter8i", 100, 100 + 4 * 32 + 3 * 32 + 7 + 1 + 12), ("HFilter8", 96, 100 + 3 + 7 * 32 + 1 + 12)])
+@pytest.mark.gpu
+def test_filter_span(name, lo, hi):
+    """filter.go's reads: edge filters touch -2..+1 (simple) / -4..+3 (normal)
+    across the edge, 16 (8 for chroma, V plane uv_delta = 12 further) along it."""
+    assert dsp.filter_span(name, 100, 32, 12) == (lo, hi)

@@ -70,10 +70,13 @@ def test_decode_1080p_batch(cuda):
     run_decode(120, 68, 2, 2, seed=2024, levels=(20, 32))
 
 
-def test_decode_kernel_switch(cuda):
+@pytest.mark.parametrize("filter_type", [0, 1, 2])
+def test_decode_kernel_switch(cuda, filter_type):
     """wg_decode_frames launches k_decode_split for few rows and k_decode_bands
-    past twice the resident split rows (decode.hip use_split); both bit-exact.
-    Narrow frames keep the oracle quick at the batch that crosses over."""
+    past twice the resident split rows (decode.hip use_split); both bit-exact,
+    for every filter type (the simple filter keeps the chroma rows of a band's
+    last row, the normal one hands them to the next band).  Narrow frames keep
+    the oracle quick at the batch that crosses over."""
     from webp_amd import _lib
     if os.environ.get("WG_DECODE_KERNEL"):
         pytest.skip("WG_DECODE_KERNEL forces one kernel")
@@ -83,7 +86,7 @@ def test_decode_kernel_switch(cuda):
     while _lib.lib.wg_decode_kernel(mbh, n) == 1:
         n *= 2
     assert _lib.lib.wg_decode_kernel(mbh, n) == 2 and n <= 1024
-    run_decode(3, mbh, n, 2, seed=n, levels=(20, 40))
+    run_decode(3, mbh, n, filter_type, seed=n + filter_type, levels=(0, 20, 40))
 
 
 def test_decode_4096_square(cuda):

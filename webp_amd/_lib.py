@@ -145,6 +145,10 @@ for _name, _args in SIGNATURES.items():
     _f.argtypes = _args
     _f.restype = _RES.get(_name, ctypes.c_int)
 
+ABI_VERSION = 2  # WG_ABI_VERSION of include/webpgpu.h this binding is written against
+if lib.wg_version() != ABI_VERSION:
+    raise WebpGpuError(f"{LIB_PATH}: ABI version {lib.wg_version()}, this binding needs {ABI_VERSION} (rebuild it)")
+
 
 def check(rc, what=""):
     if rc != 0:

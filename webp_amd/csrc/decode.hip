@@ -877,9 +877,10 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                                  sched)
                 : 99;
         // ---- dependency on the row above; ring space below (top ring) and in F's ring ----
-        // In the band the luma waits only for the luma of MB x above (its
-        // bottom row, tprog), the chroma for the rest of it (prog_r, before
-        // the chroma phase); across bands for the whole MB (its top record).
+        // The whole MB x above: through prog_r in the band, through the row
+        // above's progress word (its top record) across bands.  Only the
+        // top-right wait of an I4 block (tr_step below) goes block by block
+        // (tprog).
         if (mby > 0) {
           const int need = mbx + 1;
           if (seen < need) {

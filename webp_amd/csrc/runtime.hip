@@ -77,7 +77,7 @@ extern "C" int wg_debug_inject_timeout(int32_t family, void* stream) {
 
 extern "C" const char* wg_last_error(void) { return wg::g_last_error.c_str(); }
 
-extern "C" int wg_version(void) { return 1; }
+extern "C" int wg_version(void) { return WG_ABI_VERSION; }
 
 extern "C" int wg_device_check(void) {
   int dev = 0;

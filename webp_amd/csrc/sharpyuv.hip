@@ -397,14 +397,15 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     pf_row = load_row(ju + 3);
     pf_in = load_in(ju + 3);
     // (A) B's sums of this row pair, read now and used after A's own half:
-    // B's progress word first, then the slot, with no wait between (the LDS
-    // unit performs one wave's reads in issue order, and B wrote the slot
-    // before its release of the word), so a B that is ahead -- the usual
-    // case -- costs no round trip on A's chain
+    // B's progress word first (acquire, pairing with B's release of it),
+    // then the slot, with no wait between, so a B that is ahead -- the usual
+    // case -- costs no round trip on A's chain.  A workgroup-scope acquire of
+    // an LDS word adds no instruction on gfx950 (LDS accesses of a wave
+    // retire in order); it keeps the compiler from hoisting the slot read.
     uint4 sb = make_uint4(0, 0, 0, 0);
     int pb = 0;
     if constexpr (ROLE == 0) {
-      pb = __hip_atomic_load(&x.prog_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      pb = __hip_atomic_load(&x.prog_b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
       asm volatile("" ::: "memory");
       sb = x.sum[ju % XD][lane];
     }

@@ -10,7 +10,16 @@ GPU; there is no CPU path.
 """
 import torch
 
-from ._lib import call
+from ._lib import WebpGpuError, call
+
+WG_EINVAL = -1  # include/webpgpu.h
+
+
+class InvalidArgument(WebpGpuError, ValueError):
+    """A block call whose footprint leaves its buffer: the reference panics
+    with a Go bounds-check error; the host mirror refuses it (status WG_EINVAL)
+    before any device work, since the device entry points take bare pointers."""
+    status = WG_EINVAL
 
 BPS = 32  # internal/dsp/dsp.go:5
 YUV_SIZE = BPS * 17 + BPS * 9  # internal/lossy/constants.go:70-75
@@ -56,12 +65,46 @@ def _offs(off, n, device):
     return _dev(off.to(torch.int32).to(device).contiguous()), 0
 
 
+def _span(lo, hi, length, what):
+    """Every byte offset a call touches lies in [lo, hi); the buffer has `length`."""
+    if lo < 0 or hi > length:
+        raise InvalidArgument(f"{what}: touches bytes [{lo}, {hi}) of a {length}-byte buffer (status {WG_EINVAL})")
+
+
+def _check_offs(off, lo_rel, hi_rel, length, what):
+    """Block origin(s) `off` (int, or a tensor of per-instance origins) with the
+    footprint [off + lo_rel, off + hi_rel) inside every buffer."""
+    if isinstance(off, int):
+        _span(off + lo_rel, off + hi_rel, length, what)
+    elif off.numel():
+        o = off.to(torch.int64)
+        _span(int(o.min()) + lo_rel, int(o.max()) + hi_rel, length, what)
+
+
+def _block(off, rows, cols, stride=BPS):
+    """[lo, hi) of a rows x cols block at `off` (row stride `stride`)."""
+    return off, off + (rows - 1) * stride + cols
+
+
+def _need_cols(t, cols, what):
+    if t.dim() != 2 or t.shape[1] < cols:
+        raise InvalidArgument(f"{what}: rows of {tuple(t.shape)[1:]} elements, the call uses {cols} (status {WG_EINVAL})")
+
+
 # ---- intra predictors (predict_lossy.go, dsp.go:33-37) ----
+
+_PRED_SIZE = {"wg_pred_luma4": (4, 8), "wg_pred_luma16": (16, 16), "wg_pred_chroma8": (8, 8)}
+
 
 def _pred(name, modes, bufs, off):
     _dev(bufs, torch.uint8)
     n = bufs.shape[0]
     m = _modes(modes, n, bufs.device)
+    # the block, its left column, the top row from the top-left corner (luma4:
+    # and the 4 top-right pixels) -- predict_lossy.go's reads around off
+    size, top = _PRED_SIZE[name]
+    _check_offs(off, -BPS - 1, (size - 1) * BPS + size if size > 4 else max(3 * BPS + 4, -BPS + top),
+                bufs.shape[1], name)
     offs, o = _offs(off, n, bufs.device)
     call(name, m.data_ptr(), bufs.data_ptr(), bufs.stride(0), offs.data_ptr() if offs is not None else None, o, n,
          _stream())
@@ -84,10 +127,20 @@ def PredChroma8(modes, bufs, off):
 
 # ---- transforms (transforms.go, dsp.go:10-24) ----
 
+# kind -> (coefficients read, rows x cols of dst written)
+_T_SHAPE = {_T_ONE: (16, 4, 4), _T_TWO: (32, 4, 8), _T_AC3: (16, 4, 4), _T_DC: (16, 4, 4), _T_UV: (64, 8, 8),
+            _T_DCUV: (64, 8, 8)}
+
+
 def _transform(kind, coeffs, dst, off):
     _dev(coeffs, torch.int16)
     _dev(dst, torch.uint8)
     n = dst.shape[0]
+    nco, rows, cols = _T_SHAPE[kind]
+    _need_cols(coeffs, nco, "wg_transform coeffs")
+    if coeffs.shape[0] != n:
+        raise InvalidArgument(f"wg_transform: {coeffs.shape[0]} coefficient rows for {n} buffers")
+    _check_offs(off, 0, (rows - 1) * BPS + cols, dst.shape[1], "wg_transform dst")
     call("wg_transform", kind, coeffs.data_ptr(), coeffs.stride(0), dst.data_ptr() + off, dst.stride(0), n,
          _stream())
 
@@ -117,6 +170,8 @@ def TransformWHT(inp, out):
     """TransformWHT(in[16], out[256]) (transforms.go:223): DCs land at out[16*k]."""
     _dev(inp, torch.int16)
     _dev(out, torch.int16)
+    _need_cols(inp, 16, "TransformWHT in")
+    _need_cols(out, 241, "TransformWHT out")
     call("wg_transform_wht", inp.data_ptr(), out.data_ptr(), inp.shape[0], _stream())
 
 
@@ -124,6 +179,8 @@ def FTransformWHT(inp, out):
     """FTransformWHT on a flat 4x4 DC array (transforms.go:500)."""
     _dev(inp, torch.int16)
     _dev(out, torch.int16)
+    _need_cols(inp, 16, "FTransformWHT in")
+    _need_cols(out, 16, "FTransformWHT out")
     call("wg_ftransform_wht", inp.data_ptr(), out.data_ptr(), inp.shape[0], _stream())
 
 
@@ -134,6 +191,9 @@ def ITransform(ref, inp, dst, do_two, ref_off=0, dst_off=0):
     _dev(inp, torch.int16)
     _dev(dst, torch.uint8)
     assert ref.stride(0) == dst.stride(0) and inp.shape[1] == 32
+    cols = 8 if do_two else 4
+    _check_offs(ref_off, 0, 3 * BPS + cols, ref.shape[1], "ITransform ref")
+    _check_offs(dst_off, 0, 3 * BPS + cols, dst.shape[1], "ITransform dst")
     call("wg_itransform", ref.data_ptr() + ref_off, inp.data_ptr(), dst.data_ptr() + dst_off, ref.stride(0),
          int(do_two), ref.shape[0], _stream())
 
@@ -144,6 +204,10 @@ def FTransform(src, ref, out, src_off=0, ref_off=0, two=False):
     _dev(ref, torch.uint8)
     _dev(out, torch.int16)
     assert src.stride(0) == ref.stride(0)
+    cols = 8 if two else 4
+    _check_offs(src_off, 0, 3 * BPS + cols, src.shape[1], "FTransform src")
+    _check_offs(ref_off, 0, 3 * BPS + cols, ref.shape[1], "FTransform ref")
+    _need_cols(out, 32 if two else 16, "FTransform out")
     call("wg_ftransform", src.data_ptr() + src_off, ref.data_ptr() + ref_off, src.stride(0), out.data_ptr(),
          int(two), src.shape[0], _stream())
 
@@ -158,6 +222,9 @@ def _metric(kind, pix, ref, pix_off, ref_off):
     _dev(pix, torch.uint8)
     _dev(ref, torch.uint8)
     assert pix.stride(0) == ref.stride(0)
+    size = 4 if kind in (_M_SSE4, _M_TD4) else 16
+    _check_offs(pix_off, 0, (size - 1) * BPS + size, pix.shape[1], "wg_metric pix")
+    _check_offs(ref_off, 0, (size - 1) * BPS + size, ref.shape[1], "wg_metric ref")
     out = torch.empty(pix.shape[0], dtype=torch.int32, device=pix.device)
     call("wg_metric", kind, pix.data_ptr() + pix_off, ref.data_ptr() + ref_off, pix.stride(0), out.data_ptr(),
          pix.shape[0], _stream())
@@ -184,6 +251,7 @@ def SSIMGet(src1, src2, stride):
     """SSIMGet(src1, stride, src2, stride) (ssim.go:116) per buffer pair."""
     _dev(src1, torch.uint8)
     _dev(src2, torch.uint8)
+    _span(0, 6 * stride + 7, min(src1.shape[1], src2.shape[1]), "SSIMGet 7x7 window")
     out = torch.empty(src1.shape[0], dtype=torch.float64, device=src1.device)
     call("wg_ssim_get", src1.data_ptr(), src2.data_ptr(), src1.stride(0), stride, None, out.data_ptr(),
          src1.shape[0], _stream())
@@ -203,6 +271,23 @@ def SSIMGetClipped(src1, src2, stride, xywh):
 
 # ---- loop filters (filter.go:93-242) ----
 
+def filter_span(name, base, stride, uv_delta=0):
+    """[lo, hi) of the bytes dsp.<name> reads or writes (filter.go:93-242): an
+    edge filter at o with normal step h, edge step v over s positions touches
+    o + a*h .. o + b*h + (s - 1)*v, (a, b) = (-2, 1) simple / (-4, 3) normal;
+    the inner variants at o = base + 4k (k = 1..3, chroma k = 1) steps."""
+    simple = name.startswith("Simple")
+    a, b = (-2, 1) if simple else (-4, 3)
+    vert = "VFilter" in name
+    s = 8 if name.endswith(("8", "8i")) else 16
+    h, v = (stride, 1) if vert else (1, stride)
+    ks = ((1, 2, 3) if s == 16 else (1,)) if name.endswith("i") else (0,)
+    origins = [base + 4 * k * h for k in ks]
+    if s == 8:
+        origins += [o + uv_delta for o in origins]
+    return min(o + a * h for o in origins), max(o + b * h + (s - 1) * v for o in origins) + 1
+
+
 def filter_edge(name, p, base, stride, thresh, ithresh=None, hev=None, uv_delta=0):
     """Apply dsp.<name>(p, base, stride, thresh[, ithresh, hevT]) to every buffer.
     For the 8-pixel chroma filters the V plane is p + uv_delta."""
@@ -216,6 +301,8 @@ def filter_edge(name, p, base, stride, thresh, ithresh=None, hev=None, uv_delta=
             x = torch.full((n,), x, dtype=torch.int32, device=p.device)
         return _dev(x.to(torch.int32).contiguous())
     t, it, h = vec(thresh), vec(ithresh), vec(hev)
+    lo, hi = filter_span(name, base, stride, uv_delta)
+    _span(lo, hi, p.shape[1], name)
     call("wg_filter", FILTER_KINDS[name], p.data_ptr(), p.stride(0), base, stride, uv_delta, t.data_ptr(),
          it.data_ptr() if it is not None else None, h.data_ptr() if h is not None else None, n, _stream())
 
