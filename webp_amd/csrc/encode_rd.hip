@@ -190,8 +190,19 @@ struct Shared {
   uint8_t nzy[16], nzuv[8];
   int mode_rate[4], mode_disto[4], uv_rate[4], uv_disto[4];
   alignas(16) int16_t co_buf[16][16];  // transform coefficients handed to the trellis prep lanes (|c| < 2^12)
-  TRec trec[6][16];        // trellis position records: I4 (half, candidate) / final I16 (diagonal slot)
+  // trellis position records: I4 (half, candidate) / final I16 (block of the
+  // round).  Slots 17 records apart (WG_ENC_TPAD): at 16 (768 B, a multiple of
+  // the 256-B bank row) the six DP quads' reads of one position all hit the
+  // same banks.
+#ifndef WG_ENC_TPAD
+#define WG_ENC_TPAD 1
+#endif
+#ifndef WG_ENC_FUSE  // I4 candidates' FTransform in the pre-screen lanes (see the I4 RD)
+#define WG_ENC_FUSE 1
+#endif
+  TRec trec[6][16 + WG_ENC_TPAD];
   int64_t r0[16][3];       // the phase's level-0 trellis row (trellis_r0)
+  int64_t eobl[16][2];     // the phase's terminal costs x lam16 (trellis_r0, WG_ENC_EOBT)
   int16_t l0s[6][16];      // per position: L0 << 3 | negative << 2 | min(L0, 2) (< 2^14)
   alignas(16) int16_t cand_q[6][16];  // I4 candidates' levels for the lane-parallel token cost
   int cand_nz[6], cand_rate[6];
@@ -318,12 +329,28 @@ __device__ __forceinline__ int token_cost(const Tables& t, const QT& q, int nz_c
 //
 // The R0 table of a phase: position n, predecessor context pc -> the
 // zero-token cost of band(n + 1) * lam16 + idx pc; lane 3n + pc writes it.
+#ifndef WG_ENC_EOBT
+#define WG_ENC_EOBT 1
+#endif
+// (WG_ENC_EOBT) lanes 48 + n also write the phase's terminal costs: EOB after
+// position n from end context 1 / 2, x lam16 (0 after position 15), plus n
+// (the key's position field, see trellis_dp4), which the DP adds to a state
+// instead of multiplying the EOB cost per position.
 template <int CTX_TYPE>
-__device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16, int64_t (*r0)[3]) {
+__device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16, int64_t (*r0)[3],
+                                           int64_t (*eobl)[2]) {
   if (lane < 48) {
     const int n = lane / 3, pc = lane - 3 * n;
     r0[n][pc] = (int64_t)vc_of(t.vcost[CTX_TYPE * 8 + band_of(n + 1)][0], pc) * lam16 + pc;
   }
+#if WG_ENC_EOBT
+  else {
+    const int n = lane - 48;
+    const TokRow& tr = t.tok[CTX_TYPE * 8 + band_of(n + 1)];
+    eobl[n][0] = (n < 15 ? (int64_t)tr.eob[1] * lam16 : 0) + n;
+    eobl[n][1] = (n < 15 ? (int64_t)tr.eob[2] * lam16 : 0) + n;
+  }
+#endif
 }
 
 // The level candidates, distortion deltas and token + level costs of two
@@ -426,8 +453,9 @@ __device__ __forceinline__ int quad_bcast32(int v) {
 // chain: the quad's lane r writes positions 4r..4r+3 (raster) to q, and lane
 // 0 writes the zigzag nz count to *nz.
 template <int FIRST, int CTX_TYPE>
-__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[3], const int16_t* l0s,
-                                            int init_ctx, int lam16, int k, int16_t* q, int* nz) {
+__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[3],
+                                            const int64_t (*eobl)[2], const int16_t* l0s, int init_ctx, int lam16, int k,
+                                            int16_t* q, int* nz) {
   constexpr int64_t BIG = 1ll << 59;
   init_ctx = min(init_ctx, 2);
   const int e = min(k, 2);
@@ -438,35 +466,54 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   // lanes 0, 1 follow the terminals of context 1 (lane 0's copy is unused), lanes 2, 3 context 2
   const int tctx = e == 2 ? 2 : 1;
   int64_t best_terminal = (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16;
+#if !WG_ENC_EOBT
   int best_n = -1;
+#endif
   uint32_t best_h = 0;
   // this lane's row: R0 from the phase's table (3 words a position), R1 / R2
   // from the block's records (6 words a position)
   const int64_t* mine = e == 0 ? &r0[0][0] : &rec[0].x[e - 1][0];
   const int STRIDE = e == 0 ? 3 : (int)(sizeof(TRec) / sizeof(int64_t));
+#if WG_ENC_EOBT
+  // terminal keys carry their position in the low 4 bits (the scores there
+  // are 0: states are masked to ~15 and the EOB costs are multiples of 16), so
+  // the first strict minimum over positions, and across the two contexts the
+  // earlier position on a tie, is a plain key min with no position register
+  const int64_t* eobq = &eobl[0][tctx - 1];
+  int64_t eob_raw = eobq[2 * FIRST];
+#else
   const uint16_t* eobp = &t.tok[CTX_TYPE * 8].eob[0] + tctx;
   constexpr int TSTR = sizeof(TokRow) / 2;
+  uint32_t eob_raw = FIRST < 15 ? eobp[kBand[FIRST + 1] * TSTR] : 0;
+#endif
   // Position n's row, class and EOB cost are loaded during position n - 1
   // and pinned by the asm below, so no LDS round trip sits on the chain.
   int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
   int cls_raw = l0s[FIRST];
-  uint32_t eob_raw = FIRST < 15 ? eobp[kBand[FIRST + 1] * TSTR] : 0;
 #pragma unroll
   for (int n = FIRST; n < 16; n++) {
     int64_t nx0 = 0, nx1 = 0, nx2 = 0;
     int ncls = 0;
+#if WG_ENC_EOBT
+    int64_t neob = 0;
+#else
     uint32_t neob = 0;
+#endif
     if (n < 15) {
       nx0 = mine[(n + 1) * STRIDE];
       nx1 = mine[(n + 1) * STRIDE + 1];
       nx2 = mine[(n + 1) * STRIDE + 2];
       ncls = l0s[n + 1];
+#if WG_ENC_EOBT
+      neob = eobq[2 * (n + 1)];
+#else
       if (n + 1 < 15) neob = eobp[kBand[n + 2] * TSTR];
+#endif
     }
     asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
     const int64_t c0 = ps0 + x0, c1 = ps1 + x1, c2 = ps2 + x2;
     const bool two = (cls_raw & 2) != 0;  // class 2: L0 >= 2
-    const uint32_t eob_n = eob_raw;
+    const auto eob_n = eob_raw;
     x0 = nx0;
     x1 = nx1;
     x2 = nx2;
@@ -488,19 +535,30 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
     h2 = two && lt ? H1 : H2;
     // terminal (EOB after this position) of context tctx
     const int64_t tps = tctx == 2 ? ps2 : ps1;
+#if WG_ENC_EOBT
+    const int64_t eobs = tps + eob_n;
+#else
     const int64_t eobs = tps + (n < 15 ? (int64_t)eob_n * lam16 : 0);
+#endif
     // (an invalid state, >= 2^59, never beats best_terminal, which starts at a
     // valid EOB cost below 2^51 and only decreases: no separate validity test)
     const bool w = eobs < best_terminal;
     best_terminal = w ? eobs : best_terminal;
+#if !WG_ENC_EOBT
     best_n = w ? n : best_n;
+#endif
     best_h = w ? (tctx == 2 ? h2 : h1) : best_h;
   }
   // the first strict minimum over (position, context 1 then 2), in every lane
   const int64_t bt1 = quad_bcast<1>(best_terminal), bt2 = quad_bcast<2>(best_terminal);
-  const int bn1 = quad_bcast32<1>(best_n), bn2 = quad_bcast32<2>(best_n);
   const uint32_t bh1 = quad_bcast32<1>(best_h), bh2 = quad_bcast32<2>(best_h);
+#if WG_ENC_EOBT
+  // (both still at the all-zero start: equal keys, both histories 0)
+  const bool second = bt2 < bt1;
+#else
+  const int bn1 = quad_bcast32<1>(best_n), bn2 = quad_bcast32<2>(best_n);
   const bool second = bt2 < bt1 || (bt2 == bt1 && bn2 < bn1);
+#endif
   const uint32_t hist = second ? bh2 : bh1;  // 0 when no terminal beat the all-zero block
   // lane r: positions 4r .. 4r + 3
   const int r = k;
@@ -1045,6 +1103,19 @@ __device__ unsigned long long g_row_times[16384][4];
 #define WG_ENC_OCC (WG_ENC_GROUPS == 3 ? 3 : 2)  // waves per SIMD (VGPR budget 512 / occupancy)
 #endif
 
+// Measurement builds only (tools/gpu_enc_phase_sq.sh): -DWG_EXP_REP_<PHASE>=2
+// runs that phase twice per macroblock.  Each repeated phase is idempotent
+// (it reads only state written before it and rewrites the same values), so
+// the outputs stay bit-exact and a counter of the build minus the default
+// build's is that phase's own share -- per-phase VALU lane occupancy, LDS
+// bank conflicts and waits, with the data flow, early exits and contention of
+// the real launch.  Phases: RD (I16 + UV RD), I4 (the whole I4 RD), PRE (I4
+// value table + pre-screen), CAND (candidates' prediction + FTransform), PREP
+// (trellis position records), DP (the trellis DP), FIN (final residuals).
+// The default build compiles none of it.
+#define WG_REP_BEGIN(N) for (int rep_ = 0; rep_ < (N); rep_++) {
+#define WG_REP_END }
+
 // An image's four segment tables (4 x 224 B = 56 x 16 B) into LDS
 __device__ __forceinline__ void load_segments(const EncArgs& a, int img, Segment* dst, int lane) {
   const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.segs) + img * a.segs_pitch);
@@ -1412,6 +1483,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       if (isB) {
       // ================= I16 RD (pickBestI16ModeRDParallel :624-737) =================
       // then UV RD (pickBestUVModeRDParallel :1030-1114)
+#if defined(WG_EXP_REP_RD)
+      WG_REP_BEGIN(WG_EXP_REP_RD)
+#endif
       bool src_flat;
       {
         // isFlatSource16 (encode_analysis.go:358)
@@ -1537,6 +1611,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         }
       }
       s16 = rd_score(disto16, rate16, sg.lambda_mode);
+#if defined(WG_EXP_REP_RD)
+      WG_REP_END
+#endif
       if constexpr (PAIR) {  // for A's early exit: the score, then the flag
         if (lane == 0) {
           *reinterpret_cast<volatile uint64_t*>(&c.s16v) = s16;
@@ -1565,7 +1642,10 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           if (i < YUV / 4) reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
         }
       }
-      if constexpr (TRELLIS) trellis_r0<3>(t, lane, sg.tlambda_i4 * 16, s.r0);
+#if defined(WG_EXP_REP_I4)
+      WG_REP_BEGIN(WG_EXP_REP_I4)
+#endif
+      if constexpr (TRELLIS) trellis_r0<3>(t, lane, sg.tlambda_i4 * 16, s.r0, s.eobl);
       lds_sync();
       {
         // running totals over the finished blocks: rate, distortion and header
@@ -1613,14 +1693,26 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           load4x4(s.yin + off, src);
           SSTAMP(-1);
           // pre-screen all eligible modes by prediction SSE (lanes 0-9 of each half)
+          int sse_lane = 0;
+#if defined(WG_EXP_REP_PRE)
+      WG_REP_BEGIN(WG_EXP_REP_PRE)
+#endif
           pred4_values(s.yout2, off, hl, s.pv[half]);
           lds_sync();
-          int sse_lane = 0;
+          // (FUSE) every pre-screen lane also transforms its mode's residual:
+          // the candidates are among these lanes, so their coefficients come
+          // without a second prediction pass (its 17 LDS reads) after the pick
+          constexpr bool FUSE = TRELLIS && WG_ENC_FUSE;
+          int pco[FUSE ? 16 : 1];
           if (bvalid && hl < 10) {
             int pred[16];
             pred4_lut(t.pcode[hl], s.pv[half], pred);
             sse_lane = sse16(src, pred);
+            if constexpr (FUSE) fdct(src, pred, pco);
           }
+#if defined(WG_EXP_REP_PRE)
+      WG_REP_END
+#endif
           SSTAMP(0);
           // eligible modes (no top / no left context rules out some), candidates
           uint32_t eligible = 0x3ff;
@@ -1634,7 +1726,16 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           const int slot = half * 3 + min(hl, 2);  // candidate slot in the trellis / level buffers
           SSTAMP(1);
           // candidates: prediction + transform (lane hl = candidate hl)
-          if (cand) {
+#if defined(WG_EXP_REP_CAND)
+      WG_REP_BEGIN(WG_EXP_REP_CAND)
+#endif
+          if constexpr (FUSE) {  // the lane of mode cm[c] stores candidate c's coefficients
+            const int c = (K > 0 && cm[0] == hl) ? 0 : ((K > 1 && cm[1] == hl) ? 1 : ((K > 2 && cm[2] == hl) ? 2 : 3));
+            if (bvalid && hl < 10 && c < 3) {
+#pragma unroll
+              for (int i = 0; i < 4; i++) st_co4(&s.co_buf[half * 3 + c][4 * i], pco + 4 * i);
+            }
+          } else if (cand) {
             CSTAMP(-1);
             int pred[16], co[16];
             pred4_lut(t.pcode[mode], s.pv[half], pred);
@@ -1650,11 +1751,17 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             }
             CSTAMP(0);
           }
+#if defined(WG_EXP_REP_CAND)
+      WG_REP_END
+#endif
           lds_sync();
           if constexpr (TRELLIS) {
           // trellis positions: lane (candidate c, pair pp) prepares positions 2pp, 2pp + 1
           const int lam16 = sg.tlambda_i4 * 16;
           bool pnz = false;
+#if defined(WG_EXP_REP_PREP)
+      WG_REP_BEGIN(WG_EXP_REP_PREP)
+#endif
           if (bvalid && hl < 8 * K) {
             const int c = hl >> 3, n0 = 2 * (hl & 7), sl = half * 3 + c;
             // both positions into registers first, then stored: their table
@@ -1668,6 +1775,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               s.l0s[sl][n0 + j] = l0[j];
             }
           }
+#if defined(WG_EXP_REP_PREP)
+      WG_REP_END
+#endif
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
           DSTAMP(-1);
@@ -1678,7 +1788,13 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               // the DP is the step's serial chain: let it win issue arbitration
               // against the SIMD's other wave while it runs
               __builtin_amdgcn_s_setprio(3);
-              trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
+#if defined(WG_EXP_REP_DP)
+      WG_REP_BEGIN(WG_EXP_REP_DP)
+#endif
+              trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
+#if defined(WG_EXP_REP_DP)
+      WG_REP_END
+#endif
               __builtin_amdgcn_s_setprio(2);
             } else if ((hl & 3) == 0) {
 #pragma unroll
@@ -1838,6 +1954,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         }
         s4 = early ? ~0ull : rd_score(run_disto, run_rate + 211, sg.lambda_mode);
       }
+#if defined(WG_EXP_REP_I4)
+      WG_REP_END
+#endif
       __builtin_amdgcn_s_setprio(1);
       }  // isA
       bool is_i4 = s4 < s16;  // (PAIR: decided at the join)
@@ -1871,6 +1990,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
 
       ESTAMP(5);
       // ================= final residuals (encodeResidualsParallel :1166-1356) =================
+#if defined(WG_EXP_REP_FIN)
+      WG_REP_BEGIN(WG_EXP_REP_FIN)
+#endif
       if (run16) {
         int dc_nz = 0;
         if (lane < 16) {
@@ -1905,7 +2027,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         // followed by the reference's raster-order resolution of the actual
         // contexts.  (Walking the 7 block diagonals took 7 prep + DP rounds.)
         const int lam16 = sg.tlambda_i16 * 16;
-        trellis_r0<0>(t, lane, lam16, s.r0);  // (read after the first round's lds_sync)
+        trellis_r0<0>(t, lane, lam16, s.r0, s.eobl);  // (read after the first round's lds_sync)
         int16_t* res_q = reinterpret_cast<int16_t*>(s.yout2);  // [16 tasks][16] levels (yout2 is free for I16 MBs)
         int* res_nz = reinterpret_cast<int*>(s.yout2 + 512);   // [16]
         uint32_t nzbits = 0;  // the resolved blocks' nz flags (bit = block), a scalar across the rounds
@@ -1948,7 +2070,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             if (tj >= 0) {
               if ((pnz_mask >> (8 * tj)) & 0xff) {
                 int nzv = 0;
-                trellis_dp4<1, 0>(t, s.trec[tj], s.r0, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
+                trellis_dp4<1, 0>(t, s.trec[tj], s.r0, s.eobl, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
                 if ((lane & 3) == 0) res_nz[q] = nzv;
                 tnz = nzv;
               } else if ((lane & 3) == 0) {
@@ -2002,6 +2124,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         for (int i = 0; i < 16; i++) s.coeffs[(16 + lane) * 16 + i] = q[i];
       }
       lds_sync();
+#if defined(WG_EXP_REP_FIN)
+      WG_REP_END
+#endif
 
       ESTAMP(6);
       // ================= reconstruction (reconstructMBParallel :1358-1410) =================
