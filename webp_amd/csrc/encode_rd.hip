@@ -1694,16 +1694,16 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           SSTAMP(-1);
           // pre-screen all eligible modes by prediction SSE (lanes 0-9 of each half)
           int sse_lane = 0;
-#if defined(WG_EXP_REP_PRE)
-      WG_REP_BEGIN(WG_EXP_REP_PRE)
-#endif
-          pred4_values(s.yout2, off, hl, s.pv[half]);
-          lds_sync();
           // (FUSE) every pre-screen lane also transforms its mode's residual:
           // the candidates are among these lanes, so their coefficients come
           // without a second prediction pass (its 17 LDS reads) after the pick
           constexpr bool FUSE = TRELLIS && WG_ENC_FUSE;
           int pco[FUSE ? 16 : 1];
+#if defined(WG_EXP_REP_PRE)
+      WG_REP_BEGIN(WG_EXP_REP_PRE)
+#endif
+          pred4_values(s.yout2, off, hl, s.pv[half]);
+          lds_sync();
           if (bvalid && hl < 10) {
             int pred[16];
             pred4_lut(t.pcode[hl], s.pv[half], pred);
