@@ -309,6 +309,122 @@ __global__ __launch_bounds__(64 * SEL_WAVES) void k_vp8l_select(SelArgs a) {
   }
 }
 
+// ResidualImage phase 1 for tiles of at most 32 x 32 px (bits <= 5, so every
+// histogram count is <= 512): ONE wave per tile and one pass over its samples
+// for all modes at once.
+//   - Lane 4m + s predicts sample s of each run of four (mode m's predictor,
+//     predict_ctl: branch-free for every mode) and takes the residual; the
+//     quad then transposes (4 DPP broadcasts) so that lane 4m + c holds channel
+//     c of the run's four residuals.
+//   - Lane 4m + c owns the histogram of (mode m, channel c): bins b and
+//     b + 128 as the two 16-bit halves of word b & 127, stored [word][lane],
+//     so every lane adds to its own bank (ds_add_u32, no return, no
+//     contention however flat the content).
+//   - Lane 4m + c then runs the (mode, channel) float64 sum of
+//     estimateEntropy (encode_predictor.go:262-275) in the reference's order:
+//     fastSLog2(count) minus the bins 0..255 (an empty bin subtracts
+//     fastSLog2(0) = 0.0, which leaves the sum unchanged); the 56 sums run at
+//     once, and each mode's four channel sums are added alpha, red, green,
+//     blue from 0.0 as the reference adds them.  The argmin keeps the
+//     reference's first strict minimum in mode order (:408-418).
+// fastSLog2 of 0..512 is staged in LDS from the same device table.
+constexpr int SQW = 4;        // waves (tiles) per workgroup
+constexpr int SQ_LUT = 513;   // counts 0..512
+__device__ __forceinline__ double dpp_quad_f64(double v, int j) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
+  switch (j) {  // (j is a constant at every call)
+    case 0: lo = __builtin_amdgcn_mov_dpp(lo, 0x00, 0xf, 0xf, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x00, 0xf, 0xf, false); break;
+    case 1: lo = __builtin_amdgcn_mov_dpp(lo, 0x55, 0xf, 0xf, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x55, 0xf, 0xf, false); break;
+    case 2: lo = __builtin_amdgcn_mov_dpp(lo, 0xaa, 0xf, 0xf, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xaa, 0xf, 0xf, false); break;
+    default: lo = __builtin_amdgcn_mov_dpp(lo, 0xff, 0xf, 0xf, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xff, 0xf, 0xf, false); break;
+  }
+  return __builtin_bit_cast(double, (uint64_t)(uint32_t)hi << 32 | (uint32_t)lo);
+}
+template <int J>
+__device__ __forceinline__ uint32_t dpp_quad_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, J | J << 2 | J << 4 | J << 6, 0xf, 0xf, false);
+}
+
+__global__ __launch_bounds__(64 * SQW) void k_vp8l_select_q(SelArgs a, int64_t total) {
+  __shared__ uint32_t hist[SQW][128 * 64];
+  __shared__ double lut[SQ_LUT];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < SQ_LUT; i += 64 * SQW) lut[i] = a.lut[i];
+  uint32_t* const hg = hist[wave];
+#pragma unroll 4
+  for (int i = lane; i < 128 * 64 / 4; i += 64) reinterpret_cast<uint4*>(hg)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();  // the LUT; this wave's zeroed histograms
+  const int64_t t_idx = (int64_t)blockIdx.x * SQW + wave;
+  if (t_idx >= total) return;  // (no barrier below)
+  const int tile = (int)(t_idx % a.band_tiles) + a.ty0 * a.tiles_x;
+  const int img = (int)(t_idx / a.band_tiles);
+  const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+  const uint32_t* argb = a.argb + img * a.pitch;
+  const int ts = 1 << a.bits, w = a.width, h = a.height;
+  const int x0 = tx * ts, y0 = ty * ts;
+  const int x1 = min(x0 + ts, w), y1 = min(y0 + ts, h);
+  const int ystep = (y1 - y0 > 16) ? 2 : 1;
+  const int tw = x1 - x0, rows = (y1 - y0 + ystep - 1) / ystep;
+  const int m = lane >> 2, s = lane & 3;
+  const uint32_t ctl = m < 14 ? kPredCtl[m] : (uint32_t)C_BLACK;
+  const int shift = 24 - 8 * s;  // as the channel lane: alpha, red, green, blue
+  uint32_t* const myh = hg + lane;
+  auto add = [&](uint32_t r) {
+    const uint32_t b = (r >> shift) & 0xff;
+    __hip_atomic_fetch_add(myh + 64 * (b & 127), b < 128 ? 1u : 0x10000u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  for (int yy = 0; yy < rows; yy++) {
+    const int y = y0 + yy * ystep;
+    const uint32_t* row = argb + (int64_t)y * w;
+    const uint32_t* prev = row - w;
+    for (int cx = 0; cx < tw; cx += 4) {
+      // estimateEntropy's neighbours (encode_predictor.go:226-245): 0 outside
+      // the image, TR = T in the last column
+      const int xc = min(x0 + cx + s, x1 - 1);
+      const uint32_t p = row[xc], lraw = row[max(xc - 1, 0)];
+      uint32_t t = 0, tl = 0, tr = 0;
+      if (y > 0) {
+        const uint32_t traw = prev[xc], tlraw = prev[max(xc - 1, 0)], trraw = prev[min(xc + 1, w - 1)];
+        t = traw;
+        tl = xc > 0 ? tlraw : 0u;
+        tr = xc < w - 1 ? trraw : traw;
+      }
+      const uint32_t l = xc > 0 ? lraw : 0u;
+      const uint32_t res = sub_pixels(p, predict_ctl(ctl, l, t, tr, tl));
+      const uint32_t r0 = dpp_quad_u32<0>(res), r1 = dpp_quad_u32<1>(res), r2 = dpp_quad_u32<2>(res),
+                     r3 = dpp_quad_u32<3>(res);
+      const int nv = tw - cx;  // samples of this run inside the tile (wave-uniform)
+      add(r0);
+      if (nv > 1) add(r1);
+      if (nv > 2) add(r2);
+      if (nv > 3) add(r3);
+    }
+  }
+  wave_lds_sync();  // this wave's adds land before its reads
+  const uint32_t count = (uint32_t)(tw * rows);
+  double ce = lut[count];
+#pragma unroll 8
+  for (int k = 0; k < 128; k++) ce -= lut[myh[64 * k] & 0xffff];
+#pragma unroll 8
+  for (int k = 0; k < 128; k++) ce -= lut[myh[64 * k] >> 16];
+  const double e = (((0.0 + dpp_quad_f64(ce, 0)) + dpp_quad_f64(ce, 1)) + dpp_quad_f64(ce, 2)) + dpp_quad_f64(ce, 3);
+  const uint64_t eb = __builtin_bit_cast(uint64_t, e);
+  int best = 0;
+  double best_cost = 1.7976931348623157e308;
+  for (int mm = 0; mm < a.max_mode; mm++) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)eb, 4 * mm);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(eb >> 32), 4 * mm);
+    const double cm = __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+    if (cm < best_cost) {
+      best_cost = cm;
+      best = mm;
+    }
+  }
+  if (lane == 0) a.modes[(int64_t)img * a.tiles_x * a.tiles_y + tile] = ((uint32_t)best << 8) | ARGB_BLACK;
+}
+
 struct ResArgs {
   const uint32_t* argb;
   const uint32_t* modes;
@@ -696,8 +812,15 @@ extern "C" int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, 
   sa.band_tiles = tiles_x * (ty_end - ty_begin);
   const int64_t tiles = (int64_t)sa.band_tiles * n_images;
   WG_REQUIRE(tiles < (1ll << 31));
-  hipLaunchKernelGGL(k_vp8l_select, dim3((unsigned)tiles), dim3(64 * SEL_WAVES), 0, s, sa);
-  int rc = wg::check_launch("k_vp8l_select");
+  int rc;
+  static const int force_old = getenv("WG_VP8L_SELECT_OLD") ? 1 : 0;  // A/B against the 4-wave kernel
+  if (bits <= 5 && !force_old) {  // counts <= 512: one wave a tile, all modes in one pass
+    hipLaunchKernelGGL(k_vp8l_select_q, dim3((unsigned)((tiles + SQW - 1) / SQW)), dim3(64 * SQW), 0, s, sa, tiles);
+    rc = wg::check_launch("k_vp8l_select_q");
+  } else {
+    hipLaunchKernelGGL(k_vp8l_select, dim3((unsigned)tiles), dim3(64 * SEL_WAVES), 0, s, sa);
+    rc = wg::check_launch("k_vp8l_select");
+  }
   if (rc != WG_OK) return rc;
   ResArgs ra;
   ra.argb = argb;
