@@ -253,7 +253,8 @@ __device__ __forceinline__ int quantize(const int co[16], int16_t q[16], const S
     v = max(v, 0);
     const uint32_t iq = n == 0 ? h1.y : h0.y;
     const uint32_t bias = n == 0 ? h1.z : h0.z;
-    const int c = min((int)(((uint32_t)v * iq + bias) >> 17), 2047);
+    // (v < 2^16 and iq <= 2^15: the full-rate 24-bit multiplier is exact)
+    const int c = min((int)(((uint32_t)wg::mul_i24(v, (int)iq) + bias) >> 17), 2047);
     q[n] = (int16_t)(sign * c);
     if (c != 0) max_zz = max(max_zz, kRZig[n]);
   }
@@ -383,9 +384,10 @@ __device__ __forceinline__ bool trellis_prep2(const Tables& t, const int16_t* co
 #pragma unroll
   for (int j = 0; j < 2; j++) {
     c0[j] = max(abs(co_z[j]) + sh[j], 0);
-    L0raw[j] = (c0[j] * iquant[j]) >> 17;
+    // (c0 < 2^13, iquant <= 2^15: exact on the full-rate 24-bit multiplier)
+    L0raw[j] = (int)((uint32_t)wg::mul_i24(c0[j], iquant[j]) >> 17);
     L0[j] = min(L0raw[j], 2047);
-    thresh[j] = min((int)(((uint32_t)c0[j] * (uint32_t)iquant[j] + 65536u) >> 17), 2047);
+    thresh[j] = min((int)(((uint32_t)wg::mul_i24(c0[j], iquant[j]) + 65536u) >> 17), 2047);
     const int band = band_of(n0 + j + 1);
     lf0[j] = t.lfixed[L0[j]];
     lf1[j] = t.lfixed[min(L0[j] + 1, 2047)];
@@ -399,9 +401,10 @@ __device__ __forceinline__ bool trellis_prep2(const Tables& t, const int16_t* co
     const bool has0 = L0[j] > 0 && L0[j] <= thresh[j];
     const bool has1 = L0[j] + 1 <= 2047 && L0[j] + 1 <= thresh[j];
     const int w = w4096[j] * 4096;
-    const int e0 = c0[j] - L0[j] * quant[j], e1 = c0[j] - (L0[j] + 1) * quant[j];
-    const int64_t A0 = (int64_t)lf0[j] * lam16 + (int64_t)w * (e0 * e0 - c0[j] * c0[j]) + (has0 ? 0 : BIG);
-    const int64_t A1 = (int64_t)lf1[j] * lam16 + (int64_t)w * (e1 * e1 - c0[j] * c0[j]) + (has1 ? 0 : BIG);
+    const int e0 = c0[j] - wg::mul_i24(L0[j], quant[j]), e1 = e0 - quant[j];
+    const int c2 = wg::mul_i24(c0[j], c0[j]);
+    const int64_t A0 = (int64_t)lf0[j] * lam16 + (int64_t)w * (wg::mul_i24(e0, e0) - c2) + (has0 ? 0 : BIG);
+    const int64_t A1 = (int64_t)lf1[j] * lam16 + (int64_t)w * (wg::mul_i24(e1, e1) - c2) + (has1 ? 0 : BIG);
     const bool z = L0[j] == 0;
 #pragma unroll
     for (int pc = 0; pc < 3; pc++) {
@@ -638,7 +641,7 @@ __device__ __forceinline__ int quantize_one(int v, int b, const SQuant& sq) {
   const int4 h = b == 0 ? *reinterpret_cast<const int4*>(&sq.dc_quant) : *reinterpret_cast<const int4*>(&sq.quant);
   const int sign = v < 0 ? -1 : 1;
   const int a = max(abs(v) + sq.sharpen[b], 0);
-  const int c = min((int)(((uint32_t)a * (uint32_t)h.y + (uint32_t)h.z) >> 17), 2047);
+  const int c = min((int)(((uint32_t)wg::mul_i24(a, h.y) + (uint32_t)h.z) >> 17), 2047);
   return sign * c;
 }
 // max over the 16 lanes of a DPP row, in every lane of the row
@@ -724,9 +727,10 @@ __device__ __forceinline__ void select_i4_modes(int sse, int m, uint32_t eligibl
 template <typename QT>
 __device__ __forceinline__ void dequant(const QT& q, int dq[16], const SQuant& sq) {
   const int2 qq = make_int2(sq.quant, sq.dc_quant);
-  dq[0] = (int16_t)(lvl_at(q, 0) * qq.y);
+  // |level| <= 2047, quantisers < 2^10: full-rate 24-bit products
+  dq[0] = (int16_t)wg::mul_i24(lvl_at(q, 0), qq.y);
 #pragma unroll
-  for (int i = 1; i < 16; i++) dq[i] = (int16_t)(lvl_at(q, i) * qq.x);
+  for (int i = 1; i < 16; i++) dq[i] = (int16_t)wg::mul_i24(lvl_at(q, i), qq.x);
 }
 __device__ __forceinline__ void recon4(const int pred[16], const int dq[16], int rec[16]) {
 #pragma unroll

@@ -22,6 +22,32 @@ __device__ __forceinline__ int sclip1(int v) { return min(max(v, -128), 127); }
 __device__ __forceinline__ int sclip2(int v) { return min(max(v, -16), 15); }
 __device__ __forceinline__ int mul1(int a) { return a + __mulhi(a, 20091 << 16); }
 __device__ __forceinline__ int mul2(int a) { return a + __mulhi(a, (35468 - 65536) * 65536); }
+// The same on the full-rate 24-bit multiplier (v_mul_hi_i32 and v_mul_lo_u32
+// are quarter rate).  For |a| <= 2^16 (an int16 coefficient) a * 35468 fits
+// int32: one v_mul_i32_i24 and a shift.  For |a| < 2^23 (the inverse DCT's
+// second pass: at most ~2^17.4 from int16 inputs) the 48-bit product is
+// mul_i24 (low 32 bits) + mulhi_i24 (bits 32..47) and bits 16..47 come out
+// of one v_alignbit.  Both equal mul1 / mul2 (Go's 64-bit products) on those
+// ranges.
+// (as inline asm: hipcc turns __mul24 / __umul24 back into v_mul_lo_u32
+// wherever it loses the operands' range)
+__device__ __forceinline__ int mul_i24(int a, int c) {
+  int r;
+  asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(c), "v"(a));
+  return r;
+}
+__device__ __forceinline__ int mulhi_i24(int a, int c) {
+  int r;
+  asm("v_mul_hi_i32_i24 %0, %1, %2" : "=v"(r) : "v"(c), "v"(a));
+  return r;
+}
+__device__ __forceinline__ int mul1_16(int a) { return a + (mul_i24(a, 20091) >> 16); }
+__device__ __forceinline__ int mul2_16(int a) { return mul_i24(a, 35468) >> 16; }
+__device__ __forceinline__ int mul_sh16_24(int a, int c) {
+  return (int)__builtin_amdgcn_alignbit((uint32_t)mulhi_i24(a, c), (uint32_t)mul_i24(a, c), 16);
+}
+__device__ __forceinline__ int mul1_24(int a) { return a + mul_sh16_24(a, 20091); }
+__device__ __forceinline__ int mul2_24(int a) { return mul_sh16_24(a, 35468); }
 __device__ __forceinline__ int avg3(int a, int b, int c) { return (a + 2 * b + c + 2) >> 2; }
 __device__ __forceinline__ int avg2(int a, int b) { return (a + b + 1) >> 1; }
 __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
@@ -31,23 +57,24 @@ __device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)
 
 // ------------------------------------------------------------------------
 // Inverse 4x4 DCT, one output row per lane (transforms.go:37-136 / :265-366).
-// in[16] raster coefficients (registers), r = output row.  res[c] = (.. )>>3.
+// in[16] raster coefficients (registers; int16 values: every caller's
+// coefficients are int16), r = output row.  res[c] = (.. )>>3.
 __device__ __forceinline__ void idct_row(const int in[16], int r, int res[4]) {
   int t[4];
 #pragma unroll
   for (int c = 0; c < 4; c++) {
     const int a = in[c] + in[8 + c];
     const int b = in[c] - in[8 + c];
-    const int cc = mul2(in[4 + c]) - mul1(in[12 + c]);
-    const int d = mul1(in[4 + c]) + mul2(in[12 + c]);
+    const int cc = mul2_16(in[4 + c]) - mul1_16(in[12 + c]);
+    const int d = mul1_16(in[4 + c]) + mul2_16(in[12 + c]);
     const int s0 = (r == 0 || r == 3) ? a : b;
     const int s1 = (r == 0 || r == 3) ? d : cc;
     t[c] = (r < 2) ? s0 + s1 : s0 - s1;
   }
   const int dc = t[0] + 4;
   const int a = dc + t[2], b = dc - t[2];
-  const int cc = mul2(t[1]) - mul1(t[3]);
-  const int d = mul1(t[1]) + mul2(t[3]);
+  const int cc = mul2_24(t[1]) - mul1_24(t[3]);
+  const int d = mul1_24(t[1]) + mul2_24(t[3]);
   res[0] = (a + d) >> 3;
   res[1] = (b + cc) >> 3;
   res[2] = (b - cc) >> 3;
@@ -57,8 +84,8 @@ __device__ __forceinline__ void idct_row(const int in[16], int r, int res[4]) {
 // transformAC3 (transforms.go:170-193), one row: only in[0], in[1], in[4].
 __device__ __forceinline__ void ac3_row(int in0, int in1, int in4, int r, int res[4]) {
   const int a = in0 + 4;
-  const int c4 = mul2(in4), d4 = mul1(in4);
-  const int c1 = mul2(in1), d1 = mul1(in1);
+  const int c4 = mul2_16(in4), d4 = mul1_16(in4);
+  const int c1 = mul2_16(in1), d1 = mul1_16(in1);
   const int rv = (r == 0) ? a + d4 : (r == 1) ? a + c4 : (r == 2) ? a - c4 : a - d4;
   res[0] = (rv + d1) >> 3;
   res[1] = (rv + c1) >> 3;
