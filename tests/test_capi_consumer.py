@@ -136,4 +136,6 @@ def test_c_consumer_encode_sequence(cuda, tmp_path, w, h, kind, q, method):
     for f in frames.MB_ENC_DTYPE.names:
         if f != "pad":
             assert (got[f] == enc[f]).all(), f
-    assert (ry == ey).all() and (ru == eu).all() and (rv == ev).all()
+    # (the luma reconstruction is exported inside the image only, as the
+    # Python-path tests compare it: exportParallel's rows / columns)
+    assert (ry[:h, :w] == ey[:h, :w]).all() and (ru == eu).all() and (rv == ev).all()
