@@ -200,6 +200,9 @@ struct Shared {
 #ifndef WG_ENC_FUSE  // I4 candidates' FTransform in the pre-screen lanes (see the I4 RD)
 #define WG_ENC_FUSE 1
 #endif
+#ifndef WG_ENC_TAIL  // I4 candidates' rate from the DP, column-wise inverse DCT (see the I4 RD)
+#define WG_ENC_TAIL 1
+#endif
   TRec trec[6][16 + WG_ENC_TPAD];
   int64_t r0[16][3];       // the phase's level-0 trellis row (trellis_r0)
   int64_t eobl[16][2];     // the phase's terminal costs x lam16 (trellis_r0, WG_ENC_EOBT)
@@ -427,6 +430,23 @@ __device__ __forceinline__ int64_t quad_bcast(int64_t v) {
   const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)v >> 32), perm, 0xf, 0xf, false);
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
+// 4 x 4 transpose across a lane quad: lane r holds row r (v[c] = M[r][c])
+// and gets column r (v[k] = M[k][r]): two exchange stages, with the lane
+// r ^ 1 then r ^ 2, of the elements whose index differs from r in that bit
+template <int X>
+__device__ __forceinline__ void quad_xstage(int v[4]) {
+  constexpr int perm = X == 1 ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+  const int r = __lane_id() & 3;
+  int t[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) t[c] = __builtin_amdgcn_mov_dpp(v[c ^ X], perm, 0xf, 0xf, false);
+#pragma unroll
+  for (int c = 0; c < 4; c++) v[c] = ((c ^ r) & X) ? t[c] : v[c];
+}
+__device__ __forceinline__ void quad_transpose(int v[4]) {
+  quad_xstage<1>(v);
+  quad_xstage<2>(v);
+}
 // sum over the 4 lanes of a quad, in every lane of it
 __device__ __forceinline__ int quad_sum(int v) {
   v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
@@ -458,7 +478,7 @@ __device__ __forceinline__ int quad_bcast32(int v) {
 template <int FIRST, int CTX_TYPE>
 __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[3],
                                             const int64_t (*eobl)[2], const int16_t* l0s, int init_ctx, int lam16, int k,
-                                            int16_t* q, int* nz) {
+                                            int16_t* q, int* nz, int* rate = nullptr) {
   constexpr int64_t BIG = 1ll << 59;
   init_ctx = min(init_ctx, 2);
   const int e = min(k, 2);
@@ -565,17 +585,40 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   const uint32_t hist = second ? bh2 : bh1;  // 0 when no terminal beat the all-zero block
   // lane r: positions 4r .. 4r + 3
   const int r = k;
+  const uint32_t nzb = (hist | hist >> 1) & 0x55555555u;
+  const int nzc = nzb == 0 ? 0 : ((31 - __builtin_clz(nzb)) >> 1) + 1;
+  int mags[5];
+  {  // (the level before position 4r: the context of 4r's token)
+    const int n = max(4 * r - 1, 0);
+    const int code = r == 0 ? 0 : (int)((hist >> (2 * n)) & 3);
+    mags[0] = code == 0 ? 0 : (l0s[n] >> 3) + code - 1;
+  }
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int n = 4 * r + j;
     const int code = (int)((hist >> (2 * n)) & 3);
     const int ls = l0s[n];
     const int mag = code == 0 ? 0 : (ls >> 3) + code - 1;
+    mags[j + 1] = mag;
     q[zig_of(n)] = (int16_t)((ls & 4) ? -mag : mag);
   }
-  if (k == 0) {
-    const uint32_t nzb = (hist | hist >> 1) & 0x55555555u;
-    *nz = nzb == 0 ? 0 : ((31 - __builtin_clz(nzb)) >> 1) + 1;
+  if (k == 0) *nz = nzc;
+  if (rate) {
+    // TokenCostForCoeffs (encode_quant.go:154-223) of the chosen levels, lane r
+    // taking positions 4r .. 4r + 3 (FIRST 0 only: the I4 blocks), summed over
+    // the quad: the candidate's rate with no LDS round trip for its levels
+    int part = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int n = 4 * r + j, v = mags[j + 1];
+      const int ctx = n == 0 ? init_ctx : min(mags[j], 2);
+      const int band = band_of(n);
+      const int tokc = vc_of(t.vcost[CTX_TYPE * 8 + band][min(v, 67)], ctx) + t.lfixed[min(v, 2047)];
+      const int eobc = t.tok[CTX_TYPE * 8 + band].eob[ctx];
+      part += n < nzc ? tokc : (n == nzc ? eobc : 0);
+    }
+    part = quad_sum(part);
+    if (k == 0) *rate = part;
   }
 }
 
@@ -1795,7 +1838,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
 #if defined(WG_EXP_REP_DP)
       WG_REP_BEGIN(WG_EXP_REP_DP)
 #endif
-              trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl]);
+              trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl],
+                                WG_ENC_TAIL ? &s.cand_rate[sl] : nullptr);
 #if defined(WG_EXP_REP_DP)
       WG_REP_END
 #endif
@@ -1804,6 +1848,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
 #pragma unroll
               for (int i = 0; i < 16; i++) s.cand_q[sl][i] = 0;
               s.cand_nz[sl] = 0;
+              s.cand_rate[sl] = t.tok[3 * 8].eob[nz_ctx];  // EOB at position 0
             }
           }
           lds_sync();
@@ -1818,23 +1863,63 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           // streams interleave: lanes past the candidates repeat candidate 2's
           // work, or work on an unused slot, and nothing reads their results)
           const int qmode = min(pick3(qc, cm[0], cm[1], cm[2]) & 15, 9);
-          int16_t qv[16];
+          // (TAIL) the trellis DP leaves each candidate's rate in cand_rate, and
+          // the inverse DCT's vertical pass runs one column a quad lane,
+          // transposed across the quad by DPP: 4 levels and 4 products a lane
+          // instead of 16 and 16
+          constexpr bool TAIL = TRELLIS && WG_ENC_TAIL;
+          int16_t qv[TAIL ? 1 : 16];
           int qnz = 0, sse_r = 0, cnt = 0;
           uint32_t rec_row = 0;
-          int part;  // token cost, lane-parallel over positions: lane 8c + p takes positions 2p, 2p + 1
-          {
+          int part = 0;  // token cost, lane-parallel over positions: lane 8c + p takes positions 2p, 2p + 1
+          if constexpr (!TAIL) {
             const int c = min(hl >> 3, 2), n0 = 2 * (hl & 7), sl = half * 3 + c;
             const int nzc = s.cand_nz[sl];
             part = token_cost_pos<3>(t, s.cand_q[sl], n0, nzc, nz_ctx, 0) + token_cost_pos<3>(t, s.cand_q[sl], n0 + 1, nzc, nz_ctx, 0);
           }
           {
             CSTAMP(1);
-#pragma unroll
-            for (int i = 0; i < 16; i++) qv[i] = s.cand_q[qsl][i];
+            int res[4], pr[4], sr[4], rr[4];
             qnz = s.cand_nz[qsl];
-            int dq[16], res[4], pr[4], sr[4], rr[4];
-            dequant(qv, dq, sg.y1);
-            idct_row(dq, qr, res);
+            if constexpr (TAIL) {
+              // column qr: levels qr, 4 + qr, 8 + qr, 12 + qr (raster)
+              const int16_t* cq = s.cand_q[qsl];
+              int col[4];
+#pragma unroll
+              for (int j = 0; j < 4; j++) col[j] = cq[4 * j + qr];
+              const int2 qq = make_int2(sg.y1.quant, sg.y1.dc_quant);
+              int dc[4];
+#pragma unroll
+              for (int j = 0; j < 4; j++) dc[j] = (int16_t)wg::mul_i24(col[j], (j == 0 && qr == 0) ? qq.y : qq.x);
+              cnt = (col[0] != 0 && qr != 0) + (col[1] != 0) + (col[2] != 0) + (col[3] != 0);
+              cnt = quad_sum(cnt);  // levels 1..15 that are nonzero
+              // the vertical pass of transforms.go:37-136 for column qr: rows 0..3
+              int tv[4];
+              {
+                const int a = dc[0] + dc[2], b = dc[0] - dc[2];
+                const int cc = mul2_16(dc[1]) - mul1_16(dc[3]);
+                const int d = mul1_16(dc[1]) + mul2_16(dc[3]);
+                tv[0] = a + d;
+                tv[1] = b + cc;
+                tv[2] = b - cc;
+                tv[3] = a - d;
+              }
+              quad_transpose(tv);  // lane qr: row qr's four column outputs
+              const int d0 = tv[0] + 4;
+              const int a = d0 + tv[2], b = d0 - tv[2];
+              const int cc = mul2_24(tv[1]) - mul1_24(tv[3]);
+              const int d = mul1_24(tv[1]) + mul2_24(tv[3]);
+              res[0] = (a + d) >> 3;
+              res[1] = (b + cc) >> 3;
+              res[2] = (b - cc) >> 3;
+              res[3] = (a - d) >> 3;
+            } else {
+              int dq[16];
+#pragma unroll
+              for (int i = 0; i < 16; i++) qv[i] = s.cand_q[qsl][i];
+              dequant(qv, dq, sg.y1);
+              idct_row(dq, qr, res);
+            }
             const uint32_t cw = reinterpret_cast<const uint32_t*>(t.pcode[qmode])[qr];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -1859,8 +1944,10 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               reinterpret_cast<uint2*>(th)[0] = make_uint2(pack16(tr.x, tr.y), pack16(tr.z, tr.w));  // |values| <= 1020
               reinterpret_cast<uint2*>(th)[1] = make_uint2(pack16(ts.x, ts.y), pack16(ts.z, ts.w));
             }
+            if constexpr (!TAIL) {
 #pragma unroll
-            for (int i = 1; i < 16; i++) cnt += qv[i] != 0;
+              for (int i = 1; i < 16; i++) cnt += qv[i] != 0;
+            }
           }
           lds_sync();
           int wrec = 0, wsrc = 0;  // weighted column sums of column qr
@@ -1891,9 +1978,11 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           // the token cost summed over each candidate's 8 lanes: candidate c's
           // rate sits in lane 32 * half + 8c; read the six with
           // v_readlane (wave-uniform lanes) instead of LDS permutes
-          part = group_sum_first<8>(part);
           int tok_rate;
-          {
+          if constexpr (TAIL) {
+            tok_rate = s.cand_rate[qsl];
+          } else {
+            part = group_sum_first<8>(part);
             const int r00 = __builtin_amdgcn_readlane(part, 0), r01 = __builtin_amdgcn_readlane(part, 8);
             const int r02 = __builtin_amdgcn_readlane(part, 16), r10 = __builtin_amdgcn_readlane(part, 32);
             const int r11 = __builtin_amdgcn_readlane(part, 40), r12 = __builtin_amdgcn_readlane(part, 48);
