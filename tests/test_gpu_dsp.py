@@ -221,13 +221,15 @@ def test_block_wrappers_reject_out_of_buffer_footprints(cuda):
     check); the same call in bounds runs."""
     bufs = torch.zeros((4, O.YUV_SIZE), dtype=torch.uint8, device=cuda)
     co = torch.zeros((4, 64), dtype=torch.int16, device=cuda)
+    co16 = torch.zeros((4, 16), dtype=torch.int16, device=cuda)
+    co32 = torch.zeros((4, 32), dtype=torch.int16, device=cuda)
     bad = [
         lambda: dsp.PredLuma16(0, bufs, O.YOFF - O.BPS),               # top-left corner at -1
         lambda: dsp.PredLuma4(0, bufs, torch.tensor([O.YOFF, O.YUV_SIZE - 8])),  # one instance past the end
         lambda: dsp.PredChroma8(0, bufs, O.YUV_SIZE - 4 * O.BPS),
         lambda: dsp.Transform(co, bufs, True, O.YUV_SIZE - 2 * O.BPS),
-        lambda: dsp.TransformUV(co[:, :16], bufs, O.UOFF),             # 16 coefficients for 4 blocks
-        lambda: dsp.ITransform(bufs, co[:, :32], bufs, True, O.YUV_SIZE - 8, 0),
+        lambda: dsp.TransformUV(co16, bufs, O.UOFF),             # 16 coefficients for 4 blocks
+        lambda: dsp.ITransform(bufs, co32, bufs, True, O.YUV_SIZE - 8, 0),
         lambda: dsp.SSE16x16(bufs, bufs, O.YUV_SIZE - 15 * O.BPS, 0),
         lambda: dsp.filter_edge("VFilter16", bufs, O.YOFF, O.BPS, 20, 10, 1),       # 4 rows above row 0 of Y
         lambda: dsp.filter_edge("HFilter8i", bufs, O.UOFF, O.BPS, 20, 10, 1, uv_delta=O.YUV_SIZE),
