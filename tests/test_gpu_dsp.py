@@ -233,7 +233,7 @@ def test_block_wrappers_reject_out_of_buffer_footprints(cuda):
         lambda: dsp.SSE16x16(bufs, bufs, O.YUV_SIZE - 15 * O.BPS, 0),
         lambda: dsp.filter_edge("VFilter16", bufs, O.YOFF, O.BPS, 20, 10, 1),       # 4 rows above row 0 of Y
         lambda: dsp.filter_edge("HFilter8i", bufs, O.UOFF, O.BPS, 20, 10, 1, uv_delta=O.YUV_SIZE),
-        lambda: dsp.SSIMGet(bufs, bufs, 120),
+        lambda: dsp.SSIMGet(bufs, bufs, 140),                          # 6 rows of 140 past 832 B
     ]
     for f in bad:
         with pytest.raises(dsp.InvalidArgument) as e:

@@ -7,6 +7,9 @@ OUT=gpurun_out/prof
 mkdir -p $OUT
 ARGS="--steps ${STEPS:-5} --warmup 2 --no-cpu-baseline ${EXTRA:-}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
+# isolated launches (one batch at a time, as the bench line's stage_ms_isolated /
+# roofline.achieved time them): AverageNs of k_encode_rows is the roofline's launch
+BATCHES=64 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_iso -o run -- python3 tools/enc_scaling.py > $OUT/trace_iso.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1
 python3 tools/pmc_summary.py --json $OUT/pmc_traffic.json $(find $OUT/fetch $OUT/write -name "*counter_collection.csv")
