@@ -203,6 +203,9 @@ struct Shared {
 #ifndef WG_ENC_TAIL  // I4 candidates' rate from the DP, column-wise inverse DCT (see the I4 RD)
 #define WG_ENC_TAIL 1
 #endif
+#ifndef WG_ENC_DPAHEAD  // positions the trellis DP loads ahead (1 or 2)
+#define WG_ENC_DPAHEAD 2
+#endif
   TRec trec[6][16 + WG_ENC_TPAD];
   int64_t r0[16][3];       // the phase's level-0 trellis row (trellis_r0)
   int64_t eobl[16][2];     // the phase's terminal costs x lam16 (trellis_r0, WG_ENC_EOBT)
@@ -513,6 +516,19 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   // and pinned by the asm below, so no LDS round trip sits on the chain.
   int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
   int cls_raw = l0s[FIRST];
+#if WG_ENC_EOBT && WG_ENC_DPAHEAD == 2
+  // (two positions ahead: the LDS latency under the other waves' traffic
+  // outlasted one position of the chain)
+  int64_t y0 = 0, y1 = 0, y2 = 0, yeob = 0;
+  int ycls = 0;
+  if (FIRST < 15) {
+    y0 = mine[(FIRST + 1) * STRIDE];
+    y1 = mine[(FIRST + 1) * STRIDE + 1];
+    y2 = mine[(FIRST + 1) * STRIDE + 2];
+    ycls = l0s[FIRST + 1];
+    yeob = eobq[2 * (FIRST + 1)];
+  }
+#endif
 #pragma unroll
   for (int n = FIRST; n < 16; n++) {
     int64_t nx0 = 0, nx1 = 0, nx2 = 0;
@@ -522,6 +538,15 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
 #else
     uint32_t neob = 0;
 #endif
+#if WG_ENC_EOBT && WG_ENC_DPAHEAD == 2
+    if (n < 14) {
+      nx0 = mine[(n + 2) * STRIDE];
+      nx1 = mine[(n + 2) * STRIDE + 1];
+      nx2 = mine[(n + 2) * STRIDE + 2];
+      ncls = l0s[n + 2];
+      neob = eobq[2 * (n + 2)];
+    }
+#else
     if (n < 15) {
       nx0 = mine[(n + 1) * STRIDE];
       nx1 = mine[(n + 1) * STRIDE + 1];
@@ -533,15 +558,29 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
       if (n + 1 < 15) neob = eobp[kBand[n + 2] * TSTR];
 #endif
     }
+#endif
     asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
     const int64_t c0 = ps0 + x0, c1 = ps1 + x1, c2 = ps2 + x2;
     const bool two = (cls_raw & 2) != 0;  // class 2: L0 >= 2
     const auto eob_n = eob_raw;
+#if WG_ENC_EOBT && WG_ENC_DPAHEAD == 2
+    x0 = y0;
+    x1 = y1;
+    x2 = y2;
+    cls_raw = ycls;
+    eob_raw = yeob;
+    y0 = nx0;
+    y1 = nx1;
+    y2 = nx2;
+    ycls = ncls;
+    yeob = neob;
+#else
     x0 = nx0;
     x1 = nx1;
     x2 = nx2;
     cls_raw = ncls;
     eob_raw = neob;
+#endif
     const int64_t m01 = c1 < c0 ? c1 : c0;
     const int64_t m = c2 < m01 ? c2 : m01;
     const uint32_t idx = (uint32_t)m & 15, pc = idx >> psh;

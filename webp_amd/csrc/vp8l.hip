@@ -346,8 +346,14 @@ __device__ __forceinline__ uint32_t dpp_quad_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, J | J << 2 | J << 4 | J << 6, 0xf, 0xf, false);
 }
 
+constexpr int SQ_SW = 34;  // staged tile row: columns x0 - 1 .. x0 + 32
 __global__ __launch_bounds__(64 * SQW) void k_vp8l_select_q(SelArgs a, int64_t total) {
   __shared__ uint32_t hist[SQW][128 * 64];
+  // the tile and its border, staged with estimateEntropy's edge values
+  // already in place (0 left of column 0 and above row 0, the last pixel
+  // repeated right of the last column: TR = T there), so the sample loop
+  // reads five LDS words and has no branches
+  __shared__ uint32_t stile[SQW][33 * SQ_SW];
   __shared__ double lut[SQ_LUT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < SQ_LUT; i += 64 * SQW) lut[i] = a.lut[i];
@@ -366,6 +372,19 @@ __global__ __launch_bounds__(64 * SQW) void k_vp8l_select_q(SelArgs a, int64_t t
   const int x1 = min(x0 + ts, w), y1 = min(y0 + ts, h);
   const int ystep = (y1 - y0 > 16) ? 2 : 1;
   const int tw = x1 - x0, rows = (y1 - y0 + ystep - 1) / ystep;
+  // stage rows y0 - 1 .. y1 - 1 (only those with y0 - 1 <= y < y1 are read)
+  uint32_t* const st = stile[wave];
+  {
+    const int srows = y1 - y0 + 1, scols = x1 - x0 + 2;
+    for (int i = lane; i < srows * scols; i += 64) {
+      const int rr = i / scols, cc = i - rr * scols;
+      const int y = y0 - 1 + rr, x = x0 - 1 + cc;
+      uint32_t v = 0;
+      if (y >= 0 && x >= 0) v = argb[(int64_t)y * w + min(x, w - 1)];
+      st[rr * SQ_SW + cc] = v;
+    }
+  }
+  wave_lds_sync();
   const int m = lane >> 2, s = lane & 3;
   const uint32_t ctl = m < 14 ? kPredCtl[m] : (uint32_t)C_BLACK;
   const int shift = 24 - 8 * s;  // as the channel lane: alpha, red, green, blue
@@ -376,22 +395,15 @@ __global__ __launch_bounds__(64 * SQW) void k_vp8l_select_q(SelArgs a, int64_t t
                            __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   for (int yy = 0; yy < rows; yy++) {
-    const int y = y0 + yy * ystep;
-    const uint32_t* row = argb + (int64_t)y * w;
-    const uint32_t* prev = row - w;
-    for (int cx = 0; cx < tw; cx += 4) {
+    const uint32_t* srow = st + (1 + yy * ystep) * SQ_SW;  // staged row y0 + yy * ystep
+    const uint32_t* sprev = srow - SQ_SW;
+#pragma unroll
+    for (int cx = 0; cx < 32; cx += 4) {
+      if (cx >= tw) continue;  // (wave-uniform)
       // estimateEntropy's neighbours (encode_predictor.go:226-245): 0 outside
-      // the image, TR = T in the last column
-      const int xc = min(x0 + cx + s, x1 - 1);
-      const uint32_t p = row[xc], lraw = row[max(xc - 1, 0)];
-      uint32_t t = 0, tl = 0, tr = 0;
-      if (y > 0) {
-        const uint32_t traw = prev[xc], tlraw = prev[max(xc - 1, 0)], trraw = prev[min(xc + 1, w - 1)];
-        t = traw;
-        tl = xc > 0 ? tlraw : 0u;
-        tr = xc < w - 1 ? trraw : traw;
-      }
-      const uint32_t l = xc > 0 ? lraw : 0u;
+      // the image, TR = T in the last column (staged that way)
+      const int c = min(cx + s, tw - 1) + 1;  // staged column of x
+      const uint32_t p = srow[c], l = srow[c - 1], t = sprev[c], tl = sprev[c - 1], tr = sprev[c + 1];
       const uint32_t res = sub_pixels(p, predict_ctl(ctl, l, t, tr, tl));
       const uint32_t r0 = dpp_quad_u32<0>(res), r1 = dpp_quad_u32<1>(res), r2 = dpp_quad_u32<2>(res),
                      r3 = dpp_quad_u32<3>(res);
