@@ -23,3 +23,18 @@ def cuda():
     import webp_amd
     webp_amd.device_check()
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _gpu_drain(request):
+    """After every GPU test, wait for ALL the device's work (every stream)
+    and surface any asynchronous kernel fault there: a fault is then reported
+    as the teardown error of the test that launched the kernel, not by the
+    next test's first HIP call (a fault reported in
+    test_gpu_rescale_large whose kernel was never identified)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()

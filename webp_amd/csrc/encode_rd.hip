@@ -203,8 +203,8 @@ struct Shared {
 #ifndef WG_ENC_TAIL  // I4 candidates' rate from the DP, column-wise inverse DCT (see the I4 RD)
 #define WG_ENC_TAIL 1
 #endif
-#ifndef WG_ENC_DPAHEAD  // positions the trellis DP loads ahead (1 or 2)
-#define WG_ENC_DPAHEAD 2
+#ifndef WG_ENC_DPAHEAD  // positions the trellis DP loads ahead (1 or 2: measured equal, 1 kept)
+#define WG_ENC_DPAHEAD 1
 #endif
   TRec trec[6][16 + WG_ENC_TPAD];
   int64_t r0[16][3];       // the phase's level-0 trellis row (trellis_r0)
@@ -1908,6 +1908,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           // instead of 16 and 16
           constexpr bool TAIL = TRELLIS && WG_ENC_TAIL;
           int16_t qv[TAIL ? 1 : 16];
+          int tcol[4];  // (TAIL) column qr of the row pass: reconstruction | source << 16
           int qnz = 0, sse_r = 0, cnt = 0;
           uint32_t rec_row = 0;
           int part = 0;  // token cost, lane-parallel over positions: lane 8c + p takes positions 2p, 2p + 1
@@ -1979,7 +1980,16 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               const int a0 = sr[0] + sr[2], a1 = sr[1] + sr[3], a2 = sr[1] - sr[3], a3 = sr[0] - sr[2];
               ts = make_int4(a0 + a1, a3 + a2, a3 - a2, a0 - a1);
             }
-            if (qact) {
+            if constexpr (TAIL) {
+              // the column pass gets its inputs by a quad transpose of the row
+              // pass results, reconstruction and source packed in one word
+              // (|values| <= 1020)
+              int pk[4] = {(int)pack16(tr.x, ts.x), (int)pack16(tr.y, ts.y), (int)pack16(tr.z, ts.z),
+                           (int)pack16(tr.w, ts.w)};
+              quad_transpose(pk);
+#pragma unroll
+              for (int j = 0; j < 4; j++) tcol[j] = pk[j];
+            } else if (qact) {
               reinterpret_cast<uint2*>(th)[0] = make_uint2(pack16(tr.x, tr.y), pack16(tr.z, tr.w));  // |values| <= 1020
               reinterpret_cast<uint2*>(th)[1] = make_uint2(pack16(ts.x, ts.y), pack16(ts.z, ts.w));
             }
@@ -1988,15 +1998,23 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               for (int i = 1; i < 16; i++) cnt += qv[i] != 0;
             }
           }
-          lds_sync();
+          if constexpr (!TAIL) lds_sync();
           int wrec = 0, wsrc = 0;  // weighted column sums of column qr
           {
-            const int16_t* tx = &s.co_buf[2 * qsl][0];
             int cr[4], cs[4];
+            if constexpr (TAIL) {
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-              cr[j] = tx[8 * j + qr];
-              cs[j] = tx[8 * j + 4 + qr];
+              for (int j = 0; j < 4; j++) {
+                cr[j] = (int)(int16_t)(tcol[j] & 0xffff);
+                cs[j] = tcol[j] >> 16;
+              }
+            } else {
+              const int16_t* tx = &s.co_buf[2 * qsl][0];
+#pragma unroll
+              for (int j = 0; j < 4; j++) {
+                cr[j] = tx[8 * j + qr];
+                cs[j] = tx[8 * j + 4 + qr];
+              }
             }
             // kWeightY (ssim.go:257) column qr, one byte per row
             const uint32_t wcol = qr == 0 ? 0x09142026u : (qr == 1 ? 0x07111c20u : (qr == 2 ? 0x040a1114u : 0x02040709u));
