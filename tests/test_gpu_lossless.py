@@ -31,6 +31,18 @@ def test_residual_image_matches_oracle(cuda, bits, quality):
         assert (gr == er).all(), name
 
 
+@pytest.mark.parametrize("variant", ["0", "1", "2"])
+@pytest.mark.parametrize("bits", [2, 3, 5])
+def test_select_variants_agree(cuda, monkeypatch, bits, variant):
+    """The three tile-selection kernels (WG_VP8L_SELECT: 0 = a mode a wave,
+    1 = a wave a tile, 2 = two waves a tile, the default) on ragged tiles."""
+    monkeypatch.setenv("WG_VP8L_SELECT", variant)
+    img = argb_of(synth.blobs_rgba(203, 77, seed=11, alpha=True))
+    em, er = O.vp8l_residual_image(img, bits, 75)
+    gm, gr = gpu_residual(img, bits, 75)
+    assert (gm == em).all() and (gr == er).all()
+
+
 @pytest.mark.parametrize("bits", [6, 7, 9])
 def test_large_tiles(cuda, bits):
     """Subsampled rows (tile height > 16) and, at bits 9, histogram counts

@@ -203,6 +203,17 @@ struct Shared {
 #ifndef WG_ENC_TAIL  // I4 candidates' rate from the DP, column-wise inverse DCT (see the I4 RD)
 #define WG_ENC_TAIL 1
 #endif
+// (WG_ENC_NLAST) the DP stops after the last position of the round at which
+// any of its blocks has a non-zero level candidate: past it every state but
+// context 0's is invalid, so no terminal (EOB from context 1 / 2) can still
+// win and the histories only gain zero levels -- the result is the same as
+// walking to position 15, as the reference does
+#ifndef WG_ENC_NLAST
+#define WG_ENC_NLAST 1
+#endif
+#ifndef WG_ENC_HOIST  // I4 candidates' prediction / source rows read before the trellis (see the I4 RD)
+#define WG_ENC_HOIST 1
+#endif
 #ifndef WG_ENC_DPAHEAD  // positions the trellis DP loads ahead (1 or 2: measured equal, 1 kept)
 #define WG_ENC_DPAHEAD 1
 #endif
@@ -339,6 +350,17 @@ __device__ __forceinline__ int token_cost(const Tables& t, const QT& q, int nz_c
 #ifndef WG_ENC_EOBT
 #define WG_ENC_EOBT 1
 #endif
+// (WG_ENC_TWO, needs WG_ENC_EOBT) class-2 positions (L0 >= 2, both non-zero
+// levels end in context 2) are folded into the records: R1 = BIG, R2 =
+// min(R1, R2) per predecessor (the keys of L0 and L0 + 1 differ in their idx
+// bit, so the min is the reference's first strict minimum), and the DP keeps
+// no class test: every lane's own minimum is its context's new state
+#ifndef WG_ENC_TWO
+#define WG_ENC_TWO 1
+#endif
+#if WG_ENC_TWO && !WG_ENC_EOBT
+#error "WG_ENC_TWO needs WG_ENC_EOBT"
+#endif
 // (WG_ENC_EOBT) lanes 48 + n also write the phase's terminal costs: EOB after
 // position n from end context 1 / 2, x lam16 (0 after position 15), plus n
 // (the key's position field, see trellis_dp4), which the DP adds to a state
@@ -372,7 +394,7 @@ __device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16,
 // report no level.
 template <int CTX_TYPE, int FIRST>
 __device__ __forceinline__ bool trellis_prep2(const Tables& t, const int16_t* co, int n0, const SQuant& sq, int lam16,
-                                              TRec out[2], int l0s[2]) {
+                                              TRec out[2], int l0s[2], bool* cap = nullptr) {
   constexpr int64_t BIG = 1ll << 59;
   int co_z[2], sh[2], quant[2], iquant[2], w4096[2];
 #pragma unroll
@@ -412,16 +434,27 @@ __device__ __forceinline__ bool trellis_prep2(const Tables& t, const int16_t* co
     const int64_t A0 = (int64_t)lf0[j] * lam16 + (int64_t)w * (wg::mul_i24(e0, e0) - c2) + (has0 ? 0 : BIG);
     const int64_t A1 = (int64_t)lf1[j] * lam16 + (int64_t)w * (wg::mul_i24(e1, e1) - c2) + (has1 ? 0 : BIG);
     const bool z = L0[j] == 0;
+#if WG_ENC_TWO
+    const bool two = L0[j] >= 2;
+#endif
 #pragma unroll
     for (int pc = 0; pc < 3; pc++) {
       const int64_t r1 = (int64_t)vc_of(v0[j], pc) * lam16 + A0 + 2 * pc;
       const int64_t r2 = (int64_t)vc_of(v1[j], pc) * lam16 + A1 + 2 * pc + 1;
+#if WG_ENC_TWO
+      out[j].x[0][pc] = z ? r2 : (two ? BIG : r1);
+      out[j].x[1][pc] = z ? BIG : (two && r1 < r2 ? r1 : r2);
+#else
       out[j].x[0][pc] = z ? r2 : r1;
       out[j].x[1][pc] = z ? BIG : r2;
+#endif
     }
     l0s[j] = L0[j] << 3 | (co_z[j] < 0 ? 4 : 0) | min(L0[j], 2);
     pnz |= L0raw[j] > 0 && n0 + j >= FIRST;
   }
+  // (WG_ENC_NLAST) a non-zero level is a candidate at either position
+  // (has0 || has1 <=> thresh >= 1; thresh is 0 below FIRST)
+  if (cap) *cap = thresh[0] >= 1 || thresh[1] >= 1;
   return pnz;
 }
 
@@ -461,6 +494,17 @@ __device__ __forceinline__ int quad_bcast32(int v) {
   return __builtin_amdgcn_mov_dpp(v, J | J << 2 | J << 4 | J << 6, 0xf, 0xf, false);
 }
 
+// The last position to walk (WG_ENC_NLAST): cap_mask = ballot of the prep
+// lanes' "non-zero candidate at position 2pp or 2pp + 1", pp = lane & 7 (each
+// byte: one block's eight pairs).  Wave-uniform.
+__device__ __forceinline__ int nlast_of(uint64_t cap_mask) {
+  uint64_t m = cap_mask | cap_mask >> 32;
+  m |= m >> 16;
+  m |= m >> 8;
+  const uint32_t b = (uint32_t)m & 0xff;
+  return b ? 2 * (31 - __builtin_clz(b)) + 1 : 15;
+}
+
 // The trellis DP on a quad of lanes.  trellis_prep routes the transitions
 // by the end context they reach (TRec rows R0 / R1 / R2), so lane k of the
 // quad (e = min(k, 2); lane 3 shadows lane 2) takes the minimum of the three
@@ -481,7 +525,7 @@ __device__ __forceinline__ int quad_bcast32(int v) {
 template <int FIRST, int CTX_TYPE>
 __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[3],
                                             const int64_t (*eobl)[2], const int16_t* l0s, int init_ctx, int lam16, int k,
-                                            int16_t* q, int* nz, int* rate = nullptr) {
+                                            int16_t* q, int* nz, int* rate = nullptr, int nlast = 15) {
   constexpr int64_t BIG = 1ll << 59;
   init_ctx = min(init_ctx, 2);
   const int e = min(k, 2);
@@ -515,7 +559,7 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   // Position n's row, class and EOB cost are loaded during position n - 1
   // and pinned by the asm below, so no LDS round trip sits on the chain.
   int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
-  int cls_raw = l0s[FIRST];
+  int cls_raw = WG_ENC_TWO ? 0 : l0s[FIRST];
 #if WG_ENC_EOBT && WG_ENC_DPAHEAD == 2
   // (two positions ahead: the LDS latency under the other waves' traffic
   // outlasted one position of the chain)
@@ -525,12 +569,13 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
     y0 = mine[(FIRST + 1) * STRIDE];
     y1 = mine[(FIRST + 1) * STRIDE + 1];
     y2 = mine[(FIRST + 1) * STRIDE + 2];
-    ycls = l0s[FIRST + 1];
+    ycls = WG_ENC_TWO ? 0 : l0s[FIRST + 1];
     yeob = eobq[2 * (FIRST + 1)];
   }
 #endif
 #pragma unroll
   for (int n = FIRST; n < 16; n++) {
+    if (WG_ENC_NLAST && n > nlast) break;  // (wave-uniform)
     int64_t nx0 = 0, nx1 = 0, nx2 = 0;
     int ncls = 0;
 #if WG_ENC_EOBT
@@ -543,7 +588,7 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
       nx0 = mine[(n + 2) * STRIDE];
       nx1 = mine[(n + 2) * STRIDE + 1];
       nx2 = mine[(n + 2) * STRIDE + 2];
-      ncls = l0s[n + 2];
+      ncls = WG_ENC_TWO ? 0 : l0s[n + 2];
       neob = eobq[2 * (n + 2)];
     }
 #else
@@ -551,7 +596,7 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
       nx0 = mine[(n + 1) * STRIDE];
       nx1 = mine[(n + 1) * STRIDE + 1];
       nx2 = mine[(n + 1) * STRIDE + 2];
-      ncls = l0s[n + 1];
+      ncls = WG_ENC_TWO ? 0 : l0s[n + 1];
 #if WG_ENC_EOBT
       neob = eobq[2 * (n + 1)];
 #else
@@ -586,6 +631,23 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
     const uint32_t idx = (uint32_t)m & 15, pc = idx >> psh;
     const uint32_t code = (idx & (uint32_t)psh) + (uint32_t)psh;  // R0: 0; R1 / R2: 1 (L0) or 2 (L0 + 1)
     const uint32_t hm = (pc == 0 ? h0 : (pc == 1 ? h1 : h2)) | code << (2 * n);
+#if WG_ENC_TWO
+    (void)two;
+    // the new states, masked to the score before the broadcasts; lane 1's own
+    // state is context 1's, lanes 2 and 3's context 2's: the terminal of the
+    // lane's context (lane 0's is unused) needs no select
+    const int64_t mm = m & ~15ll;
+    ps0 = quad_bcast<0>(mm);
+    ps1 = quad_bcast<1>(mm);
+    ps2 = quad_bcast<2>(mm);
+    h0 = quad_bcast32<0>(hm);
+    h1 = quad_bcast32<1>(hm);
+    h2 = quad_bcast32<2>(hm);
+    const int64_t eobs = mm + eob_n;
+    const bool w = eobs < best_terminal;
+    best_terminal = w ? eobs : best_terminal;
+    best_h = w ? hm : best_h;
+#else
     const int64_t M0 = quad_bcast<0>(m), M1 = quad_bcast<1>(m), M2 = quad_bcast<2>(m);
     const uint32_t H0 = quad_bcast32<0>(hm), H1 = quad_bcast32<1>(hm), H2 = quad_bcast32<2>(hm);
     const bool lt = M1 < M2;
@@ -610,6 +672,7 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
     best_n = w ? n : best_n;
 #endif
     best_h = w ? (tctx == 2 ? h2 : h1) : best_h;
+#endif
   }
   // the first strict minimum over (position, context 1 then 2), in every lane
   const int64_t bt1 = quad_bcast<1>(best_terminal), bt2 = quad_bcast<2>(best_terminal);
@@ -1005,11 +1068,13 @@ __device__ __forceinline__ void pred4_values(const uint8_t* buf, int off, int i,
     v[48 + p] = (uint8_t)clip8(d[-1 + y * BPS] + d[x - BPS] - d[-1 - BPS]);
   }
 }
-__device__ __forceinline__ void pred4_lut(const uint8_t* code, const uint8_t* v, int pred[16]) {
-  const uint4 c = *reinterpret_cast<const uint4*>(code);
+__device__ __forceinline__ void pred4_lut(const uint4 c, const uint8_t* v, int pred[16]) {
   const uint32_t w[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
   for (int p = 0; p < 16; p++) pred[p] = v[(w[p >> 2] >> (8 * (p & 3))) & 0xff];
+}
+__device__ __forceinline__ void pred4_lut(const uint8_t* code, const uint8_t* v, int pred[16]) {
+  pred4_lut(*reinterpret_cast<const uint4*>(code), v, pred);
 }
 __device__ __forceinline__ int check_mode(int mbx, int mby, int mode) {
   const int edge = (mbx == 0) ? ((mby == 0) ? 6 : 5) : ((mby == 0) ? 4 : 0);
@@ -1788,11 +1853,13 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
 #if defined(WG_EXP_REP_PRE)
       WG_REP_BEGIN(WG_EXP_REP_PRE)
 #endif
+          // (the lane's mode code read first: in flight while the table is built)
+          const uint4 pcw = *reinterpret_cast<const uint4*>(t.pcode[min(hl, 9)]);
           pred4_values(s.yout2, off, hl, s.pv[half]);
           lds_sync();
           if (bvalid && hl < 10) {
             int pred[16];
-            pred4_lut(t.pcode[hl], s.pv[half], pred);
+            pred4_lut(pcw, s.pv[half], pred);
             sse_lane = sse16(src, pred);
             if constexpr (FUSE) fdct(src, pred, pco);
           }
@@ -1810,6 +1877,20 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           const bool cand = bvalid && hl < K;
           const int mode = pick3(hl, cm[0], cm[1], cm[2]);
           const int slot = half * 3 + min(hl, 2);  // candidate slot in the trellis / level buffers
+          // (HOIST) the reconstruction quad's prediction and source rows (lane
+          // 4c + r: row r of candidate c), read now: the reads overlap the
+          // trellis instead of sitting on the chain after it
+          const int qc = min(hl >> 2, 2), qr = hl & 3, qsl = half * 3 + qc;
+          const int qmode = min(pick3(qc, cm[0], cm[1], cm[2]) & 15, 9);
+          uint32_t pred_row = 0, src_row = 0;
+          if constexpr (WG_ENC_HOIST) {
+            const uint32_t cw = reinterpret_cast<const uint32_t*>(t.pcode[qmode])[qr];
+            int pr[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) pr[k] = s.pv[half][(cw >> (8 * k)) & 0xff];
+            pred_row = pack4(pr[0], pr[1], pr[2], pr[3]);
+            src_row = *reinterpret_cast<const uint32_t*>(s.yin + off + qr * BPS);
+          }
           SSTAMP(1);
           // candidates: prediction + transform (lane hl = candidate hl)
 #if defined(WG_EXP_REP_CAND)
@@ -1844,7 +1925,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           if constexpr (TRELLIS) {
           // trellis positions: lane (candidate c, pair pp) prepares positions 2pp, 2pp + 1
           const int lam16 = sg.tlambda_i4 * 16;
-          bool pnz = false;
+          bool pnz = false, pcap = false;
 #if defined(WG_EXP_REP_PREP)
       WG_REP_BEGIN(WG_EXP_REP_PREP)
 #endif
@@ -1854,7 +1935,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             // reads issue together instead of waiting behind the first one's stores
             TRec rr[2];
             int l0[2];
-            pnz = trellis_prep2<3, 0>(t, s.co_buf[sl], n0, sg.y1, lam16, rr, l0);
+            pnz = trellis_prep2<3, 0>(t, s.co_buf[sl], n0, sg.y1, lam16, rr, l0, &pcap);
 #pragma unroll
             for (int j = 0; j < 2; j++) {
               s.trec[sl][n0 + j] = rr[j];
@@ -1865,6 +1946,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       WG_REP_END
 #endif
           const uint64_t pnz_mask = __ballot(pnz);
+          const int nlast = nlast_of(__ballot(pcap));
           lds_sync();
           DSTAMP(-1);
           // the trellis DP: one lane quad per candidate (lane 4c + k owns end context k)
@@ -1878,7 +1960,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       WG_REP_BEGIN(WG_EXP_REP_DP)
 #endif
               trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl],
-                                WG_ENC_TAIL ? &s.cand_rate[sl] : nullptr);
+                                WG_ENC_TAIL ? &s.cand_rate[sl] : nullptr, nlast);
 #if defined(WG_EXP_REP_DP)
       WG_REP_END
 #endif
@@ -1897,11 +1979,10 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           // (lane 4c + r owns row r; the TDisto column pass reads the row pass
           // results back from LDS; sums are quad reductions)
           const bool qact = bvalid && hl < 4 * K;
-          const int qc = min(hl >> 2, 2), qr = hl & 3, qsl = half * 3 + qc;
-          // (unconditional, so that the reconstruction, TDisto and token-cost
-          // streams interleave: lanes past the candidates repeat candidate 2's
-          // work, or work on an unused slot, and nothing reads their results)
-          const int qmode = min(pick3(qc, cm[0], cm[1], cm[2]) & 15, 9);
+          // (qc, qr, qsl, qmode above: unconditional, so that the
+          // reconstruction, TDisto and token-cost streams interleave: lanes past
+          // the candidates repeat candidate 2's work, or work on an unused
+          // slot, and nothing reads their results)
           // (TAIL) the trellis DP leaves each candidate's rate in cand_rate, and
           // the inverse DCT's vertical pass runs one column a quad lane,
           // transposed across the quad by DPP: 4 levels and 4 products a lane
@@ -1960,11 +2041,18 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               dequant(qv, dq, sg.y1);
               idct_row(dq, qr, res);
             }
-            const uint32_t cw = reinterpret_cast<const uint32_t*>(t.pcode[qmode])[qr];
+            if constexpr (!WG_ENC_HOIST) {
+              const uint32_t cw = reinterpret_cast<const uint32_t*>(t.pcode[qmode])[qr];
+#pragma unroll
+              for (int k = 0; k < 4; k++) pr[k] = s.pv[half][(cw >> (8 * k)) & 0xff];
+              src_row = *reinterpret_cast<const uint32_t*>(s.yin + off + qr * BPS);
+            } else {
+#pragma unroll
+              for (int k = 0; k < 4; k++) pr[k] = (pred_row >> (8 * k)) & 0xff;
+            }
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-              pr[k] = s.pv[half][(cw >> (8 * k)) & 0xff];
-              sr[k] = s.yin[off + qr * BPS + k];
+              sr[k] = (src_row >> (8 * k)) & 0xff;
               rr[k] = clip8(pr[k] + res[k]);
               sse_r += (sr[k] - rr[k]) * (sr[k] - rr[k]);
             }
@@ -2185,13 +2273,13 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           Shared& s = launder(s_waves[wave]);
           Tables& t = launder(t_lds);
           const int first = r == 0 ? 0 : (r == 1 ? 6 : 11), m = r == 0 ? 6 : 5;
-          bool pnz = false;
+          bool pnz = false, pcap = false;
           if (lane < 8 * m) {
             const int j = lane >> 3, n0 = 2 * (lane & 7), pb = first + j;
             TRec rr[2];
             int l0[2];
             // (position 0, the DC coded by the WHT, is not part of this trellis)
-            pnz = trellis_prep2<0, 1>(t, s.co_buf[pb], n0, sg.y1, lam16, rr, l0);
+            pnz = trellis_prep2<0, 1>(t, s.co_buf[pb], n0, sg.y1, lam16, rr, l0, &pcap);
 #pragma unroll
             for (int k = 0; k < 2; k++)
               if (n0 + k >= 1) {
@@ -2200,6 +2288,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               }
           }
           const uint64_t pnz_mask = __ballot(pnz);
+          const int nlast = nlast_of(__ballot(pcap));
           lds_sync();
           // quad q runs task q: walk the round's blocks to find its (block, context)
           int tnz = 0;  // this quad's task: nz of its levels
@@ -2220,7 +2309,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             if (tj >= 0) {
               if ((pnz_mask >> (8 * tj)) & 0xff) {
                 int nzv = 0;
-                trellis_dp4<1, 0>(t, s.trec[tj], s.r0, s.eobl, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
+                trellis_dp4<1, 0>(t, s.trec[tj], s.r0, s.eobl, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv,
+                                  nullptr, nlast);
                 if ((lane & 3) == 0) res_nz[q] = nzv;
                 tnz = nzv;
               } else if ((lane & 3) == 0) {

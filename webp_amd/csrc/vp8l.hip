@@ -437,6 +437,136 @@ __global__ __launch_bounds__(64 * SQW) void k_vp8l_select_q(SelArgs a, int64_t t
   if (lane == 0) a.modes[(int64_t)img * a.tiles_x * a.tiles_y + tile] = ((uint32_t)best << 8) | ARGB_BLACK;
 }
 
+// The same phase with TWO waves a tile and two tiles' waves a SIMD.
+// k_vp8l_select_q issues at one wave per SIMD (four 37-KB tiles' histograms
+// fill the LDS), i.e. at half the SIMD's VALU rate, with every LDS round
+// trip exposed.  Here a 2-wave workgroup takes one tile:
+//   - the histograms hold only the 56 (mode, channel) columns (stride 56
+//     words, 28 KB): 37.3 KB a workgroup with the staged tile and the LUT, so
+//     four workgroups (8 waves, two a SIMD) fit in the CU's 160 KB;
+//   - wave h takes the sample rows h, h + 2, ... and adds into the shared
+//     histograms (ds_add: the two waves' adds to one word serialise in the
+//     LDS); each row's 40 staged words are read before its first add, so a
+//     row waits on the LDS once;
+//   - after the barrier wave 1 exits and wave 0 runs the 56 float64 sums
+//     (the whole column read first, then the LUT in batches) and the argmin.
+constexpr int SQ2_COLS = 56;
+__global__ __launch_bounds__(128) void k_vp8l_select_q2(SelArgs a, int64_t total) {
+  __shared__ uint32_t hist[128 * SQ2_COLS];
+  __shared__ uint32_t stile[33 * SQ_SW];
+  __shared__ double lut[SQ_LUT];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t t_idx = blockIdx.x;
+  if (t_idx >= total) return;  // (grid = total: never; no barrier skipped)
+  const int tile = (int)(t_idx % a.band_tiles) + a.ty0 * a.tiles_x;
+  const int img = (int)(t_idx / a.band_tiles);
+  const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+  const uint32_t* argb = a.argb + img * a.pitch;
+  const int ts = 1 << a.bits, w = a.width, h = a.height;
+  const int x0 = tx * ts, y0 = ty * ts;
+  const int x1 = min(x0 + ts, w), y1 = min(y0 + ts, h);
+  const int ystep = (y1 - y0 > 16) ? 2 : 1;
+  const int tw = x1 - x0, rows = (y1 - y0 + ystep - 1) / ystep;
+  {
+    // staged rows y0 - 1 .. y1 - 1 with estimateEntropy's edge values (as
+    // k_vp8l_select_q), every load issued before the first store
+    const int srows = y1 - y0 + 1, scols = x1 - x0 + 2, n = srows * scols;
+    constexpr int SN = (33 * SQ_SW + 127) / 128;
+    uint32_t v[SN];
+#pragma unroll
+    for (int j = 0; j < SN; j++) {
+      const int i = (int)threadIdx.x + 128 * j;
+      v[j] = 0;
+      if (i < n) {
+        const int rr = i / scols, cc = i - rr * scols;
+        const int y = y0 - 1 + rr, x = x0 - 1 + cc;
+        if (y >= 0 && x >= 0) v[j] = argb[(int64_t)y * w + min(x, w - 1)];
+      }
+    }
+    for (int i = threadIdx.x; i < SQ_LUT; i += 128) lut[i] = a.lut[i];
+    for (int i = threadIdx.x; i < 128 * SQ2_COLS / 4; i += 128) reinterpret_cast<uint4*>(hist)[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < SN; j++) {
+      const int i = (int)threadIdx.x + 128 * j;
+      if (i < n) stile[(i / scols) * SQ_SW + i % scols] = v[j];
+    }
+  }
+  __syncthreads();
+  const int m = lane >> 2, s = lane & 3;
+  const uint32_t ctl = m < 14 ? kPredCtl[m] : (uint32_t)C_BLACK;
+  const int shift = 24 - 8 * s;  // as the channel lane: alpha, red, green, blue
+  const bool col = lane < SQ2_COLS;
+  uint32_t* const myh = hist + lane;
+  for (int yy = wave; yy < rows; yy += 2) {
+    const uint32_t* srow = stile + (1 + yy * ystep) * SQ_SW;  // staged row y0 + yy * ystep
+    const uint32_t* sprev = srow - SQ_SW;
+    uint32_t P[8], L[8], T[8], TL[8], TR[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      P[j] = L[j] = T[j] = TL[j] = TR[j] = 0;
+      if (4 * j >= tw) continue;  // (wave-uniform)
+      const int c = min(4 * j + s, tw - 1) + 1;  // staged column of x
+      P[j] = srow[c];
+      L[j] = srow[c - 1];
+      T[j] = sprev[c];
+      TL[j] = sprev[c - 1];
+      TR[j] = sprev[c + 1];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (4 * j >= tw) continue;
+      const uint32_t res = sub_pixels(P[j], predict_ctl(ctl, L[j], T[j], TR[j], TL[j]));
+      const uint32_t rq[4] = {dpp_quad_u32<0>(res), dpp_quad_u32<1>(res), dpp_quad_u32<2>(res), dpp_quad_u32<3>(res)};
+      const int nv = tw - 4 * j;  // samples of this run inside the tile (wave-uniform)
+      if (col) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (q > 0 && nv <= q) break;
+          const uint32_t r = rq[q];
+          const uint32_t b = (r >> shift) & 0xff;
+          __hip_atomic_fetch_add(myh + SQ2_COLS * (b & 127), 1u << ((b >> 7) << 4), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (wave != 0) return;  // (no barrier below)
+  const uint32_t count = (uint32_t)(tw * rows);
+  double ce = 0.0;
+  if (col) {
+    uint32_t hv[128];
+#pragma unroll
+    for (int k = 0; k < 128; k++) hv[k] = myh[SQ2_COLS * k];
+    ce = lut[count];
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 32) {
+        double lv[32];
+#pragma unroll
+        for (int k = 0; k < 32; k++) lv[k] = lut[half ? hv[k0 + k] >> 16 : hv[k0 + k] & 0xffff];
+#pragma unroll
+        for (int k = 0; k < 32; k++) ce -= lv[k];
+      }
+    }
+  }
+  const double e = (((0.0 + dpp_quad_f64(ce, 0)) + dpp_quad_f64(ce, 1)) + dpp_quad_f64(ce, 2)) + dpp_quad_f64(ce, 3);
+  const uint64_t eb = __builtin_bit_cast(uint64_t, e);
+  int best = 0;
+  double best_cost = 1.7976931348623157e308;
+  for (int mm = 0; mm < a.max_mode; mm++) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)eb, 4 * mm);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(eb >> 32), 4 * mm);
+    const double cm = __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+    if (cm < best_cost) {
+      best_cost = cm;
+      best = mm;
+    }
+  }
+  if (lane == 0) a.modes[(int64_t)img * a.tiles_x * a.tiles_y + tile] = ((uint32_t)best << 8) | ARGB_BLACK;
+}
+
 struct ResArgs {
   const uint32_t* argb;
   const uint32_t* modes;
@@ -825,8 +955,14 @@ extern "C" int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, 
   const int64_t tiles = (int64_t)sa.band_tiles * n_images;
   WG_REQUIRE(tiles < (1ll << 31));
   int rc;
-  static const int force_old = getenv("WG_VP8L_SELECT_OLD") ? 1 : 0;  // A/B against the 4-wave kernel
-  if (bits <= 5 && !force_old) {  // counts <= 512: one wave a tile, all modes in one pass
+  // A/B switch: 0 = k_vp8l_select (4 waves a tile, a mode a wave), 1 =
+  // k_vp8l_select_q (a wave a tile), default 2 = k_vp8l_select_q2
+  const char* sel_env = getenv("WG_VP8L_SELECT");  // (read per call: the tests switch it)
+  const int variant = sel_env ? atoi(sel_env) : 2;
+  if (bits <= 5 && variant == 2) {  // counts <= 512: all modes in one pass over the samples
+    hipLaunchKernelGGL(k_vp8l_select_q2, dim3((unsigned)tiles), dim3(128), 0, s, sa, tiles);
+    rc = wg::check_launch("k_vp8l_select_q2");
+  } else if (bits <= 5 && variant == 1) {
     hipLaunchKernelGGL(k_vp8l_select_q, dim3((unsigned)((tiles + SQW - 1) / SQW)), dim3(64 * SQW), 0, s, sa, tiles);
     rc = wg::check_launch("k_vp8l_select_q");
   } else {
