@@ -73,6 +73,22 @@ def test_inverse_random_modes_multiband(cuda):
         assert (got[i] == O.vp8l_inverse_predictor(modes[i], bits, res[i])).all()
 
 
+@pytest.mark.parametrize("variant", ["0", "1"])
+@pytest.mark.parametrize("shape", [(1, 200, 171, 3), (3, 300, 97, 4), (2, 130, 4100, 2), (1, 31, 64, 5)])
+def test_inverse_variants(cuda, monkeypatch, variant, shape):
+    """The 4-wave band-group kernel (LDS hand-offs inside a group; default,
+    widths <= 4096) and the one-wave-a-band kernel (WG_VP8L_INVERSE=1, and
+    wider images): partial last groups, several images, arbitrary modes."""
+    monkeypatch.setenv("WG_VP8L_INVERSE", variant)
+    n, h, w, bits = shape
+    rng = np.random.default_rng(h * w + n)
+    res = rng.integers(0, 2 ** 32, (n, h, w), dtype=np.uint64).astype(np.uint32)
+    modes = ((rng.integers(0, 16, (n, L.subsample(h, bits), L.subsample(w, bits))) << 8) | 0xff000000).astype(np.uint32)
+    got = L.from_argb_tensor(L.predictor_inverse(L.to_argb_tensor(modes), bits, L.to_argb_tensor(res), check=True))
+    for i in range(n):
+        assert (got[i] == O.vp8l_inverse_predictor(modes[i], bits, res[i])).all(), i
+
+
 def test_batch_of_images(cuda):
     imgs = np.stack([argb_of(synth.noise_rgba(96, 80, seed=s)) for s in range(3)])
     m, r = L.ResidualImage(L.to_argb_tensor(imgs), 4, 75)

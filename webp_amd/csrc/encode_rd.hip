@@ -203,11 +203,14 @@ struct Shared {
 #ifndef WG_ENC_TAIL  // I4 candidates' rate from the DP, column-wise inverse DCT (see the I4 RD)
 #define WG_ENC_TAIL 1
 #endif
-// (WG_ENC_NLAST) the DP stops after the last position of the round at which
-// any of its blocks has a non-zero level candidate: past it every state but
-// context 0's is invalid, so no terminal (EOB from context 1 / 2) can still
-// win and the histories only gain zero levels -- the result is the same as
-// walking to position 15, as the reference does
+// (WG_ENC_NLAST) the DP may stop after the last position of the round at
+// which any of its blocks has a non-zero level candidate: past it every state
+// but context 0's is invalid, so no terminal (EOB from context 1 / 2) can
+// still win and the histories only gain zero levels -- the result is the same
+// as walking to position 15, as the reference does.  The walk's length is a
+// template bucket (positions < 8 or all 16): a run-time exit made the
+// compiler re-roll the loop and wait on every position's loads (slower
+// than walking all 16).
 #ifndef WG_ENC_NLAST
 #define WG_ENC_NLAST 1
 #endif
@@ -522,10 +525,10 @@ __device__ __forceinline__ int nlast_of(uint64_t cap_mask) {
 // ended, and the levels then follow position by position with no serial
 // chain: the quad's lane r writes positions 4r..4r+3 (raster) to q, and lane
 // 0 writes the zigzag nz count to *nz.
-template <int FIRST, int CTX_TYPE>
+template <int FIRST, int CTX_TYPE, int NEND = 16>
 __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[3],
                                             const int64_t (*eobl)[2], const int16_t* l0s, int init_ctx, int lam16, int k,
-                                            int16_t* q, int* nz, int* rate = nullptr, int nlast = 15) {
+                                            int16_t* q, int* nz, int* rate = nullptr) {
   constexpr int64_t BIG = 1ll << 59;
   init_ctx = min(init_ctx, 2);
   const int e = min(k, 2);
@@ -565,7 +568,7 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   // outlasted one position of the chain)
   int64_t y0 = 0, y1 = 0, y2 = 0, yeob = 0;
   int ycls = 0;
-  if (FIRST < 15) {
+  if (FIRST + 1 < NEND) {
     y0 = mine[(FIRST + 1) * STRIDE];
     y1 = mine[(FIRST + 1) * STRIDE + 1];
     y2 = mine[(FIRST + 1) * STRIDE + 2];
@@ -574,8 +577,7 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   }
 #endif
 #pragma unroll
-  for (int n = FIRST; n < 16; n++) {
-    if (WG_ENC_NLAST && n > nlast) break;  // (wave-uniform)
+  for (int n = FIRST; n < NEND; n++) {
     int64_t nx0 = 0, nx1 = 0, nx2 = 0;
     int ncls = 0;
 #if WG_ENC_EOBT
@@ -584,7 +586,7 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
     uint32_t neob = 0;
 #endif
 #if WG_ENC_EOBT && WG_ENC_DPAHEAD == 2
-    if (n < 14) {
+    if (n + 2 < NEND) {
       nx0 = mine[(n + 2) * STRIDE];
       nx1 = mine[(n + 2) * STRIDE + 1];
       nx2 = mine[(n + 2) * STRIDE + 2];
@@ -592,7 +594,7 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
       neob = eobq[2 * (n + 2)];
     }
 #else
-    if (n < 15) {
+    if (n + 1 < NEND) {
       nx0 = mine[(n + 1) * STRIDE];
       nx1 = mine[(n + 1) * STRIDE + 1];
       nx2 = mine[(n + 1) * STRIDE + 2];
@@ -1883,7 +1885,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           const int qc = min(hl >> 2, 2), qr = hl & 3, qsl = half * 3 + qc;
           const int qmode = min(pick3(qc, cm[0], cm[1], cm[2]) & 15, 9);
           uint32_t pred_row = 0, src_row = 0;
+          int hdr_h = 0;  // (HOIST) the mode's header bits
           if constexpr (WG_ENC_HOIST) {
+            hdr_h = t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];
             const uint32_t cw = reinterpret_cast<const uint32_t*>(t.pcode[qmode])[qr];
             int pr[4];
 #pragma unroll
@@ -1959,8 +1963,14 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
 #if defined(WG_EXP_REP_DP)
       WG_REP_BEGIN(WG_EXP_REP_DP)
 #endif
+#if WG_ENC_NLAST
+              if (nlast < 8)
+                trellis_dp4<0, 3, 8>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl],
+                                     &s.cand_nz[sl], WG_ENC_TAIL ? &s.cand_rate[sl] : nullptr);
+              else
+#endif
               trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl],
-                                WG_ENC_TAIL ? &s.cand_rate[sl] : nullptr, nlast);
+                                WG_ENC_TAIL ? &s.cand_rate[sl] : nullptr);
 #if defined(WG_EXP_REP_DP)
       WG_REP_END
 #endif
@@ -2136,7 +2146,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           uint64_t score = ~0ull;
           int rate = 0, hdr = 0;
           if (qact) {
-            hdr = t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];
+            hdr = WG_ENC_HOIST ? hdr_h : t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];
             rate = (qmode > 0 && cnt <= 3) ? 140 : 0;
             rate += tok_rate + hdr;
             score = rd_score(disto, rate, sg.lambda_i4);
@@ -2309,8 +2319,12 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             if (tj >= 0) {
               if ((pnz_mask >> (8 * tj)) & 0xff) {
                 int nzv = 0;
-                trellis_dp4<1, 0>(t, s.trec[tj], s.r0, s.eobl, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv,
-                                  nullptr, nlast);
+#if WG_ENC_NLAST
+                if (nlast < 8)
+                  trellis_dp4<1, 0, 8>(t, s.trec[tj], s.r0, s.eobl, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
+                else
+#endif
+                trellis_dp4<1, 0>(t, s.trec[tj], s.r0, s.eobl, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
                 if ((lane & 3) == 0) res_nz[q] = nzv;
                 tnz = nzv;
               } else if ((lane & 3) == 0) {

@@ -609,6 +609,7 @@ struct InvArgs {
   int* ctl;        // [0] band dequeue counter, [1] error flag (wait timeout)
   int* diag;       // wg::diag_words + DIAG_VP8L_INVERSE
   uint64_t* hand;  // [n_img][bands][width] {pixel, tag} granules of each band's last row
+  uint64_t* stamps;  // (WG_INV_STAMPS builds) [band idx][4]: start, end, poll ticks | polls << 32, block
   int64_t pitch;
   int width, height, bits, tiles_x, tiles_y, bands, n_img;
 };
@@ -693,24 +694,33 @@ __device__ __forceinline__ uint32_t from_pair_above(uint32_t v, uint32_t even, u
   return (uint32_t)__builtin_amdgcn_update_dpp((int)even, (int)s1, 0x138, 0xf, 0xf, false);
 }
 
-template <bool TILE16>
-__global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
-  __shared__ int sh_band;
-  // The control words' select masks, 64 B a row: rows 0-15 kPredCtl[mode],
-  // then the border rules 16 x = 0 (T), 17 x = 0 on row 0 (black), 18 row 0
-  // (L); rows 19-37 the same with C_EDGE (x = w - 1).  A step reads its row
-  // with three 16-B reads and one 4-B read, a step ahead, instead of
-  // extracting 13 bit masks on the VALU.
-  constexpr int MROWS = 38;
-  __shared__ uint32_t mtab[MROWS][16];
-  const int lane = threadIdx.x;
-  for (int i = lane; i < MROWS * 16; i += 64) {
+// The control words' select masks, 64 B a row: rows 0-15 kPredCtl[mode],
+// then the border rules 16 x = 0 (T), 17 x = 0 on row 0 (black), 18 row 0
+// (L); rows 19-37 the same with C_EDGE (x = w - 1).  A step reads its row
+// with three 16-B reads and one 4-B read, a step ahead, instead of
+// extracting 13 bit masks on the VALU.
+constexpr int MROWS = 38;
+__device__ __forceinline__ void fill_mtab(uint32_t (*mtab)[16], int tid, int nthreads) {
+  for (int i = tid; i < MROWS * 16; i += nthreads) {
     const int row = i >> 4, b = i & 15, id = row % 19;
     const uint32_t ctl = (id < 16 ? kPredCtl[id] : (id == 16 ? kPredCtl[2] : (id == 17 ? kPredCtl[0] : kPredCtl[1]))) |
                          (row >= 19 ? (uint32_t)C_EDGE : 0u);
     mtab[row][b] = b < 13 && ((ctl >> b) & 1) ? ~0u : 0u;
   }
-  __syncthreads();
+}
+
+// One band's walk.  The row above arrives as {pixel, tag} granules from
+// `up_row` -- global memory written by another workgroup's wave (SRC_LDS
+// false: the tag 1 set, cleared by the launch's memset) or this workgroup's
+// LDS row buffer written by the wave of the band above (SRC_LDS: the tag the
+// group's sequence number, so a granule of an earlier group never matches);
+// `want` is the tag to wait for.  The band's last row leaves the same way to
+// `hand_mine` with tag `wtag`.  `band_above` false: the image's first band
+// (no row above).
+template <bool TILE16, bool SRC_LDS, bool DST_LDS>
+__device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab)[16], int band, int img, int lane,
+                                         const uint64_t* up_row, uint64_t* hand_mine, uint32_t want, uint32_t wtag,
+                                         int64_t stamp_idx) {
   auto ld_masks = [&](uint32_t row) {
     SelMasks k;
     const uint4 a0 = *reinterpret_cast<const uint4*>(&mtab[row][0]), a1 = *reinterpret_cast<const uint4*>(&mtab[row][4]);
@@ -722,24 +732,14 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
     return k;
   };
   const int w = a.width;
-  const int total = a.bands * a.n_img;
   const int k = lane >> 1;  // the lane pair's row in the band
   const uint32_t sel = (lane & 1) ? C2_ODD : C2_EVEN;
   const uint32_t black = (lane & 1) ? 0x00ff0000u : 0u;  // ARGB_BLACK's channels (alpha 255)
-  for (;;) {
-    if (lane == 0) sh_band = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int idx = __builtin_amdgcn_readfirstlane(sh_band);
-    __syncthreads();
-    if (idx >= total) break;
-    const int band = idx / a.n_img, img = idx % a.n_img;
+  {
     const int y = band * INV_ROWS + k;
     const bool live = y < a.height;
     const uint32_t* in = a.in + img * a.pitch;
     uint32_t* out = a.out + img * a.pitch;
-    const int hs = (w + 1) & ~1;  // granules per hand-off row (even: 16-B aligned pairs)
-    const uint64_t* hand_above = a.hand + ((int64_t)img * a.bands + band - 1) * hs;  // band > 0
-    uint64_t* hand_mine = a.hand + ((int64_t)img * a.bands + band) * hs;
     const int last_row = min(INV_ROWS - 1, a.height - 1 - band * INV_ROWS);
     const bool hands_off = band + 1 < a.bands && lane == 2 * last_row;  // the last row's even lane
     const uint32_t* mrow =
@@ -747,24 +747,39 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
     const uint32_t* inrow = in + (int64_t)min(y, a.height - 1) * w;
     uint32_t* orow = out + (int64_t)min(y, a.height - 1) * w;
     uint32_t o1 = 0, first = 0;  // this lane's output (c2) at x - 1; at x = 0
+#ifdef WG_INV_STAMPS
+    // the per-band timeline (tools/inv_timeline.py): s_memrealtime (100 MHz)
+    // at the band's start and end, and the ticks spent re-polling the band above
+    const uint64_t t_band = __builtin_amdgcn_s_memrealtime();
+    uint64_t poll_ticks = 0, polls = 0;
+#endif
     const int steps = w + 2 * last_row;
     // the band above's row, one granule a step: column c sits in gr[c & 15],
     // loaded UPD steps before step c - 1 (where it is TR); up_take re-polls it
     // until its tag is set and returns the pixel
     // (unconditional loads at clamped addresses: a load inside a branch makes
     // the compiler drain every load before its use)
-    const uint64_t* up_row = band > 0 ? hand_above : hand_mine;  // band 0: any valid row, values unused
+    // (band 0: up_row is any valid row, values unused)
     auto up_load = [&](int c) -> uint64_t {
-      return __hip_atomic_load(up_row + min(c, w - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (SRC_LDS)
+        return __hip_atomic_load(up_row + min(c, w - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      else
+        return __hip_atomic_load(up_row + min(c, w - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto up_take = [&](int c, uint64_t g) -> uint32_t {
       const uint2 gw = __builtin_bit_cast(uint2, g);
-      if (band > 0 && c < w && __builtin_amdgcn_readfirstlane((int)gw.y) == 0) {
+      if (band > 0 && c < w && (uint32_t)__builtin_amdgcn_readfirstlane((int)gw.y) != want) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (uint32_t it = 0;; it++) {
           __builtin_amdgcn_s_sleep(1);
           g = up_load(c);
-          if (__builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) != 0) break;
+          if ((uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) == want) {
+#ifdef WG_INV_STAMPS
+            poll_ticks += __builtin_amdgcn_s_memrealtime() - t0;
+            polls++;
+#endif
+            break;
+          }
           if ((it & 15) == 15 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
                                   __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
             if (lane == 0) {
@@ -878,11 +893,17 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
         // (the hand-off lane's row is live)
         if (u & 1) {
           if (hands_off && (uint32_t)x < (uint32_t)w) {
-            const u32x4_t g2 = {ov[u - 1], 1u, full, 1u};
-            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(hand_mine + x - 1), "v"(g2) : "memory");
+            const u32x4_t g2 = {ov[u - 1], wtag, full, wtag};
+            if constexpr (DST_LDS)
+              *reinterpret_cast<u32x4_t*>(hand_mine + x - 1) = g2;
+            else
+              asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(hand_mine + x - 1), "v"(g2) : "memory");
           }
         } else if (hands_off && x == w - 1) {
-          __hip_atomic_store(hand_mine + x, 1ull << 32 | full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if constexpr (DST_LDS)
+            __hip_atomic_store(hand_mine + x, (uint64_t)wtag << 32 | full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          else
+            __hip_atomic_store(hand_mine + x, (uint64_t)wtag << 32 | full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (starts) first = x == 0 ? v : first;
         // (outputs at x outside the row are never read: at x = 0 the row
@@ -908,6 +929,83 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
 #pragma unroll
       for (int u = 0; u < 16; u++) rc[u] = rn[u];
       mc = mn;
+    }
+#ifdef WG_INV_STAMPS
+    if (lane == 0) {
+      uint64_t* st = a.stamps + 4 * stamp_idx;
+      st[0] = t_band;
+      st[1] = __builtin_amdgcn_s_memrealtime();
+      st[2] = poll_ticks | polls << 32;
+      st[3] = blockIdx.x;
+    }
+#endif
+  }
+}
+
+// One wave a band, bands dequeued in (band, image) order from a counter (a
+// band only ever waits on a band owned by a running wave); every hand-off
+// through global memory.
+template <bool TILE16>
+__global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
+  __shared__ int sh_band;
+  __shared__ uint32_t mtab[MROWS][16];
+  const int lane = threadIdx.x;
+  fill_mtab(mtab, lane, 64);
+  __syncthreads();
+  const int total = a.bands * a.n_img;
+  const int hs = (a.width + 1) & ~1;  // granules per hand-off row (even: 16-B aligned pairs)
+  for (;;) {
+    if (lane == 0) sh_band = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int idx = __builtin_amdgcn_readfirstlane(sh_band);
+    __syncthreads();
+    if (idx >= total) break;
+    const int band = idx / a.n_img, img = idx % a.n_img;
+    uint64_t* hand_mine = a.hand + ((int64_t)img * a.bands + band) * hs;
+    const uint64_t* up_row = band > 0 ? hand_mine - hs : hand_mine;
+    inv_band<TILE16, false, false>(a, mtab, band, img, lane, up_row, hand_mine, 1u, 1u, idx);
+  }
+}
+
+// Four waves a workgroup, one a band, taking four consecutive bands of one
+// image (groups dequeued in (band group, image) order): the hand-offs between
+// the group's bands go through LDS row buffers (a poll that misses costs an
+// LDS round trip, not an L2 one), only the group's first band waits on
+// global granules (the previous group's last band).  The per-band timeline
+// (tools/inv_timeline.py) showed the global hand-off, a few L2 re-polls a band
+// of ~0.5 us each, as a fifth of the 32-row band's lag.  Widths up to INV_GW.
+constexpr int INV_GW = 4096;
+template <bool TILE16>
+__global__ __launch_bounds__(256) void k_vp8l_inverse_g(InvArgs a) {
+  __shared__ int sh_grp;
+  __shared__ uint32_t mtab[MROWS][16];
+  __shared__ uint64_t rowbuf[3][INV_GW];  // the last rows of the group's bands 0..2
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  fill_mtab(mtab, tid, 256);
+  // tags start clear: LDS keeps a previous workgroup's bytes
+  for (int i = tid; i < 3 * INV_GW / 2; i += 256) reinterpret_cast<uint4*>(&rowbuf[0][0])[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const int groups = (a.bands + 3) >> 2, total = groups * a.n_img;
+  const int hs = (a.width + 1) & ~1;
+  for (;;) {
+    if (tid == 0) sh_grp = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int gidx = __builtin_amdgcn_readfirstlane(sh_grp);
+    __syncthreads();  // (also: the previous group's LDS rows are no longer read)
+    if (gidx >= total) break;
+    const int bg = gidx / a.n_img, img = gidx % a.n_img;
+    const int band = 4 * bg + wave;
+    if (band < a.bands) {
+      const uint32_t tag = (uint32_t)gidx + 1;  // > 0, unique per group of the launch
+      uint64_t* hand_g = a.hand + ((int64_t)img * a.bands + band) * hs;
+      const int64_t sidx = (int64_t)band * a.n_img + img;
+      if (wave == 0)
+        inv_band<TILE16, false, true>(a, mtab, band, img, lane, band > 0 ? hand_g - hs : hand_g, rowbuf[0], 1u, tag,
+                                      sidx);
+      else if (wave == 3)
+        inv_band<TILE16, true, false>(a, mtab, band, img, lane, rowbuf[2], hand_g, tag, 1u, sidx);
+      else
+        inv_band<TILE16, true, true>(a, mtab, band, img, lane, rowbuf[wave - 1], rowbuf[wave], tag, tag, sidx);
     }
   }
 }
@@ -997,7 +1095,12 @@ extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32
 
 extern "C" size_t wg_vp8l_inverse_work_bytes(int32_t width, int32_t height, int32_t n_images) {
   if (width <= 0 || height <= 0 || n_images <= 0) return 0;
-  return 16 + sizeof(uint64_t) * (size_t)n_images * ((height + INV_ROWS - 1) / INV_ROWS) * ((width + 1) & ~1);
+  const size_t bands = (size_t)n_images * ((height + INV_ROWS - 1) / INV_ROWS);
+#ifdef WG_INV_STAMPS
+  return 16 + sizeof(uint64_t) * bands * ((width + 1) & ~1) + 32 * bands;  // + the timeline records
+#else
+  return 16 + sizeof(uint64_t) * bands * ((width + 1) & ~1);
+#endif
 }
 
 extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, int32_t width, int32_t height,
@@ -1018,6 +1121,7 @@ extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, in
   if (!a.diag) return WG_EHIP;
   a.diag += wg::DIAG_VP8L_INVERSE;
   a.hand = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(work) + 16);
+  a.stamps = a.hand + (size_t)n_images * a.bands * ((width + 1) & ~1);
   a.pitch = image_pitch;
   a.width = width;
   a.height = height;
@@ -1027,6 +1131,17 @@ extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, in
   // counters and every granule's tag start clear
   if (hipMemsetAsync(work, 0, wg_vp8l_inverse_work_bytes(width, height, n_images), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(vp8l work)");
+  // WG_VP8L_INVERSE=1: the one-wave-a-band kernel everywhere (A/B)
+  const char* inv_env = getenv("WG_VP8L_INVERSE");  // (read per call: the tests switch it)
+  if (width <= INV_GW && !(inv_env && atoi(inv_env) == 1)) {
+    const int total = ((a.bands + 3) >> 2) * n_images;
+    const int grid = total < 256 ? total : 256;  // one 4-wave workgroup a CU (99 KB of LDS)
+    if (bits >= 4)
+      hipLaunchKernelGGL(k_vp8l_inverse_g<true>, dim3((unsigned)grid), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_vp8l_inverse_g<false>, dim3((unsigned)grid), dim3(256), 0, s, a);
+    return wg::check_launch("k_vp8l_inverse_g");
+  }
   const int total = a.bands * n_images;
   const int grid = total < 2048 ? total : 2048;
   if (bits >= 4)
