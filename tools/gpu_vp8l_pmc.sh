@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU box: counter passes over the C5 stages (tools/bench_c5.py) for the
-# VP8L kernels (k_vp8l_select_q2, k_vp8l_inverse_g, ...): two SQ passes and
-# one HBM pass, each its own rocprofv3 run, summarised per kernel into
+# VP8L kernels (k_vp8l_select_q3, k_vp8l_inverse, ...): two SQ passes and
+# two HBM passes, each its own rocprofv3 run, summarised per kernel into
 # gpurun_out/vp8l_pmc/*.json (tools/pmc_summary.py).
 OUT=gpurun_out/vp8l_pmc; mkdir -p $OUT && export TMPDIR=/tmp
 pass() {  # name counters...
@@ -11,7 +11,9 @@ pass() {  # name counters...
 }
 pass sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY
 pass sq2 SQ_WAIT_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_THREAD_CYCLES_VALU SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE
-pass hbm FETCH_SIZE WRITE_SIZE
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+python3 tools/pmc_summary.py --json $OUT/hbm.json $(find $OUT/fetch $OUT/write -name "*counter_collection.csv") > /dev/null || exit 1
 python3 - <<'EOF'
 import json
 out = {}

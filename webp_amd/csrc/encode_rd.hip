@@ -210,9 +210,11 @@ struct Shared {
 // as walking to position 15, as the reference does.  The walk's length is a
 // template bucket (positions < 8 or all 16): a run-time exit made the
 // compiler re-roll the loop and wait on every position's loads (slower
-// than walking all 16).
+// than walking all 16).  Measured (round 5, isolated 64 x 1080p launch, A/B):
+// the run-time exit 20.2-20.4 -> 21.2-21.3 ms, the buckets 20.3-20.6 ->
+// 20.6-20.7 ms (the second DP copy's registers and code): off.
 #ifndef WG_ENC_NLAST
-#define WG_ENC_NLAST 1
+#define WG_ENC_NLAST 0
 #endif
 #ifndef WG_ENC_HOIST  // I4 candidates' prediction / source rows read before the trellis (see the I4 RD)
 #define WG_ENC_HOIST 1

@@ -710,17 +710,14 @@ __device__ __forceinline__ void fill_mtab(uint32_t (*mtab)[16], int tid, int nth
 }
 
 // One band's walk.  The row above arrives as {pixel, tag} granules from
-// `up_row` -- global memory written by another workgroup's wave (SRC_LDS
-// false: the tag 1 set, cleared by the launch's memset) or this workgroup's
-// LDS row buffer written by the wave of the band above (SRC_LDS: the tag the
-// group's sequence number, so a granule of an earlier group never matches);
-// `want` is the tag to wait for.  The band's last row leaves the same way to
-// `hand_mine` with tag `wtag`.  `band_above` false: the image's first band
-// (no row above).
-template <bool TILE16, bool SRC_LDS, bool DST_LDS>
+// `up_row` (global memory written by the wave of the band above; tag 1 set,
+// cleared by the launch's memset); the band's last row leaves the same way
+// to `hand_mine`.  (Round 5 measured bands grouped four to a workgroup with
+// LDS hand-offs inside the group once more: 3.46 -> 3.71 ms at 4096², as in
+// round 4 -- co-resident waves slow each other's steps.)
+template <bool TILE16>
 __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab)[16], int band, int img, int lane,
-                                         const uint64_t* up_row, uint64_t* hand_mine, uint32_t want, uint32_t wtag,
-                                         int64_t stamp_idx) {
+                                         const uint64_t* up_row, uint64_t* hand_mine, int64_t stamp_idx) {
   auto ld_masks = [&](uint32_t row) {
     SelMasks k;
     const uint4 a0 = *reinterpret_cast<const uint4*>(&mtab[row][0]), a1 = *reinterpret_cast<const uint4*>(&mtab[row][4]);
@@ -761,19 +758,16 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
     // the compiler drain every load before its use)
     // (band 0: up_row is any valid row, values unused)
     auto up_load = [&](int c) -> uint64_t {
-      if constexpr (SRC_LDS)
-        return __hip_atomic_load(up_row + min(c, w - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      else
-        return __hip_atomic_load(up_row + min(c, w - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return __hip_atomic_load(up_row + min(c, w - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto up_take = [&](int c, uint64_t g) -> uint32_t {
       const uint2 gw = __builtin_bit_cast(uint2, g);
-      if (band > 0 && c < w && (uint32_t)__builtin_amdgcn_readfirstlane((int)gw.y) != want) {
+      if (band > 0 && c < w && __builtin_amdgcn_readfirstlane((int)gw.y) == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (uint32_t it = 0;; it++) {
           __builtin_amdgcn_s_sleep(1);
           g = up_load(c);
-          if ((uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) == want) {
+          if (__builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) != 0) {
 #ifdef WG_INV_STAMPS
             poll_ticks += __builtin_amdgcn_s_memrealtime() - t0;
             polls++;
@@ -893,17 +887,11 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
         // (the hand-off lane's row is live)
         if (u & 1) {
           if (hands_off && (uint32_t)x < (uint32_t)w) {
-            const u32x4_t g2 = {ov[u - 1], wtag, full, wtag};
-            if constexpr (DST_LDS)
-              *reinterpret_cast<u32x4_t*>(hand_mine + x - 1) = g2;
-            else
-              asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(hand_mine + x - 1), "v"(g2) : "memory");
+            const u32x4_t g2 = {ov[u - 1], 1u, full, 1u};
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(hand_mine + x - 1), "v"(g2) : "memory");
           }
         } else if (hands_off && x == w - 1) {
-          if constexpr (DST_LDS)
-            __hip_atomic_store(hand_mine + x, (uint64_t)wtag << 32 | full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          else
-            __hip_atomic_store(hand_mine + x, (uint64_t)wtag << 32 | full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(hand_mine + x, 1ull << 32 | full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (starts) first = x == 0 ? v : first;
         // (outputs at x outside the row are never read: at x = 0 the row
@@ -963,50 +951,7 @@ __global__ __launch_bounds__(64) void k_vp8l_inverse(InvArgs a) {
     const int band = idx / a.n_img, img = idx % a.n_img;
     uint64_t* hand_mine = a.hand + ((int64_t)img * a.bands + band) * hs;
     const uint64_t* up_row = band > 0 ? hand_mine - hs : hand_mine;
-    inv_band<TILE16, false, false>(a, mtab, band, img, lane, up_row, hand_mine, 1u, 1u, idx);
-  }
-}
-
-// Four waves a workgroup, one a band, taking four consecutive bands of one
-// image (groups dequeued in (band group, image) order): the hand-offs between
-// the group's bands go through LDS row buffers (a poll that misses costs an
-// LDS round trip, not an L2 one), only the group's first band waits on
-// global granules (the previous group's last band).  The per-band timeline
-// (tools/inv_timeline.py) showed the global hand-off, a few L2 re-polls a band
-// of ~0.5 us each, as a fifth of the 32-row band's lag.  Widths up to INV_GW.
-constexpr int INV_GW = 4096;
-template <bool TILE16>
-__global__ __launch_bounds__(256) void k_vp8l_inverse_g(InvArgs a) {
-  __shared__ int sh_grp;
-  __shared__ uint32_t mtab[MROWS][16];
-  __shared__ uint64_t rowbuf[3][INV_GW];  // the last rows of the group's bands 0..2
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  fill_mtab(mtab, tid, 256);
-  // tags start clear: LDS keeps a previous workgroup's bytes
-  for (int i = tid; i < 3 * INV_GW / 2; i += 256) reinterpret_cast<uint4*>(&rowbuf[0][0])[i] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  const int groups = (a.bands + 3) >> 2, total = groups * a.n_img;
-  const int hs = (a.width + 1) & ~1;
-  for (;;) {
-    if (tid == 0) sh_grp = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int gidx = __builtin_amdgcn_readfirstlane(sh_grp);
-    __syncthreads();  // (also: the previous group's LDS rows are no longer read)
-    if (gidx >= total) break;
-    const int bg = gidx / a.n_img, img = gidx % a.n_img;
-    const int band = 4 * bg + wave;
-    if (band < a.bands) {
-      const uint32_t tag = (uint32_t)gidx + 1;  // > 0, unique per group of the launch
-      uint64_t* hand_g = a.hand + ((int64_t)img * a.bands + band) * hs;
-      const int64_t sidx = (int64_t)band * a.n_img + img;
-      if (wave == 0)
-        inv_band<TILE16, false, true>(a, mtab, band, img, lane, band > 0 ? hand_g - hs : hand_g, rowbuf[0], 1u, tag,
-                                      sidx);
-      else if (wave == 3)
-        inv_band<TILE16, true, false>(a, mtab, band, img, lane, rowbuf[2], hand_g, tag, 1u, sidx);
-      else
-        inv_band<TILE16, true, true>(a, mtab, band, img, lane, rowbuf[wave - 1], rowbuf[wave], tag, tag, sidx);
-    }
+    inv_band<TILE16>(a, mtab, band, img, lane, up_row, hand_mine, idx);
   }
 }
 
@@ -1054,7 +999,10 @@ extern "C" int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, 
   WG_REQUIRE(tiles < (1ll << 31));
   int rc;
   // A/B switch: 0 = k_vp8l_select (4 waves a tile, a mode a wave), 1 =
-  // k_vp8l_select_q (a wave a tile), default 2 = k_vp8l_select_q2
+  // k_vp8l_select_q (a wave a tile), default 2 = k_vp8l_select_q2 (two waves
+  // a tile).  (Round 5 also measured q2 in persistent workgroups, three
+  // 10-bit bins a histogram word and the next tile staged by wave 1 while
+  // wave 0 sums: 0.60 -> 0.65 ms at 4096².)
   const char* sel_env = getenv("WG_VP8L_SELECT");  // (read per call: the tests switch it)
   const int variant = sel_env ? atoi(sel_env) : 2;
   if (bits <= 5 && variant == 2) {  // counts <= 512: all modes in one pass over the samples
@@ -1131,17 +1079,6 @@ extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, in
   // counters and every granule's tag start clear
   if (hipMemsetAsync(work, 0, wg_vp8l_inverse_work_bytes(width, height, n_images), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(vp8l work)");
-  // WG_VP8L_INVERSE=1: the one-wave-a-band kernel everywhere (A/B)
-  const char* inv_env = getenv("WG_VP8L_INVERSE");  // (read per call: the tests switch it)
-  if (width <= INV_GW && !(inv_env && atoi(inv_env) == 1)) {
-    const int total = ((a.bands + 3) >> 2) * n_images;
-    const int grid = total < 256 ? total : 256;  // one 4-wave workgroup a CU (99 KB of LDS)
-    if (bits >= 4)
-      hipLaunchKernelGGL(k_vp8l_inverse_g<true>, dim3((unsigned)grid), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL(k_vp8l_inverse_g<false>, dim3((unsigned)grid), dim3(256), 0, s, a);
-    return wg::check_launch("k_vp8l_inverse_g");
-  }
   const int total = a.bands * n_images;
   const int grid = total < 2048 ? total : 2048;
   if (bits >= 4)
