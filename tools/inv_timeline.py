@@ -6,9 +6,11 @@
 The stamps build records per band (32 rows) the s_memrealtime (100 MHz) at
 its start and end and the ticks it spent re-polling the band above's
 hand-off granules.  Printed: the launch span, each band's walk time and
-per-step time (steps = width + 2 * 31), the start-to-start lag between
-consecutive bands in steps, and the poll share -- what the walk's
-(2 * height + width) x step-time bound and the hand-offs each cost."""
+per-step time (steps = width + 2 * 31; band 0, which waits on nothing, gives
+the free-running step), the end-to-end lag between consecutive bands in
+steps and beyond the 64 the diagonal needs, and the poll time -- what the
+walk's (2 * height + width) x step-time chain and the hand-offs each cost.
+`python tools/inv_timeline.py --from saved.json` recomputes from a record."""
 import json
 import os
 import sys
@@ -26,7 +28,36 @@ BITS = 5
 TICK_NS = 10.0  # s_memrealtime: 100 MHz
 
 
+def summarize(start, end, poll, polls):
+    walk = end - start
+    steps = N + 2 * 31
+    step_ns = walk / steps * 1e3
+    lag = np.diff(end)
+    return {
+        "span_us": round(float(end.max()), 1),
+        "walk_us": {"median": round(float(np.median(walk)), 1), "min": round(float(walk.min()), 1)},
+        "step_ns_free": round(float(step_ns.min()), 1),
+        "lag_us": {"median": round(float(np.median(lag)), 2), "min": round(float(lag.min()), 2),
+                   "max": round(float(lag.max()), 2)},
+        "lag_steps_median": round(float(np.median(lag) * 1e3 / step_ns.min()), 1),
+        "lag_steps_over_diagonal": round(float(np.median(lag) * 1e3 / step_ns.min() - 64), 1),
+        "poll_us_per_band": {"median": round(float(np.median(poll)), 1), "max": round(float(poll.max()), 1)},
+        "polls_per_band_median": int(np.median(polls)) if polls is not None else None,
+        "chain_bound_us": round(float((2 * N + N) * step_ns.min() / 1e3), 1),
+    }
+
+
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--from":
+        rec = json.load(open(sys.argv[2]))
+        b = np.array(rec["bands"], dtype=np.float64)
+        rec.update(summarize(b[:, 0], b[:, 1], b[:, 2], None))
+        for k in ("step_ns", "lag_steps_median_old"):
+            rec.pop(k, None)
+        print(json.dumps({k: v for k, v in rec.items() if k != "bands"}))
+        if len(sys.argv) > 3:
+            json.dump(rec, open(sys.argv[3], "w"), indent=1)
+        return
     rgba = synth.blobs_rgba(N, N, seed=5, alpha=True).astype(np.uint32)
     argb = (rgba[..., 3] << 24) | (rgba[..., 0] << 16) | (rgba[..., 1] << 8) | rgba[..., 2]
     t = L.to_argb_tensor(argb[None])
@@ -47,26 +78,12 @@ def main():
     st = work[hand:].cpu().numpy().view(np.uint64).reshape(bands, 4).astype(np.int64)
     t0 = st[:, 0].min()
     start, end = (st[:, 0] - t0) * TICK_NS / 1e3, (st[:, 1] - t0) * TICK_NS / 1e3  # us
-    walk = end - start
-    steps = N + 2 * 31
-    step_ns = walk / steps * 1e3
-    lag = np.diff(start)
     poll = (st[:, 2] & 0xFFFFFFFF) * TICK_NS / 1e3
     polls = st[:, 2] >> 32
-    rec = {
-        "config": f"C5 {N}x{N} bits {BITS}: k_vp8l_inverse, one wave per 32-row band",
-        "span_us": round(float(end.max()), 1),
-        "walk_us": {"median": round(float(np.median(walk)), 1), "min": round(float(walk.min()), 1),
-                    "max": round(float(walk.max()), 1)},
-        "step_ns": {"median": round(float(np.median(step_ns)), 1), "min": round(float(step_ns.min()), 1)},
-        "lag_us": {"median": round(float(np.median(lag)), 2), "min": round(float(lag.min()), 2),
-                   "max": round(float(lag.max()), 2)},
-        "lag_steps_median": round(float(np.median(lag) * 1e3 / np.median(step_ns)), 1),
-        "poll_us_per_band": {"median": round(float(np.median(poll)), 1), "max": round(float(poll.max()), 1)},
-        "polls_per_band_median": int(np.median(polls)),
-        "chain_bound_us": round(float((2 * N + N) * np.median(step_ns) / 1e3), 1),
-        "bands": [[round(float(a), 2), round(float(b), 2), round(float(c), 2)] for a, b, c in zip(start, end, poll)],
-    }
+    # every band starts at once (all resident) and waits: the lag shows in the ends
+    rec = {"config": f"C5 {N}x{N} bits {BITS}: k_vp8l_inverse, one wave per 32-row band",
+           **summarize(start, end, poll, polls),
+           "bands": [[round(float(a), 2), round(float(b), 2), round(float(c), 2)] for a, b, c in zip(start, end, poll)]}
     line = json.dumps({k: v for k, v in rec.items() if k != "bands"})
     print(line)
     if len(sys.argv) > 1:

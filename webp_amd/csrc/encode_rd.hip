@@ -108,14 +108,15 @@ __device__ __forceinline__ int band_of(int n) { return (int)((pack_band() >> (3 
 // consumed by the lane quad running the DP (trellis_dp4).
 struct alignas(8) TRec {
   // x[row][pc]: the transition from predecessor context pc, as a key
-  // (score x16 + order idx) to add to that predecessor's state, with the
-  // rows routed by the end context they reach:
+  // (score x16 + idx, idx = 4 pc + the level code: 0 level 0, 1 L0, 2 L0 + 1)
+  // to add to that predecessor's state, with the rows routed by the end
+  // context they reach:
   //   R1  level 1 or L0 >= 2: (nz token + level cost) * lam16 + distortion,
-  //       idx 2pc for level L0, 2pc + 1 for level L0 + 1 (= 1 when L0 = 0)
-  //   R2  level L0 + 1 >= 2 (idx 2pc + 1), all BIG when L0 = 0
+  //       idx 4pc + 1 for level L0, 4pc + 2 for level L0 + 1 (= 1 when L0 = 0)
+  //   R2  level L0 + 1 >= 2 (idx 4pc + 2), all BIG when L0 = 0
   // + BIG when that level is not a candidate.  The level-0 row R0 (end
-  // context 0: zero-token cost * lam16 + idx pc) depends only on the position
-  // and the segment's lambda: one table per macroblock and phase
+  // context 0: zero-token cost * lam16 + idx 4pc) depends only on the
+  // position and the segment's lambda: one table per macroblock and phase
   // (Shared::r0, trellis_r0), not a row of every record.
   int64_t x[2][3];
 };
@@ -223,7 +224,7 @@ struct Shared {
 #define WG_ENC_DPAHEAD 1
 #endif
   TRec trec[6][16 + WG_ENC_TPAD];
-  int64_t r0[16][3];       // the phase's level-0 trellis row (trellis_r0)
+  int64_t r0[16][6];       // the phase's level-0 trellis row (trellis_r0; [3..5] unused: a TRec's stride)
   int64_t eobl[16][2];     // the phase's terminal costs x lam16 (trellis_r0, WG_ENC_EOBT)
   int16_t l0s[6][16];      // per position: L0 << 3 | negative << 2 | min(L0, 2) (< 2^14)
   alignas(16) int16_t cand_q[6][16];  // I4 candidates' levels for the lane-parallel token cost
@@ -335,9 +336,10 @@ __device__ __forceinline__ int token_cost(const Tables& t, const QT& q, int nz_c
 // Scores are kept x16 so the low 4 bits of a 64-bit key can carry the
 // candidate's position in the reference's update order; "first strict
 // minimum in order" then is a plain min over keys.  Candidates per position
-// and end context: level 0 from predecessor pc (key idx = pc, end ctx 0),
-// level L0 (idx 2pc) and L0 + 1 (idx 2pc + 1), whose end context is
-// min(level, 2).  Invalid states carry scores >= 2^58 (valid ones stay below
+// and end context: level 0 from predecessor pc (key idx = 4pc, end ctx 0),
+// level L0 (idx 4pc + 1) and L0 + 1 (idx 4pc + 2), whose end context is
+// min(level, 2): idx grows in the reference's update order, and its low two
+// bits are the level code the DP's histories keep.  Invalid states carry scores >= 2^58 (valid ones stay below
 // 2^51), so they never win against a valid candidate.  The path keeps the
 // winning idx per end context (4 bits each, 16 bits per position); levels
 // are re-derived from the position records when walking back.
@@ -351,7 +353,7 @@ __device__ __forceinline__ int token_cost(const Tables& t, const QT& q, int nz_c
 // (trellis_r0).
 //
 // The R0 table of a phase: position n, predecessor context pc -> the
-// zero-token cost of band(n + 1) * lam16 + idx pc; lane 3n + pc writes it.
+// zero-token cost of band(n + 1) * lam16 + idx 4pc; lane 3n + pc writes it.
 #ifndef WG_ENC_EOBT
 #define WG_ENC_EOBT 1
 #endif
@@ -371,11 +373,11 @@ __device__ __forceinline__ int token_cost(const Tables& t, const QT& q, int nz_c
 // (the key's position field, see trellis_dp4), which the DP adds to a state
 // instead of multiplying the EOB cost per position.
 template <int CTX_TYPE>
-__device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16, int64_t (*r0)[3],
+__device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16, int64_t (*r0)[6],
                                            int64_t (*eobl)[2]) {
   if (lane < 48) {
     const int n = lane / 3, pc = lane - 3 * n;
-    r0[n][pc] = (int64_t)vc_of(t.vcost[CTX_TYPE * 8 + band_of(n + 1)][0], pc) * lam16 + pc;
+    r0[n][pc] = (int64_t)vc_of(t.vcost[CTX_TYPE * 8 + band_of(n + 1)][0], pc) * lam16 + 4 * pc;
   }
 #if WG_ENC_EOBT
   else {
@@ -444,8 +446,8 @@ __device__ __forceinline__ bool trellis_prep2(const Tables& t, const int16_t* co
 #endif
 #pragma unroll
     for (int pc = 0; pc < 3; pc++) {
-      const int64_t r1 = (int64_t)vc_of(v0[j], pc) * lam16 + A0 + 2 * pc;
-      const int64_t r2 = (int64_t)vc_of(v1[j], pc) * lam16 + A1 + 2 * pc + 1;
+      const int64_t r1 = (int64_t)vc_of(v0[j], pc) * lam16 + A0 + 4 * pc + 1;
+      const int64_t r2 = (int64_t)vc_of(v1[j], pc) * lam16 + A1 + 4 * pc + 2;
 #if WG_ENC_TWO
       out[j].x[0][pc] = z ? r2 : (two ? BIG : r1);
       out[j].x[1][pc] = z ? BIG : (two && r1 < r2 ? r1 : r2);
@@ -528,13 +530,12 @@ __device__ __forceinline__ int nlast_of(uint64_t cap_mask) {
 // chain: the quad's lane r writes positions 4r..4r+3 (raster) to q, and lane
 // 0 writes the zigzag nz count to *nz.
 template <int FIRST, int CTX_TYPE, int NEND = 16>
-__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[3],
+__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[6],
                                             const int64_t (*eobl)[2], const int16_t* l0s, int init_ctx, int lam16, int k,
                                             int16_t* q, int* nz, int* rate = nullptr) {
   constexpr int64_t BIG = 1ll << 59;
   init_ctx = min(init_ctx, 2);
   const int e = min(k, 2);
-  const int psh = e == 0 ? 0 : 1;  // index -> predecessor context shift; also the level-code offset
   int64_t ps0 = init_ctx == 0 ? 0 : BIG, ps1 = init_ctx == 1 ? 0 : BIG, ps2 = init_ctx == 2 ? 0 : BIG;
   uint32_t h0 = 0, h1 = 0, h2 = 0;  // the states' histories
   const TokRow& t_init = t.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
@@ -548,7 +549,7 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   // this lane's row: R0 from the phase's table (3 words a position), R1 / R2
   // from the block's records (6 words a position)
   const int64_t* mine = e == 0 ? &r0[0][0] : &rec[0].x[e - 1][0];
-  const int STRIDE = e == 0 ? 3 : (int)(sizeof(TRec) / sizeof(int64_t));
+  constexpr int STRIDE = (int)(sizeof(TRec) / sizeof(int64_t));  // (R0's table rows padded to it)
 #if WG_ENC_EOBT
   // terminal keys carry their position in the low 4 bits (the scores there
   // are 0: states are masked to ~15 and the EOB costs are multiples of 16), so
@@ -630,11 +631,15 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
     cls_raw = ncls;
     eob_raw = neob;
 #endif
-    const int64_t m01 = c1 < c0 ? c1 : c0;
-    const int64_t m = c2 < m01 ? c2 : m01;
-    const uint32_t idx = (uint32_t)m & 15, pc = idx >> psh;
-    const uint32_t code = (idx & (uint32_t)psh) + (uint32_t)psh;  // R0: 0; R1 / R2: 1 (L0) or 2 (L0 + 1)
-    const uint32_t hm = (pc == 0 ? h0 : (pc == 1 ? h1 : h2)) | code << (2 * n);
+    // the winner's predecessor history by the min's own compares (its key's
+    // idx names the same predecessor: keys of different predecessors differ
+    // in idx, so the argmin is the key's pc)
+    const bool lt1 = c1 < c0;
+    const int64_t m01 = lt1 ? c1 : c0;
+    const bool lt2 = c2 < m01;
+    const int64_t m = lt2 ? c2 : m01;
+    const uint32_t code = (uint32_t)m & 3;  // the key's level code: R0 0; R1 / R2 1 (L0) or 2 (L0 + 1)
+    const uint32_t hm = (lt2 ? h2 : (lt1 ? h1 : h0)) | code << (2 * n);
 #if WG_ENC_TWO
     (void)two;
     // the new states, masked to the score before the broadcasts; lane 1's own
@@ -1952,7 +1957,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       WG_REP_END
 #endif
           const uint64_t pnz_mask = __ballot(pnz);
-          const int nlast = nlast_of(__ballot(pcap));
+          [[maybe_unused]] const int nlast = nlast_of(__ballot(pcap));
           lds_sync();
           DSTAMP(-1);
           // the trellis DP: one lane quad per candidate (lane 4c + k owns end context k)
@@ -2300,7 +2305,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               }
           }
           const uint64_t pnz_mask = __ballot(pnz);
-          const int nlast = nlast_of(__ballot(pcap));
+          [[maybe_unused]] const int nlast = nlast_of(__ballot(pcap));
           lds_sync();
           // quad q runs task q: walk the round's blocks to find its (block, context)
           int tnz = 0;  // this quad's task: nz of its levels
