@@ -42,6 +42,8 @@
 // All integer; bit-exact with the C restatement (oracle/lossy_rd.c).
 #include <cstdlib>
 #include <mutex>
+#include <random>
+#include <atomic>
 
 #include "vp8_tables.h"
 #include "wg_common.h"
@@ -186,7 +188,7 @@ struct Shared {
   uint8_t yin[YUV], yout[YUV], yout2[YUV];
   alignas(16) int16_t coeffs[400];
   uint8_t mbtail[64];  // wg_mb_enc bytes 800..863, staged so the record leaves in one 16-B-per-lane store
-  alignas(16) uint32_t handoff[12];  // the 48-B hand-off record, staged for three 16-B write-through stores
+  alignas(16) uint32_t handoff[16];  // the hand-off record, staged for its 16-B write-through stores
   uint8_t modes4[16];
   uint8_t nzy[16], nzuv[8];
   int mode_rate[4], mode_disto[4], uv_rate[4], uv_disto[4];
@@ -1167,6 +1169,23 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_sc1_128(uint8_t* p, u32x4_t v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
+__device__ __forceinline__ uint4 ld_sc1_128(const uint8_t* p) {
+  uint4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+// (WG_ENC_TAGGED) the row hand-off as four tagged 16-B granules a column:
+// word 3 of each is the writing row's tag (launch epoch x 2^14 + row + 1),
+// the other three carry the record's words 3p .. 3p + 2 (Y bottom row 0-3,
+// U 4-5, V 6-7, top nz 8, top modes 9, top DC nz 10).  A 16-B sc1 store is
+// seen whole (MI355X_MICROARCH.md, R2 granules), so the row below polls the
+// granules themselves: no progress counter, no store drain before a flag,
+// and the record arrives with the poll that finds it.  Stale granules carry
+// an older row's or launch's tag.
+#ifndef WG_ENC_TAGGED
+#define WG_ENC_TAGGED 1
+#endif
+__device__ __forceinline__ uint32_t row_tag(uint32_t epoch, int row) { return epoch * 0x4000u + (uint32_t)row + 1u; }
 
 struct EncArgs {
   const uint8_t* y;  // source planes (stride 16*mbw / 8*mbw), pitch per image
@@ -1189,6 +1208,7 @@ struct EncArgs {
   const int* order_tag;  // {ORDER_TAG ^ n_img, ~(ORDER_TAG ^ mbh)} when the schedule was built for this batch shape, else (row, image) order
   int64_t y_pitch, uv_pitch;
   int width, height, mbw, mbh, n_img, quality;
+  uint32_t epoch;  // this launch's tag base (WG_ENC_TAGGED)
 };
 
 constexpr uint64_t SPIN_TICKS = 200000000ull;
@@ -1535,7 +1555,35 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           seen = __shfl(v, 0, 64);
         }
       };
+#if WG_ENC_TAGGED
+      // the tagged record of column x of the row above (lane p < 4: granule p),
+      // polled until all four carry the row's tag
+      const uint32_t want = row_tag(a.epoch, mby - 1);
+      auto poll_rec = [&](const uint8_t* rec, int n) -> uint4 {
+        uint4 g = make_uint4(0, 0, 0, 0);
+        if (mby > 0) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          for (uint32_t it = 0;; it++) {
+            if (lane < n) g = ld_sc1_128(rec + 16 * lane);
+            if (__ballot(lane < n && g.w != want) == 0) break;
+            if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+                                    __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+              if (lane == 0) {
+                __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                wg::note_timeout(a.diag, mby, img, mbx, n, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x);
+              }
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+        return g;
+      };
+      uint4 above = make_uint4(0, 0, 0, 0);
+      if (isA) above = poll_rec(top + mbx * REC, 4);
+#else
       if (isA) wait_above(mbx + 1);
+#endif
       ESTAMP(1);
       const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
       const Segment& sg = s_seg[PAIR ? 0 : (LOOSE ? (q & 1) : grp)][segid];
@@ -1589,6 +1637,21 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       {
         const uint8_t* rec = top + mbx * REC;
         if (mby > 0) {
+#if WG_ENC_TAGGED
+          // lane p holds words 3p .. 3p + 2 (Y16 U8 V8 of the row above: words 0-7)
+          auto put = [&](int i, uint32_t w) {
+            const int o = i < 4 ? YOFF - BPS + 4 * i : (i < 6 ? UOFF - BPS + 4 * (i - 4) : VOFF - BPS + 4 * (i - 6));
+            *reinterpret_cast<uint32_t*>(s.yout + o) = w;
+          };
+          if (lane < 3) {
+            put(3 * lane, above.x);
+            put(3 * lane + 1, above.y);
+            if (lane < 2) put(3 * lane + 2, above.z);
+          }
+          top_nz = (uint32_t)__builtin_amdgcn_readlane((int)above.z, 2);
+          top_modes = (uint32_t)__builtin_amdgcn_readlane((int)above.x, 3);
+          top_nz_dc = __builtin_amdgcn_readlane((int)above.y, 3);
+#else
           if (lane < 8) {  // Y16 U8 V8 of the row above
             const uint32_t w = ld_sc1_32(rec + 4 * lane);
             const int o = lane < 4 ? YOFF - BPS + 4 * lane : (lane < 6 ? UOFF - BPS + 4 * (lane - 4) : VOFF - BPS + 4 * (lane - 6));
@@ -1597,6 +1660,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           top_nz = ld_sc1_32(rec + 32);
           top_modes = ld_sc1_32(rec + 36);
           top_nz_dc = (int)ld_sc1_32(rec + 40);
+#endif
         } else {
           if (lane < 21) s.yout[YOFF - BPS + lane] = 127;  // cols 0..20 (top-right incl.)
           else if (lane < 29) s.yout[UOFF - BPS + lane - 21] = 127;
@@ -1823,12 +1887,23 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             // row from the context fill) and its copies beside rows 3, 7, 11
             // for blocks 7, 11, 15 (fillPredContextParallel :455-562)
             if (mby > 0) {
+#if WG_ENC_TAGGED
+              // (granule 0 of column x + 1: its word 0 is the Y bottom row's pixels 0-3)
+              const uint32_t trn = mbx < mbw - 1 ? (uint32_t)__builtin_amdgcn_readfirstlane(
+                                                       (int)poll_rec(top + (mbx + 1) * REC, 1).x)
+                                                 : 0u;
+              if (lane == 0) {
+                const uint32_t tr = mbx < mbw - 1 ? trn : 0x01010101u * s.yout2[YOFF - BPS + 15];
+                *reinterpret_cast<uint32_t*>(s.yout2 + YOFF - BPS + 16) = tr;
+              }
+#else
               if (mbx < mbw - 1) wait_above(mbx + 2);
               if (lane == 0) {
                 const uint32_t tr = mbx < mbw - 1 ? ld_sc1_32(top + (mbx + 1) * REC)
                                                   : 0x01010101u * s.yout2[YOFF - BPS + 15];
                 *reinterpret_cast<uint32_t*>(s.yout2 + YOFF - BPS + 16) = tr;
               }
+#endif
               lds_sync();
             }
             if (lane < 12) {
@@ -2512,6 +2587,31 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       left_nz = out_l;
       // hand-off record for the row below, then publish: staged in LDS and
       // written as three 16-B write-through stores
+#if WG_ENC_TAGGED
+      // word i of the record at slot 4 (i / 3) + i % 3 of the staged granules,
+      // each granule's word 3 the row's tag; no drain, no flag
+      if (mby < mbh - 1) {
+        if (lane < 16) {
+          const int i = lane - lane / 4;  // (word 3 of a granule: lane 4p + 3)
+          uint32_t v = row_tag(a.epoch, mby);
+          if ((lane & 3) != 3) {
+            if (i < 8) {
+              const int so = i < 4 ? YOFF + 15 * BPS + 4 * i : (i < 6 ? UOFF + 7 * BPS + 4 * (i - 4) : VOFF + 7 * BPS + 4 * (i - 6));
+              v = *reinterpret_cast<const uint32_t*>(s.yout + so);
+            } else {
+              v = i == 8 ? out_t : (i == 9 ? new_top_modes : (i == 10 ? (uint32_t)new_top_dc : 0u));
+            }
+          }
+          s.handoff[lane] = v;
+        }
+        lds_sync();
+        if (lane < 4) {
+          const uint4 w = reinterpret_cast<const uint4*>(s.handoff)[lane];
+          u32x4_t v = {w.x, w.y, w.z, w.w};
+          st_sc1_128(top + mbx * REC + 16 * lane, v);
+        }
+      }
+#else
       if (mby < mbh - 1) {
         if (lane < 8) {
           const int so = lane < 4 ? YOFF + 15 * BPS + 4 * lane : (lane < 6 ? UOFF + 7 * BPS + 4 * (lane - 4) : VOFF + 7 * BPS + 4 * (lane - 6));
@@ -2534,6 +2634,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record is visible before the flag
       if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       // ================= outputs, export, contexts (exportParallel :1412-1495) =================
       MbEnc* o = a.out + mbi;
       {  // the record's tail (bytes 800..863) staged next to the levels in LDS
@@ -2817,6 +2918,7 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   // only for mbH >= 4; smaller frames take the serial encodeFrame (chroma DC
   // error diffusion, mid-frame proba refresh), which this kernel is not.
   if (mbh < 4) return wg::invalid("wg_encode_mbs needs mbh >= 4 (height > 48): encode.go:1356 encodes smaller frames serially");
+  WG_REQUIRE(mbh < 0x4000);  // (the hand-off tags hold the row in 14 bits)
   WG_REQUIRE(((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(work)) & 15) == 0);
   // Y rows move as 16-B pieces, U / V rows as 8-B pieces (k_encode_rows import / export)
   WG_REQUIRE(((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(ry)) & 15) == 0 &&
@@ -2875,6 +2977,12 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   a.diag = wg::diag_words(s);
   if (!a.diag) return WG_EHIP;
   a.diag += wg::DIAG_ENCODE;
+  {
+    // the hand-off tags' base: a fresh value per launch (from a random start,
+    // so a work buffer another process used does not hold this process's tags)
+    static std::atomic<uint32_t> g_epoch{std::random_device{}()};
+    a.epoch = g_epoch.fetch_add(1, std::memory_order_relaxed);
+  }
   if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(encode ctl)");
   int cus = 0, per_cu = 0, per_cu_pair = 0;
