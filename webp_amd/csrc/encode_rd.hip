@@ -124,6 +124,10 @@ struct alignas(8) TRec {
 };
 static_assert(sizeof(TRec) == 48, "TRec layout");
 
+// two int16 lanes of one word (packed 16-bit arithmetic: v_pk_*_i16 / v_dot2)
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int as_int(s16x2 v) { return __builtin_bit_cast(int, v); }
+__device__ __forceinline__ s16x2 as_s16x2(int v) { return __builtin_bit_cast(s16x2, v); }
 // two int16 values in one word (low = a)
 __device__ __forceinline__ uint32_t pack16(int a, int b) { return (uint32_t)(a & 0xffff) | (uint32_t)b << 16; }
 // four coefficients (each fits int16) into an 8-B aligned int16 row piece
@@ -1030,7 +1034,40 @@ __device__ __forceinline__ int ttrans_p(const P4& b) {
   }
   return sum;
 }
-__device__ __forceinline__ int tdisto_p(const P4& a, const P4& b) { return abs(ttrans_p(b) - ttrans_p(a)) >> 5; }
+// ttrans_p(b) - ttrans_p(a) in one pass: each pixel pair (b, a) as the two
+// int16 halves of a word (v_perm), the transform's butterflies packed
+// (|values| <= 4080), and sum_j w_j (|Tb_j| - |Ta_j|) as signed dot products
+// with (w_j, -w_j): the same integer as the two sums' difference
+__device__ __forceinline__ int ttrans_diff_p(const P4& a, const P4& b) {
+  const short kw[16] = {38, 32, 20, 9, 32, 28, 17, 7, 20, 17, 10, 4, 9, 7, 4, 2};
+  s16x2 tmp[16];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    s16x2 p[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)  // {b byte k, a byte k} as int16 halves
+      p[k] = as_s16x2((int)__builtin_amdgcn_perm(a.r[i], b.r[i], 0x0c000c00u | (uint32_t)(4 + k) << 16 | (uint32_t)k));
+    const s16x2 a0 = p[0] + p[2], a1 = p[1] + p[3], a2 = p[1] - p[3], a3 = p[0] - p[2];
+    tmp[4 * i] = a0 + a1;
+    tmp[4 * i + 1] = a3 + a2;
+    tmp[4 * i + 2] = a3 - a2;
+    tmp[4 * i + 3] = a0 - a1;
+  }
+  int sum = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const s16x2 a0 = tmp[i] + tmp[8 + i], a1 = tmp[4 + i] + tmp[12 + i];
+    const s16x2 a2 = tmp[4 + i] - tmp[12 + i], a3 = tmp[i] - tmp[8 + i];
+    const s16x2 o[4] = {a0 + a1, a3 + a2, a3 - a2, a0 - a1};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const short w = kw[4 * j + i];
+      sum = __builtin_amdgcn_sdot2(__builtin_elementwise_max(o[j], -o[j]), (s16x2){w, (short)-w}, sum, false);
+    }
+  }
+  return sum;
+}
+__device__ __forceinline__ int tdisto_p(const P4& a, const P4& b) { return abs(ttrans_diff_p(a, b)) >> 5; }
 __device__ __forceinline__ P4 predsq_p(int mode, const uint8_t* base, int size, int px, int py) {
   const int dc = predsq_dc(mode, base, size);
   P4 o;
@@ -2151,25 +2188,29 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             rec_row = pack4(rr[0], rr[1], rr[2], rr[3]);
             // tTransform row pass (ssim.go:266-304) of the reconstruction and the source
             int16_t* th = &s.co_buf[2 * qsl][0] + 8 * qr;  // co_buf is free again after the trellis prep
-            int4 tr, ts;
-            {
-              const int a0 = rr[0] + rr[2], a1 = rr[1] + rr[3], a2 = rr[1] - rr[3], a3 = rr[0] - rr[2];
-              tr = make_int4(a0 + a1, a3 + a2, a3 - a2, a0 - a1);
-            }
-            {
-              const int a0 = sr[0] + sr[2], a1 = sr[1] + sr[3], a2 = sr[1] - sr[3], a3 = sr[0] - sr[2];
-              ts = make_int4(a0 + a1, a3 + a2, a3 - a2, a0 - a1);
-            }
+            int4 tr = make_int4(0, 0, 0, 0), ts = tr;
             if constexpr (TAIL) {
-              // the column pass gets its inputs by a quad transpose of the row
-              // pass results, reconstruction and source packed in one word
-              // (|values| <= 1020)
-              int pk[4] = {(int)pack16(tr.x, ts.x), (int)pack16(tr.y, ts.y), (int)pack16(tr.z, ts.z),
-                           (int)pack16(tr.w, ts.w)};
+              // reconstruction and source as the two int16 halves of one word
+              // through both passes (|values| <= 4080): the row pass, then the
+              // column pass's inputs by a quad transpose
+              const s16x2 p0 = {(short)rr[0], (short)sr[0]}, p1 = {(short)rr[1], (short)sr[1]};
+              const s16x2 p2 = {(short)rr[2], (short)sr[2]}, p3 = {(short)rr[3], (short)sr[3]};
+              const s16x2 a0 = p0 + p2, a1 = p1 + p3, a2 = p1 - p3, a3 = p0 - p2;
+              int pk[4] = {as_int(a0 + a1), as_int(a3 + a2), as_int(a3 - a2), as_int(a0 - a1)};
               quad_transpose(pk);
 #pragma unroll
               for (int j = 0; j < 4; j++) tcol[j] = pk[j];
-            } else if (qact) {
+            } else {
+              {
+                const int a0 = rr[0] + rr[2], a1 = rr[1] + rr[3], a2 = rr[1] - rr[3], a3 = rr[0] - rr[2];
+                tr = make_int4(a0 + a1, a3 + a2, a3 - a2, a0 - a1);
+              }
+              {
+                const int a0 = sr[0] + sr[2], a1 = sr[1] + sr[3], a2 = sr[1] - sr[3], a3 = sr[0] - sr[2];
+                ts = make_int4(a0 + a1, a3 + a2, a3 - a2, a0 - a1);
+              }
+            }
+            if (!TAIL && qact) {
               reinterpret_cast<uint2*>(th)[0] = make_uint2(pack16(tr.x, tr.y), pack16(tr.z, tr.w));  // |values| <= 1020
               reinterpret_cast<uint2*>(th)[1] = make_uint2(pack16(ts.x, ts.y), pack16(ts.z, ts.w));
             }
@@ -2180,15 +2221,24 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           }
           if constexpr (!TAIL) lds_sync();
           int wrec = 0, wsrc = 0;  // weighted column sums of column qr
-          {
-            int cr[4], cs[4];
-            if constexpr (TAIL) {
+          if constexpr (TAIL) {
+            // the column pass on the packed pairs, then sum_j w_j (|rec_j| - |src_j|)
+            // as one signed dot product a coefficient with (w_j, -w_j): the
+            // TDisto difference of the quad's sums is the sum of these
+            const s16x2 c0 = as_s16x2(tcol[0]), c1 = as_s16x2(tcol[1]), c2 = as_s16x2(tcol[2]), c3 = as_s16x2(tcol[3]);
+            const s16x2 a0 = c0 + c2, a1 = c1 + c3, a2 = c1 - c3, a3 = c0 - c2;
+            const s16x2 o[4] = {a0 + a1, a3 + a2, a3 - a2, a0 - a1};
+            // kWeightY (ssim.go:257) column qr, one byte per row
+            const uint32_t wcol = qr == 0 ? 0x09142026u : (qr == 1 ? 0x07111c20u : (qr == 2 ? 0x040a1114u : 0x02040709u));
 #pragma unroll
-              for (int j = 0; j < 4; j++) {
-                cr[j] = (int)(int16_t)(tcol[j] & 0xffff);
-                cs[j] = tcol[j] >> 16;
-              }
-            } else {
+            for (int j = 0; j < 4; j++) {
+              const short w = (short)((wcol >> (8 * j)) & 0xff);
+              const s16x2 m = __builtin_elementwise_max(o[j], -o[j]);
+              wrec = __builtin_amdgcn_sdot2(m, (s16x2){w, (short)-w}, wrec, false);
+            }
+          } else {
+            int cr[4], cs[4];
+            {
               const int16_t* tx = &s.co_buf[2 * qsl][0];
 #pragma unroll
               for (int j = 0; j < 4; j++) {
@@ -2208,7 +2258,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               wsrc = w0 * abs(a0 + a1) + w1 * abs(a3 + a2) + w2 * abs(a3 - a2) + w3 * abs(a0 - a1);
             }
           }
-          const int sse_q = quad_sum(sse_r), wrec_q = quad_sum(wrec), wsrc_q = quad_sum(wsrc);
+          const int sse_q = quad_sum(sse_r), wrec_q = quad_sum(wrec), wsrc_q = TAIL ? 0 : quad_sum(wsrc);
           int disto = sse_q;
           if (sg.tlambda_sd > 0) disto += (sg.tlambda_sd * (abs(wrec_q - wsrc_q) >> 5) + 128) >> 8;
           CSTAMP(2);
