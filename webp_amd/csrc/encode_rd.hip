@@ -929,7 +929,19 @@ __device__ __forceinline__ int ttrans(const int px[16]) {  // tTransform (ssim.g
   return sum;
 }
 __device__ __forceinline__ int tdisto(const int a[16], const int b[16]) { return abs(ttrans(b) - ttrans(a)) >> 5; }
+#ifndef WG_ENC_FDCT_PK  // FTransform on packed int16 row pairs (wg::fdct4x4_pk)
+#define WG_ENC_FDCT_PK 1
+#endif
 __device__ __forceinline__ void fdct(const int src[16], const int pred[16], int co[16]) {
+#if WG_ENC_FDCT_PK
+  wg::s16x2_t d01[4], d32[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    d01[k] = (wg::s16x2_t){(short)(src[k] - pred[k]), (short)(src[4 + k] - pred[4 + k])};
+    d32[k] = (wg::s16x2_t){(short)(src[12 + k] - pred[12 + k]), (short)(src[8 + k] - pred[8 + k])};
+  }
+  wg::fdct4x4_pk(d01, d32, co);
+#else
   int d[16];
   int16_t o[16];
 #pragma unroll
@@ -937,6 +949,7 @@ __device__ __forceinline__ void fdct(const int src[16], const int pred[16], int 
   fdct4x4(d, o);
 #pragma unroll
   for (int i = 0; i < 16; i++) co[i] = o[i];
+#endif
 }
 __device__ __forceinline__ void store4x4(uint8_t* p, const int v[16]) {
 #pragma unroll
@@ -979,6 +992,20 @@ __device__ __forceinline__ int sse_p(const P4& a, const P4& b) {
 }
 // FTransform of (src - pred), rows unpacked one at a time
 __device__ __forceinline__ void fdct_p(const P4& s, const P4& p, int co[16]) {
+#if WG_ENC_FDCT_PK
+  // (byte k of rows a and b as the int16 halves of a word: one v_perm each)
+  wg::s16x2_t d01[4], d32[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t sel = 0x0c000c00u | (uint32_t)(4 + k) << 16 | (uint32_t)k;
+    d01[k] = __builtin_bit_cast(wg::s16x2_t, __builtin_amdgcn_perm(s.r[1], s.r[0], sel)) -
+             __builtin_bit_cast(wg::s16x2_t, __builtin_amdgcn_perm(p.r[1], p.r[0], sel));
+    d32[k] = __builtin_bit_cast(wg::s16x2_t, __builtin_amdgcn_perm(s.r[2], s.r[3], sel)) -
+             __builtin_bit_cast(wg::s16x2_t, __builtin_amdgcn_perm(p.r[2], p.r[3], sel));
+  }
+  wg::fdct4x4_pk(d01, d32, co);
+  return;
+#endif
   int tmp[16];
 #pragma unroll
   for (int r = 0; r < 4; r++) {

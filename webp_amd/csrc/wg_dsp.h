@@ -190,6 +190,47 @@ __device__ __forceinline__ void fdct4x4(const int d[16], int16_t out[16]) {
   }
 }
 
+// The same FTransform on packed int16 pairs: dp01[k] = (d[k], d[4 + k])
+// (rows 0 and 1 of column k), dp32[k] = (d[12 + k], d[8 + k]) (rows 3 and 2).
+// The row pass runs two rows an instruction; its rotations and the column
+// pass's four outputs are signed dot products (v_dot2_i32_i16) of the pairs
+// (row sums P + Q = (a0, a1), differences P - Q = (a3, a2)).  Every value
+// fits int16 (row outputs <= 8160 in magnitude, column sums <= 16320) and
+// every dot product is exact in int32: the outputs equal fdct4x4's.
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+// VOP3P v_dot2_i32_i16 with its accumulator as an operand (the builtin's
+// v_dot2c form accumulates in place: a v_mov of the constant before each)
+__device__ __forceinline__ int sdot2_acc(s16x2_t a, s16x2_t b, int c) {
+  int r;
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ void fdct4x4_rowpair(const s16x2_t d[4], s16x2_t t[4]) {
+  const s16x2_t a0 = d[0] + d[3], a1 = d[1] + d[2], a2 = d[1] - d[2], a3 = d[0] - d[3];
+  t[0] = (a0 + a1) << (short)3;
+  t[2] = (a0 - a1) << (short)3;
+  const s16x2_t x = {a2.x, a3.x}, y = {a2.y, a3.y};  // (a2, a3) of each row
+  const s16x2_t k1 = {2217, 5352}, k3 = {-5352, 2217};
+  t[1] = (s16x2_t){(short)(sdot2_acc(x, k1, 1812) >> 9),
+                   (short)(sdot2_acc(y, k1, 1812) >> 9)};
+  t[3] = (s16x2_t){(short)(sdot2_acc(x, k3, 937) >> 9),
+                   (short)(sdot2_acc(y, k3, 937) >> 9)};
+}
+__device__ __forceinline__ void fdct4x4_pk(const s16x2_t dp01[4], const s16x2_t dp32[4], int out[16]) {
+  s16x2_t P[4], Q[4];  // P[c] = (row 0, row 1), Q[c] = (row 3, row 2) of the row pass
+  fdct4x4_rowpair(dp01, P);
+  fdct4x4_rowpair(dp32, Q);
+  const s16x2_t one = {1, 1}, pm = {1, -1}, k4 = {5352, 2217}, k12 = {2217, -5352};
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const s16x2_t S = P[c] + Q[c], D = P[c] - Q[c];  // (a0, a1), (a3, a2)
+    out[c] = (int16_t)(sdot2_acc(S, one, 7) >> 4);
+    out[8 + c] = (int16_t)(sdot2_acc(S, pm, 7) >> 4);
+    out[4 + c] = (int16_t)((sdot2_acc(D, k4, 12000) >> 16) + (D.x != 0));
+    out[12 + c] = (int16_t)(sdot2_acc(D, k12, 51000) >> 16);
+  }
+}
+
 // ------------------------------------------------------------------------
 // 4x4 intra prediction, one row per lane (predict_lossy.go:185-424).
 // ctx: X = top-left, T[0..7] = top row incl. top-right, L[0..3] = left column.
