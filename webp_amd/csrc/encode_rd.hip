@@ -568,6 +568,11 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   constexpr int TSTR = sizeof(TokRow) / 2;
   uint32_t eob_raw = FIRST < 15 ? eobp[kBand[FIRST + 1] * TSTR] : 0;
 #endif
+  // The tail's level records (lane r: positions 4r - 1 .. 4r + 3), loaded
+  // now: their latency hides under the walk instead of adding a round trip
+  // after it (l0s rows are 32 B, 8-B aligned at 4r)
+  const uint2 l0w = *reinterpret_cast<const uint2*>(l0s + 4 * k);
+  const int l0prev = l0s[max(4 * k - 1, 0)];
   // Position n's row, class and EOB cost are loaded during position n - 1
   // and pinned by the asm below, so no LDS round trip sits on the chain.
   int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
@@ -708,18 +713,18 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   {  // (the level before position 4r: the context of 4r's token)
     const int n = max(4 * r - 1, 0);
     const int code = r == 0 ? 0 : (int)((hist >> (2 * n)) & 3);
-    mags[0] = code == 0 ? 0 : (l0s[n] >> 3) + code - 1;
+    mags[0] = code == 0 ? 0 : (l0prev >> 3) + code - 1;
   }
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int n = 4 * r + j;
     const int code = (int)((hist >> (2 * n)) & 3);
-    const int ls = l0s[n];
+    const int ls = (int)(((j < 2 ? l0w.x : l0w.y) >> (16 * (j & 1))) & 0xffff);  // (l0s values are < 2^14)
     const int mag = code == 0 ? 0 : (ls >> 3) + code - 1;
     mags[j + 1] = mag;
     q[zig_of(n)] = (int16_t)((ls & 4) ? -mag : mag);
   }
-  if (k == 0) *nz = nzc;
+  *nz = nzc;  // (every lane of the quad: the callers pass registers)
   if (rate) {
     // TokenCostForCoeffs (encode_quant.go:154-223) of the chosen levels, lane r
     // taking positions 4r .. 4r + 3 (FIRST 0 only: the I4 blocks), summed over
@@ -735,7 +740,7 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
       part += n < nzc ? tokc : (n == nzc ? eobc : 0);
     }
     part = quad_sum(part);
-    if (k == 0) *rate = part;
+    *rate = part;  // (the quad's sum, in every lane)
   }
 }
 
@@ -2072,6 +2077,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       WG_REP_END
 #endif
           lds_sync();
+          // (TRELLIS + TAIL) the candidate's nz count and rate, straight from
+          // the DP into the reconstruction quad's registers (the same lanes)
+          int dp_nz = 0, dp_rate = 0;
           if constexpr (TRELLIS) {
           // trellis positions: lane (candidate c, pair pp) prepares positions 2pp, 2pp + 1
           const int lam16 = sg.tlambda_i4 * 16;
@@ -2112,20 +2120,26 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
 #if WG_ENC_NLAST
               if (nlast < 8)
                 trellis_dp4<0, 3, 8>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl],
-                                     &s.cand_nz[sl], WG_ENC_TAIL ? &s.cand_rate[sl] : nullptr);
+                                     &dp_nz, WG_ENC_TAIL ? &dp_rate : nullptr);
               else
 #endif
-              trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &s.cand_nz[sl],
-                                WG_ENC_TAIL ? &s.cand_rate[sl] : nullptr);
+              trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &dp_nz,
+                                WG_ENC_TAIL ? &dp_rate : nullptr);
+              if constexpr (!WG_ENC_TAIL) {
+                if ((hl & 3) == 0) s.cand_nz[sl] = dp_nz;
+              }
 #if defined(WG_EXP_REP_DP)
       WG_REP_END
 #endif
               __builtin_amdgcn_s_setprio(2);
-            } else if ((hl & 3) == 0) {
+            } else {
+              dp_nz = 0;
+              dp_rate = t.tok[3 * 8].eob[nz_ctx];  // EOB at position 0
+              if ((hl & 3) == 0) {
 #pragma unroll
-              for (int i = 0; i < 16; i++) s.cand_q[sl][i] = 0;
-              s.cand_nz[sl] = 0;
-              s.cand_rate[sl] = t.tok[3 * 8].eob[nz_ctx];  // EOB at position 0
+                for (int i = 0; i < 16; i++) s.cand_q[sl][i] = 0;
+                s.cand_nz[sl] = 0;
+              }
             }
           }
           lds_sync();
@@ -2139,7 +2153,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           // reconstruction, TDisto and token-cost streams interleave: lanes past
           // the candidates repeat candidate 2's work, or work on an unused
           // slot, and nothing reads their results)
-          // (TAIL) the trellis DP leaves each candidate's rate in cand_rate, and
+          // (TAIL) the trellis DP leaves each candidate's rate in dp_rate, and
           // the inverse DCT's vertical pass runs one column a quad lane,
           // transposed across the quad by DPP: 4 levels and 4 products a lane
           // instead of 16 and 16
@@ -2157,7 +2171,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           {
             CSTAMP(1);
             int res[4], pr[4], sr[4], rr[4];
-            qnz = s.cand_nz[qsl];
+            qnz = (TRELLIS && WG_ENC_TAIL) ? dp_nz : s.cand_nz[qsl];
             if constexpr (TAIL) {
               // column qr: levels qr, 4 + qr, 8 + qr, 12 + qr (raster)
               const int16_t* cq = s.cand_q[qsl];
@@ -2294,7 +2308,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           // v_readlane (wave-uniform lanes) instead of LDS permutes
           int tok_rate;
           if constexpr (TAIL) {
-            tok_rate = s.cand_rate[qsl];
+            tok_rate = dp_rate;
           } else {
             part = group_sum_first<8>(part);
             const int r00 = __builtin_amdgcn_readlane(part, 0), r01 = __builtin_amdgcn_readlane(part, 8);
