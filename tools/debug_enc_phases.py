@@ -34,6 +34,8 @@ if STAMPED:
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record(); frames.encode_mbs(Yt, Ut, Vt, W, H, seg_ids, segs, O.default_proba(), out=out, recon=rec); e1.record()
 torch.cuda.synchronize()
+mbt = out[:, 848].cpu().numpy()  # wg_mb_enc mb_type (0 = I16, 1 = I4)
+print(f"[{content}] I16 share {float((mbt == 0).mean()):.3f}")
 if not STAMPED:
     print(f"[{content}] {e0.elapsed_time(e1):.3f} ms")
     sys.exit(0)

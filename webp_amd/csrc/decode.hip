@@ -91,6 +91,32 @@ __device__ __forceinline__ int4 ld_stream(const int4* p) {
 #endif
 }
 __device__ __forceinline__ uint64_t lds64(const uint8_t* p) { return *reinterpret_cast<const uint64_t*>(p); }
+
+// Diagnostic builds only (WRITE_SIZE per store site, tools/gpu_dec_write_sites.sh):
+// bit k of WG_DEC_SKIPW drops k_decode_bands' store site k (1 top record,
+// 2 bottom record, 4 Y rows, 8 U/V rows, 16 Y rows 13..15 above, 32 U/V rows
+// 5..7 above); the output is then wrong, the control flow unchanged.
+#ifndef WG_DEC_SKIPW
+#define WG_DEC_SKIPW 0
+#endif
+#define DEC_SITE(bit) ((WG_DEC_SKIPW & (bit)) == 0)
+// k_decode_bands' frame stores (WG_DEC_NTST: non-temporal, an experiment on
+// the partial-line write-backs tools/gpu_dec_write_sites.sh measures)
+__device__ __forceinline__ void frame_st16(uint8_t* p, uint4 w) {
+#ifdef WG_DEC_NTST
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(v4u{w.x, w.y, w.z, w.w}, reinterpret_cast<v4u*>(p));
+#else
+  *reinterpret_cast<uint4*>(p) = w;
+#endif
+}
+__device__ __forceinline__ void frame_st8(uint8_t* p, uint64_t w) {
+#ifdef WG_DEC_NTST
+  __builtin_nontemporal_store(w, reinterpret_cast<uint64_t*>(p));
+#else
+  *reinterpret_cast<uint64_t*>(p) = w;
+#endif
+}
 __device__ __forceinline__ uint32_t lds32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 
 static_assert(sizeof(wg_mb_info) == 32 && offsetof(wg_mb_info, imodes) == 8 && offsetof(wg_mb_info, is_i4x4) == 24 &&
@@ -552,7 +578,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
               const uint64_t u = lds64(wb + LU + 7 * WG_BPS), v = lds64(wb + LV + 7 * WG_BPS);
               w = make_uint4((uint32_t)u, (uint32_t)(u >> 32), (uint32_t)v, (uint32_t)(v >> 32));
             }
-            st_sc1_128(top + mbx * TOP_BYTES + 16 * k, w);
+            if (DEC_SITE(1)) st_sc1_128(top + mbx * TOP_BYTES + 16 * k, w);
           }
         }
         if (lane < 16) {
@@ -599,7 +625,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
               const uint64_t a0 = lds64(src), a1 = lds64(src + FC_STRIDE);
               w = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
             }
-            st_sc1_128(bot_img + x * BOT_BYTES + 16 * k, w);
+            if (DEC_SITE(2)) st_sc1_128(bot_img + x * BOT_BYTES + 16 * k, w);
           }
         }
         {
@@ -629,17 +655,17 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
           const int ylim = to_lds || hand ? 13 : 16, clim = to_lds || (hand && !luma_only) ? 5 : 8;
           if (lane < 48) {  // Y: row lane & 15, MB y0 + (lane >> 4)
             const int j = lane & 15, x = y0 + (lane >> 4);
-            if (y0 >= 0 && j < ylim && x <= y1) {
+            if (DEC_SITE(4) && y0 >= 0 && j < ylim && x <= y1) {
               const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
-              *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby + j) * ys + 16 * x) = w;
+              frame_st16(Yp + (int64_t)(16 * mby + j) * ys + 16 * x, w);
             }
           }
 #pragma unroll
           for (int h = 0; h < 2; h++) {  // U, V: row (i & 15), MB c0 + (i >> 4)
             const int i = lane + 64 * h, pl = (i >> 3) & 1, j = i & 7, x = c0 + (i >> 4);
-            if (c0 >= 0 && i < 80 && j < clim && x <= c1)
-              *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x) =
-                  lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx));
+            if (DEC_SITE(8) && c0 >= 0 && i < 80 && j < clim && x <= c1)
+              frame_st8((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x,
+                        lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
           }
           if (mby > 0) {
             // rows 13..15 / 5..7 of the MBs above, final after our top-edge
@@ -659,14 +685,14 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
             }
             if (lane < 6) {
               const int rr = 1 + (lane >> 1), part = lane & 1, x = t0 + part;
-              if (t0 >= 0 && x <= t1)
-                *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * x) =
-                    *reinterpret_cast<const uint4*>(fy + rr * FY_STRIDE + FY_X0 + 16 * (x - mbx));
+              if (DEC_SITE(16) && t0 >= 0 && x <= t1)
+                frame_st16(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * x,
+                           *reinterpret_cast<const uint4*>(fy + rr * FY_STRIDE + FY_X0 + 16 * (x - mbx)));
             } else if ((from_lds || !luma_only) && lane >= 8 && lane < 32) {
               const int k = lane - 8, pl = k >= 12, rr = 1 + (k % 12) / 4, q = k & 3, x = u0 + q;
-              if (u0 >= 0 && x <= u1)
-                *reinterpret_cast<uint64_t*>((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * x) =
-                    lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0 + 8 * (x - mbx));
+              if (DEC_SITE(32) && u0 >= 0 && x <= u1)
+                frame_st8((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * x,
+                          lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
             }
           }
         }

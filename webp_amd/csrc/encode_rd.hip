@@ -226,13 +226,32 @@ struct Shared {
 #ifndef WG_ENC_HOIST  // I4 candidates' prediction / source rows read before the trellis (see the I4 RD)
 #define WG_ENC_HOIST 1
 #endif
+#ifndef WG_ENC_I16ONE  // the final I16 trellis in one round, every block's DP for its three start contexts (see there)
+#define WG_ENC_I16ONE 1
+#endif
 #ifndef WG_ENC_DPAHEAD  // positions the trellis DP loads ahead (1 or 2: measured equal, 1 kept)
 #define WG_ENC_DPAHEAD 1
 #endif
+#if WG_ENC_I16ONE
+  // (the final I16 trellis, WG_ENC_I16ONE: the 16 blocks' records of one
+  // half of the positions at a time, 9 records apart, and all 16 blocks'
+  // level records)
+  union {
+    TRec trec[6][16 + WG_ENC_TPAD];
+    TRec trec16[16][9];
+  };
+  int64_t r0[16][6];       // the phase's level-0 trellis row (trellis_r0; [3..5] unused: a TRec's stride)
+  int64_t eobl[16][2];     // the phase's terminal costs x lam16 (trellis_r0, WG_ENC_EOBT)
+  union {
+    int16_t l0s[6][16];    // per position: L0 << 3 | negative << 2 | min(L0, 2) (< 2^14)
+    int16_t l0s16[16][16];
+  };
+#else
   TRec trec[6][16 + WG_ENC_TPAD];
   int64_t r0[16][6];       // the phase's level-0 trellis row (trellis_r0; [3..5] unused: a TRec's stride)
   int64_t eobl[16][2];     // the phase's terminal costs x lam16 (trellis_r0, WG_ENC_EOBT)
   int16_t l0s[6][16];      // per position: L0 << 3 | negative << 2 | min(L0, 2) (< 2^14)
+#endif
   alignas(16) int16_t cand_q[6][16];  // I4 candidates' levels for the lane-parallel token cost
   int cand_nz[6], cand_rate[6];
   alignas(16) uint8_t pv[2][64];  // per half-wave: the I4 block's prediction value table
@@ -742,6 +761,98 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
     part = quad_sum(part);
     *rate = part;  // (the quad's sum, in every lane)
   }
+}
+
+// The I16 AC blocks' trellis for all three start contexts at once
+// (WG_ENC_I16ONE).  A block's start context enters the DP only as its initial
+// state, so the three DPs of trellis_dp4 share every record and terminal
+// load: the quad carries three independent state sets (start s: context
+// states ps[s][], histories h[s][], best terminal bt[s] / bh[s]), each
+// updated exactly as trellis_dp4 updates its one (same keys, same compares,
+// WG_ENC_TWO / EOBT records), so start s's result is trellis_dp4's for
+// init_ctx s.  Walked in two halves (positions [NB, NE)), the records of
+// the half at `mine` (`mine[n * STRIDE]` = this lane's row at position n).
+struct DP3 {
+  int64_t ps[3][3];  // [start context][context]: the states, masked to the score
+  uint32_t h[3][3];
+  int64_t bt[3];     // the best terminal of the lane's context, per start
+  uint32_t bh[3];
+};
+__device__ __forceinline__ void dp3_init(DP3& S, const Tables& t, int lam16) {
+  constexpr int64_t BIG = 1ll << 59;
+  const TokRow& t_init = t.tok[1];  // type 0, kBand[1] = 1
+#pragma unroll
+  for (int s = 0; s < 3; s++) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      S.ps[s][c] = c == s ? 0 : BIG;
+      S.h[s][c] = 0;
+    }
+    S.bt[s] = (int64_t)t_init.eob[s] * lam16;
+    S.bh[s] = 0;
+  }
+}
+template <int NB, int NE>
+__device__ __forceinline__ void dp3_walk(DP3& S, const int64_t* mine, const int64_t* eobq) {
+  constexpr int STRIDE = (int)(sizeof(TRec) / sizeof(int64_t));
+  int64_t x0 = mine[NB * STRIDE], x1 = mine[NB * STRIDE + 1], x2 = mine[NB * STRIDE + 2];
+  int64_t eob_raw = eobq[2 * NB];
+#pragma unroll
+  for (int n = NB; n < NE; n++) {
+    int64_t nx0 = 0, nx1 = 0, nx2 = 0, neob = 0;
+    if (n + 1 < NE) {
+      nx0 = mine[(n + 1) * STRIDE];
+      nx1 = mine[(n + 1) * STRIDE + 1];
+      nx2 = mine[(n + 1) * STRIDE + 2];
+      neob = eobq[2 * (n + 1)];
+    }
+    asm volatile("" : "+v"(S.ps[0][0]), "+v"(S.ps[1][1]), "+v"(S.ps[2][2]), "+v"(S.bt[0]), "+v"(S.bt[1]),
+                 "+v"(S.bt[2])::"memory");
+    const int64_t eob_n = eob_raw;
+#pragma unroll
+    for (int s = 0; s < 3; s++) {
+      const int64_t c0 = S.ps[s][0] + x0, c1 = S.ps[s][1] + x1, c2 = S.ps[s][2] + x2;
+      const bool lt1 = c1 < c0;
+      const int64_t m01 = lt1 ? c1 : c0;
+      const bool lt2 = c2 < m01;
+      const int64_t m = lt2 ? c2 : m01;
+      const uint32_t code = (uint32_t)m & 3;
+      // (values, not lvalues: a conditional of two array elements compiles
+      // to a select of their addresses and a load, i.e. S in scratch)
+      const uint32_t hv0 = S.h[s][0], hv1 = S.h[s][1], hv2 = S.h[s][2];
+      const uint32_t hm = (lt2 ? hv2 : (lt1 ? hv1 : hv0)) | code << (2 * n);
+      const int64_t mm = m & ~15ll;
+      S.ps[s][0] = quad_bcast<0>(mm);
+      S.ps[s][1] = quad_bcast<1>(mm);
+      S.ps[s][2] = quad_bcast<2>(mm);
+      S.h[s][0] = quad_bcast32<0>(hm);
+      S.h[s][1] = quad_bcast32<1>(hm);
+      S.h[s][2] = quad_bcast32<2>(hm);
+      const int64_t eobs = mm + eob_n;
+      const bool w = eobs < S.bt[s];
+      S.bt[s] = w ? eobs : S.bt[s];
+      S.bh[s] = w ? hm : S.bh[s];
+    }
+    x0 = nx0;
+    x1 = nx1;
+    x2 = nx2;
+    eob_raw = neob;
+  }
+}
+// start s's chosen history: the first strict minimum over (position, context
+// 1 then 2) of its terminals, as at the end of trellis_dp4
+__device__ __forceinline__ uint32_t dp3_hist(const DP3& S, int s) {
+  const int64_t b0 = S.bt[0], b1 = S.bt[1], b2 = S.bt[2];
+  const uint32_t g0 = S.bh[0], g1 = S.bh[1], g2 = S.bh[2];
+  const int64_t b = s == 0 ? b0 : (s == 1 ? b1 : b2);
+  const uint32_t h = s == 0 ? g0 : (s == 1 ? g1 : g2);
+  const int64_t bt1 = quad_bcast<1>(b), bt2 = quad_bcast<2>(b);
+  const uint32_t bh1 = quad_bcast32<1>(h), bh2 = quad_bcast32<2>(h);
+  return bt2 < bt1 ? bh2 : bh1;
+}
+__device__ __forceinline__ int hist_nz(uint32_t hist) {
+  const uint32_t nzb = (hist | hist >> 1) & 0x55555555u;
+  return nzb == 0 ? 0 : ((31 - __builtin_clz(nzb)) >> 1) + 1;
 }
 
 // TokenCostForCoeffs's term for position n alone (lane-parallel form of
@@ -2449,6 +2560,79 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         // contexts.  (Walking the 7 block diagonals took 7 prep + DP rounds.)
         const int lam16 = sg.tlambda_i16 * 16;
         trellis_r0<0>(t, lane, lam16, s.r0, s.eobl);  // (read after the first round's lds_sync)
+#if WG_ENC_I16ONE
+        // One round (WG_ENC_I16ONE): quad q runs block q's DP for all three
+        // start contexts at once (dp3_walk), over the records of positions
+        // 0..7, then (the same LDS, rewritten) 8..15; lane 4q + r preps
+        // positions 2r, 2r + 1 of each half.  Then the raster-order
+        // resolution on scalars, and each quad writes its block's levels for
+        // the context it resolved to.  Measured against the three rounds of
+        // up to 16 speculative DPs below: see DESIGN.md (round 5).
+        {
+          const int q = lane >> 2, r = lane & 3, e = min(r, 2);
+          uint64_t pnz_mask = 0;
+          DP3 S;
+          dp3_init(S, t, lam16);
+          const int64_t* eobq = &s.eobl[0][(e == 2 ? 2 : 1) - 1];
+#pragma unroll
+          for (int half = 0; half < 2; half++) {
+            {
+              TRec rr[2];
+              int l0[2];
+              const int n0 = 8 * half + 2 * r;
+              const bool pnz = trellis_prep2<0, 1>(t, s.co_buf[q], n0, sg.y1, lam16, rr, l0);
+              pnz_mask |= __ballot(pnz);
+#pragma unroll
+              for (int k = 0; k < 2; k++) {
+                if (n0 + k >= 1) s.trec16[q][2 * r + k] = rr[k];
+                s.l0s16[q][n0 + k] = (int16_t)l0[k];
+              }
+            }
+            lds_sync();
+            // this lane's row at position n: R0 from the phase's table, R1 / R2
+            // from the half's records (position n at record n - 8 half)
+            const int64_t* mine =
+                e == 0 ? &s.r0[0][0]
+                       : reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(&s.trec16[q][0].x[e - 1][0]) -
+                                                          8 * half * (int)sizeof(TRec));
+            if (half == 0) dp3_walk<1, 8>(S, mine, eobq);
+            else dp3_walk<8, 16>(S, mine, eobq);
+            lds_sync();  // (the second half's records overwrite the first's)
+          }
+          const uint32_t hs0 = dp3_hist(S, 0), hs1 = dp3_hist(S, 1), hs2 = dp3_hist(S, 2);
+          // bit 4 q: block q's levels from start context s are non-zero (the
+          // all-zero pre-scan: a block with no level at any position is zero)
+          const bool bnz = ((pnz_mask >> (4 * q)) & 15) != 0;
+          const uint64_t nzm0 = __ballot(r == 0 && bnz && hs0 != 0);
+          const uint64_t nzm1 = __ballot(r == 0 && bnz && hs1 != 0);
+          const uint64_t nzm2 = __ballot(r == 0 && bnz && hs2 != 0);
+          // the reference's raster order, on scalars: block qb's context from
+          // its left / top neighbours' resolved nz
+          uint32_t nzbits = 0, ctxs = 0;
+          for (int qb = 0; qb < 16; qb++) {
+            const int qbx = qb & 3, qby = qb >> 2;
+            const int l = qbx > 0 ? (int)((nzbits >> (qb - 1)) & 1) : (int)((left_nz >> qby) & 1);
+            const int tp = qby > 0 ? (int)((nzbits >> (qb - 4)) & 1) : (int)((top_nz >> qbx) & 1);
+            const int cx = min(l + tp, 2);
+            const uint64_t nzm = cx == 0 ? nzm0 : (cx == 1 ? nzm1 : nzm2);
+            nzbits |= (uint32_t)((nzm >> (4 * qb)) & 1) << qb;
+            ctxs |= (uint32_t)cx << (2 * qb);
+          }
+          const int cq = (int)(ctxs >> (2 * q)) & 3;
+          const uint32_t hist = !bnz ? 0u : (cq == 0 ? hs0 : (cq == 1 ? hs1 : hs2));
+          const uint2 l0w = *reinterpret_cast<const uint2*>(&s.l0s16[q][4 * r]);
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int n = 4 * r + j;
+            const int code = (int)((hist >> (2 * n)) & 3);
+            const int ls = (int)(((j < 2 ? l0w.x : l0w.y) >> (16 * (j & 1))) & 0xffff);
+            const int mag = code == 0 ? 0 : (ls >> 3) + code - 1;
+            s.coeffs[q * 16 + zig_of(n)] = (int16_t)((ls & 4) ? -mag : mag);
+          }
+          if (r == 0) s.nzy[q] = (uint8_t)hist_nz(hist);
+          lds_sync();
+        }
+#else
         int16_t* res_q = reinterpret_cast<int16_t*>(s.yout2);  // [16 tasks][16] levels (yout2 is free for I16 MBs)
         int* res_nz = reinterpret_cast<int*>(s.yout2 + 512);   // [16]
         uint32_t nzbits = 0;  // the resolved blocks' nz flags (bit = block), a scalar across the rounds
@@ -2535,6 +2719,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           }
           lds_sync();
         }
+#endif
         }  // TRELLIS
       }
       if (lane < 8) {  // chroma
