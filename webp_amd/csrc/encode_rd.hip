@@ -526,6 +526,37 @@ __device__ __forceinline__ int quad_bcast32(int v) {
   return __builtin_amdgcn_mov_dpp(v, J | J << 2 | J << 4 | J << 6, 0xf, 0xf, false);
 }
 
+// (WG_ENC_DPPADD) c_j = (lane j of this lane's quad's s) + x_j, j = 0, 1, 2,
+// 64-bit: the quad broadcasts fused into the adds' DPP source operand (two
+// VOP2 DPP adds each, instead of two v_mov_dpp and two adds).  NOP: the
+// wait states before the first DPP read of s (2 after a VALU write of it,
+// 5 after an EXEC write: the walks' first position takes 5).
+#ifndef WG_ENC_DPPADD
+#define WG_ENC_DPPADD 1
+#endif
+template <int NOP>
+__device__ __forceinline__ void quad_bcast_add3(int64_t s, int64_t x0, int64_t x1, int64_t x2, int64_t& c0,
+                                                int64_t& c1, int64_t& c2) {
+  static_assert(NOP == 1 || NOP == 4, "s_nop count");
+  uint32_t a0, b0, a1, b1, a2, b2;
+  asm volatile(
+      "s_nop %c14\n\t"
+      "v_add_co_u32_dpp %0, vcc, %6, %8 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t"
+      "v_addc_co_u32_dpp %1, vcc, %7, %9, vcc quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_co_u32_dpp %2, vcc, %6, %10 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t"
+      "v_addc_co_u32_dpp %3, vcc, %7, %11, vcc quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_co_u32_dpp %4, vcc, %6, %12 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_addc_co_u32_dpp %5, vcc, %7, %13, vcc quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf"
+      : "=&v"(a0), "=&v"(b0), "=&v"(a1), "=&v"(b1), "=&v"(a2), "=&v"(b2)
+      : "v"((uint32_t)s), "v"((uint32_t)((uint64_t)s >> 32)), "v"((uint32_t)x0), "v"((uint32_t)((uint64_t)x0 >> 32)),
+        "v"((uint32_t)x1), "v"((uint32_t)((uint64_t)x1 >> 32)), "v"((uint32_t)x2), "v"((uint32_t)((uint64_t)x2 >> 32)),
+        "i"(NOP)
+      : "vcc");
+  c0 = (int64_t)((uint64_t)b0 << 32 | a0);
+  c1 = (int64_t)((uint64_t)b1 << 32 | a1);
+  c2 = (int64_t)((uint64_t)b2 << 32 | a2);
+}
+
 // The last position to walk (WG_ENC_NLAST): cap_mask = ballot of the prep
 // lanes' "non-zero candidate at position 2pp or 2pp + 1", pp = lane & 7 (each
 // byte: one block's eight pairs).  Wave-uniform.
@@ -561,7 +592,13 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   constexpr int64_t BIG = 1ll << 59;
   init_ctx = min(init_ctx, 2);
   const int e = min(k, 2);
+#if WG_ENC_TWO && WG_ENC_DPPADD
+  // lane j's own state (context min(j, 2)'s, masked to the score); the
+  // others' reach it as the DPP source of the next position's adds
+  int64_t st = k == init_ctx ? 0 : BIG;
+#else
   int64_t ps0 = init_ctx == 0 ? 0 : BIG, ps1 = init_ctx == 1 ? 0 : BIG, ps2 = init_ctx == 2 ? 0 : BIG;
+#endif
   uint32_t h0 = 0, h1 = 0, h2 = 0;  // the states' histories
   const TokRow& t_init = t.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
   // lanes 0, 1 follow the terminals of context 1 (lane 0's copy is unused), lanes 2, 3 context 2
@@ -639,8 +676,15 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
 #endif
     }
 #endif
+#if WG_ENC_TWO && WG_ENC_DPPADD
+    asm volatile("" : "+v"(st), "+v"(best_terminal)::"memory");
+    int64_t c0, c1, c2;
+    if (n == FIRST) quad_bcast_add3<4>(st, x0, x1, x2, c0, c1, c2);
+    else quad_bcast_add3<1>(st, x0, x1, x2, c0, c1, c2);
+#else
     asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
     const int64_t c0 = ps0 + x0, c1 = ps1 + x1, c2 = ps2 + x2;
+#endif
     const bool two = (cls_raw & 2) != 0;  // class 2: L0 >= 2
     const auto eob_n = eob_raw;
 #if WG_ENC_EOBT && WG_ENC_DPAHEAD == 2
@@ -676,9 +720,13 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
     // state is context 1's, lanes 2 and 3's context 2's: the terminal of the
     // lane's context (lane 0's is unused) needs no select
     const int64_t mm = m & ~15ll;
+#if WG_ENC_DPPADD
+    st = mm;
+#else
     ps0 = quad_bcast<0>(mm);
     ps1 = quad_bcast<1>(mm);
     ps2 = quad_bcast<2>(mm);
+#endif
     h0 = quad_bcast32<0>(hm);
     h1 = quad_bcast32<1>(hm);
     h2 = quad_bcast32<2>(hm);
@@ -773,19 +821,28 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
 // init_ctx s.  Walked in two halves (positions [NB, NE)), the records of
 // the half at `mine` (`mine[n * STRIDE]` = this lane's row at position n).
 struct DP3 {
+#if WG_ENC_DPPADD
+  int64_t st[3];     // [start context]: the lane's own state (quad_bcast_add3)
+#else
   int64_t ps[3][3];  // [start context][context]: the states, masked to the score
+#endif
   uint32_t h[3][3];
   int64_t bt[3];     // the best terminal of the lane's context, per start
   uint32_t bh[3];
 };
-__device__ __forceinline__ void dp3_init(DP3& S, const Tables& t, int lam16) {
+__device__ __forceinline__ void dp3_init(DP3& S, const Tables& t, int lam16, int k) {
   constexpr int64_t BIG = 1ll << 59;
   const TokRow& t_init = t.tok[1];  // type 0, kBand[1] = 1
 #pragma unroll
   for (int s = 0; s < 3; s++) {
+#if WG_ENC_DPPADD
+    S.st[s] = k == s ? 0 : BIG;
+#endif
 #pragma unroll
     for (int c = 0; c < 3; c++) {
+#if !WG_ENC_DPPADD
       S.ps[s][c] = c == s ? 0 : BIG;
+#endif
       S.h[s][c] = 0;
     }
     S.bt[s] = (int64_t)t_init.eob[s] * lam16;
@@ -806,12 +863,23 @@ __device__ __forceinline__ void dp3_walk(DP3& S, const int64_t* mine, const int6
       nx2 = mine[(n + 1) * STRIDE + 2];
       neob = eobq[2 * (n + 1)];
     }
+#if WG_ENC_DPPADD
+    asm volatile("" : "+v"(S.st[0]), "+v"(S.st[1]), "+v"(S.st[2]), "+v"(S.bt[0]), "+v"(S.bt[1]),
+                 "+v"(S.bt[2])::"memory");
+#else
     asm volatile("" : "+v"(S.ps[0][0]), "+v"(S.ps[1][1]), "+v"(S.ps[2][2]), "+v"(S.bt[0]), "+v"(S.bt[1]),
                  "+v"(S.bt[2])::"memory");
+#endif
     const int64_t eob_n = eob_raw;
 #pragma unroll
     for (int s = 0; s < 3; s++) {
+#if WG_ENC_DPPADD
+      int64_t c0, c1, c2;
+      if (n == NB && s == 0) quad_bcast_add3<4>(S.st[s], x0, x1, x2, c0, c1, c2);
+      else quad_bcast_add3<1>(S.st[s], x0, x1, x2, c0, c1, c2);
+#else
       const int64_t c0 = S.ps[s][0] + x0, c1 = S.ps[s][1] + x1, c2 = S.ps[s][2] + x2;
+#endif
       const bool lt1 = c1 < c0;
       const int64_t m01 = lt1 ? c1 : c0;
       const bool lt2 = c2 < m01;
@@ -822,9 +890,13 @@ __device__ __forceinline__ void dp3_walk(DP3& S, const int64_t* mine, const int6
       const uint32_t hv0 = S.h[s][0], hv1 = S.h[s][1], hv2 = S.h[s][2];
       const uint32_t hm = (lt2 ? hv2 : (lt1 ? hv1 : hv0)) | code << (2 * n);
       const int64_t mm = m & ~15ll;
+#if WG_ENC_DPPADD
+      S.st[s] = mm;
+#else
       S.ps[s][0] = quad_bcast<0>(mm);
       S.ps[s][1] = quad_bcast<1>(mm);
       S.ps[s][2] = quad_bcast<2>(mm);
+#endif
       S.h[s][0] = quad_bcast32<0>(hm);
       S.h[s][1] = quad_bcast32<1>(hm);
       S.h[s][2] = quad_bcast32<2>(hm);
@@ -2572,7 +2644,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           const int q = lane >> 2, r = lane & 3, e = min(r, 2);
           uint64_t pnz_mask = 0;
           DP3 S;
-          dp3_init(S, t, lam16);
+          dp3_init(S, t, lam16, r);
           const int64_t* eobq = &s.eobl[0][(e == 2 ? 2 : 1) - 1];
 #pragma unroll
           for (int half = 0; half < 2; half++) {
