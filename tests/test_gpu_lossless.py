@@ -31,7 +31,7 @@ def test_residual_image_matches_oracle(cuda, bits, quality):
         assert (gr == er).all(), name
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "2"])
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("bits", [2, 3, 5])
 def test_select_variants_agree(cuda, monkeypatch, bits, variant):
     """The tile-selection kernels (WG_VP8L_SELECT: 0 = a mode a wave, 1 = a

@@ -567,6 +567,146 @@ __global__ __launch_bounds__(128) void k_vp8l_select_q2(SelArgs a, int64_t total
   if (lane == 0) a.modes[(int64_t)img * a.tiles_x * a.tiles_y + tile] = ((uint32_t)best << 8) | ARGB_BLACK;
 }
 
+// The same phase with the predictions on SAMPLE lanes (variant 3, the
+// default).  In k_vp8l_select_q2 lane (mode m, sample s) runs the generic
+// branch-free predictor for its one mode: ~57 instructions for one of the
+// 56 (mode, sample) pairs.  Here lane l takes one sample (two sample rows of
+// up to 32 per pass) and forms all 14 predictions at once -- modes 1-4 are
+// its neighbours, the averages share their avg2 terms, only Select and the
+// two clamps cost more -- and its 14 residuals go to an LDS transpose buffer
+// (rows of 68 words: the column lanes' 16-B reads of one sample quad land on
+// 14 disjoint bank quads).  The column lanes (lane 4m + c, as in q2) then
+// read mode m's 64 residuals back and add channel c's bins: a bin's address
+// and increment are two bit-field extracts and two 24-bit multiply-adds.
+// Histogram columns 64 words apart (no bank conflicts between the column
+// lanes' adds); 48.5 KB a workgroup, three workgroups (six waves) a CU.
+// The entropy sums and the argmin are q2's.
+constexpr int SQ3_XS = 68;  // transpose buffer row stride (words)
+__global__ __launch_bounds__(128) void k_vp8l_select_q3(SelArgs a, int64_t total) {
+  __shared__ uint32_t hist[128 * 64];
+  __shared__ uint32_t stile[33 * SQ_SW];
+  __shared__ double lut[SQ_LUT];
+  __shared__ uint4 xbuf_all[2][14 * SQ3_XS / 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t t_idx = blockIdx.x;
+  if (t_idx >= total) return;  // (grid = total: never; no barrier skipped)
+  const int tile = (int)(t_idx % a.band_tiles) + a.ty0 * a.tiles_x;
+  const int img = (int)(t_idx / a.band_tiles);
+  const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+  const uint32_t* argb = a.argb + img * a.pitch;
+  const int ts = 1 << a.bits, w = a.width, h = a.height;
+  const int x0 = tx * ts, y0 = ty * ts;
+  const int x1 = min(x0 + ts, w), y1 = min(y0 + ts, h);
+  const int ystep = (y1 - y0 > 16) ? 2 : 1;
+  const int tw = x1 - x0, rows = (y1 - y0 + ystep - 1) / ystep;
+  {
+    // staged rows y0 - 1 .. y1 - 1 with estimateEntropy's edge values (as
+    // k_vp8l_select_q); i / scols by a multiply (exact: i < 2^16 / scols)
+    const int srows = y1 - y0 + 1, scols = x1 - x0 + 2, n = srows * scols;
+    const uint32_t inv = (65535u + (uint32_t)scols) / (uint32_t)scols;  // ceil(2^16 / scols)
+    constexpr int SN = (33 * SQ_SW + 127) / 128;
+    uint32_t v[SN];
+    int at[SN];
+#pragma unroll
+    for (int j = 0; j < SN; j++) {
+      const int i = (int)threadIdx.x + 128 * j;
+      const int rr = (int)(((uint32_t)i * inv) >> 16), cc = i - rr * scols;
+      v[j] = 0;
+      at[j] = rr * SQ_SW + cc;
+      if (i < n) {
+        const int y = y0 - 1 + rr, x = x0 - 1 + cc;
+        if (y >= 0 && x >= 0) v[j] = argb[(int64_t)y * w + min(x, w - 1)];
+      }
+    }
+    for (int i = threadIdx.x; i < SQ_LUT; i += 128) lut[i] = a.lut[i];
+    for (int i = threadIdx.x; i < 128 * 64 / 4; i += 128) reinterpret_cast<uint4*>(hist)[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < SN; j++)
+      if ((int)threadIdx.x + 128 * j < n) stile[at[j]] = v[j];
+  }
+  __syncthreads();
+  uint32_t* const xb = reinterpret_cast<uint32_t*>(xbuf_all[wave]);
+  const int col_m = lane >> 2, shift = 24 - 8 * (lane & 3);  // column lane: mode, channel (alpha, red, green, blue)
+  const bool col = lane < SQ2_COLS;
+  const uint32_t* const xrow = xb + (col ? col_m : 0) * SQ3_XS;
+  uint32_t* const myh = hist + lane;
+  const int half = lane >> 5, sx = lane & 31;
+  // wave w: sample rows w, w + 2, ...; a pass takes two of them (lanes 0-31 /
+  // 32-63), so pass k covers rows w + 4k and w + 4k + 2
+  for (int yy0 = wave; yy0 < rows; yy0 += 4) {
+    const int yy = yy0 + 2 * half;
+    {
+      const int c = min(sx, tw - 1) + 1;                                  // staged column of x
+      const uint32_t* srow = stile + (1 + min(yy, rows - 1) * ystep) * SQ_SW;  // staged row y0 + yy * ystep
+      const uint32_t* sprev = srow - SQ_SW;
+      const uint32_t p = srow[c], l = srow[c - 1], t = sprev[c], tl = sprev[c - 1], tr = sprev[c + 1];
+#pragma unroll
+      for (int m = 0; m < 14; m++) xb[m * SQ3_XS + lane] = sub_pixels(p, predict(m, l, t, tr, tl));
+    }
+    // (the LDS unit runs one wave's DS instructions in issue order: the reads
+    // below see every lane's writes above with no wait, and the next pass's
+    // writes come after these reads; only the compiler must keep the order)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int n0 = min(tw, 32), n1 = yy0 + 2 < rows ? n0 : 0;  // live samples of each row (wave-uniform)
+    if (col) {
+#pragma unroll
+      for (int hh = 0; hh < 2; hh++) {
+        const int nv = hh ? n1 : n0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          if (4 * q >= nv) break;  // (wave-uniform)
+          const uint4 r4 = *reinterpret_cast<const uint4*>(xrow + 32 * hh + 4 * q);
+          const uint32_t rv[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            if (k > 0 && 4 * q + k >= nv) break;
+            const uint32_t b7 = __builtin_amdgcn_ubfe(rv[k], shift, 7), hi = __builtin_amdgcn_ubfe(rv[k], shift + 7, 1);
+            __hip_atomic_fetch_add(myh + 64 * b7, 1u + 65535u * hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if (wave != 0) return;  // (no barrier below)
+  const uint32_t count = (uint32_t)(tw * rows);
+  double ce = 0.0;
+  if (col) {
+    uint32_t hv[128];
+#pragma unroll
+    for (int k = 0; k < 128; k++) hv[k] = myh[64 * k];
+    ce = lut[count];
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 32) {
+        double lv[32];
+#pragma unroll
+        for (int k = 0; k < 32; k++) lv[k] = lut[hh ? hv[k0 + k] >> 16 : hv[k0 + k] & 0xffff];
+#pragma unroll
+        for (int k = 0; k < 32; k++) ce -= lv[k];
+      }
+    }
+  }
+  const double e = (((0.0 + dpp_quad_f64(ce, 0)) + dpp_quad_f64(ce, 1)) + dpp_quad_f64(ce, 2)) + dpp_quad_f64(ce, 3);
+  const uint64_t eb = __builtin_bit_cast(uint64_t, e);
+  int best = 0;
+  double best_cost = 1.7976931348623157e308;
+  for (int mm = 0; mm < a.max_mode; mm++) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)eb, 4 * mm);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(eb >> 32), 4 * mm);
+    const double cm = __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+    if (cm < best_cost) {
+      best_cost = cm;
+      best = mm;
+    }
+  }
+  if (lane == 0) a.modes[(int64_t)img * a.tiles_x * a.tiles_y + tile] = ((uint32_t)best << 8) | ARGB_BLACK;
+}
+
 struct ResArgs {
   const uint32_t* argb;
   const uint32_t* modes;
@@ -579,13 +719,13 @@ struct ResArgs {
 // copyImageWithPrediction: one thread per pixel, predictions from original
 // pixels; at the right edge TR is the current row's first pixel
 // (upperRow[width]); row 0 / column 0 use black / left / top.
-__global__ __launch_bounds__(256) void k_vp8l_residual(ResArgs a, int64_t total) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;
-  const int64_t per = (int64_t)a.width * a.rows;
-  const int img = (int)(gid / per);
-  const int64_t p = gid - img * per + (int64_t)a.y0 * a.width;
-  const int y = (int)(p / a.width), x = (int)(p - (int64_t)y * a.width);
+// Grid (column blocks, rows, images): no index division (a 64-bit divide per
+// pixel was most of this kernel's instructions).
+__global__ __launch_bounds__(256) void k_vp8l_residual(ResArgs a) {
+  const int x = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  if (x >= a.width) return;
+  const int y = a.y0 + (int)blockIdx.y, img = (int)blockIdx.z;
+  const int64_t p = (int64_t)y * a.width + x;
   const uint32_t* cur = a.argb + img * a.pitch + (int64_t)y * a.width;
   uint32_t pred;
   if (y == 0) {
@@ -979,6 +1119,7 @@ extern "C" int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, 
   WG_REQUIRE(bits >= 2 && bits <= 9 && image_pitch >= (int64_t)width * height);
   const int tiles_x = subsample(width, bits), tiles_y = subsample(height, bits);
   WG_REQUIRE(ty_begin >= 0 && ty_begin < ty_end && ty_end <= tiles_y);
+  WG_REQUIRE(height <= 65535 && n_images <= 65535);  // (k_vp8l_residual's grid y / z)
   const double* lut = wg::vp8l_slog2_lut_device();
   if (!lut) return WG_EHIP;
   hipStream_t s = wg::as_stream(stream);
@@ -1004,8 +1145,11 @@ extern "C" int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, 
   // 10-bit bins a histogram word and the next tile staged by wave 1 while
   // wave 0 sums: 0.60 -> 0.65 ms at 4096².)
   const char* sel_env = getenv("WG_VP8L_SELECT");  // (read per call: the tests switch it)
-  const int variant = sel_env ? atoi(sel_env) : 2;
-  if (bits <= 5 && variant == 2) {  // counts <= 512: all modes in one pass over the samples
+  const int variant = sel_env ? atoi(sel_env) : 3;
+  if (bits <= 5 && variant == 3) {  // counts <= 512: all modes in one pass over the samples
+    hipLaunchKernelGGL(k_vp8l_select_q3, dim3((unsigned)tiles), dim3(128), 0, s, sa, tiles);
+    rc = wg::check_launch("k_vp8l_select_q3");
+  } else if (bits <= 5 && variant == 2) {
     hipLaunchKernelGGL(k_vp8l_select_q2, dim3((unsigned)tiles), dim3(128), 0, s, sa, tiles);
     rc = wg::check_launch("k_vp8l_select_q2");
   } else if (bits <= 5 && variant == 1) {
@@ -1028,8 +1172,8 @@ extern "C" int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, 
   ra.tiles_y = tiles_y;
   ra.y0 = ty_begin << bits;
   ra.rows = min(ty_end << bits, height) - ra.y0;
-  const int64_t total = (int64_t)width * ra.rows * n_images;
-  hipLaunchKernelGGL(k_vp8l_residual, dim3(wg::blocks_for(total, 256)), dim3(256), 0, s, ra, total);
+  hipLaunchKernelGGL(k_vp8l_residual, dim3((unsigned)((width + 255) / 256), (unsigned)ra.rows, (unsigned)n_images),
+                     dim3(256), 0, s, ra);
   return wg::check_launch("k_vp8l_residual");
 }
 
