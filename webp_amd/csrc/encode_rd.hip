@@ -2640,14 +2640,31 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         // resolution on scalars, and each quad writes its block's levels for
         // the context it resolved to.  Measured against the three rounds of
         // up to 16 speculative DPs below: see DESIGN.md (round 5).
+        //
+        // Positions with no non-zero level candidate (thresh < 1: the
+        // prep's `cap`) contribute only level-0 transitions into context
+        // 0, so no terminal past them can win and the histories stay zero
+        // there: a half with none in any block needs no walk, and an MB
+        // with none at all is zero (the all-zero pre-scan says the same).
+        // A pre-scan of the 16 blocks' caps decides both, wave-uniformly.
         {
           const int q = lane >> 2, r = lane & 3, e = min(r, 2);
+          bool capl = false;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int n = 4 * r + j, zig = zig_of(n);
+            const int c0 = max(abs((int)s.co_buf[q][zig]) + (int)sg.y1.sharpen[zig], 0);
+            capl |= n >= 1 && wg::mul_i24(c0, sg.y1.iquant) >= 65536;
+          }
+          const uint64_t capm = __ballot(capl);
+          const bool cap_hi = (capm & 0xCCCCCCCCCCCCCCCCull) != 0;  // lanes r = 2, 3: positions 8..15
           uint64_t pnz_mask = 0;
           DP3 S;
           dp3_init(S, t, lam16, r);
           const int64_t* eobq = &s.eobl[0][(e == 2 ? 2 : 1) - 1];
 #pragma unroll
           for (int half = 0; half < 2; half++) {
+            if (capm == 0 || (half == 1 && !cap_hi)) break;  // (wave-uniform)
             {
               TRec rr[2];
               int l0[2];
