@@ -229,6 +229,9 @@ struct Shared {
 #ifndef WG_ENC_I16ONE  // the final I16 trellis in one round, every block's DP for its three start contexts (see there)
 #define WG_ENC_I16ONE 1
 #endif
+#ifndef WG_ENC_TLANE  // trellis DPs: the best terminal as the quad's fourth state (trellis_dp4t)
+#define WG_ENC_TLANE 1
+#endif
 #ifndef WG_ENC_DPAHEAD  // positions the trellis DP loads ahead (1 or 2: measured equal, 1 kept)
 #define WG_ENC_DPAHEAD 1
 #endif
@@ -240,7 +243,7 @@ struct Shared {
     TRec trec[6][16 + WG_ENC_TPAD];
     TRec trec16[16][9];
   };
-  int64_t r0[16][6];       // the phase's level-0 trellis row (trellis_r0; [3..5] unused: a TRec's stride)
+  int64_t r0[17][6];       // the phase's level-0 trellis row [0..2] and terminal row [3..5] (trellis_r0)
   int64_t eobl[16][2];     // the phase's terminal costs x lam16 (trellis_r0, WG_ENC_EOBT)
   union {
     int16_t l0s[6][16];    // per position: L0 << 3 | negative << 2 | min(L0, 2) (< 2^14)
@@ -248,7 +251,7 @@ struct Shared {
   };
 #else
   TRec trec[6][16 + WG_ENC_TPAD];
-  int64_t r0[16][6];       // the phase's level-0 trellis row (trellis_r0; [3..5] unused: a TRec's stride)
+  int64_t r0[17][6];       // the phase's level-0 trellis row [0..2] and terminal row [3..5] (trellis_r0)
   int64_t eobl[16][2];     // the phase's terminal costs x lam16 (trellis_r0, WG_ENC_EOBT)
   int16_t l0s[6][16];      // per position: L0 << 3 | negative << 2 | min(L0, 2) (< 2^14)
 #endif
@@ -393,6 +396,7 @@ __device__ __forceinline__ int token_cost(const Tables& t, const QT& q, int nz_c
 #if WG_ENC_TWO && !WG_ENC_EOBT
 #error "WG_ENC_TWO needs WG_ENC_EOBT"
 #endif
+
 // (WG_ENC_EOBT) lanes 48 + n also write the phase's terminal costs: EOB after
 // position n from end context 1 / 2, x lam16 (0 after position 15), plus n
 // (the key's position field, see trellis_dp4), which the DP adds to a state
@@ -410,6 +414,22 @@ __device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16,
     const TokRow& tr = t.tok[CTX_TYPE * 8 + band_of(n + 1)];
     eobl[n][0] = (n < 15 ? (int64_t)tr.eob[1] * lam16 : 0) + n;
     eobl[n][1] = (n < 15 ? (int64_t)tr.eob[2] * lam16 : 0) + n;
+#if WG_ENC_TLANE
+    // the terminal lane's row of step n + 1 (trellis_dp4t): {0, EOB after
+    // position n from context 1, from context 2}; none before the walk's
+    // first position (FIRST: 0 for the I4 blocks, 1 for the I16 AC blocks)
+    constexpr int64_t BIG = 1ll << 59;
+    constexpr int FIRST = CTX_TYPE == 0 ? 1 : 0;
+    const bool none = n + 1 == FIRST;
+    r0[n + 1][3] = 0;
+    r0[n + 1][4] = none ? BIG : (n < 15 ? (int64_t)tr.eob[1] * lam16 : 0);
+    r0[n + 1][5] = none ? BIG : (n < 15 ? (int64_t)tr.eob[2] * lam16 : 0);
+    if (n == 0) {
+      r0[0][3] = 0;
+      r0[0][4] = BIG;
+      r0[0][5] = BIG;
+    }
+#endif
   }
 #endif
 }
@@ -534,11 +554,28 @@ __device__ __forceinline__ int quad_bcast32(int v) {
 #ifndef WG_ENC_DPPADD
 #define WG_ENC_DPPADD 1
 #endif
-template <int NOP>
+// (T3: lane 3 adds its OWN value to x0 -- quad_perm [0,0,0,3] -- the
+// terminal lane of trellis_dp4t)
+template <int NOP, bool T3 = false>
 __device__ __forceinline__ void quad_bcast_add3(int64_t s, int64_t x0, int64_t x1, int64_t x2, int64_t& c0,
                                                 int64_t& c1, int64_t& c2) {
   static_assert(NOP == 1 || NOP == 4, "s_nop count");
   uint32_t a0, b0, a1, b1, a2, b2;
+  if constexpr (T3)
+    asm volatile(
+        "s_nop %c14\n\t"
+        "v_add_co_u32_dpp %0, vcc, %6, %8 quad_perm:[0,0,0,3] row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32_dpp %1, vcc, %7, %9, vcc quad_perm:[0,0,0,3] row_mask:0xf bank_mask:0xf\n\t"
+        "v_add_co_u32_dpp %2, vcc, %6, %10 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32_dpp %3, vcc, %7, %11, vcc quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_add_co_u32_dpp %4, vcc, %6, %12 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32_dpp %5, vcc, %7, %13, vcc quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf"
+        : "=&v"(a0), "=&v"(b0), "=&v"(a1), "=&v"(b1), "=&v"(a2), "=&v"(b2)
+        : "v"((uint32_t)s), "v"((uint32_t)((uint64_t)s >> 32)), "v"((uint32_t)x0), "v"((uint32_t)((uint64_t)x0 >> 32)),
+          "v"((uint32_t)x1), "v"((uint32_t)((uint64_t)x1 >> 32)), "v"((uint32_t)x2), "v"((uint32_t)((uint64_t)x2 >> 32)),
+          "i"(NOP)
+        : "vcc");
+  else
   asm volatile(
       "s_nop %c14\n\t"
       "v_add_co_u32_dpp %0, vcc, %6, %8 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t"
@@ -585,6 +622,9 @@ __device__ __forceinline__ int nlast_of(uint64_t cap_mask) {
 // ended, and the levels then follow position by position with no serial
 // chain: the quad's lane r writes positions 4r..4r+3 (raster) to q, and lane
 // 0 writes the zigzag nz count to *nz.
+template <int CTX_TYPE>
+__device__ __forceinline__ void trellis_levels(const Tables& t, uint32_t hist, int k, uint2 l0w, int l0prev, int init_ctx,
+                                               int16_t* q, int* nz, int* rate);
 template <int FIRST, int CTX_TYPE, int NEND = 16>
 __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[6],
                                             const int64_t (*eobl)[2], const int16_t* l0s, int init_ctx, int lam16, int k,
@@ -772,6 +812,77 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
   const bool second = bt2 < bt1 || (bt2 == bt1 && bn2 < bn1);
 #endif
   const uint32_t hist = second ? bh2 : bh1;  // 0 when no terminal beat the all-zero block
+  trellis_levels<CTX_TYPE>(t, hist, k, l0w, l0prev, init_ctx, q, nz, rate);
+}
+
+#if WG_ENC_TLANE && !(WG_ENC_TWO && WG_ENC_EOBT && WG_ENC_DPPADD)
+#error "WG_ENC_TLANE needs WG_ENC_TWO, WG_ENC_EOBT and WG_ENC_DPPADD"
+#endif
+// trellis_dp4 with the best terminal as the quad's fourth state
+// (WG_ENC_TLANE).  Lane 3 shadowed lane 2 there, and every lane kept a
+// best-terminal key and its history with a 64-bit add, compare and three
+// selects a position.  Here lane 3 is the terminal: at step n it takes the
+// same three-way minimum as the context lanes, over its own previous value
+// (DPP quad_perm [0,0,0,3]: lane 3 reads itself) and the context-1 / -2
+// states after position n - 1 plus their EOB costs, its row {0, EOB1, EOB2}
+// of step n in the phase's R0 table (columns 3..5, trellis_r0), so the
+// terminal costs no instruction of its own; one step past the last position
+// takes the EOB after it.  The keys of its row carry no position bits: ties
+// keep the earlier terminal (strict compares, the previous value first) and
+// context 1 before context 2 at one position (c1 before c2), the
+// reference's first strict minimum; its low bits stay 0, so its "level
+// code" is 0 and its history is the winner's as is.
+template <int FIRST, int CTX_TYPE>
+__device__ __forceinline__ void trellis_dp4t(const Tables& t, const TRec* rec, const int64_t (*r0)[6],
+                                             const int16_t* l0s, int init_ctx, int lam16, int k, int16_t* q, int* nz,
+                                             int* rate = nullptr) {
+  constexpr int64_t BIG = 1ll << 59;
+  init_ctx = min(init_ctx, 2);
+  const TokRow& t_init = t.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
+  // lanes 0..2: context k's state; lane 3: the best terminal (the all-zero block to start)
+  int64_t st = k == 3 ? (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16
+                      : (k == init_ctx ? 0 : BIG);
+  uint32_t h0 = 0, h1 = 0, h2 = 0, hm = 0;
+  const int64_t* mine = k == 3 ? &r0[0][3] : (k == 0 ? &r0[0][0] : &rec[0].x[k - 1][0]);
+  constexpr int STRIDE = (int)(sizeof(TRec) / sizeof(int64_t));
+  const uint2 l0w = *reinterpret_cast<const uint2*>(l0s + 4 * k);
+  const int l0prev = l0s[max(4 * k - 1, 0)];
+  int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
+#pragma unroll
+  for (int n = FIRST; n <= 16; n++) {  // (step 16: the terminal lane only)
+    int64_t nx0 = 0, nx1 = 0, nx2 = 0;
+    if (n + 1 <= 16) {
+      nx0 = mine[(n + 1) * STRIDE];
+      nx1 = mine[(n + 1) * STRIDE + 1];
+      nx2 = mine[(n + 1) * STRIDE + 2];
+    }
+    asm volatile("" : "+v"(st)::"memory");
+    int64_t c0, c1, c2;
+    if (n == FIRST) quad_bcast_add3<4, true>(st, x0, x1, x2, c0, c1, c2);
+    else quad_bcast_add3<1, true>(st, x0, x1, x2, c0, c1, c2);
+    x0 = nx0;
+    x1 = nx1;
+    x2 = nx2;
+    const bool lt1 = c1 < c0;
+    const int64_t m01 = lt1 ? c1 : c0;
+    const bool lt2 = c2 < m01;
+    const int64_t m = lt2 ? c2 : m01;
+    const uint32_t hsel = lt2 ? h2 : (lt1 ? h1 : h0);
+    hm = n < 16 ? hsel | ((uint32_t)m & 3) << (2 * (n & 15)) : hsel;
+    st = m & ~15ll;
+    h0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)hm, 0xC0, 0xf, 0xf, false);  // quad_perm [0,0,0,3]
+    h1 = quad_bcast32<1>(hm);
+    h2 = quad_bcast32<2>(hm);
+  }
+  trellis_levels<CTX_TYPE>(t, quad_bcast32<3>(hm), k, l0w, l0prev, init_ctx, q, nz, rate);
+}
+
+// The chosen levels from the winning history (2 bits a position): the quad's
+// lane r writes positions 4r..4r+3 (raster) to q, every lane gets the zigzag
+// nz count in *nz and, with `rate`, the block's token cost (FIRST 0 only).
+template <int CTX_TYPE>
+__device__ __forceinline__ void trellis_levels(const Tables& t, uint32_t hist, int k, uint2 l0w, int l0prev, int init_ctx,
+                                               int16_t* q, int* nz, int* rate) {
   // lane r: positions 4r .. 4r + 3
   const int r = k;
   const uint32_t nzb = (hist | hist >> 1) & 0x55555555u;
@@ -820,6 +931,65 @@ __device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, co
 // WG_ENC_TWO / EOBT records), so start s's result is trellis_dp4's for
 // init_ctx s.  Walked in two halves (positions [NB, NE)), the records of
 // the half at `mine` (`mine[n * STRIDE]` = this lane's row at position n).
+#if WG_ENC_TLANE
+// (WG_ENC_TLANE: lane 3 of the quad is each start's best terminal, as in
+// trellis_dp4t: its row is the phase table's columns 3..5, one step past the
+// last position takes the EOB after it)
+struct DP3 {
+  int64_t st[3];     // [start]: lanes 0..2 context k's state, lane 3 the best terminal
+  uint32_t h[3][3];  // [start][j]: lane j's history (lane 3 reads its own as j = 0)
+};
+__device__ __forceinline__ void dp3_init(DP3& S, const Tables& t, int lam16, int k) {
+  constexpr int64_t BIG = 1ll << 59;
+  const TokRow& t_init = t.tok[1];  // type 0, kBand[1] = 1
+#pragma unroll
+  for (int s = 0; s < 3; s++) {
+    S.st[s] = k == 3 ? (int64_t)t_init.eob[s] * lam16 : (k == s ? 0 : BIG);
+#pragma unroll
+    for (int c = 0; c < 3; c++) S.h[s][c] = 0;
+  }
+}
+template <int NB, int NE>
+__device__ __forceinline__ void dp3_walk(DP3& S, const int64_t* mine, const int64_t*) {
+  constexpr int STRIDE = (int)(sizeof(TRec) / sizeof(int64_t));
+  int64_t x0 = mine[NB * STRIDE], x1 = mine[NB * STRIDE + 1], x2 = mine[NB * STRIDE + 2];
+#pragma unroll
+  for (int n = NB; n < NE; n++) {  // (step 16: the terminal lane only)
+    int64_t nx0 = 0, nx1 = 0, nx2 = 0;
+    if (n + 1 < NE) {
+      nx0 = mine[(n + 1) * STRIDE];
+      nx1 = mine[(n + 1) * STRIDE + 1];
+      nx2 = mine[(n + 1) * STRIDE + 2];
+    }
+    asm volatile("" : "+v"(S.st[0]), "+v"(S.st[1]), "+v"(S.st[2])::"memory");
+#pragma unroll
+    for (int s = 0; s < 3; s++) {
+      int64_t c0, c1, c2;
+      if (n == NB && s == 0) quad_bcast_add3<4, true>(S.st[s], x0, x1, x2, c0, c1, c2);
+      else quad_bcast_add3<1, true>(S.st[s], x0, x1, x2, c0, c1, c2);
+      const bool lt1 = c1 < c0;
+      const int64_t m01 = lt1 ? c1 : c0;
+      const bool lt2 = c2 < m01;
+      const int64_t m = lt2 ? c2 : m01;
+      const uint32_t hv0 = S.h[s][0], hv1 = S.h[s][1], hv2 = S.h[s][2];  // (values: see below)
+      const uint32_t hsel = lt2 ? hv2 : (lt1 ? hv1 : hv0);
+      const uint32_t hm = n < 16 ? hsel | ((uint32_t)m & 3) << (2 * (n & 15)) : hsel;
+      S.st[s] = m & ~15ll;
+      S.h[s][0] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hm, 0xC0, 0xf, 0xf, false);  // quad_perm [0,0,0,3]
+      S.h[s][1] = quad_bcast32<1>(hm);
+      S.h[s][2] = quad_bcast32<2>(hm);
+    }
+    x0 = nx0;
+    x1 = nx1;
+    x2 = nx2;
+  }
+}
+// start s's chosen history: the terminal lane's
+__device__ __forceinline__ uint32_t dp3_hist(const DP3& S, int s) {
+  const uint32_t g0 = S.h[0][0], g1 = S.h[1][0], g2 = S.h[2][0];
+  return quad_bcast32<3>(s == 0 ? g0 : (s == 1 ? g1 : g2));
+}
+#else
 struct DP3 {
 #if WG_ENC_DPPADD
   int64_t st[3];     // [start context]: the lane's own state (quad_bcast_add3)
@@ -922,6 +1092,7 @@ __device__ __forceinline__ uint32_t dp3_hist(const DP3& S, int s) {
   const uint32_t bh1 = quad_bcast32<1>(h), bh2 = quad_bcast32<2>(h);
   return bt2 < bt1 ? bh2 : bh1;
 }
+#endif
 __device__ __forceinline__ int hist_nz(uint32_t hist) {
   const uint32_t nzb = (hist | hist >> 1) & 0x55555555u;
   return nzb == 0 ? 0 : ((31 - __builtin_clz(nzb)) >> 1) + 1;
@@ -2306,8 +2477,13 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
                                      &dp_nz, WG_ENC_TAIL ? &dp_rate : nullptr);
               else
 #endif
+#if WG_ENC_TLANE
+              trellis_dp4t<0, 3>(t, s.trec[sl], s.r0, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &dp_nz,
+                                 WG_ENC_TAIL ? &dp_rate : nullptr);
+#else
               trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &dp_nz,
                                 WG_ENC_TAIL ? &dp_rate : nullptr);
+#endif
               if constexpr (!WG_ENC_TAIL) {
                 if ((hl & 3) == 0) s.cand_nz[sl] = dp_nz;
               }
@@ -2664,7 +2840,23 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           const int64_t* eobq = &s.eobl[0][(e == 2 ? 2 : 1) - 1];
 #pragma unroll
           for (int half = 0; half < 2; half++) {
-            if (capm == 0 || (half == 1 && !cap_hi)) break;  // (wave-uniform)
+            if (capm == 0) break;  // (wave-uniform)
+            // this lane's row at position n: R0 from the phase's table, R1 / R2
+            // from the half's records (position n at record n - 8 half); the
+            // terminal lane's (WG_ENC_TLANE) from the phase table's columns 3..5
+            const int64_t* mine =
+                (WG_ENC_TLANE && r == 3) ? &s.r0[0][3]
+                : e == 0 ? &s.r0[0][0]
+                         : reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(&s.trec16[q][0].x[e - 1][0]) -
+                                                            8 * half * (int)sizeof(TRec));
+            if (half == 1 && !cap_hi) {
+#if WG_ENC_TLANE
+              // (no candidates past position 7: one step more for the terminal
+              // lane, the EOB after position 7; the context lanes' rows are stale)
+              dp3_walk<8, 9>(S, mine, eobq);
+#endif
+              break;
+            }
             {
               TRec rr[2];
               int l0[2];
@@ -2678,14 +2870,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               }
             }
             lds_sync();
-            // this lane's row at position n: R0 from the phase's table, R1 / R2
-            // from the half's records (position n at record n - 8 half)
-            const int64_t* mine =
-                e == 0 ? &s.r0[0][0]
-                       : reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(&s.trec16[q][0].x[e - 1][0]) -
-                                                          8 * half * (int)sizeof(TRec));
             if (half == 0) dp3_walk<1, 8>(S, mine, eobq);
-            else dp3_walk<8, 16>(S, mine, eobq);
+            else dp3_walk<8, WG_ENC_TLANE ? 17 : 16>(S, mine, eobq);
             lds_sync();  // (the second half's records overwrite the first's)
           }
           const uint32_t hs0 = dp3_hist(S, 0), hs1 = dp3_hist(S, 1), hs2 = dp3_hist(S, 2);
@@ -2770,7 +2956,11 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
                   trellis_dp4<1, 0, 8>(t, s.trec[tj], s.r0, s.eobl, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
                 else
 #endif
+#if WG_ENC_TLANE
+                trellis_dp4t<1, 0>(t, s.trec[tj], s.r0, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
+#else
                 trellis_dp4<1, 0>(t, s.trec[tj], s.r0, s.eobl, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
+#endif
                 if ((lane & 3) == 0) res_nz[q] = nzv;
                 tnz = nzv;
               } else if ((lane & 3) == 0) {
