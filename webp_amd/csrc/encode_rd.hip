@@ -229,6 +229,9 @@ struct Shared {
 #ifndef WG_ENC_I16ONE  // the final I16 trellis in one round, every block's DP for its three start contexts (see there)
 #define WG_ENC_I16ONE 1
 #endif
+#ifndef WG_ENC_NZBITS  // the MB's nz masks and context update from ballots (see the export)
+#define WG_ENC_NZBITS 1
+#endif
 #ifndef WG_ENC_TLANE  // trellis DPs: the best terminal as the quad's fourth state (trellis_dp4t)
 #define WG_ENC_TLANE 1
 #endif
@@ -3085,15 +3088,34 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         }
       }
       if (isA) {
-      for (int i = 0; i < 16; i++) nzy_mask |= (s.nzy[i] > 0 ? 1u : 0u) << i;
-      if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
-      for (int i = 0; i < 8; i++) nzuv_mask |= (s.nzuv[i] > 0 ? 1u : 0u) << i;
-
       // The hand-off record and the progress flag go first: the row below
       // waits on them (at its MB start and its I4 step 3), while the MBEncInfo
       // record and the reconstruction rows are outputs only and leave after.
       // NZ context update (updateNZContextParallel :343-430)
       uint32_t out_t, out_l;
+#if WG_ENC_NZBITS
+      // (one LDS read a lane and three ballots: bit b of ym = luma block b's
+      // levels past `first`, of uvm = chroma block b's; the reference's
+      // shift-register walk then reduces to the blocks of the last row /
+      // column: out_t = row 3's luma and row 1's U, V blocks, out_l = column
+      // 3's / column 1's)
+      {
+        const int first = is_i4 ? 0 : 1;
+        const int nzl = lane < 16 ? (int)s.nzy[lane] : (lane < 24 ? (int)s.nzuv[lane - 16] : 0);
+        const uint32_t any = (uint32_t)__ballot(nzl > 0);
+        const uint32_t ym = (uint32_t)__ballot(lane < 16 && nzl > first) & 0xffffu;
+        nzy_mask = any & 0xffffu;
+        nzuv_mask = (any >> 16) & 0xffu;
+        const uint32_t uvm = nzuv_mask;
+        out_t = (ym >> 12) | ((uvm >> 2) & 3u) << 4 | ((uvm >> 6) & 3u) << 6;
+        out_l = ((ym >> 3) & 1u) | ((ym >> 6) & 2u) | ((ym >> 9) & 4u) | ((ym >> 12) & 8u) |
+                (((uvm >> 1) & 1u) | ((uvm >> 2) & 2u)) << 4 | (((uvm >> 5) & 1u) | ((uvm >> 6) & 2u)) << 6;
+      }
+      if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
+#else
+      for (int i = 0; i < 16; i++) nzy_mask |= (s.nzy[i] > 0 ? 1u : 0u) << i;
+      if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
+      for (int i = 0; i < 8; i++) nzuv_mask |= (s.nzuv[i] > 0 ? 1u : 0u) << i;
       {
         const int first = is_i4 ? 0 : 1;
         uint32_t tnz = top_nz & 0x0f, lnz = left_nz & 0x0f;
@@ -3124,6 +3146,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           out_l |= (lnz & 0xf0) << ch;
         }
       }
+#endif
       int new_top_dc = top_nz_dc;
       if (!is_i4) {
         new_top_dc = nz_dc > 0;
