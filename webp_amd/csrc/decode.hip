@@ -100,6 +100,21 @@ __device__ __forceinline__ uint64_t lds64(const uint8_t* p) { return *reinterpre
 #define WG_DEC_SKIPW 0
 #endif
 #define DEC_SITE(bit) ((WG_DEC_SKIPW & (bit)) == 0)
+// Diagnostic builds only (WG_BOUNDS, tools/gpu_bounds_suite.sh): every global
+// access of k_decode_bands checked against its buffer's extent; one outside
+// it is skipped and sets bit 2 of the error word (the row waits then give up
+// and wg_decode_status reports the launch as failed).
+#ifdef WG_BOUNDS
+__device__ __forceinline__ bool in_buf(const void* p, int bytes, const void* base, int64_t size, int* flag) {
+  const int64_t o = static_cast<const char*>(p) - static_cast<const char*>(base);
+  const bool ok = o >= 0 && o + bytes <= size;
+  if (!ok) __hip_atomic_fetch_or(flag, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ok;
+}
+#define WG_IN(p, bytes, base, size) in_buf((p), (bytes), (base), (size), &a.ctl[1])
+#else
+#define WG_IN(p, bytes, base, size) true
+#endif
 // k_decode_bands' frame stores (WG_DEC_NTST: non-temporal, an experiment on
 // the partial-line write-backs tools/gpu_dec_write_sites.sh measures)
 __device__ __forceinline__ void frame_st16(uint8_t* p, uint4 w) {
@@ -344,6 +359,9 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
   const int ys = 16 * mbw, uvs = 8 * mbw;
   const bool luma_only = a.filter_type == 1;
   STAMP_DECL;
+  // (WG_BOUNDS) the buffers' extents
+  [[maybe_unused]] const int64_t n_mb = (int64_t)a.n_img * mbh * mbw, y_size = n_mb * 256, uv_size = n_mb * 64,
+                                 top_size = (int64_t)a.n_img * mbw * TOP_BYTES, bot_size = (int64_t)a.n_img * mbw * BOT_BYTES;
 
   for (;;) {
     if (threadIdx.x == 0) sh_word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -381,8 +399,13 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
       // earlier would make every wait on a hand-off load wait for it too).
       const int64_t row_mb0 = ((int64_t)img * mbh + mby) * mbw;
       int4 pf = make_int4(0, 0, 0, 0);
-      if (lane < 48) pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384) + lane);
-      else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + row_mb0)[lane - 48];
+      if (lane < 48) {
+        const int4* pp = reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384) + lane;
+        if (WG_IN(pp, 16, a.coeffs, n_mb * 768)) pf = ld_stream(pp);
+      } else if (lane < 50) {
+        const int4* pp = reinterpret_cast<const int4*>(a.mb + row_mb0) + (lane - 48);
+        if (WG_IN(pp, 16, a.mb, n_mb * 32)) pf = *pp;
+      }
 
       for (int mbx = 0; mbx < mbw; mbx++) {
         const int64_t mbi = ((int64_t)img * mbh + mby) * mbw + mbx;
@@ -458,25 +481,28 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
         } else if (mby > 0) {
           const uint8_t* tc = top + mbx * TOP_BYTES;
           if (lane >= 48 && lane < 52) {  // unfiltered top context Y16 U8 V8
-            const uint64_t w = ld_sc1_64(tc + 8 * (lane - 48));
+            const uint64_t w = WG_IN(tc + 8 * (lane - 48), 8, a.top, top_size) ? ld_sc1_64(tc + 8 * (lane - 48)) : 0;
             const int k = lane - 48;
             uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
             *reinterpret_cast<uint64_t*>(dst) = w;
           } else if (lane >= 52 && lane < 60) {  // the previous band's record: Y rows 16y-4..16y-1
             const int k = lane - 52, rr = k >> 1, half = k & 1;
-            const uint64_t w = ld_sc1_64(bot_img + mbx * BOT_BYTES + 16 * rr + 8 * half);
+            const uint8_t* bp = bot_img + mbx * BOT_BYTES + 16 * rr + 8 * half;
+            const uint64_t w = WG_IN(bp, 8, a.bot, bot_size) ? ld_sc1_64(bp) : 0;
             *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = w;
           } else if (lane >= 60) {  // U rows 8y-4..8y-1
             const int rr = lane - 60;
-            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) = ld_sc1_64(bot_img + mbx * BOT_BYTES + 64 + 8 * rr);
+            const uint8_t* bp = bot_img + mbx * BOT_BYTES + 64 + 8 * rr;
+            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) = WG_IN(bp, 8, a.bot, bot_size) ? ld_sc1_64(bp) : 0;
           } else if (lane >= 44) {  // V rows (lanes 44..47)
             const int rr = lane - 44;
-            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = ld_sc1_64(bot_img + mbx * BOT_BYTES + 96 + 8 * rr);
+            const uint8_t* bp = bot_img + mbx * BOT_BYTES + 96 + 8 * rr;
+            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = WG_IN(bp, 8, a.bot, bot_size) ? ld_sc1_64(bp) : 0;
           }
           if (lane == 0) {  // top-right: next MB's top context, or replicate top[15] at the right edge
             uint32_t tr;
-            if (mbx < mbw - 1) tr = (uint32_t)ld_sc1_64(tc + TOP_BYTES);
-            else tr = 0x01010101u * (uint32_t)(ld_sc1_64(tc + 8) >> 56);
+            if (mbx < mbw - 1) tr = WG_IN(tc + TOP_BYTES, 8, a.top, top_size) ? (uint32_t)ld_sc1_64(tc + TOP_BYTES) : 0u;
+            else tr = 0x01010101u * (uint32_t)((WG_IN(tc + 8, 8, a.top, top_size) ? ld_sc1_64(tc + 8) : 0ull) >> 56);
             *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
           }
         } else {  // first row: everything above is 127 (decode_frame.go:104-108)
@@ -486,8 +512,13 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
         }
         lds_sync();
         if (mbx + 1 < mbw) {  // prefetch the next MB (see above)
-          if (lane < 48) pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384) + lane);
-          else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + mbi + 1)[lane - 48];
+          if (lane < 48) {
+            const int4* pp = reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384) + lane;
+            if (WG_IN(pp, 16, a.coeffs, n_mb * 768)) pf = ld_stream(pp);
+          } else if (lane < 50) {
+            const int4* pp = reinterpret_cast<const int4*>(a.mb + mbi + 1) + (lane - 48);
+            if (WG_IN(pp, 16, a.mb, n_mb * 32)) pf = *pp;
+          }
         }
         const uint32_t* iw = reinterpret_cast<const uint32_t*>(stage + 48);  // wg_mb_info words
         const uint32_t nz_y = __builtin_amdgcn_readfirstlane(iw[0]), nz_uv = __builtin_amdgcn_readfirstlane(iw[1]);
@@ -578,7 +609,8 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
               const uint64_t u = lds64(wb + LU + 7 * WG_BPS), v = lds64(wb + LV + 7 * WG_BPS);
               w = make_uint4((uint32_t)u, (uint32_t)(u >> 32), (uint32_t)v, (uint32_t)(v >> 32));
             }
-            if (DEC_SITE(1)) st_sc1_128(top + mbx * TOP_BYTES + 16 * k, w);
+            if (DEC_SITE(1) && WG_IN(top + mbx * TOP_BYTES + 16 * k, 16, a.top, top_size))
+              st_sc1_128(top + mbx * TOP_BYTES + 16 * k, w);
           }
         }
         if (lane < 16) {
@@ -625,7 +657,8 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
               const uint64_t a0 = lds64(src), a1 = lds64(src + FC_STRIDE);
               w = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
             }
-            if (DEC_SITE(2)) st_sc1_128(bot_img + x * BOT_BYTES + 16 * k, w);
+            if (DEC_SITE(2) && WG_IN(bot_img + x * BOT_BYTES + 16 * k, 16, a.bot, bot_size))
+              st_sc1_128(bot_img + x * BOT_BYTES + 16 * k, w);
           }
         }
         {
@@ -657,13 +690,15 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
             const int j = lane & 15, x = y0 + (lane >> 4);
             if (DEC_SITE(4) && y0 >= 0 && j < ylim && x <= y1) {
               const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
-              frame_st16(Yp + (int64_t)(16 * mby + j) * ys + 16 * x, w);
+              if (WG_IN(Yp + (int64_t)(16 * mby + j) * ys + 16 * x, 16, a.Y, y_size))
+                frame_st16(Yp + (int64_t)(16 * mby + j) * ys + 16 * x, w);
             }
           }
 #pragma unroll
           for (int h = 0; h < 2; h++) {  // U, V: row (i & 15), MB c0 + (i >> 4)
             const int i = lane + 64 * h, pl = (i >> 3) & 1, j = i & 7, x = c0 + (i >> 4);
-            if (DEC_SITE(8) && c0 >= 0 && i < 80 && j < clim && x <= c1)
+            if (DEC_SITE(8) && c0 >= 0 && i < 80 && j < clim && x <= c1 &&
+                WG_IN((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x, 8, pl ? a.V : a.U, uv_size))
               frame_st8((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x,
                         lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
           }
@@ -685,12 +720,13 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
             }
             if (lane < 6) {
               const int rr = 1 + (lane >> 1), part = lane & 1, x = t0 + part;
-              if (DEC_SITE(16) && t0 >= 0 && x <= t1)
+              if (DEC_SITE(16) && t0 >= 0 && x <= t1 && WG_IN(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * x, 16, a.Y, y_size))
                 frame_st16(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * x,
                            *reinterpret_cast<const uint4*>(fy + rr * FY_STRIDE + FY_X0 + 16 * (x - mbx)));
             } else if ((from_lds || !luma_only) && lane >= 8 && lane < 32) {
               const int k = lane - 8, pl = k >= 12, rr = 1 + (k % 12) / 4, q = k & 3, x = u0 + q;
-              if (DEC_SITE(32) && u0 >= 0 && x <= u1)
+              if (DEC_SITE(32) && u0 >= 0 && x <= u1 &&
+                  WG_IN((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * x, 8, pl ? a.V : a.U, uv_size))
                 frame_st8((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * x,
                           lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
             }
@@ -737,7 +773,8 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
         } else {
           // every store of this MB is complete before the flag
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0 && WG_IN(prog_mine, 4, a.progress, (int64_t)a.n_img * mbh * 4))
+            __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (from_lds && lane == 0) {
           // our progress is also what the row above's ring waits on
