@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: counter passes over the C5 stages (tools/bench_c5.py) for the
-# VP8L kernels (k_vp8l_select_q3, k_vp8l_inverse, ...): two SQ passes and
+# VP8L kernels (k_vp8l_select_q3 -- the default tile selection --, k_vp8l_residual, k_vp8l_inverse, ...): two SQ passes and
 # two HBM passes, each its own rocprofv3 run, summarised per kernel into
 # gpurun_out/vp8l_pmc/*.json (tools/pmc_summary.py).
 OUT=gpurun_out/vp8l_pmc; mkdir -p $OUT && export TMPDIR=/tmp
