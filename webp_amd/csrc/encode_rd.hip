@@ -229,6 +229,9 @@ struct Shared {
 #ifndef WG_ENC_I16ONE  // the final I16 trellis in one round, every block's DP for its three start contexts (see there)
 #define WG_ENC_I16ONE 1
 #endif
+#ifndef WG_ENC_PREPK  // the I4 pre-screen's SSE and FTransform on packed differences (sse_fdct_pk)
+#define WG_ENC_PREPK 0
+#endif
 #ifndef WG_ENC_NZBITS  // the MB's nz masks and context update from ballots (see the export)
 #define WG_ENC_NZBITS 1
 #endif
@@ -1353,6 +1356,27 @@ __device__ __forceinline__ int sse_p(const P4& a, const P4& b) {
   return (int)(aa + bb - 2 * ab);
 }
 // FTransform of (src - pred), rows unpacked one at a time
+// (WG_ENC_PREPK) the pre-screen's SSE and FTransform of one mode from the
+// source rows (packed bytes) and the prediction (16 ints): the differences
+// formed once, as the int16 column pairs fdct4x4_pk takes (rows 0 | 1 and
+// 3 | 2), and the SSE as eight v_dot2_i32_i16 of them with themselves
+// (exact: |d| <= 255, the sum < 2^21)
+__device__ __forceinline__ int sse_fdct_pk(const P4& s, const int pred[16], int co[16]) {
+  wg::s16x2_t d01[4], d32[4];
+  int sse = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t sel = 0x0c000c00u | (uint32_t)(4 + k) << 16 | (uint32_t)k;
+    d01[k] = __builtin_bit_cast(wg::s16x2_t, __builtin_amdgcn_perm(s.r[1], s.r[0], sel)) -
+             __builtin_bit_cast(wg::s16x2_t, (uint32_t)pred[k] | (uint32_t)pred[4 + k] << 16);
+    d32[k] = __builtin_bit_cast(wg::s16x2_t, __builtin_amdgcn_perm(s.r[2], s.r[3], sel)) -
+             __builtin_bit_cast(wg::s16x2_t, (uint32_t)pred[12 + k] | (uint32_t)pred[8 + k] << 16);
+    sse = wg::sdot2_acc(d01[k], d01[k], sse);
+    sse = wg::sdot2_acc(d32[k], d32[k], sse);
+  }
+  wg::fdct4x4_pk(d01, d32, co);
+  return sse;
+}
 __device__ __forceinline__ void fdct_p(const P4& s, const P4& p, int co[16]) {
 #if WG_ENC_FDCT_PK
   // (byte k of rows a and b as the int16 halves of a word: one v_perm each)
@@ -2370,8 +2394,13 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           if (bvalid && hl < 10) {
             int pred[16];
             pred4_lut(pcw, s.pv[half], pred);
+#if WG_ENC_PREPK && WG_ENC_FDCT_PK
+            if constexpr (FUSE) sse_lane = sse_fdct_pk(ld4(s.yin + off), pred, pco);
+            else sse_lane = sse16(src, pred);
+#else
             sse_lane = sse16(src, pred);
             if constexpr (FUSE) fdct(src, pred, pco);
+#endif
           }
 #if defined(WG_EXP_REP_PRE)
       WG_REP_END
