@@ -229,6 +229,9 @@ struct Shared {
 #ifndef WG_ENC_I16ONE  // the final I16 trellis in one round, every block's DP for its three start contexts (see there)
 #define WG_ENC_I16ONE 1
 #endif
+#ifndef WG_ENC_QSKIP  // the final I16 trellis walks no quarter of positions past the last candidate (see there)
+#define WG_ENC_QSKIP 0
+#endif
 #ifndef WG_ENC_PREPK  // the I4 pre-screen's SSE and FTransform on packed differences (sse_fdct_pk)
 #define WG_ENC_PREPK 0
 #endif
@@ -2866,6 +2869,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           }
           const uint64_t capm = __ballot(capl);
           const bool cap_hi = (capm & 0xCCCCCCCCCCCCCCCCull) != 0;  // lanes r = 2, 3: positions 8..15
+          // (WG_ENC_QSKIP) by quarter: lanes r = 1 (positions 4..7), r = 3 (12..15)
+          [[maybe_unused]] const bool cap_q1 = (capm & 0x2222222222222222ull) != 0,
+                                      cap_q3 = (capm & 0x8888888888888888ull) != 0;
           uint64_t pnz_mask = 0;
           DP3 S;
           dp3_init(S, t, lam16, r);
@@ -2902,8 +2908,24 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               }
             }
             lds_sync();
-            if (half == 0) dp3_walk<1, 8>(S, mine, eobq);
-            else dp3_walk<8, WG_ENC_TLANE ? 17 : 16>(S, mine, eobq);
+            if (half == 0) {
+#if WG_ENC_TLANE && WG_ENC_QSKIP
+              if (!cap_q1 && !cap_hi) {  // no candidates past position 3: the walk stops
+                dp3_walk<1, 4>(S, mine, eobq);
+                dp3_walk<4, 5>(S, mine, eobq);  // (the terminal lane's EOB after position 3)
+                break;
+              }
+#endif
+              dp3_walk<1, 8>(S, mine, eobq);
+            } else {
+#if WG_ENC_TLANE && WG_ENC_QSKIP
+              if (!cap_q3) {  // none past position 11
+                dp3_walk<8, 12>(S, mine, eobq);
+                dp3_walk<12, 13>(S, mine, eobq);
+              } else
+#endif
+                dp3_walk<8, WG_ENC_TLANE ? 17 : 16>(S, mine, eobq);
+            }
             lds_sync();  // (the second half's records overwrite the first's)
           }
           const uint32_t hs0 = dp3_hist(S, 0), hs1 = dp3_hist(S, 1), hs2 = dp3_hist(S, 2);
