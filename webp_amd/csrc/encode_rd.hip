@@ -229,6 +229,9 @@ struct Shared {
 #ifndef WG_ENC_I16ONE  // the final I16 trellis in one round, every block's DP for its three start contexts (see there)
 #define WG_ENC_I16ONE 1
 #endif
+#ifndef WG_ENC_RECPF  // the row above's next record prefetched at the end of each MB (see the MB loop)
+#define WG_ENC_RECPF 0
+#endif
 #ifndef WG_ENC_QSKIP  // the final I16 trellis walks no quarter of positions past the last candidate (see there)
 #define WG_ENC_QSKIP 0
 #endif
@@ -1970,6 +1973,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
     // reconstruction rows held back for a whole-sector store (export)
     uint4 stg0 = make_uint4(0, 0, 0, 0), stg1 = stg0, rst0 = stg0;
     uint2 rst1 = make_uint2(0, 0);
+    // (WG_ENC_RECPF) column x + 1's record of the row above, loaded at the end
+    // of MB x so that MB x + 1's first tag check has it in registers
+    [[maybe_unused]] uint4 pre_above = make_uint4(0, 0, 0, 0);
 
     for (int mbx = 0; live && mbx < mbw; mbx++) {
       Shared& s = launder(s_waves[wave]);
@@ -2012,12 +2018,13 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       // the tagged record of column x of the row above (lane p < 4: granule p),
       // polled until all four carry the row's tag
       const uint32_t want = row_tag(a.epoch, mby - 1);
-      auto poll_rec = [&](const uint8_t* rec, int n) -> uint4 {
+      auto poll_rec = [&](const uint8_t* rec, int n, bool pre = false) -> uint4 {
         uint4 g = make_uint4(0, 0, 0, 0);
         if (mby > 0) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           for (uint32_t it = 0;; it++) {
-            if (lane < n) g = ld_sc1_128(rec + 16 * lane);
+            if (pre && it == 0) g = pre_above;  // (the prefetched granules: checked like a load)
+            else if (lane < n) g = ld_sc1_128(rec + 16 * lane);
             if (__ballot(lane < n && g.w != want) == 0) break;
             if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
                                     __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
@@ -2033,7 +2040,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         return g;
       };
       uint4 above = make_uint4(0, 0, 0, 0);
-      if (isA) above = poll_rec(top + mbx * REC, 4);
+      if (isA) above = poll_rec(top + mbx * REC, 4, WG_ENC_RECPF && mbx > 0);
 #else
       if (isA) wait_above(mbx + 1);
 #endif
@@ -3348,6 +3355,16 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         }
 #endif
       }
+#if WG_ENC_TAGGED && WG_ENC_RECPF
+      if (mby > 0 && mbx + 1 < mbw) {  // (a buffer load: sc1 like ld_sc1_128, its wait left to the compiler)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(top, (short)0, mbw * REC, 0x00020000);
+        typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+        if (lane < 4) {
+          const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (mbx + 1) * REC + 16 * lane, 0, 16);
+          pre_above = make_uint4(v.x, v.y, v.z, v.w);
+        }
+      }
+#endif
       // new top-left: the row above's bottom-right of this column (before we overwrite it)
       tl_y = s.yout[YOFF - BPS + 15];
       tl_u = s.yout[UOFF - BPS + 7];
