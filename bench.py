@@ -136,8 +136,8 @@ def slot_model(launch_ms, batch, enc_waves_per_simd=2):
         "lds_array_busy": round(rec["SQ_LDS_IDX_ACTIVE"] / (SIMDS / 4 * launch_cyc), 3),
         "lds_bank_conflict_share": round(rec["SQ_LDS_BANK_CONFLICT"] / rec["SQ_LDS_IDX_ACTIVE"], 3),
         "note": "slot_fill < 1 is the launch's ramp and tail (fewer rows than slots); per-wave time is issue + "
-                "LDS round trips of an in-order wave: a third wave per SIMD (tools/gpu_ab.sh, WG_ENC_GROUPS=3 / "
-                "WG_ENC_OCC=3) did not raise throughput",
+                "LDS round trips of an in-order wave: a third wave per SIMD (12-wave workgroups, round 4) did not "
+                "raise throughput",
     }
 
 

@@ -60,9 +60,9 @@ def test_work_size_helpers():
     assert _lib.lib.wg_vp8l_inverse_work_bytes(100, 0, 2) == 0
     assert _lib.lib.wg_plane_ssim_work_bytes(33, 17, 1) == 8 * 1 * 2  # one 58-column strip, two tile rows
     assert _lib.lib.wg_plane_ssim_row_partials(59) == 2 and _lib.lib.wg_plane_ssim_row_partials(58) == 1
-    # hand-off records | ctl[4] | progress | row-schedule tag[4] | order | slack (wg_encode_row_order)
-    # records | ctl[4] + progress | tag[4] + row order + slack + band order (17 bands of 4 rows per frame)
-    assert _lib.lib.wg_encode_work_bytes(120, 68, 2) == 2 * 120 * 64 + 4 * (2 * 68 + 4) + 4 * (4 + 2 * 68 + 2 + 2 * 17)
+    # hand-off records (128 B a column: 11 {word, tag} granules) | ctl[4] | row-schedule tag[4] | row order |
+    # slack | band order (17 bands of 4 rows per frame) (wg_encode_row_order)
+    assert _lib.lib.wg_encode_work_bytes(120, 68, 2) == 2 * 120 * 128 + 4 * 4 + 4 * (4 + 2 * 68 + 2 + 2 * 17)
     assert _lib.lib.wg_encode_work_bytes(120, 0, 2) == 0
 
 

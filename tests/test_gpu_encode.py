@@ -192,7 +192,7 @@ def test_row_schedule_table(cuda):
     alphas, _ = frames.analysis_alphas(Y, U, V, w, h)
     n, rows = 7, 7 * mbh
     work = frames.encode_row_order(alphas, mbw, mbh).cpu().numpy()
-    base = n * mbw * 64 // 4 + 4 + rows  # int32 index of the tag: records | ctl[4] | progress | tag
+    base = n * mbw * 128 // 4 + 4  # int32 index of the tag: records | ctl[4] | tag
     words = work.view(np.int32)
     order, slack = words[base + 4:base + 4 + rows], words[base + 4 + rows:base + 4 + rows + n]
     a = np.clip(alphas.cpu().numpy().astype(np.int64), 0, 255)

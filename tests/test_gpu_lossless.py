@@ -31,12 +31,10 @@ def test_residual_image_matches_oracle(cuda, bits, quality):
         assert (gr == er).all(), name
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("bits", [2, 3, 5])
-def test_select_variants_agree(cuda, monkeypatch, bits, variant):
-    """The tile-selection kernels (WG_VP8L_SELECT: 0 = a mode a wave, 1 = a
-    wave a tile, 2 = two waves a tile, the default) on ragged tiles."""
-    monkeypatch.setenv("WG_VP8L_SELECT", variant)
+def test_select_ragged_tiles(cuda, bits):
+    """k_vp8l_select_q3 (bits <= 5) on ragged tiles: a 260 x 90 image leaves a
+    partial tile column and row at every tile size."""
     img = argb_of(synth.blobs_rgba(260, 90, seed=11, alpha=True))
     em, er = O.vp8l_residual_image(img, bits, 75)
     gm, gr = gpu_residual(img, bits, 75)

@@ -30,6 +30,7 @@
 
 #include "wg_common.h"
 #include "wg_dsp.h"
+#include "wg_instr.h"
 
 namespace {
 
@@ -82,55 +83,20 @@ __device__ __forceinline__ void st_sc1_128(uint8_t* p, uint4 w) {
 // (2 B / coefficient, the kernel's largest input) does not push the frame's
 // partly written output lines out of L2 before their other pieces arrive.
 __device__ __forceinline__ int4 ld_stream(const int4* p) {
-#ifdef WG_DEC_NO_NT
-  return *p;
-#else
   typedef int v4i __attribute__((ext_vector_type(4)));
   const v4i v = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
   return make_int4(v.x, v.y, v.z, v.w);
-#endif
 }
 __device__ __forceinline__ uint64_t lds64(const uint8_t* p) { return *reinterpret_cast<const uint64_t*>(p); }
 
-// Diagnostic builds only (WRITE_SIZE per store site, tools/gpu_dec_write_sites.sh):
-// bit k of WG_DEC_SKIPW drops k_decode_bands' store site k (1 top record,
-// 2 bottom record, 4 Y rows, 8 U/V rows, 16 Y rows 13..15 above, 32 U/V rows
-// 5..7 above); the output is then wrong, the control flow unchanged.
-#ifndef WG_DEC_SKIPW
-#define WG_DEC_SKIPW 0
-#endif
-#define DEC_SITE(bit) ((WG_DEC_SKIPW & (bit)) == 0)
-// Diagnostic builds only (WG_BOUNDS, tools/gpu_bounds_suite.sh): every global
-// access of k_decode_bands checked against its buffer's extent; one outside
-// it is skipped and sets bit 2 of the error word (the row waits then give up
-// and wg_decode_status reports the launch as failed).
-#ifdef WG_BOUNDS
-__device__ __forceinline__ bool in_buf(const void* p, int bytes, const void* base, int64_t size, int* flag) {
-  const int64_t o = static_cast<const char*>(p) - static_cast<const char*>(base);
-  const bool ok = o >= 0 && o + bytes <= size;
-  if (!ok) __hip_atomic_fetch_or(flag, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return ok;
-}
-#define WG_IN(p, bytes, base, size) in_buf((p), (bytes), (base), (size), &a.ctl[1])
-#else
-#define WG_IN(p, bytes, base, size) true
-#endif
-// k_decode_bands' frame stores (WG_DEC_NTST: non-temporal, an experiment on
-// the partial-line write-backs tools/gpu_dec_write_sites.sh measures)
+// (WG_DEC_SKIPW / WG_BOUNDS builds, wg_instr.h: DEC_SITE(bit) drops a store
+// site of k_decode_bands, WG_IN checks an access against its buffer)
+// k_decode_bands' frame stores
 __device__ __forceinline__ void frame_st16(uint8_t* p, uint4 w) {
-#ifdef WG_DEC_NTST
-  typedef unsigned v4u __attribute__((ext_vector_type(4)));
-  __builtin_nontemporal_store(v4u{w.x, w.y, w.z, w.w}, reinterpret_cast<v4u*>(p));
-#else
   *reinterpret_cast<uint4*>(p) = w;
-#endif
 }
 __device__ __forceinline__ void frame_st8(uint8_t* p, uint64_t w) {
-#ifdef WG_DEC_NTST
-  __builtin_nontemporal_store(w, reinterpret_cast<uint64_t*>(p));
-#else
   *reinterpret_cast<uint64_t*>(p) = w;
-#endif
 }
 __device__ __forceinline__ uint32_t lds32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 
@@ -152,41 +118,16 @@ struct DecArgs {
   int filter_type, mbw, mbh, n_img;
 };
 
-#ifdef WG_STAMPS
-// Diagnostic build only: cycles spent per phase, summed over all macroblocks.
-__device__ unsigned long long g_phase[16];
-#define STAMP_DECL unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0
-#define STAMP(k)                                                                   \
-  do {                                                                             \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    unsigned long long ts_;                                                        \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");  \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    if ((k) > 0) st_acc[(k)-1] += ts_ - st_prev;                                   \
-    st_prev = ts_;                                                                 \
-  } while (0)
-#define STAMP_FLUSH()                                                          \
-  do {                                                                         \
-    if (lane == 0)                                                             \
-      for (int k_ = 0; k_ < 10; k_++) atomicAdd(&g_phase[k_], st_acc[k_]);     \
-  } while (0)
-#else
-#define STAMP_DECL int st_unused_ = 0
-#define STAMP(k) (void)st_unused_
-#define STAMP_FLUSH() (void)st_unused_
-#endif
+// (WG_STAMPS builds, wg_instr.h) cycles spent per phase, summed over all macroblocks
+WG_IF_STAMPS(__device__ unsigned long long g_phase[16];)
 
 // wave-level LDS ordering: this wave's LDS accesses retire before what follows
 // (the LDS unit executes one wave's DS instructions in issue order, so a
 // read after a write of the same wave -- or another wave's read after this
 // wave's later flag store -- sees the write without draining the queue; the
-// drain cost C3 3.6%: 4.75 -> 4.58 ms.  WG_DEC_DRAIN restores it, A/B.)
+// drain cost C3 3.6%: 4.75 -> 4.58 ms.)
 __device__ __forceinline__ void lds_sync() {
-#ifdef WG_DEC_DRAIN
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
   asm volatile("" ::: "memory");
-#endif
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -401,10 +342,10 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
       int4 pf = make_int4(0, 0, 0, 0);
       if (lane < 48) {
         const int4* pp = reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384) + lane;
-        if (WG_IN(pp, 16, a.coeffs, n_mb * 768)) pf = ld_stream(pp);
+        if (WG_IN(pp, 16, a.coeffs, n_mb * 768, &a.ctl[1])) pf = ld_stream(pp);
       } else if (lane < 50) {
         const int4* pp = reinterpret_cast<const int4*>(a.mb + row_mb0) + (lane - 48);
-        if (WG_IN(pp, 16, a.mb, n_mb * 32)) pf = *pp;
+        if (WG_IN(pp, 16, a.mb, n_mb * 32, &a.ctl[1])) pf = *pp;
       }
 
       for (int mbx = 0; mbx < mbw; mbx++) {
@@ -481,28 +422,28 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
         } else if (mby > 0) {
           const uint8_t* tc = top + mbx * TOP_BYTES;
           if (lane >= 48 && lane < 52) {  // unfiltered top context Y16 U8 V8
-            const uint64_t w = WG_IN(tc + 8 * (lane - 48), 8, a.top, top_size) ? ld_sc1_64(tc + 8 * (lane - 48)) : 0;
+            const uint64_t w = WG_IN(tc + 8 * (lane - 48), 8, a.top, top_size, &a.ctl[1]) ? ld_sc1_64(tc + 8 * (lane - 48)) : 0;
             const int k = lane - 48;
             uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
             *reinterpret_cast<uint64_t*>(dst) = w;
           } else if (lane >= 52 && lane < 60) {  // the previous band's record: Y rows 16y-4..16y-1
             const int k = lane - 52, rr = k >> 1, half = k & 1;
             const uint8_t* bp = bot_img + mbx * BOT_BYTES + 16 * rr + 8 * half;
-            const uint64_t w = WG_IN(bp, 8, a.bot, bot_size) ? ld_sc1_64(bp) : 0;
+            const uint64_t w = WG_IN(bp, 8, a.bot, bot_size, &a.ctl[1]) ? ld_sc1_64(bp) : 0;
             *reinterpret_cast<uint64_t*>(fy + rr * FY_STRIDE + FY_X0 + 8 * half) = w;
           } else if (lane >= 60) {  // U rows 8y-4..8y-1
             const int rr = lane - 60;
             const uint8_t* bp = bot_img + mbx * BOT_BYTES + 64 + 8 * rr;
-            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) = WG_IN(bp, 8, a.bot, bot_size) ? ld_sc1_64(bp) : 0;
+            *reinterpret_cast<uint64_t*>(fu + rr * FC_STRIDE + FC_X0) = WG_IN(bp, 8, a.bot, bot_size, &a.ctl[1]) ? ld_sc1_64(bp) : 0;
           } else if (lane >= 44) {  // V rows (lanes 44..47)
             const int rr = lane - 44;
             const uint8_t* bp = bot_img + mbx * BOT_BYTES + 96 + 8 * rr;
-            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = WG_IN(bp, 8, a.bot, bot_size) ? ld_sc1_64(bp) : 0;
+            *reinterpret_cast<uint64_t*>(fv + rr * FC_STRIDE + FC_X0) = WG_IN(bp, 8, a.bot, bot_size, &a.ctl[1]) ? ld_sc1_64(bp) : 0;
           }
           if (lane == 0) {  // top-right: next MB's top context, or replicate top[15] at the right edge
             uint32_t tr;
-            if (mbx < mbw - 1) tr = WG_IN(tc + TOP_BYTES, 8, a.top, top_size) ? (uint32_t)ld_sc1_64(tc + TOP_BYTES) : 0u;
-            else tr = 0x01010101u * (uint32_t)((WG_IN(tc + 8, 8, a.top, top_size) ? ld_sc1_64(tc + 8) : 0ull) >> 56);
+            if (mbx < mbw - 1) tr = WG_IN(tc + TOP_BYTES, 8, a.top, top_size, &a.ctl[1]) ? (uint32_t)ld_sc1_64(tc + TOP_BYTES) : 0u;
+            else tr = 0x01010101u * (uint32_t)((WG_IN(tc + 8, 8, a.top, top_size, &a.ctl[1]) ? ld_sc1_64(tc + 8) : 0ull) >> 56);
             *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
           }
         } else {  // first row: everything above is 127 (decode_frame.go:104-108)
@@ -514,10 +455,10 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
         if (mbx + 1 < mbw) {  // prefetch the next MB (see above)
           if (lane < 48) {
             const int4* pp = reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384) + lane;
-            if (WG_IN(pp, 16, a.coeffs, n_mb * 768)) pf = ld_stream(pp);
+            if (WG_IN(pp, 16, a.coeffs, n_mb * 768, &a.ctl[1])) pf = ld_stream(pp);
           } else if (lane < 50) {
             const int4* pp = reinterpret_cast<const int4*>(a.mb + mbi + 1) + (lane - 48);
-            if (WG_IN(pp, 16, a.mb, n_mb * 32)) pf = *pp;
+            if (WG_IN(pp, 16, a.mb, n_mb * 32, &a.ctl[1])) pf = *pp;
           }
         }
         const uint32_t* iw = reinterpret_cast<const uint32_t*>(stage + 48);  // wg_mb_info words
@@ -609,7 +550,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
               const uint64_t u = lds64(wb + LU + 7 * WG_BPS), v = lds64(wb + LV + 7 * WG_BPS);
               w = make_uint4((uint32_t)u, (uint32_t)(u >> 32), (uint32_t)v, (uint32_t)(v >> 32));
             }
-            if (DEC_SITE(1) && WG_IN(top + mbx * TOP_BYTES + 16 * k, 16, a.top, top_size))
+            if (DEC_SITE(1) && WG_IN(top + mbx * TOP_BYTES + 16 * k, 16, a.top, top_size, &a.ctl[1]))
               st_sc1_128(top + mbx * TOP_BYTES + 16 * k, w);
           }
         }
@@ -657,7 +598,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
               const uint64_t a0 = lds64(src), a1 = lds64(src + FC_STRIDE);
               w = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
             }
-            if (DEC_SITE(2) && WG_IN(bot_img + x * BOT_BYTES + 16 * k, 16, a.bot, bot_size))
+            if (DEC_SITE(2) && WG_IN(bot_img + x * BOT_BYTES + 16 * k, 16, a.bot, bot_size, &a.ctl[1]))
               st_sc1_128(bot_img + x * BOT_BYTES + 16 * k, w);
           }
         }
@@ -690,7 +631,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
             const int j = lane & 15, x = y0 + (lane >> 4);
             if (DEC_SITE(4) && y0 >= 0 && j < ylim && x <= y1) {
               const uint4 w = *reinterpret_cast<const uint4*>(fy + (j + 4) * FY_STRIDE + FY_X0 + 16 * (x - mbx));
-              if (WG_IN(Yp + (int64_t)(16 * mby + j) * ys + 16 * x, 16, a.Y, y_size))
+              if (WG_IN(Yp + (int64_t)(16 * mby + j) * ys + 16 * x, 16, a.Y, y_size, &a.ctl[1]))
                 frame_st16(Yp + (int64_t)(16 * mby + j) * ys + 16 * x, w);
             }
           }
@@ -698,7 +639,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
           for (int h = 0; h < 2; h++) {  // U, V: row (i & 15), MB c0 + (i >> 4)
             const int i = lane + 64 * h, pl = (i >> 3) & 1, j = i & 7, x = c0 + (i >> 4);
             if (DEC_SITE(8) && c0 >= 0 && i < 80 && j < clim && x <= c1 &&
-                WG_IN((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x, 8, pl ? a.V : a.U, uv_size))
+                WG_IN((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x, 8, pl ? a.V : a.U, uv_size, &a.ctl[1]))
               frame_st8((pl ? Vp : Up) + (int64_t)(8 * mby + j) * uvs + 8 * x,
                         lds64((pl ? fv : fu) + (j + 4) * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
           }
@@ -720,13 +661,13 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
             }
             if (lane < 6) {
               const int rr = 1 + (lane >> 1), part = lane & 1, x = t0 + part;
-              if (DEC_SITE(16) && t0 >= 0 && x <= t1 && WG_IN(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * x, 16, a.Y, y_size))
+              if (DEC_SITE(16) && t0 >= 0 && x <= t1 && WG_IN(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * x, 16, a.Y, y_size, &a.ctl[1]))
                 frame_st16(Yp + (int64_t)(16 * mby - 4 + rr) * ys + 16 * x,
                            *reinterpret_cast<const uint4*>(fy + rr * FY_STRIDE + FY_X0 + 16 * (x - mbx)));
             } else if ((from_lds || !luma_only) && lane >= 8 && lane < 32) {
               const int k = lane - 8, pl = k >= 12, rr = 1 + (k % 12) / 4, q = k & 3, x = u0 + q;
               if (DEC_SITE(32) && u0 >= 0 && x <= u1 &&
-                  WG_IN((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * x, 8, pl ? a.V : a.U, uv_size))
+                  WG_IN((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * x, 8, pl ? a.V : a.U, uv_size, &a.ctl[1]))
                 frame_st8((pl ? Vp : Up) + (int64_t)(8 * mby - 4 + rr) * uvs + 8 * x,
                           lds64((pl ? fv : fu) + rr * FC_STRIDE + FC_X0 + 8 * (x - mbx)));
             }
@@ -773,7 +714,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
         } else {
           // every store of this MB is complete before the flag
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lane == 0 && WG_IN(prog_mine, 4, a.progress, (int64_t)a.n_img * mbh * 4))
+          if (lane == 0 && WG_IN(prog_mine, 4, a.progress, (int64_t)a.n_img * mbh * 4, &a.ctl[1]))
             __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (from_lds && lane == 0) {
@@ -810,14 +751,8 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
 // wherever the MB above-right is not needed.  Cross-band hand-off: R by
 // progress_r + the top records, F by progress_f + the frame rows (sc1 stores,
 // drained before the flag), as in k_decode_bands.
-#ifndef WG_DEC_SW
-#define WG_DEC_SW 4
-#endif
-#ifndef WG_DEC_RING_M
-#define WG_DEC_RING_M 4
-#endif
-constexpr int SW = WG_DEC_SW;          // rows per band (one R and one F wave each)
-constexpr int RING_M = WG_DEC_RING_M;  // R -> F ring depth (R's work buffers of unfiltered MBs)
+constexpr int SW = 4;         // rows per band (one R and one F wave each)
+constexpr int RING_M = 4; // R -> F ring depth (R's work buffers of unfiltered MBs)
 
 // The first I4 wavefront step (i4_schedule) that reads the MB above-right,
 // or 99: blocks 3, 7, 11, 15 read it in VE4 / LD4 / VL4 (wg_dsp.h pred4_row).
@@ -1403,13 +1338,11 @@ bool use_split(const DecConfig& cfg, int32_t mbh, int32_t n_images) {
 
 }  // namespace
 
-#ifdef WG_STAMPS
-extern "C" int wg_debug_phases(unsigned long long* host, int n) {
+WG_IF_STAMPS(extern "C" int wg_debug_phases(unsigned long long* host, int n) {
   (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n);
   unsigned long long z[16] = {0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) == hipSuccess ? 0 : -2;
-}
-#endif
+})
 
 extern "C" size_t wg_decode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images) {
   if (mbw <= 0 || mbh <= 0 || n_images <= 0) return 0;

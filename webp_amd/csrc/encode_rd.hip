@@ -10,8 +10,8 @@
 // finished MB x and waits for MB x+1 only at I4 step 3, the first read of the
 // top-right pixels (the reference waits for x+1 up front, :286-295; the
 // outputs are the same).  The shared top arrays (topY/U/V, topModes, topNz,
-// topNzDC) become one 48-byte record per MB column (64-B granule), handed
-// down with sc1 stores + a per-row progress counter; the left context stays
+// topNzDC) become one record of 11 {word, tag} granules per MB column, each
+// handed down as one 64-bit atomic store and polled by the row below; the left context stays
 // in LDS.  Two workgroup shapes:
 //   4-wave workgroups, one wave a row, sharing the cost tables in LDS (batch
 //   launches with more rows than twice the pair slots); and
@@ -42,12 +42,11 @@
 // All integer; bit-exact with the C restatement (oracle/lossy_rd.c).
 #include <cstdlib>
 #include <mutex>
-#include <random>
-#include <atomic>
 
 #include "vp8_tables.h"
 #include "wg_common.h"
 #include "wg_dsp.h"
+#include "wg_instr.h"
 
 namespace {
 
@@ -58,7 +57,8 @@ constexpr int YOFF = BPS * 1 + 8;
 constexpr int UOFF = YOFF + BPS * 16 + BPS;
 constexpr int VOFF = UOFF + 16;
 constexpr int YUV = BPS * 17 + BPS * 9;
-constexpr int REC = 64;  // per MB column hand-off record (48 B used), one 64-B memory granule
+constexpr int REC = 128;  // per MB column hand-off record: REC_WORDS {word, tag} 8-B granules (88 B used)
+constexpr int REC_WORDS = 11;
 
 struct SQuant {  // SegmentQuant (encode.go:311-323); layout = wg_squant
   int32_t quant, iquant, bias, zthresh;
@@ -192,7 +192,6 @@ struct Shared {
   uint8_t yin[YUV], yout[YUV], yout2[YUV];
   alignas(16) int16_t coeffs[400];
   uint8_t mbtail[64];  // wg_mb_enc bytes 800..863, staged so the record leaves in one 16-B-per-lane store
-  alignas(16) uint32_t handoff[16];  // the hand-off record, staged for its 16-B write-through stores
   uint8_t modes4[16];
   uint8_t nzy[16], nzuv[8];
   int mode_rate[4], mode_disto[4], uv_rate[4], uv_disto[4];
@@ -201,15 +200,6 @@ struct Shared {
   // round).  Slots 17 records apart (WG_ENC_TPAD): at 16 (768 B, a multiple of
   // the 256-B bank row) the six DP quads' reads of one position all hit the
   // same banks.
-#ifndef WG_ENC_TPAD
-#define WG_ENC_TPAD 1
-#endif
-#ifndef WG_ENC_FUSE  // I4 candidates' FTransform in the pre-screen lanes (see the I4 RD)
-#define WG_ENC_FUSE 1
-#endif
-#ifndef WG_ENC_TAIL  // I4 candidates' rate from the DP, column-wise inverse DCT (see the I4 RD)
-#define WG_ENC_TAIL 1
-#endif
 // (WG_ENC_NLAST) the DP may stop after the last position of the round at
 // which any of its blocks has a non-zero level candidate: past it every state
 // but context 0's is invalid, so no terminal (EOB from context 1 / 2) can
@@ -220,39 +210,11 @@ struct Shared {
 // than walking all 16).  Measured (round 5, isolated 64 x 1080p launch, A/B):
 // the run-time exit 20.2-20.4 -> 21.2-21.3 ms, the buckets 20.3-20.6 ->
 // 20.6-20.7 ms (the second DP copy's registers and code): off.
-#ifndef WG_ENC_NLAST
-#define WG_ENC_NLAST 0
-#endif
-#ifndef WG_ENC_HOIST  // I4 candidates' prediction / source rows read before the trellis (see the I4 RD)
-#define WG_ENC_HOIST 1
-#endif
-#ifndef WG_ENC_I16ONE  // the final I16 trellis in one round, every block's DP for its three start contexts (see there)
-#define WG_ENC_I16ONE 1
-#endif
-#ifndef WG_ENC_RECPF  // the row above's next record prefetched at the end of each MB (see the MB loop)
-#define WG_ENC_RECPF 0
-#endif
-#ifndef WG_ENC_QSKIP  // the final I16 trellis walks no quarter of positions past the last candidate (see there)
-#define WG_ENC_QSKIP 0
-#endif
-#ifndef WG_ENC_PREPK  // the I4 pre-screen's SSE and FTransform on packed differences (sse_fdct_pk)
-#define WG_ENC_PREPK 0
-#endif
-#ifndef WG_ENC_NZBITS  // the MB's nz masks and context update from ballots (see the export)
-#define WG_ENC_NZBITS 1
-#endif
-#ifndef WG_ENC_TLANE  // trellis DPs: the best terminal as the quad's fourth state (trellis_dp4t)
-#define WG_ENC_TLANE 1
-#endif
-#ifndef WG_ENC_DPAHEAD  // positions the trellis DP loads ahead (1 or 2: measured equal, 1 kept)
-#define WG_ENC_DPAHEAD 1
-#endif
-#if WG_ENC_I16ONE
   // (the final I16 trellis, WG_ENC_I16ONE: the 16 blocks' records of one
   // half of the positions at a time, 9 records apart, and all 16 blocks'
   // level records)
   union {
-    TRec trec[6][16 + WG_ENC_TPAD];
+    TRec trec[6][17];
     TRec trec16[16][9];
   };
   int64_t r0[17][6];       // the phase's level-0 trellis row [0..2] and terminal row [3..5] (trellis_r0)
@@ -261,12 +223,6 @@ struct Shared {
     int16_t l0s[6][16];    // per position: L0 << 3 | negative << 2 | min(L0, 2) (< 2^14)
     int16_t l0s16[16][16];
   };
-#else
-  TRec trec[6][16 + WG_ENC_TPAD];
-  int64_t r0[17][6];       // the phase's level-0 trellis row [0..2] and terminal row [3..5] (trellis_r0)
-  int64_t eobl[16][2];     // the phase's terminal costs x lam16 (trellis_r0, WG_ENC_EOBT)
-  int16_t l0s[6][16];      // per position: L0 << 3 | negative << 2 | min(L0, 2) (< 2^14)
-#endif
   alignas(16) int16_t cand_q[6][16];  // I4 candidates' levels for the lane-parallel token cost
   int cand_nz[6], cand_rate[6];
   alignas(16) uint8_t pv[2][64];  // per half-wave: the I4 block's prediction value table
@@ -283,10 +239,7 @@ constexpr int WAVES = 4;  // rows per band: the waves of a group (one wave a row
 // CU, three waves per SIMD (149 VGPRs, 161 KB of LDS): measured slower in the
 // bench than two 4-wave workgroups per CU ("Three waves per SIMD"),
 // so 1 is the default.
-#ifndef WG_ENC_GROUPS
-#define WG_ENC_GROUPS 1
-#endif
-constexpr int GROUPS = WG_ENC_GROUPS;
+constexpr int GROUPS = 1;
 
 __device__ __forceinline__ int ecost(const Tables& t, int p) { return t.ecost[p]; }
 __device__ __forceinline__ int bit_cost(const Tables& t, int bit, int p) { return t.ecost[bit ? 255 - p : p]; }
@@ -394,20 +347,11 @@ __device__ __forceinline__ int token_cost(const Tables& t, const QT& q, int nz_c
 //
 // The R0 table of a phase: position n, predecessor context pc -> the
 // zero-token cost of band(n + 1) * lam16 + idx 4pc; lane 3n + pc writes it.
-#ifndef WG_ENC_EOBT
-#define WG_ENC_EOBT 1
-#endif
 // (WG_ENC_TWO, needs WG_ENC_EOBT) class-2 positions (L0 >= 2, both non-zero
 // levels end in context 2) are folded into the records: R1 = BIG, R2 =
 // min(R1, R2) per predecessor (the keys of L0 and L0 + 1 differ in their idx
 // bit, so the min is the reference's first strict minimum), and the DP keeps
 // no class test: every lane's own minimum is its context's new state
-#ifndef WG_ENC_TWO
-#define WG_ENC_TWO 1
-#endif
-#if WG_ENC_TWO && !WG_ENC_EOBT
-#error "WG_ENC_TWO needs WG_ENC_EOBT"
-#endif
 
 // (WG_ENC_EOBT) lanes 48 + n also write the phase's terminal costs: EOB after
 // position n from end context 1 / 2, x lam16 (0 after position 15), plus n
@@ -420,13 +364,11 @@ __device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16,
     const int n = lane / 3, pc = lane - 3 * n;
     r0[n][pc] = (int64_t)vc_of(t.vcost[CTX_TYPE * 8 + band_of(n + 1)][0], pc) * lam16 + 4 * pc;
   }
-#if WG_ENC_EOBT
   else {
     const int n = lane - 48;
     const TokRow& tr = t.tok[CTX_TYPE * 8 + band_of(n + 1)];
     eobl[n][0] = (n < 15 ? (int64_t)tr.eob[1] * lam16 : 0) + n;
     eobl[n][1] = (n < 15 ? (int64_t)tr.eob[2] * lam16 : 0) + n;
-#if WG_ENC_TLANE
     // the terminal lane's row of step n + 1 (trellis_dp4t): {0, EOB after
     // position n from context 1, from context 2}; none before the walk's
     // first position (FIRST: 0 for the I4 blocks, 1 for the I16 AC blocks)
@@ -441,9 +383,7 @@ __device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16,
       r0[0][4] = BIG;
       r0[0][5] = BIG;
     }
-#endif
   }
-#endif
 }
 
 // The level candidates, distortion deltas and token + level costs of two
@@ -458,7 +398,7 @@ __device__ __forceinline__ void trellis_r0(const Tables& t, int lane, int lam16,
 // report no level.
 template <int CTX_TYPE, int FIRST>
 __device__ __forceinline__ bool trellis_prep2(const Tables& t, const int16_t* co, int n0, const SQuant& sq, int lam16,
-                                              TRec out[2], int l0s[2], bool* cap = nullptr) {
+                                              TRec out[2], int l0s[2]) {
   constexpr int64_t BIG = 1ll << 59;
   int co_z[2], sh[2], quant[2], iquant[2], w4096[2];
 #pragma unroll
@@ -498,27 +438,17 @@ __device__ __forceinline__ bool trellis_prep2(const Tables& t, const int16_t* co
     const int64_t A0 = (int64_t)lf0[j] * lam16 + (int64_t)w * (wg::mul_i24(e0, e0) - c2) + (has0 ? 0 : BIG);
     const int64_t A1 = (int64_t)lf1[j] * lam16 + (int64_t)w * (wg::mul_i24(e1, e1) - c2) + (has1 ? 0 : BIG);
     const bool z = L0[j] == 0;
-#if WG_ENC_TWO
     const bool two = L0[j] >= 2;
-#endif
 #pragma unroll
     for (int pc = 0; pc < 3; pc++) {
       const int64_t r1 = (int64_t)vc_of(v0[j], pc) * lam16 + A0 + 4 * pc + 1;
       const int64_t r2 = (int64_t)vc_of(v1[j], pc) * lam16 + A1 + 4 * pc + 2;
-#if WG_ENC_TWO
       out[j].x[0][pc] = z ? r2 : (two ? BIG : r1);
       out[j].x[1][pc] = z ? BIG : (two && r1 < r2 ? r1 : r2);
-#else
-      out[j].x[0][pc] = z ? r2 : r1;
-      out[j].x[1][pc] = z ? BIG : r2;
-#endif
     }
     l0s[j] = L0[j] << 3 | (co_z[j] < 0 ? 4 : 0) | min(L0[j], 2);
     pnz |= L0raw[j] > 0 && n0 + j >= FIRST;
   }
-  // (WG_ENC_NLAST) a non-zero level is a candidate at either position
-  // (has0 || has1 <=> thresh >= 1; thresh is 0 below FIRST)
-  if (cap) *cap = thresh[0] >= 1 || thresh[1] >= 1;
   return pnz;
 }
 
@@ -563,9 +493,6 @@ __device__ __forceinline__ int quad_bcast32(int v) {
 // VOP2 DPP adds each, instead of two v_mov_dpp and two adds).  NOP: the
 // wait states before the first DPP read of s (2 after a VALU write of it,
 // 5 after an EXEC write: the walks' first position takes 5).
-#ifndef WG_ENC_DPPADD
-#define WG_ENC_DPPADD 1
-#endif
 // (T3: lane 3 adds its OWN value to x0 -- quad_perm [0,0,0,3] -- the
 // terminal lane of trellis_dp4t)
 template <int NOP, bool T3 = false>
@@ -606,17 +533,6 @@ __device__ __forceinline__ void quad_bcast_add3(int64_t s, int64_t x0, int64_t x
   c2 = (int64_t)((uint64_t)b2 << 32 | a2);
 }
 
-// The last position to walk (WG_ENC_NLAST): cap_mask = ballot of the prep
-// lanes' "non-zero candidate at position 2pp or 2pp + 1", pp = lane & 7 (each
-// byte: one block's eight pairs).  Wave-uniform.
-__device__ __forceinline__ int nlast_of(uint64_t cap_mask) {
-  uint64_t m = cap_mask | cap_mask >> 32;
-  m |= m >> 16;
-  m |= m >> 8;
-  const uint32_t b = (uint32_t)m & 0xff;
-  return b ? 2 * (31 - __builtin_clz(b)) + 1 : 15;
-}
-
 // The trellis DP on a quad of lanes.  trellis_prep routes the transitions
 // by the end context they reach (TRec rows R0 / R1 / R2), so lane k of the
 // quad (e = min(k, 2); lane 3 shadows lane 2) takes the minimum of the three
@@ -637,203 +553,9 @@ __device__ __forceinline__ int nlast_of(uint64_t cap_mask) {
 template <int CTX_TYPE>
 __device__ __forceinline__ void trellis_levels(const Tables& t, uint32_t hist, int k, uint2 l0w, int l0prev, int init_ctx,
                                                int16_t* q, int* nz, int* rate);
-template <int FIRST, int CTX_TYPE, int NEND = 16>
-__device__ __forceinline__ void trellis_dp4(const Tables& t, const TRec* rec, const int64_t (*r0)[6],
-                                            const int64_t (*eobl)[2], const int16_t* l0s, int init_ctx, int lam16, int k,
-                                            int16_t* q, int* nz, int* rate = nullptr) {
-  constexpr int64_t BIG = 1ll << 59;
-  init_ctx = min(init_ctx, 2);
-  const int e = min(k, 2);
-#if WG_ENC_TWO && WG_ENC_DPPADD
-  // lane j's own state (context min(j, 2)'s, masked to the score); the
-  // others' reach it as the DPP source of the next position's adds
-  int64_t st = k == init_ctx ? 0 : BIG;
-#else
-  int64_t ps0 = init_ctx == 0 ? 0 : BIG, ps1 = init_ctx == 1 ? 0 : BIG, ps2 = init_ctx == 2 ? 0 : BIG;
-#endif
-  uint32_t h0 = 0, h1 = 0, h2 = 0;  // the states' histories
-  const TokRow& t_init = t.tok[CTX_TYPE * 8 + FIRST];  // kBand[0] = 0, kBand[1] = 1
-  // lanes 0, 1 follow the terminals of context 1 (lane 0's copy is unused), lanes 2, 3 context 2
-  const int tctx = e == 2 ? 2 : 1;
-  int64_t best_terminal = (int64_t)pick3(init_ctx, t_init.eob[0], t_init.eob[1], t_init.eob[2]) * lam16;
-#if !WG_ENC_EOBT
-  int best_n = -1;
-#endif
-  uint32_t best_h = 0;
-  // this lane's row: R0 from the phase's table (3 words a position), R1 / R2
-  // from the block's records (6 words a position)
-  const int64_t* mine = e == 0 ? &r0[0][0] : &rec[0].x[e - 1][0];
-  constexpr int STRIDE = (int)(sizeof(TRec) / sizeof(int64_t));  // (R0's table rows padded to it)
-#if WG_ENC_EOBT
-  // terminal keys carry their position in the low 4 bits (the scores there
-  // are 0: states are masked to ~15 and the EOB costs are multiples of 16), so
-  // the first strict minimum over positions, and across the two contexts the
-  // earlier position on a tie, is a plain key min with no position register
-  const int64_t* eobq = &eobl[0][tctx - 1];
-  int64_t eob_raw = eobq[2 * FIRST];
-#else
-  const uint16_t* eobp = &t.tok[CTX_TYPE * 8].eob[0] + tctx;
-  constexpr int TSTR = sizeof(TokRow) / 2;
-  uint32_t eob_raw = FIRST < 15 ? eobp[kBand[FIRST + 1] * TSTR] : 0;
-#endif
-  // The tail's level records (lane r: positions 4r - 1 .. 4r + 3), loaded
-  // now: their latency hides under the walk instead of adding a round trip
-  // after it (l0s rows are 32 B, 8-B aligned at 4r)
-  const uint2 l0w = *reinterpret_cast<const uint2*>(l0s + 4 * k);
-  const int l0prev = l0s[max(4 * k - 1, 0)];
-  // Position n's row, class and EOB cost are loaded during position n - 1
-  // and pinned by the asm below, so no LDS round trip sits on the chain.
-  int64_t x0 = mine[FIRST * STRIDE], x1 = mine[FIRST * STRIDE + 1], x2 = mine[FIRST * STRIDE + 2];
-  int cls_raw = WG_ENC_TWO ? 0 : l0s[FIRST];
-#if WG_ENC_EOBT && WG_ENC_DPAHEAD == 2
-  // (two positions ahead: the LDS latency under the other waves' traffic
-  // outlasted one position of the chain)
-  int64_t y0 = 0, y1 = 0, y2 = 0, yeob = 0;
-  int ycls = 0;
-  if (FIRST + 1 < NEND) {
-    y0 = mine[(FIRST + 1) * STRIDE];
-    y1 = mine[(FIRST + 1) * STRIDE + 1];
-    y2 = mine[(FIRST + 1) * STRIDE + 2];
-    ycls = WG_ENC_TWO ? 0 : l0s[FIRST + 1];
-    yeob = eobq[2 * (FIRST + 1)];
-  }
-#endif
-#pragma unroll
-  for (int n = FIRST; n < NEND; n++) {
-    int64_t nx0 = 0, nx1 = 0, nx2 = 0;
-    int ncls = 0;
-#if WG_ENC_EOBT
-    int64_t neob = 0;
-#else
-    uint32_t neob = 0;
-#endif
-#if WG_ENC_EOBT && WG_ENC_DPAHEAD == 2
-    if (n + 2 < NEND) {
-      nx0 = mine[(n + 2) * STRIDE];
-      nx1 = mine[(n + 2) * STRIDE + 1];
-      nx2 = mine[(n + 2) * STRIDE + 2];
-      ncls = WG_ENC_TWO ? 0 : l0s[n + 2];
-      neob = eobq[2 * (n + 2)];
-    }
-#else
-    if (n + 1 < NEND) {
-      nx0 = mine[(n + 1) * STRIDE];
-      nx1 = mine[(n + 1) * STRIDE + 1];
-      nx2 = mine[(n + 1) * STRIDE + 2];
-      ncls = WG_ENC_TWO ? 0 : l0s[n + 1];
-#if WG_ENC_EOBT
-      neob = eobq[2 * (n + 1)];
-#else
-      if (n + 1 < 15) neob = eobp[kBand[n + 2] * TSTR];
-#endif
-    }
-#endif
-#if WG_ENC_TWO && WG_ENC_DPPADD
-    asm volatile("" : "+v"(st), "+v"(best_terminal)::"memory");
-    int64_t c0, c1, c2;
-    if (n == FIRST) quad_bcast_add3<4>(st, x0, x1, x2, c0, c1, c2);
-    else quad_bcast_add3<1>(st, x0, x1, x2, c0, c1, c2);
-#else
-    asm volatile("" : "+v"(ps0), "+v"(ps1), "+v"(ps2), "+v"(best_terminal)::"memory");
-    const int64_t c0 = ps0 + x0, c1 = ps1 + x1, c2 = ps2 + x2;
-#endif
-    const bool two = (cls_raw & 2) != 0;  // class 2: L0 >= 2
-    const auto eob_n = eob_raw;
-#if WG_ENC_EOBT && WG_ENC_DPAHEAD == 2
-    x0 = y0;
-    x1 = y1;
-    x2 = y2;
-    cls_raw = ycls;
-    eob_raw = yeob;
-    y0 = nx0;
-    y1 = nx1;
-    y2 = nx2;
-    ycls = ncls;
-    yeob = neob;
-#else
-    x0 = nx0;
-    x1 = nx1;
-    x2 = nx2;
-    cls_raw = ncls;
-    eob_raw = neob;
-#endif
-    // the winner's predecessor history by the min's own compares (its key's
-    // idx names the same predecessor: keys of different predecessors differ
-    // in idx, so the argmin is the key's pc)
-    const bool lt1 = c1 < c0;
-    const int64_t m01 = lt1 ? c1 : c0;
-    const bool lt2 = c2 < m01;
-    const int64_t m = lt2 ? c2 : m01;
-    const uint32_t code = (uint32_t)m & 3;  // the key's level code: R0 0; R1 / R2 1 (L0) or 2 (L0 + 1)
-    const uint32_t hm = (lt2 ? h2 : (lt1 ? h1 : h0)) | code << (2 * n);
-#if WG_ENC_TWO
-    (void)two;
-    // the new states, masked to the score before the broadcasts; lane 1's own
-    // state is context 1's, lanes 2 and 3's context 2's: the terminal of the
-    // lane's context (lane 0's is unused) needs no select
-    const int64_t mm = m & ~15ll;
-#if WG_ENC_DPPADD
-    st = mm;
-#else
-    ps0 = quad_bcast<0>(mm);
-    ps1 = quad_bcast<1>(mm);
-    ps2 = quad_bcast<2>(mm);
-#endif
-    h0 = quad_bcast32<0>(hm);
-    h1 = quad_bcast32<1>(hm);
-    h2 = quad_bcast32<2>(hm);
-    const int64_t eobs = mm + eob_n;
-    const bool w = eobs < best_terminal;
-    best_terminal = w ? eobs : best_terminal;
-    best_h = w ? hm : best_h;
-#else
-    const int64_t M0 = quad_bcast<0>(m), M1 = quad_bcast<1>(m), M2 = quad_bcast<2>(m);
-    const uint32_t H0 = quad_bcast32<0>(hm), H1 = quad_bcast32<1>(hm), H2 = quad_bcast32<2>(hm);
-    const bool lt = M1 < M2;
-    ps0 = M0 & ~15ll;
-    ps1 = two ? BIG : (M1 & ~15ll);
-    ps2 = (two && lt ? M1 : M2) & ~15ll;
-    h0 = H0;
-    h1 = H1;
-    h2 = two && lt ? H1 : H2;
-    // terminal (EOB after this position) of context tctx
-    const int64_t tps = tctx == 2 ? ps2 : ps1;
-#if WG_ENC_EOBT
-    const int64_t eobs = tps + eob_n;
-#else
-    const int64_t eobs = tps + (n < 15 ? (int64_t)eob_n * lam16 : 0);
-#endif
-    // (an invalid state, >= 2^59, never beats best_terminal, which starts at a
-    // valid EOB cost below 2^51 and only decreases: no separate validity test)
-    const bool w = eobs < best_terminal;
-    best_terminal = w ? eobs : best_terminal;
-#if !WG_ENC_EOBT
-    best_n = w ? n : best_n;
-#endif
-    best_h = w ? (tctx == 2 ? h2 : h1) : best_h;
-#endif
-  }
-  // the first strict minimum over (position, context 1 then 2), in every lane
-  const int64_t bt1 = quad_bcast<1>(best_terminal), bt2 = quad_bcast<2>(best_terminal);
-  const uint32_t bh1 = quad_bcast32<1>(best_h), bh2 = quad_bcast32<2>(best_h);
-#if WG_ENC_EOBT
-  // (both still at the all-zero start: equal keys, both histories 0)
-  const bool second = bt2 < bt1;
-#else
-  const int bn1 = quad_bcast32<1>(best_n), bn2 = quad_bcast32<2>(best_n);
-  const bool second = bt2 < bt1 || (bt2 == bt1 && bn2 < bn1);
-#endif
-  const uint32_t hist = second ? bh2 : bh1;  // 0 when no terminal beat the all-zero block
-  trellis_levels<CTX_TYPE>(t, hist, k, l0w, l0prev, init_ctx, q, nz, rate);
-}
-
-#if WG_ENC_TLANE && !(WG_ENC_TWO && WG_ENC_EOBT && WG_ENC_DPPADD)
-#error "WG_ENC_TLANE needs WG_ENC_TWO, WG_ENC_EOBT and WG_ENC_DPPADD"
-#endif
-// trellis_dp4 with the best terminal as the quad's fourth state
-// (WG_ENC_TLANE).  Lane 3 shadowed lane 2 there, and every lane kept a
-// best-terminal key and its history with a 64-bit add, compare and three
-// selects a position.  Here lane 3 is the terminal: at step n it takes the
+// Lane 3 of the quad is the best terminal (rather than a shadow of lane 2
+// with every lane keeping a best-terminal key and its history, a 64-bit add,
+// compare and three selects a position): at step n it takes the
 // same three-way minimum as the context lanes, over its own previous value
 // (DPP quad_perm [0,0,0,3]: lane 3 reads itself) and the context-1 / -2
 // states after position n - 1 plus their EOB costs, its row {0, EOB1, EOB2}
@@ -943,7 +665,6 @@ __device__ __forceinline__ void trellis_levels(const Tables& t, uint32_t hist, i
 // WG_ENC_TWO / EOBT records), so start s's result is trellis_dp4's for
 // init_ctx s.  Walked in two halves (positions [NB, NE)), the records of
 // the half at `mine` (`mine[n * STRIDE]` = this lane's row at position n).
-#if WG_ENC_TLANE
 // (WG_ENC_TLANE: lane 3 of the quad is each start's best terminal, as in
 // trellis_dp4t: its row is the phase table's columns 3..5, one step past the
 // last position takes the EOB after it)
@@ -1001,110 +722,6 @@ __device__ __forceinline__ uint32_t dp3_hist(const DP3& S, int s) {
   const uint32_t g0 = S.h[0][0], g1 = S.h[1][0], g2 = S.h[2][0];
   return quad_bcast32<3>(s == 0 ? g0 : (s == 1 ? g1 : g2));
 }
-#else
-struct DP3 {
-#if WG_ENC_DPPADD
-  int64_t st[3];     // [start context]: the lane's own state (quad_bcast_add3)
-#else
-  int64_t ps[3][3];  // [start context][context]: the states, masked to the score
-#endif
-  uint32_t h[3][3];
-  int64_t bt[3];     // the best terminal of the lane's context, per start
-  uint32_t bh[3];
-};
-__device__ __forceinline__ void dp3_init(DP3& S, const Tables& t, int lam16, int k) {
-  constexpr int64_t BIG = 1ll << 59;
-  const TokRow& t_init = t.tok[1];  // type 0, kBand[1] = 1
-#pragma unroll
-  for (int s = 0; s < 3; s++) {
-#if WG_ENC_DPPADD
-    S.st[s] = k == s ? 0 : BIG;
-#endif
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-#if !WG_ENC_DPPADD
-      S.ps[s][c] = c == s ? 0 : BIG;
-#endif
-      S.h[s][c] = 0;
-    }
-    S.bt[s] = (int64_t)t_init.eob[s] * lam16;
-    S.bh[s] = 0;
-  }
-}
-template <int NB, int NE>
-__device__ __forceinline__ void dp3_walk(DP3& S, const int64_t* mine, const int64_t* eobq) {
-  constexpr int STRIDE = (int)(sizeof(TRec) / sizeof(int64_t));
-  int64_t x0 = mine[NB * STRIDE], x1 = mine[NB * STRIDE + 1], x2 = mine[NB * STRIDE + 2];
-  int64_t eob_raw = eobq[2 * NB];
-#pragma unroll
-  for (int n = NB; n < NE; n++) {
-    int64_t nx0 = 0, nx1 = 0, nx2 = 0, neob = 0;
-    if (n + 1 < NE) {
-      nx0 = mine[(n + 1) * STRIDE];
-      nx1 = mine[(n + 1) * STRIDE + 1];
-      nx2 = mine[(n + 1) * STRIDE + 2];
-      neob = eobq[2 * (n + 1)];
-    }
-#if WG_ENC_DPPADD
-    asm volatile("" : "+v"(S.st[0]), "+v"(S.st[1]), "+v"(S.st[2]), "+v"(S.bt[0]), "+v"(S.bt[1]),
-                 "+v"(S.bt[2])::"memory");
-#else
-    asm volatile("" : "+v"(S.ps[0][0]), "+v"(S.ps[1][1]), "+v"(S.ps[2][2]), "+v"(S.bt[0]), "+v"(S.bt[1]),
-                 "+v"(S.bt[2])::"memory");
-#endif
-    const int64_t eob_n = eob_raw;
-#pragma unroll
-    for (int s = 0; s < 3; s++) {
-#if WG_ENC_DPPADD
-      int64_t c0, c1, c2;
-      if (n == NB && s == 0) quad_bcast_add3<4>(S.st[s], x0, x1, x2, c0, c1, c2);
-      else quad_bcast_add3<1>(S.st[s], x0, x1, x2, c0, c1, c2);
-#else
-      const int64_t c0 = S.ps[s][0] + x0, c1 = S.ps[s][1] + x1, c2 = S.ps[s][2] + x2;
-#endif
-      const bool lt1 = c1 < c0;
-      const int64_t m01 = lt1 ? c1 : c0;
-      const bool lt2 = c2 < m01;
-      const int64_t m = lt2 ? c2 : m01;
-      const uint32_t code = (uint32_t)m & 3;
-      // (values, not lvalues: a conditional of two array elements compiles
-      // to a select of their addresses and a load, i.e. S in scratch)
-      const uint32_t hv0 = S.h[s][0], hv1 = S.h[s][1], hv2 = S.h[s][2];
-      const uint32_t hm = (lt2 ? hv2 : (lt1 ? hv1 : hv0)) | code << (2 * n);
-      const int64_t mm = m & ~15ll;
-#if WG_ENC_DPPADD
-      S.st[s] = mm;
-#else
-      S.ps[s][0] = quad_bcast<0>(mm);
-      S.ps[s][1] = quad_bcast<1>(mm);
-      S.ps[s][2] = quad_bcast<2>(mm);
-#endif
-      S.h[s][0] = quad_bcast32<0>(hm);
-      S.h[s][1] = quad_bcast32<1>(hm);
-      S.h[s][2] = quad_bcast32<2>(hm);
-      const int64_t eobs = mm + eob_n;
-      const bool w = eobs < S.bt[s];
-      S.bt[s] = w ? eobs : S.bt[s];
-      S.bh[s] = w ? hm : S.bh[s];
-    }
-    x0 = nx0;
-    x1 = nx1;
-    x2 = nx2;
-    eob_raw = neob;
-  }
-}
-// start s's chosen history: the first strict minimum over (position, context
-// 1 then 2) of its terminals, as at the end of trellis_dp4
-__device__ __forceinline__ uint32_t dp3_hist(const DP3& S, int s) {
-  const int64_t b0 = S.bt[0], b1 = S.bt[1], b2 = S.bt[2];
-  const uint32_t g0 = S.bh[0], g1 = S.bh[1], g2 = S.bh[2];
-  const int64_t b = s == 0 ? b0 : (s == 1 ? b1 : b2);
-  const uint32_t h = s == 0 ? g0 : (s == 1 ? g1 : g2);
-  const int64_t bt1 = quad_bcast<1>(b), bt2 = quad_bcast<2>(b);
-  const uint32_t bh1 = quad_bcast32<1>(h), bh2 = quad_bcast32<2>(h);
-  return bt2 < bt1 ? bh2 : bh1;
-}
-#endif
 __device__ __forceinline__ int hist_nz(uint32_t hist) {
   const uint32_t nzb = (hist | hist >> 1) & 0x55555555u;
   return nzb == 0 ? 0 : ((31 - __builtin_clz(nzb)) >> 1) + 1;
@@ -1299,12 +916,7 @@ __device__ __forceinline__ int ttrans(const int px[16]) {  // tTransform (ssim.g
   }
   return sum;
 }
-__device__ __forceinline__ int tdisto(const int a[16], const int b[16]) { return abs(ttrans(b) - ttrans(a)) >> 5; }
-#ifndef WG_ENC_FDCT_PK  // FTransform on packed int16 row pairs (wg::fdct4x4_pk)
-#define WG_ENC_FDCT_PK 1
-#endif
 __device__ __forceinline__ void fdct(const int src[16], const int pred[16], int co[16]) {
-#if WG_ENC_FDCT_PK
   wg::s16x2_t d01[4], d32[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -1312,15 +924,6 @@ __device__ __forceinline__ void fdct(const int src[16], const int pred[16], int 
     d32[k] = (wg::s16x2_t){(short)(src[12 + k] - pred[12 + k]), (short)(src[8 + k] - pred[8 + k])};
   }
   wg::fdct4x4_pk(d01, d32, co);
-#else
-  int d[16];
-  int16_t o[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) d[i] = src[i] - pred[i];
-  fdct4x4(d, o);
-#pragma unroll
-  for (int i = 0; i < 16; i++) co[i] = o[i];
-#endif
 }
 __device__ __forceinline__ void store4x4(uint8_t* p, const int v[16]) {
 #pragma unroll
@@ -1362,29 +965,7 @@ __device__ __forceinline__ int sse_p(const P4& a, const P4& b) {
   return (int)(aa + bb - 2 * ab);
 }
 // FTransform of (src - pred), rows unpacked one at a time
-// (WG_ENC_PREPK) the pre-screen's SSE and FTransform of one mode from the
-// source rows (packed bytes) and the prediction (16 ints): the differences
-// formed once, as the int16 column pairs fdct4x4_pk takes (rows 0 | 1 and
-// 3 | 2), and the SSE as eight v_dot2_i32_i16 of them with themselves
-// (exact: |d| <= 255, the sum < 2^21)
-__device__ __forceinline__ int sse_fdct_pk(const P4& s, const int pred[16], int co[16]) {
-  wg::s16x2_t d01[4], d32[4];
-  int sse = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const uint32_t sel = 0x0c000c00u | (uint32_t)(4 + k) << 16 | (uint32_t)k;
-    d01[k] = __builtin_bit_cast(wg::s16x2_t, __builtin_amdgcn_perm(s.r[1], s.r[0], sel)) -
-             __builtin_bit_cast(wg::s16x2_t, (uint32_t)pred[k] | (uint32_t)pred[4 + k] << 16);
-    d32[k] = __builtin_bit_cast(wg::s16x2_t, __builtin_amdgcn_perm(s.r[2], s.r[3], sel)) -
-             __builtin_bit_cast(wg::s16x2_t, (uint32_t)pred[12 + k] | (uint32_t)pred[8 + k] << 16);
-    sse = wg::sdot2_acc(d01[k], d01[k], sse);
-    sse = wg::sdot2_acc(d32[k], d32[k], sse);
-  }
-  wg::fdct4x4_pk(d01, d32, co);
-  return sse;
-}
 __device__ __forceinline__ void fdct_p(const P4& s, const P4& p, int co[16]) {
-#if WG_ENC_FDCT_PK
   // (byte k of rows a and b as the int16 halves of a word: one v_perm each)
   wg::s16x2_t d01[4], d32[4];
 #pragma unroll
@@ -1397,7 +978,6 @@ __device__ __forceinline__ void fdct_p(const P4& s, const P4& p, int co[16]) {
   }
   wg::fdct4x4_pk(d01, d32, co);
   return;
-#endif
   int tmp[16];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -1500,12 +1080,6 @@ __device__ __forceinline__ void predsq_block(int mode, const uint8_t* base, int 
 #pragma unroll
   for (int r = 0; r < 4; r++) unpack_rows(predsq_row4(mode, base, px, py + r, dc), pred + 4 * r);
 }
-__device__ __forceinline__ void pred4_block(int mode, const uint8_t* buf, int off, int pred[16]) {
-  int X, T[8], L[4];
-  pred4_ctx(buf, off, X, T, L);
-#pragma unroll
-  for (int r = 0; r < 4; r++) unpack_rows(pred4_row(mode, r, X, T, L), pred + 4 * r);
-}
 // Build the block's value table V (see kPred4Code) from the context around
 // buf + off in one pass of the caller's half-wave (lane i < 32): lanes 0..14
 // load the edge E[i] and take their neighbours' by DPP row shifts for the
@@ -1578,11 +1152,7 @@ __device__ __forceinline__ T group_sum(T v, int width) {  // sum over aligned gr
 // Cross-wave exchanges (the pair schedule's join, the I16 score flag) keep
 // their barriers and explicit waits.
 __device__ __forceinline__ void lds_sync() {
-#ifdef WG_ENC_DRAIN
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
   asm volatile("" ::: "memory");
-#endif
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -1612,36 +1182,23 @@ __device__ __forceinline__ T& launder(T& s) {
   return *(T*)p;
 }
 
-// sc1 hand-off helpers (see decode.hip)
-__device__ __forceinline__ uint32_t ld_sc1_32(const uint8_t* p) {
-  return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// The row hand-off: a record of REC_WORDS words per MB column (the Y bottom
+// row's pixels 0-3, U 4-5, V 6-7, top nz 8, top modes 9, top DC nz 10), each
+// word in an 8-B granule {word, tag} that is written and read as ONE 64-bit
+// atomic (single-copy atomic in the AMDGPU memory model), tag = the writing
+// row + 1.  The row below polls the granules themselves -- no progress
+// counter, no store drain before a flag, and the record arrives with the poll
+// that finds it -- and no granule can pass the poll with a word other than
+// the one stored beside its tag.  Every launch clears the records first (with
+// its control words, wg_encode_mbs), so a granule holds 0 until its row of
+// THIS launch writes it: no record of an earlier launch on the buffer passes.
+__device__ __forceinline__ uint64_t ld_granule(const uint8_t* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_sc1_32(uint8_t* p, uint32_t v) {
-  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void st_granule(uint8_t* p, uint32_t word, uint32_t tag) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), (uint64_t)tag << 32 | word, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
-// one 16-B write-through (sc1) store: a hand-off record leaves as whole
-// 16-B pieces of one 64-B granule instead of eleven 4-B partial writes
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st_sc1_128(uint8_t* p, u32x4_t v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ uint4 ld_sc1_128(const uint8_t* p) {
-  uint4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-// (WG_ENC_TAGGED) the row hand-off as four tagged 16-B granules a column:
-// word 3 of each is the writing row's tag (launch epoch x 2^14 + row + 1),
-// the other three carry the record's words 3p .. 3p + 2 (Y bottom row 0-3,
-// U 4-5, V 6-7, top nz 8, top modes 9, top DC nz 10).  A 16-B sc1 store is
-// seen whole (MI355X_MICROARCH.md, R2 granules), so the row below polls the
-// granules themselves: no progress counter, no store drain before a flag,
-// and the record arrives with the poll that finds it.  Stale granules carry
-// an older row's or launch's tag.
-#ifndef WG_ENC_TAGGED
-#define WG_ENC_TAGGED 1
-#endif
-__device__ __forceinline__ uint32_t row_tag(uint32_t epoch, int row) { return epoch * 0x4000u + (uint32_t)row + 1u; }
 
 struct EncArgs {
   const uint8_t* y;  // source planes (stride 16*mbw / 8*mbw), pitch per image
@@ -1656,7 +1213,6 @@ struct EncArgs {
   const uint8_t* proba;     // 1056
   MbEnc* out;
   uint8_t* top;   // [n_img][mbw][REC]
-  int* progress;  // [n_img][mbh]
   int* ctl;       // [0] dequeue, [1] error
   int* diag;      // wg::diag_words + DIAG_ENCODE
   const int* order;  // the work buffer's row schedule (wg_encode_row_order): dequeue index -> row * n_img + image
@@ -1664,93 +1220,21 @@ struct EncArgs {
   const int* order_tag;  // {ORDER_TAG ^ n_img, ~(ORDER_TAG ^ mbh)} when the schedule was built for this batch shape, else (row, image) order
   int64_t y_pitch, uv_pitch;
   int width, height, mbw, mbh, n_img, quality;
-  uint32_t epoch;  // this launch's tag base (WG_ENC_TAGGED)
 };
 
 constexpr uint64_t SPIN_TICKS = 200000000ull;
 
 constexpr int ORDER_TAG = 0x5e0d0000;  // marks a row schedule in the work buffer (xor the batch shape)
 
-#ifdef WG_STAMPS
-// Diagnostic build only: cycles per phase summed over macroblocks.
-__device__ unsigned long long g_enc_phase[16];
-#define ESTAMP_DECL unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0, sub_prev = 0, cst_prev = 0, dst_prev = 0
-#define ESTAMP(k)                                                                  \
-  do {                                                                             \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    unsigned long long ts_;                                                        \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");   \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    if ((k) > 0) st_acc[(k)-1] += ts_ - st_prev;                                   \
-    st_prev = ts_;                                                                 \
-  } while (0)
-#define ESTAMP_FLUSH()                                                              \
-  do {                                                                              \
-    if (lane == 0)                                                                  \
-      for (int k_ = 0; k_ < 16; k_++) atomicAdd(&g_enc_phase[k_], st_acc[k_]);      \
-  } while (0)
-// sub-phase stamps (inside a phase): accumulate into st_acc[8 + k], k >= 0
-#define SSTAMP(k)                                                                  \
-  do {                                                                             \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    unsigned long long ts_;                                                        \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");   \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    if ((k) >= 0) st_acc[8 + (k)] += ts_ - sub_prev;                              \
-    sub_prev = ts_;                                                                \
-  } while (0)
-// candidate-internal stamps: accumulate into st_acc[12 + k], k >= 0
-#define CSTAMP(k)                                                                  \
-  do {                                                                             \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    unsigned long long ts_;                                                        \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");   \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    if ((k) >= 0) st_acc[12 + (k)] += ts_ - cst_prev;                             \
-    cst_prev = ts_;                                                                \
-  } while (0)
-// the I4 trellis DP alone (inside c:trellis): st_acc[7]
-#define DSTAMP(k)                                                                  \
-  do {                                                                             \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    unsigned long long ts_;                                                        \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");   \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    if ((k) >= 0) st_acc[7] += ts_ - dst_prev;                                     \
-    dst_prev = ts_;                                                                \
-  } while (0)
-#else
-#define DSTAMP(k) (void)0
-#define CSTAMP(k) (void)0
-#define SSTAMP(k) (void)0
-#define ESTAMP_DECL int st_unused_ = 0
-#define ESTAMP(k) (void)st_unused_
-#define ESTAMP_FLUSH() (void)st_unused_
-#endif
+// (WG_STAMPS builds, wg_instr.h) cycles per phase summed over macroblocks
+WG_IF_STAMPS(__device__ unsigned long long g_enc_phase[16];)
 
-#ifdef WG_ROWTIMES
-// Diagnostic build only: per dequeued row, {ro, start, end, block} in
+// (WG_ROWTIMES builds) per dequeued row, {ro, start, end, block} in
 // s_memrealtime ticks (100 MHz) -- the launch's row timeline
-// (tools/enc_timeline.py).
-__device__ unsigned long long g_row_times[16384][4];
-#endif
+WG_IF_ROWTIMES(__device__ unsigned long long g_row_times[16384][4];)
 
-#ifndef WG_ENC_OCC
-#define WG_ENC_OCC (WG_ENC_GROUPS == 3 ? 3 : 2)  // waves per SIMD (VGPR budget 512 / occupancy)
-#endif
 
-// Measurement builds only (tools/gpu_enc_phase_sq.sh): -DWG_EXP_REP_<PHASE>=2
-// runs that phase twice per macroblock.  Each repeated phase is idempotent
-// (it reads only state written before it and rewrites the same values), so
-// the outputs stay bit-exact and a counter of the build minus the default
-// build's is that phase's own share -- per-phase VALU lane occupancy, LDS
-// bank conflicts and waits, with the data flow, early exits and contention of
-// the real launch.  Phases: RD (I16 + UV RD), I4 (the whole I4 RD), PRE (I4
-// value table + pre-screen), CAND (candidates' prediction + FTransform), PREP
-// (trellis position records), DP (the trellis DP), FIN (final residuals).
-// The default build compiles none of it.
-#define WG_REP_BEGIN(N) for (int rep_ = 0; rep_ < (N); rep_++) {
-#define WG_REP_END }
+// (WG_EXP_REP_<P> builds: WG_REP_BEGIN(P) / WG_REP_END around a phase, wg_instr.h)
 
 // An image's four segment tables (4 x 224 B = 56 x 16 B) into LDS
 __device__ __forceinline__ void load_segments(const EncArgs& a, int img, Segment* dst, int lane) {
@@ -1785,7 +1269,7 @@ __device__ __forceinline__ void group_barrier(int* cnt, int& gen, int lane) {
 // roughly halves a macroblock's latency for launches whose rows fit the
 // wave slots twice over (one frame, C2); a full batch keeps one wave a row.
 template <bool TRELLIS, bool PAIR>
-__global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC_OCC) void k_encode_rows(EncArgs a) {
+__global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) void k_encode_rows(EncArgs a) {
   constexpr int NW = PAIR ? 2 : WAVES * GROUPS;
   __shared__ Tables t_lds;
   __shared__ Shared s_waves[NW];
@@ -1947,9 +1431,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       row = WAVES * band + gw;
     }
     const bool live = mby < mbh;  // (the last band of an image may have fewer rows)
-#ifdef WG_ROWTIMES
-    const unsigned long long row_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
+    WG_IF_ROWTIMES(const unsigned long long row_t0 = __builtin_amdgcn_s_memrealtime();)
     const uint8_t* Y = a.y + img * a.y_pitch;
     const uint8_t* U = a.u + img * a.uv_pitch;
     const uint8_t* V = a.v + img * a.uv_pitch;
@@ -1957,8 +1439,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
     uint8_t* RU = a.ru + img * a.uv_pitch;
     uint8_t* RV = a.rv + img * a.uv_pitch;
     uint8_t* top = a.top + (int64_t)img * mbw * REC;
-    int* prog_above = a.progress + (int64_t)img * mbh + mby - 1;
-    int* prog_mine = a.progress + (int64_t)img * mbh + mby;
     if (PAIR && isA) load_segments(a, img, s_seg[0], lane);  // (B reads them after the MB's first join barrier)
     // left context (encodeRow :257-282)
     if (lane < 16) s.yout[YOFF - 1 + lane * BPS] = 129;
@@ -1968,14 +1448,10 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
     int left_nz_dc = 0;
     uint32_t left_modes = 0;  // 4 x 8 bits, B_DC_PRED = 0
     int tl_y = 127, tl_u = 127, tl_v = 127;
-    int seen = 0;
     // source rows loaded ahead for the next MBs of the pair / quad (import),
     // reconstruction rows held back for a whole-sector store (export)
     uint4 stg0 = make_uint4(0, 0, 0, 0), stg1 = stg0, rst0 = stg0;
     uint2 rst1 = make_uint2(0, 0);
-    // (WG_ENC_RECPF) column x + 1's record of the row above, loaded at the end
-    // of MB x so that MB x + 1's first tag check has it in registers
-    [[maybe_unused]] uint4 pre_above = make_uint4(0, 0, 0, 0);
 
     for (int mbx = 0; live && mbx < mbw; mbx++) {
       Shared& s = launder(s_waves[wave]);
@@ -1990,42 +1466,19 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       // (3, 7, 11, 15) read MB x+1 of the row above (its first 4 bottom
       // pixels, the top-right context), and the first of them runs at I4
       // step 3.  So the MB starts once MB x of the row above is done, and
-      // waits for MB x+1 only there (wait_above(mbx + 2)): the outputs are
+      // waits for MB x+1 only there (the top-right poll): the outputs are
       // the reference's, the rows just trail each other by less.
-      auto wait_above = [&](int need) {
-        if (mby > 0 && seen < need) {
-          int v = 0;
-          if (lane == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (uint32_t it = 0;; it++) {
-              v = __hip_atomic_load(prog_above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if (v >= need) break;
-              if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
-                                      __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                wg::note_timeout(a.diag, mby, img, need, v, (int)(__builtin_amdgcn_s_memrealtime() - t0),
-                                 (int)blockIdx.x);
-                v = mbw;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(2);
-            }
-          }
-          seen = __shfl(v, 0, 64);
-        }
-      };
-#if WG_ENC_TAGGED
-      // the tagged record of column x of the row above (lane p < 4: granule p),
-      // polled until all four carry the row's tag
-      const uint32_t want = row_tag(a.epoch, mby - 1);
-      auto poll_rec = [&](const uint8_t* rec, int n, bool pre = false) -> uint4 {
-        uint4 g = make_uint4(0, 0, 0, 0);
+      // the record of column x of the row above (lane i < n: word i), polled
+      // until every granule carries the row's tag
+      auto poll_rec = [&](const uint8_t* rec, int n) -> uint32_t {
+        uint32_t w = 0;
         if (mby > 0) {
+          const uint32_t want = (uint32_t)mby;  // row mby - 1's tag
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           for (uint32_t it = 0;; it++) {
-            if (pre && it == 0) g = pre_above;  // (the prefetched granules: checked like a load)
-            else if (lane < n) g = ld_sc1_128(rec + 16 * lane);
-            if (__ballot(lane < n && g.w != want) == 0) break;
+            const uint64_t g = lane < n ? ld_granule(rec + 8 * lane) : 0;
+            w = (uint32_t)g;
+            if (__ballot(lane < n && (uint32_t)(g >> 32) != want) == 0) break;
             if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
                                     __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
               if (lane == 0) {
@@ -2037,13 +1490,10 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             __builtin_amdgcn_s_sleep(2);
           }
         }
-        return g;
+        return w;
       };
-      uint4 above = make_uint4(0, 0, 0, 0);
-      if (isA) above = poll_rec(top + mbx * REC, 4, WG_ENC_RECPF && mbx > 0);
-#else
-      if (isA) wait_above(mbx + 1);
-#endif
+      uint32_t above = 0;
+      if (isA) above = poll_rec(top + mbx * REC, REC_WORDS);
       ESTAMP(1);
       const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
       const Segment& sg = s_seg[PAIR ? 0 : (LOOSE ? (q & 1) : grp)][segid];
@@ -2095,32 +1545,15 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       }
       // ---- prediction context (fillPredContextParallel :455-562) ----
       {
-        const uint8_t* rec = top + mbx * REC;
         if (mby > 0) {
-#if WG_ENC_TAGGED
-          // lane p holds words 3p .. 3p + 2 (Y16 U8 V8 of the row above: words 0-7)
-          auto put = [&](int i, uint32_t w) {
-            const int o = i < 4 ? YOFF - BPS + 4 * i : (i < 6 ? UOFF - BPS + 4 * (i - 4) : VOFF - BPS + 4 * (i - 6));
-            *reinterpret_cast<uint32_t*>(s.yout + o) = w;
-          };
-          if (lane < 3) {
-            put(3 * lane, above.x);
-            put(3 * lane + 1, above.y);
-            if (lane < 2) put(3 * lane + 2, above.z);
-          }
-          top_nz = (uint32_t)__builtin_amdgcn_readlane((int)above.z, 2);
-          top_modes = (uint32_t)__builtin_amdgcn_readlane((int)above.x, 3);
-          top_nz_dc = __builtin_amdgcn_readlane((int)above.y, 3);
-#else
-          if (lane < 8) {  // Y16 U8 V8 of the row above
-            const uint32_t w = ld_sc1_32(rec + 4 * lane);
+          // lane i holds word i (Y16 U8 V8 of the row above: words 0-7)
+          if (lane < 8) {
             const int o = lane < 4 ? YOFF - BPS + 4 * lane : (lane < 6 ? UOFF - BPS + 4 * (lane - 4) : VOFF - BPS + 4 * (lane - 6));
-            *reinterpret_cast<uint32_t*>(s.yout + o) = w;
-          }  // (the top-right: at I4 step 3)
-          top_nz = ld_sc1_32(rec + 32);
-          top_modes = ld_sc1_32(rec + 36);
-          top_nz_dc = (int)ld_sc1_32(rec + 40);
-#endif
+            *reinterpret_cast<uint32_t*>(s.yout + o) = above;
+          }
+          top_nz = (uint32_t)__builtin_amdgcn_readlane((int)above, 8);
+          top_modes = (uint32_t)__builtin_amdgcn_readlane((int)above, 9);
+          top_nz_dc = __builtin_amdgcn_readlane((int)above, 10);
         } else {
           if (lane < 21) s.yout[YOFF - BPS + lane] = 127;  // cols 0..20 (top-right incl.)
           else if (lane < 29) s.yout[UOFF - BPS + lane - 21] = 127;
@@ -2167,9 +1600,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       if (isB) {
       // ================= I16 RD (pickBestI16ModeRDParallel :624-737) =================
       // then UV RD (pickBestUVModeRDParallel :1030-1114)
-#if defined(WG_EXP_REP_RD)
-      WG_REP_BEGIN(WG_EXP_REP_RD)
-#endif
+      WG_REP_BEGIN(RD)
       bool src_flat;
       {
         // isFlatSource16 (encode_analysis.go:358)
@@ -2295,9 +1726,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         }
       }
       s16 = rd_score(disto16, rate16, sg.lambda_mode);
-#if defined(WG_EXP_REP_RD)
       WG_REP_END
-#endif
       if constexpr (PAIR) {  // for A's early exit: the score, then the flag
         if (lane == 0) {
           *reinterpret_cast<volatile uint64_t*>(&c.s16v) = s16;
@@ -2326,9 +1755,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           if (i < YUV / 4) reinterpret_cast<uint32_t*>(s.yout2)[i] = reinterpret_cast<const uint32_t*>(s.yout)[i];
         }
       }
-#if defined(WG_EXP_REP_I4)
-      WG_REP_BEGIN(WG_EXP_REP_I4)
-#endif
+      WG_REP_BEGIN(I4)
       if constexpr (TRELLIS) trellis_r0<3>(t, lane, sg.tlambda_i4 * 16, s.r0, s.eobl);
       lds_sync();
       {
@@ -2347,23 +1774,14 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             // row from the context fill) and its copies beside rows 3, 7, 11
             // for blocks 7, 11, 15 (fillPredContextParallel :455-562)
             if (mby > 0) {
-#if WG_ENC_TAGGED
-              // (granule 0 of column x + 1: its word 0 is the Y bottom row's pixels 0-3)
+              // (granule 0 of column x + 1: word 0, the Y bottom row's pixels 0-3)
               const uint32_t trn = mbx < mbw - 1 ? (uint32_t)__builtin_amdgcn_readfirstlane(
-                                                       (int)poll_rec(top + (mbx + 1) * REC, 1).x)
+                                                       (int)poll_rec(top + (mbx + 1) * REC, 1))
                                                  : 0u;
               if (lane == 0) {
                 const uint32_t tr = mbx < mbw - 1 ? trn : 0x01010101u * s.yout2[YOFF - BPS + 15];
                 *reinterpret_cast<uint32_t*>(s.yout2 + YOFF - BPS + 16) = tr;
               }
-#else
-              if (mbx < mbw - 1) wait_above(mbx + 2);
-              if (lane == 0) {
-                const uint32_t tr = mbx < mbw - 1 ? ld_sc1_32(top + (mbx + 1) * REC)
-                                                  : 0x01010101u * s.yout2[YOFF - BPS + 15];
-                *reinterpret_cast<uint32_t*>(s.yout2 + YOFF - BPS + 16) = tr;
-              }
-#endif
               lds_sync();
             }
             if (lane < 12) {
@@ -2392,11 +1810,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           // (FUSE) every pre-screen lane also transforms its mode's residual:
           // the candidates are among these lanes, so their coefficients come
           // without a second prediction pass (its 17 LDS reads) after the pick
-          constexpr bool FUSE = TRELLIS && WG_ENC_FUSE;
+          constexpr bool FUSE = TRELLIS;
           int pco[FUSE ? 16 : 1];
-#if defined(WG_EXP_REP_PRE)
-      WG_REP_BEGIN(WG_EXP_REP_PRE)
-#endif
+      WG_REP_BEGIN(PRE)
           // (the lane's mode code read first: in flight while the table is built)
           const uint4 pcw = *reinterpret_cast<const uint4*>(t.pcode[min(hl, 9)]);
           pred4_values(s.yout2, off, hl, s.pv[half]);
@@ -2404,17 +1820,10 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           if (bvalid && hl < 10) {
             int pred[16];
             pred4_lut(pcw, s.pv[half], pred);
-#if WG_ENC_PREPK && WG_ENC_FDCT_PK
-            if constexpr (FUSE) sse_lane = sse_fdct_pk(ld4(s.yin + off), pred, pco);
-            else sse_lane = sse16(src, pred);
-#else
             sse_lane = sse16(src, pred);
             if constexpr (FUSE) fdct(src, pred, pco);
-#endif
           }
-#if defined(WG_EXP_REP_PRE)
       WG_REP_END
-#endif
           SSTAMP(0);
           // eligible modes (no top / no left context rules out some), candidates
           uint32_t eligible = 0x3ff;
@@ -2432,9 +1841,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           const int qc = min(hl >> 2, 2), qr = hl & 3, qsl = half * 3 + qc;
           const int qmode = min(pick3(qc, cm[0], cm[1], cm[2]) & 15, 9);
           uint32_t pred_row = 0, src_row = 0;
-          int hdr_h = 0;  // (HOIST) the mode's header bits
-          if constexpr (WG_ENC_HOIST) {
-            hdr_h = t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];
+          const int hdr_h = t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];  // the mode's header bits
+          {
             const uint32_t cw = reinterpret_cast<const uint32_t*>(t.pcode[qmode])[qr];
             int pr[4];
 #pragma unroll
@@ -2444,9 +1852,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           }
           SSTAMP(1);
           // candidates: prediction + transform (lane hl = candidate hl)
-#if defined(WG_EXP_REP_CAND)
-      WG_REP_BEGIN(WG_EXP_REP_CAND)
-#endif
+      WG_REP_BEGIN(CAND)
           if constexpr (FUSE) {  // the lane of mode cm[c] stores candidate c's coefficients
             const int c = (K > 0 && cm[0] == hl) ? 0 : ((K > 1 && cm[1] == hl) ? 1 : ((K > 2 && cm[2] == hl) ? 2 : 3));
             if (bvalid && hl < 10 && c < 3) {
@@ -2469,9 +1875,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             }
             CSTAMP(0);
           }
-#if defined(WG_EXP_REP_CAND)
       WG_REP_END
-#endif
           lds_sync();
           // (TRELLIS + TAIL) the candidate's nz count and rate, straight from
           // the DP into the reconstruction quad's registers (the same lanes)
@@ -2479,28 +1883,23 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           if constexpr (TRELLIS) {
           // trellis positions: lane (candidate c, pair pp) prepares positions 2pp, 2pp + 1
           const int lam16 = sg.tlambda_i4 * 16;
-          bool pnz = false, pcap = false;
-#if defined(WG_EXP_REP_PREP)
-      WG_REP_BEGIN(WG_EXP_REP_PREP)
-#endif
+          bool pnz = false;
+      WG_REP_BEGIN(PREP)
           if (bvalid && hl < 8 * K) {
             const int c = hl >> 3, n0 = 2 * (hl & 7), sl = half * 3 + c;
             // both positions into registers first, then stored: their table
             // reads issue together instead of waiting behind the first one's stores
             TRec rr[2];
             int l0[2];
-            pnz = trellis_prep2<3, 0>(t, s.co_buf[sl], n0, sg.y1, lam16, rr, l0, &pcap);
+            pnz = trellis_prep2<3, 0>(t, s.co_buf[sl], n0, sg.y1, lam16, rr, l0);
 #pragma unroll
             for (int j = 0; j < 2; j++) {
               s.trec[sl][n0 + j] = rr[j];
               s.l0s[sl][n0 + j] = l0[j];
             }
           }
-#if defined(WG_EXP_REP_PREP)
       WG_REP_END
-#endif
           const uint64_t pnz_mask = __ballot(pnz);
-          [[maybe_unused]] const int nlast = nlast_of(__ballot(pcap));
           lds_sync();
           DSTAMP(-1);
           // the trellis DP: one lane quad per candidate (lane 4c + k owns end context k)
@@ -2510,28 +1909,10 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               // the DP is the step's serial chain: let it win issue arbitration
               // against the SIMD's other wave while it runs
               __builtin_amdgcn_s_setprio(3);
-#if defined(WG_EXP_REP_DP)
-      WG_REP_BEGIN(WG_EXP_REP_DP)
-#endif
-#if WG_ENC_NLAST
-              if (nlast < 8)
-                trellis_dp4<0, 3, 8>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl],
-                                     &dp_nz, WG_ENC_TAIL ? &dp_rate : nullptr);
-              else
-#endif
-#if WG_ENC_TLANE
+      WG_REP_BEGIN(DP)
               trellis_dp4t<0, 3>(t, s.trec[sl], s.r0, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &dp_nz,
-                                 WG_ENC_TAIL ? &dp_rate : nullptr);
-#else
-              trellis_dp4<0, 3>(t, s.trec[sl], s.r0, s.eobl, s.l0s[sl], nz_ctx, lam16, hl & 3, s.cand_q[sl], &dp_nz,
-                                WG_ENC_TAIL ? &dp_rate : nullptr);
-#endif
-              if constexpr (!WG_ENC_TAIL) {
-                if ((hl & 3) == 0) s.cand_nz[sl] = dp_nz;
-              }
-#if defined(WG_EXP_REP_DP)
+                                 &dp_rate);
       WG_REP_END
-#endif
               __builtin_amdgcn_s_setprio(2);
             } else {
               dp_nz = 0;
@@ -2558,7 +1939,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           // the inverse DCT's vertical pass runs one column a quad lane,
           // transposed across the quad by DPP: 4 levels and 4 products a lane
           // instead of 16 and 16
-          constexpr bool TAIL = TRELLIS && WG_ENC_TAIL;
+          constexpr bool TAIL = TRELLIS;
           int16_t qv[TAIL ? 1 : 16];
           int tcol[4];  // (TAIL) column qr of the row pass: reconstruction | source << 16
           int qnz = 0, sse_r = 0, cnt = 0;
@@ -2572,7 +1953,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           {
             CSTAMP(1);
             int res[4], pr[4], sr[4], rr[4];
-            qnz = (TRELLIS && WG_ENC_TAIL) ? dp_nz : s.cand_nz[qsl];
+            qnz = TRELLIS ? dp_nz : s.cand_nz[qsl];
             if constexpr (TAIL) {
               // column qr: levels qr, 4 + qr, 8 + qr, 12 + qr (raster)
               const int16_t* cq = s.cand_q[qsl];
@@ -2612,15 +1993,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
               dequant(qv, dq, sg.y1);
               idct_row(dq, qr, res);
             }
-            if constexpr (!WG_ENC_HOIST) {
-              const uint32_t cw = reinterpret_cast<const uint32_t*>(t.pcode[qmode])[qr];
 #pragma unroll
-              for (int k = 0; k < 4; k++) pr[k] = s.pv[half][(cw >> (8 * k)) & 0xff];
-              src_row = *reinterpret_cast<const uint32_t*>(s.yin + off + qr * BPS);
-            } else {
-#pragma unroll
-              for (int k = 0; k < 4; k++) pr[k] = (pred_row >> (8 * k)) & 0xff;
-            }
+            for (int k = 0; k < 4; k++) pr[k] = (pred_row >> (8 * k)) & 0xff;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
               sr[k] = (src_row >> (8 * k)) & 0xff;
@@ -2720,7 +2094,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           uint64_t score = ~0ull;
           int rate = 0, hdr = 0;
           if (qact) {
-            hdr = WG_ENC_HOIST ? hdr_h : t.fixed_i4[(top_mode * 10 + left_mode) * 10 + qmode];
+            hdr = hdr_h;
             rate = (qmode > 0 && cnt <= 3) ? 140 : 0;
             rate += tok_rate + hdr;
             score = rd_score(disto, rate, sg.lambda_i4);
@@ -2776,9 +2150,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         }
         s4 = early ? ~0ull : rd_score(run_disto, run_rate + 211, sg.lambda_mode);
       }
-#if defined(WG_EXP_REP_I4)
       WG_REP_END
-#endif
       __builtin_amdgcn_s_setprio(1);
       }  // isA
       bool is_i4 = s4 < s16;  // (PAIR: decided at the join)
@@ -2812,9 +2184,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
 
       ESTAMP(5);
       // ================= final residuals (encodeResidualsParallel :1166-1356) =================
-#if defined(WG_EXP_REP_FIN)
-      WG_REP_BEGIN(WG_EXP_REP_FIN)
-#endif
+      WG_REP_BEGIN(FIN)
       if (run16) {
         int dc_nz = 0;
         if (lane < 16) {
@@ -2850,7 +2220,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         // contexts.  (Walking the 7 block diagonals took 7 prep + DP rounds.)
         const int lam16 = sg.tlambda_i16 * 16;
         trellis_r0<0>(t, lane, lam16, s.r0, s.eobl);  // (read after the first round's lds_sync)
-#if WG_ENC_I16ONE
         // One round (WG_ENC_I16ONE): quad q runs block q's DP for all three
         // start contexts at once (dp3_walk), over the records of positions
         // 0..7, then (the same LDS, rewritten) 8..15; lane 4q + r preps
@@ -2890,16 +2259,14 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             // from the half's records (position n at record n - 8 half); the
             // terminal lane's (WG_ENC_TLANE) from the phase table's columns 3..5
             const int64_t* mine =
-                (WG_ENC_TLANE && r == 3) ? &s.r0[0][3]
+                (r == 3) ? &s.r0[0][3]
                 : e == 0 ? &s.r0[0][0]
                          : reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(&s.trec16[q][0].x[e - 1][0]) -
                                                             8 * half * (int)sizeof(TRec));
             if (half == 1 && !cap_hi) {
-#if WG_ENC_TLANE
               // (no candidates past position 7: one step more for the terminal
               // lane, the EOB after position 7; the context lanes' rows are stale)
               dp3_walk<8, 9>(S, mine, eobq);
-#endif
               break;
             }
             {
@@ -2916,22 +2283,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             }
             lds_sync();
             if (half == 0) {
-#if WG_ENC_TLANE && WG_ENC_QSKIP
-              if (!cap_q1 && !cap_hi) {  // no candidates past position 3: the walk stops
-                dp3_walk<1, 4>(S, mine, eobq);
-                dp3_walk<4, 5>(S, mine, eobq);  // (the terminal lane's EOB after position 3)
-                break;
-              }
-#endif
               dp3_walk<1, 8>(S, mine, eobq);
             } else {
-#if WG_ENC_TLANE && WG_ENC_QSKIP
-              if (!cap_q3) {  // none past position 11
-                dp3_walk<8, 12>(S, mine, eobq);
-                dp3_walk<12, 13>(S, mine, eobq);
-              } else
-#endif
-                dp3_walk<8, WG_ENC_TLANE ? 17 : 16>(S, mine, eobq);
+                dp3_walk<8, 17>(S, mine, eobq);
             }
             lds_sync();  // (the second half's records overwrite the first's)
           }
@@ -2968,98 +2322,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
           if (r == 0) s.nzy[q] = (uint8_t)hist_nz(hist);
           lds_sync();
         }
-#else
-        int16_t* res_q = reinterpret_cast<int16_t*>(s.yout2);  // [16 tasks][16] levels (yout2 is free for I16 MBs)
-        int* res_nz = reinterpret_cast<int*>(s.yout2 + 512);   // [16]
-        uint32_t nzbits = 0;  // the resolved blocks' nz flags (bit = block), a scalar across the rounds
-        for (int r = 0; r < 3; r++) {
-          Shared& s = launder(s_waves[wave]);
-          Tables& t = launder(t_lds);
-          const int first = r == 0 ? 0 : (r == 1 ? 6 : 11), m = r == 0 ? 6 : 5;
-          bool pnz = false, pcap = false;
-          if (lane < 8 * m) {
-            const int j = lane >> 3, n0 = 2 * (lane & 7), pb = first + j;
-            TRec rr[2];
-            int l0[2];
-            // (position 0, the DC coded by the WHT, is not part of this trellis)
-            pnz = trellis_prep2<0, 1>(t, s.co_buf[pb], n0, sg.y1, lam16, rr, l0, &pcap);
-#pragma unroll
-            for (int k = 0; k < 2; k++)
-              if (n0 + k >= 1) {
-                s.trec[j][n0 + k] = rr[k];
-                s.l0s[j][n0 + k] = l0[k];
-              }
-          }
-          const uint64_t pnz_mask = __ballot(pnz);
-          [[maybe_unused]] const int nlast = nlast_of(__ballot(pcap));
-          lds_sync();
-          // quad q runs task q: walk the round's blocks to find its (block, context)
-          int tnz = 0;  // this quad's task: nz of its levels
-          {
-            const int q = lane >> 2;
-            int acc = 0, tj = -1, tctx = 0;
-            for (int j = 0; j < m; j++) {
-              const int qb = first + j, qbx = qb & 3, qby = qb >> 2;
-              const int nfix = (qbx == 0) + (qby == 0);
-              const int fixed = (qbx == 0 ? (int)((left_nz >> qby) & 1) : 0) + (qby == 0 ? (int)((top_nz >> qbx) & 1) : 0);
-              const int nopt = 3 - nfix;  // contexts fixed + 0 .. fixed + nopt - 1
-              if (tj < 0 && q < acc + nopt) {
-                tj = j;
-                tctx = fixed + (q - acc);
-              }
-              acc += nopt;
-            }
-            if (tj >= 0) {
-              if ((pnz_mask >> (8 * tj)) & 0xff) {
-                int nzv = 0;
-#if WG_ENC_NLAST
-                if (nlast < 8)
-                  trellis_dp4<1, 0, 8>(t, s.trec[tj], s.r0, s.eobl, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
-                else
-#endif
-#if WG_ENC_TLANE
-                trellis_dp4t<1, 0>(t, s.trec[tj], s.r0, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
-#else
-                trellis_dp4<1, 0>(t, s.trec[tj], s.r0, s.eobl, s.l0s[tj], tctx, lam16, lane & 3, res_q + q * 16, &nzv);
-#endif
-                if ((lane & 3) == 0) res_nz[q] = nzv;
-                tnz = nzv;
-              } else if ((lane & 3) == 0) {
-#pragma unroll
-                for (int i = 0; i < 16; i++) res_q[q * 16 + i] = 0;
-                res_nz[q] = 0;
-              }
-            }
-          }
-          // bit 4 q: task q's levels are nonzero (a ballot, not an LDS round trip)
-          const uint64_t tmask = __ballot((lane & 3) == 0 && tnz > 0);
-          lds_sync();
-          // the reference's raster order: each block's actual context picks its
-          // task -- on scalars (the task of the round's block j in bits 4j..4j+3)
-          uint32_t tasks = 0;
-          {
-            int acc = 0;
-            for (int j = 0; j < m; j++) {
-              const int qb = first + j, qbx = qb & 3, qby = qb >> 2;
-              const int nfix = (qbx == 0) + (qby == 0);
-              const int fixed = (qbx == 0 ? (int)((left_nz >> qby) & 1) : 0) + (qby == 0 ? (int)((top_nz >> qbx) & 1) : 0);
-              const int l = qbx > 0 ? (int)((nzbits >> (qb - 1)) & 1) : (int)((left_nz >> qby) & 1);
-              const int tp = qby > 0 ? (int)((nzbits >> (qb - 4)) & 1) : (int)((top_nz >> qbx) & 1);
-              const int task = acc + min(l + tp, 2) - fixed;
-              nzbits |= (uint32_t)((tmask >> (4 * task)) & 1) << qb;
-              tasks |= (uint32_t)task << (4 * j);
-              acc += 3 - nfix;
-            }
-          }
-          if (lane < 8 * m) {  // copy the chosen levels, two per lane, and the block's nz
-            const int j = lane >> 3, qb = first + j, task = (int)(tasks >> (4 * j)) & 15;
-            reinterpret_cast<uint32_t*>(s.coeffs + qb * 16)[lane & 7] =
-                reinterpret_cast<const uint32_t*>(res_q + task * 16)[lane & 7];
-            if ((lane & 7) == 0) s.nzy[qb] = (uint8_t)res_nz[task];
-          }
-          lds_sync();
-        }
-#endif
         }  // TRELLIS
       }
       if (lane < 8) {  // chroma
@@ -3076,9 +2338,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         for (int i = 0; i < 16; i++) s.coeffs[(16 + lane) * 16 + i] = q[i];
       }
       lds_sync();
-#if defined(WG_EXP_REP_FIN)
       WG_REP_END
-#endif
 
       ESTAMP(6);
       // ================= reconstruction (reconstructMBParallel :1358-1410) =================
@@ -3151,7 +2411,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       // record and the reconstruction rows are outputs only and leave after.
       // NZ context update (updateNZContextParallel :343-430)
       uint32_t out_t, out_l;
-#if WG_ENC_NZBITS
       // (one LDS read a lane and three ballots: bit b of ym = luma block b's
       // levels past `first`, of uvm = chroma block b's; the reference's
       // shift-register walk then reduces to the blocks of the last row /
@@ -3170,41 +2429,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
                 (((uvm >> 1) & 1u) | ((uvm >> 2) & 2u)) << 4 | (((uvm >> 5) & 1u) | ((uvm >> 6) & 2u)) << 6;
       }
       if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
-#else
-      for (int i = 0; i < 16; i++) nzy_mask |= (s.nzy[i] > 0 ? 1u : 0u) << i;
-      if (!is_i4 && nz_dc > 0) nzy_mask |= 1u << 24;
-      for (int i = 0; i < 8; i++) nzuv_mask |= (s.nzuv[i] > 0 ? 1u : 0u) << i;
-      {
-        const int first = is_i4 ? 0 : 1;
-        uint32_t tnz = top_nz & 0x0f, lnz = left_nz & 0x0f;
-        for (int yy = 0; yy < 4; yy++) {
-          uint32_t l = lnz & 1;
-          for (int xx = 0; xx < 4; xx++) {
-            l = s.nzy[yy * 4 + xx] > first;
-            tnz = (tnz >> 1) | (l << 7);
-          }
-          tnz >>= 4;
-          lnz = (lnz >> 1) | (l << 7);
-        }
-        out_t = tnz;
-        out_l = lnz >> 4;
-        for (int ch = 0; ch < 4; ch += 2) {
-          tnz = (top_nz >> (4 + ch)) & 0x0f;
-          lnz = (left_nz >> (4 + ch)) & 0x0f;
-          for (int yy = 0; yy < 2; yy++) {
-            uint32_t l = lnz & 1;
-            for (int xx = 0; xx < 2; xx++) {
-              l = s.nzuv[(ch / 2) * 4 + yy * 2 + xx] > 0;
-              tnz = (tnz >> 1) | (l << 3);
-            }
-            tnz >>= 2;
-            lnz = (lnz >> 1) | (l << 5);
-          }
-          out_t |= (tnz << 4) << ch;
-          out_l |= (lnz & 0xf0) << ch;
-        }
-      }
-#endif
       int new_top_dc = top_nz_dc;
       if (!is_i4) {
         new_top_dc = nz_dc > 0;
@@ -3221,56 +2445,19 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         left_modes = 0;
       }
       left_nz = out_l;
-      // hand-off record for the row below, then publish: staged in LDS and
-      // written as three 16-B write-through stores
-#if WG_ENC_TAGGED
-      // word i of the record at slot 4 (i / 3) + i % 3 of the staged granules,
-      // each granule's word 3 the row's tag; no drain, no flag
-      if (mby < mbh - 1) {
-        if (lane < 16) {
-          const int i = lane - lane / 4;  // (word 3 of a granule: lane 4p + 3)
-          uint32_t v = row_tag(a.epoch, mby);
-          if ((lane & 3) != 3) {
-            if (i < 8) {
-              const int so = i < 4 ? YOFF + 15 * BPS + 4 * i : (i < 6 ? UOFF + 7 * BPS + 4 * (i - 4) : VOFF + 7 * BPS + 4 * (i - 6));
-              v = *reinterpret_cast<const uint32_t*>(s.yout + so);
-            } else {
-              v = i == 8 ? out_t : (i == 9 ? new_top_modes : (i == 10 ? (uint32_t)new_top_dc : 0u));
-            }
-          }
-          s.handoff[lane] = v;
-        }
-        lds_sync();
-        if (lane < 4) {
-          const uint4 w = reinterpret_cast<const uint4*>(s.handoff)[lane];
-          u32x4_t v = {w.x, w.y, w.z, w.w};
-          st_sc1_128(top + mbx * REC + 16 * lane, v);
-        }
-      }
-#else
-      if (mby < mbh - 1) {
+      // hand-off record for the row below: lane i publishes word i with the
+      // row's tag in one 64-bit store (no drain, no flag)
+      if (mby < mbh - 1 && lane < REC_WORDS) {
+        uint32_t v;
         if (lane < 8) {
-          const int so = lane < 4 ? YOFF + 15 * BPS + 4 * lane : (lane < 6 ? UOFF + 7 * BPS + 4 * (lane - 4) : VOFF + 7 * BPS + 4 * (lane - 6));
-          s.handoff[lane] = *reinterpret_cast<const uint32_t*>(s.yout + so);
-        } else if (lane == 8) {
-          s.handoff[8] = out_t;
-        } else if (lane == 9) {
-          s.handoff[9] = new_top_modes;
-        } else if (lane == 10) {
-          s.handoff[10] = (uint32_t)new_top_dc;
-        } else if (lane == 11) {
-          s.handoff[11] = 0;
+          const int so = lane < 4 ? YOFF + 15 * BPS + 4 * lane
+                                  : (lane < 6 ? UOFF + 7 * BPS + 4 * (lane - 4) : VOFF + 7 * BPS + 4 * (lane - 6));
+          v = *reinterpret_cast<const uint32_t*>(s.yout + so);
+        } else {
+          v = lane == 8 ? out_t : (lane == 9 ? new_top_modes : (uint32_t)new_top_dc);
         }
-        lds_sync();
-        if (lane < 3) {
-          const uint4 w = reinterpret_cast<const uint4*>(s.handoff)[lane];
-          u32x4_t v = {w.x, w.y, w.z, w.w};
-          st_sc1_128(top + mbx * REC + 16 * lane, v);
-        }
+        st_granule(top + mbx * REC + 8 * lane, v, (uint32_t)mby + 1);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record is visible before the flag
-      if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
       // ================= outputs, export, contexts (exportParallel :1412-1495) =================
       MbEnc* o = a.out + mbi;
       {  // the record's tail (bytes 800..863) staged next to the levels in LDS
@@ -3296,14 +2483,11 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         // the whole 864-B record: 54 lanes x 16 B, one store instruction
         uint4* dst = reinterpret_cast<uint4*>(o);
         const uint4* srcv = reinterpret_cast<const uint4*>(s.coeffs);
-#ifndef WG_EXP_NO_MBENC
         if (lane < 54) dst[lane] = srcv[lane];
-#endif
       }
       {
         const int x = 16 * mbx, y = 16 * mby;
         const int wy = min(a.width - x, 16), hy = min(a.height - y, 16);
-#ifndef WG_EXP_NO_RECON
         // Rows leave in whole 32-B sectors where the MB pair (Y) / quad (U, V)
         // is whole: the earlier MBs' rows wait in registers (rst0 / rst1) and
         // go out back to back with the last one's, so L2 never writes a
@@ -3353,18 +2537,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
             *drow = v;
           }
         }
-#endif
       }
-#if WG_ENC_TAGGED && WG_ENC_RECPF
-      if (mby > 0 && mbx + 1 < mbw) {  // (a buffer load: sc1 like ld_sc1_128, its wait left to the compiler)
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(top, (short)0, mbw * REC, 0x00020000);
-        typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-        if (lane < 4) {
-          const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (mbx + 1) * REC + 16 * lane, 0, 16);
-          pre_above = make_uint4(v.x, v.y, v.z, v.w);
-        }
-      }
-#endif
       // new top-left: the row above's bottom-right of this column (before we overwrite it)
       tl_y = s.yout[YOFF - BPS + 15];
       tl_u = s.yout[UOFF - BPS + 7];
@@ -3379,7 +2552,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
       }  // isA
       ESTAMP(7);
     }
-#ifdef WG_ROWTIMES
+    WG_IF_ROWTIMES(
     if (live && (tid == 0 || (!PAIR && lane == 0))) {
       if (row < 16384) {
         g_row_times[row][0] = (unsigned long long)ro;
@@ -3387,8 +2560,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : WG_ENC
         g_row_times[row][2] = __builtin_amdgcn_s_memrealtime();
         g_row_times[row][3] = (unsigned long long)blockIdx.x << 8 | (unsigned long long)wave;
       }
-    }
-#endif
+    })
     // the band is done: LOOSE, count this wave out of it; else the group
     // dequeues the next one together
     if constexpr (LOOSE) {
@@ -3440,35 +2612,28 @@ extern "C" int wg_fixed_costs_i4_host(uint16_t* out) {
   return WG_OK;
 }
 
-#ifdef WG_STAMPS
-extern "C" int wg_debug_enc_phases(unsigned long long* host, int n) {
+WG_IF_STAMPS(extern "C" int wg_debug_enc_phases(unsigned long long* host, int n) {
   (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_enc_phase), sizeof(unsigned long long) * n);
   unsigned long long z[16] = {0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_enc_phase), z, sizeof(z)) == hipSuccess ? 0 : -2;
-}
-#endif
+})
 
-#ifdef WG_ROWTIMES
-extern "C" int wg_debug_enc_rows(unsigned long long* host, int n_rows) {
+WG_IF_ROWTIMES(extern "C" int wg_debug_enc_rows(unsigned long long* host, int n_rows) {
   if (n_rows > 16384) n_rows = 16384;
   (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_row_times), sizeof(unsigned long long) * 4 * n_rows);
   return 0;
-}
-#endif
+})
 
-// work: hand-off records [n][mbw][REC] | ctl[4] | progress[n*mbh] (cleared by
-// every wg_encode_mbs) | tag[4] | row schedule order[n*mbh] | slack[n] |
+// work: hand-off records [n][mbw][REC] | ctl[4] (both cleared by every
+// wg_encode_mbs) | tag[4] | row schedule order[n*mbh] | slack[n] |
 // band schedule border[n*ceil(mbh/4)] (wg_encode_row_order; kept across calls)
 extern "C" size_t wg_encode_work_bytes(int32_t mbw, int32_t mbh, int32_t n_images) {
   if (mbw <= 0 || mbh <= 0 || n_images <= 0) return 0;
   const size_t bands = (size_t)n_images * ((mbh + WAVES - 1) / WAVES);
-  return (size_t)n_images * mbw * REC + sizeof(int) * ((size_t)n_images * mbh + 4) +
+  return (size_t)n_images * mbw * REC + sizeof(int) * 4 +
          sizeof(int) * (4 + (size_t)n_images * mbh + (size_t)n_images + bands);
 }
 
-#ifndef WG_ENC_SLACK_DIV
-#define WG_ENC_SLACK_DIV 4  // the largest head start is mbh / WG_ENC_SLACK_DIV rows
-#endif
 namespace {
 // ---- the row schedule (wg_encode_row_order) ----
 // A launch over many frames ends on the critical path of its slowest frame:
@@ -3493,7 +2658,7 @@ __global__ __launch_bounds__(256) void k_row_slack(const int32_t* alphas, int n_
   }
   if (threadIdx.x == 0) {
     const int mean = (int)(part[0] / n_mb);
-    slack[blockIdx.x] = (mbh / WG_ENC_SLACK_DIV) * (255 - mean) / 255;
+    slack[blockIdx.x] = (mbh / 4) * (255 - mean) / 255;
     if (blockIdx.x == 0) {  // the encoder reads it after k_row_order (same stream)
       tag[0] = ORDER_TAG ^ (int)gridDim.x;
       tag[1] = ~(ORDER_TAG ^ mbh);
@@ -3537,8 +2702,7 @@ extern "C" int wg_encode_row_order(const int32_t* alphas, int32_t mbw, int32_t m
   WG_REQUIRE(alphas && work && mbw > 0 && mbh > 0 && n_images > 0);
   WG_REQUIRE((reinterpret_cast<uintptr_t>(work) & 15) == 0);
   const int rows = n_images * mbh;
-  int* progress = reinterpret_cast<int*>(static_cast<uint8_t*>(work) + (size_t)n_images * mbw * REC) + 4;
-  int* tag = progress + rows;
+  int* tag = reinterpret_cast<int*>(static_cast<uint8_t*>(work) + (size_t)n_images * mbw * REC) + 4;
   int* order = tag + 4;
   int* slack = order + rows;
   int* border = slack + n_images;
@@ -3608,7 +2772,6 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   a.out = static_cast<MbEnc*>(out);
   a.top = static_cast<uint8_t*>(work);
   a.ctl = reinterpret_cast<int*>(a.top + (size_t)n_images * mbw * REC);
-  a.progress = a.ctl + 4;
   a.y_pitch = y_pitch;
   a.uv_pitch = uv_pitch;
   a.width = width;
@@ -3617,20 +2780,16 @@ extern "C" int wg_encode_mbs(const uint8_t* y, const uint8_t* u, const uint8_t* 
   a.mbh = mbh;
   a.n_img = n_images;
   a.quality = quality;
-  a.order = a.progress + (size_t)n_images * mbh + 4;  // work: ... | progress | tag[4] | order | slack | border
+  a.order = a.ctl + 8;  // work: records | ctl[4] | tag[4] | order | slack | border
   a.order_tag = a.order - 4;
   a.border = a.order + (size_t)n_images * mbh + n_images;
   a.diag = wg::diag_words(s);
   if (!a.diag) return WG_EHIP;
   a.diag += wg::DIAG_ENCODE;
-  {
-    // the hand-off tags' base: a fresh value per launch (from a random start,
-    // so a work buffer another process used does not hold this process's tags)
-    static std::atomic<uint32_t> g_epoch{std::random_device{}()};
-    a.epoch = g_epoch.fetch_add(1, std::memory_order_relaxed);
-  }
-  if (hipMemsetAsync(a.ctl, 0, sizeof(int) * ((size_t)n_images * mbh + 4), s) != hipSuccess)
-    return wg::check_launch("hipMemsetAsync(encode ctl)");
+  // the hand-off records (every tag 0: no row has written), the control words
+  // and the progress words, cleared for this launch
+  if (hipMemsetAsync(a.top, 0, (size_t)n_images * mbw * REC + sizeof(int) * 4, s) != hipSuccess)
+    return wg::check_launch("hipMemsetAsync(encode records + ctl)");
   int cus = 0, per_cu = 0, per_cu_pair = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_rows<true, false>, 64 * WAVES * GROUPS, 0) != hipSuccess ||

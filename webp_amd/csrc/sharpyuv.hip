@@ -176,10 +176,7 @@ __device__ __forceinline__ void st_sc1_16(void* p, uint16_t v) {
 // prev, the only row this iteration produces itself; cur / next / luma come
 // from the previous state in memory every step), so every WB_HALO row pairs
 // the halo lanes reload prev from the neighbour bands' published output.
-#ifndef WG_SHARP_OWN
-#define WG_SHARP_OWN 32
-#endif
-constexpr int WB_OWN = WG_SHARP_OWN, WB_HALO = (64 - WB_OWN) / 2, WB_PUB = WB_HALO;
+constexpr int WB_OWN = 32, WB_HALO = (64 - WB_OWN) / 2, WB_PUB = WB_HALO;
 static_assert(WB_OWN + 2 * WB_HALO == 64 && WB_HALO % WB_PUB == 0, "wave band layout");
 
 // (bound_ctrl: the wave's end lanes, always halo lanes, read 0 -- no register to initialise)

@@ -16,6 +16,7 @@
 // vp8l_host.cpp's restatement of Go's math.Log2).  No FMA contraction anywhere
 // in this file.
 #include "wg_common.h"
+#include "wg_instr.h"
 
 #pragma clang fp contract(off)
 
@@ -162,32 +163,6 @@ constexpr uint32_t kPredCtl[16] = {
     C_CF,                             // 12
     C_CH | C_PL,                      // 13 (avg2(L, T) first)
     C_BLACK, C_BLACK};
-// bit `bit` of c set ? a : b, through a sign-extended bit mask (v_bfe_i32 + v_bfi_b32)
-// (v_bfi_b32 written out: the compiler turns the mask form back into
-// compare + v_cndmask pairs, with VCC hazard nops between them)
-template <int BIT>
-__device__ __forceinline__ uint32_t bsel(uint32_t c, uint32_t a, uint32_t b) {
-  const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)c, BIT, 1);
-  uint32_t r;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ uint32_t predict_ctl(uint32_t c, uint32_t l, uint32_t t, uint32_t tr, uint32_t tl) {
-  // what does not depend on L (the walk's serial input) first
-  const uint32_t pc = bsel<3>(c, tl, bsel<2>(c, tr, t));
-  const uint32_t r1 = bsel<4>(c, tl, tr);
-  const uint32_t qc = bsel<7>(c, bsel<6>(c, avg2(t, tr), tl), bsel<6>(c, tr, t));
-  const int sad_t = (int)__builtin_amdgcn_sad_u8(t, tl, 0u);
-  const uint32_t q = bsel<5>(c, l, qc);
-  const uint32_t p = bsel<0>(c, avg2(l, r1), bsel<1>(c, l, pc));
-  const uint32_t pavg = avg2(p, q);
-  const int pa = (int)__builtin_amdgcn_sad_u8(l, tl, 0u) - sad_t;
-  uint32_t r = bsel<8>(c, pa <= 0 ? t : l, pavg);
-  r = bsel<9>(c, clamp_add_sub_full(l, t, tl), r);
-  r = bsel<10>(c, clamp_add_sub_half(pavg, tl), r);
-  return bsel<11>(c, ARGB_BLACK, r);
-}
-
 // Go math.Log / math.Log2 (src/math/log.go, log10.go) for counts beyond the
 // LUT (tiles of 512 px at bits = 9); same operation sequence as the host LUT.
 __device__ double go_log(double x) {
@@ -310,25 +285,38 @@ __global__ __launch_bounds__(64 * SEL_WAVES) void k_vp8l_select(SelArgs a) {
 }
 
 // ResidualImage phase 1 for tiles of at most 32 x 32 px (bits <= 5, so every
-// histogram count is <= 512): ONE wave per tile and one pass over its samples
-// for all modes at once.
-//   - Lane 4m + s predicts sample s of each run of four (mode m's predictor,
-//     predict_ctl: branch-free for every mode) and takes the residual; the
-//     quad then transposes (4 DPP broadcasts) so that lane 4m + c holds channel
-//     c of the run's four residuals.
-//   - Lane 4m + c owns the histogram of (mode m, channel c): bins b and
-//     b + 128 as the two 16-bit halves of word b & 127, stored [word][lane],
-//     so every lane adds to its own bank (ds_add_u32, no return, no
-//     contention however flat the content).
-//   - Lane 4m + c then runs the (mode, channel) float64 sum of
-//     estimateEntropy (encode_predictor.go:262-275) in the reference's order:
-//     fastSLog2(count) minus the bins 0..255 (an empty bin subtracts
-//     fastSLog2(0) = 0.0, which leaves the sum unchanged); the 56 sums run at
-//     once, and each mode's four channel sums are added alpha, red, green,
-//     blue from 0.0 as the reference adds them.  The argmin keeps the
-//     reference's first strict minimum in mode order (:408-418).
-// fastSLog2 of 0..512 is staged in LDS from the same device table.
-constexpr int SQW = 4;        // waves (tiles) per workgroup
+// histogram count is <= 512): a 2-wave workgroup a tile and one pass over
+// its samples for all modes at once.
+//   - The tile and its border are staged in LDS with estimateEntropy's edge
+//     values already in place (0 left of column 0 and above row 0, the last
+//     pixel repeated right of the last column: TR = T there), every load
+//     issued before the first store.
+//   - Sample lanes: lane l takes one sample (two sample rows of up to 32 per
+//     pass; wave h the rows h, h + 2, ...) and forms all 14 predictions at
+//     once -- modes 1-4 are its neighbours, the averages share their avg2
+//     terms, only Select and the two clamps cost more -- and its 14 residuals
+//     go to an LDS transpose buffer (rows of 68 words: the column lanes' 16-B
+//     reads of one sample quad land on 14 disjoint bank quads).
+//   - Column lanes: lane 4m + c owns the histogram of (mode m, channel c),
+//     bins b and b + 128 as the two 16-bit halves of word b & 127, columns 64
+//     words apart (every lane adds to its own bank: ds_add_u32, no return, no
+//     contention however flat the content); it reads mode m's residuals back
+//     and adds channel c's bins (address and increment: two bit-field
+//     extracts).  The two waves' adds to one word serialise in the LDS.
+//   - After the barrier wave 1 exits and lane 4m + c of wave 0 runs the
+//     (mode, channel) float64 sum of estimateEntropy
+//     (encode_predictor.go:262-275) in the reference's order: fastSLog2(count)
+//     minus the bins 0..255 (an empty bin subtracts fastSLog2(0) = 0.0, which
+//     leaves the sum unchanged); the 56 sums run at once (the whole column read
+//     first, then the LUT in batches), and each mode's four channel sums are
+//     added alpha, red, green, blue from 0.0 as the reference adds them.  The
+//     argmin keeps the reference's first strict minimum in mode order
+//     (:408-418).
+// fastSLog2 of 0..512 is staged in LDS from the same device table.  48.5 KB a
+// workgroup, three workgroups (six waves) a CU.  (Round 5 measured the
+// alternatives -- one wave a tile with lane (mode, sample) running the
+// branch-free predictor of its one mode, and the same on two waves -- at
+// 1.27 / 0.60 ms against this kernel's 0.43 ms at 4096^2)
 constexpr int SQ_LUT = 513;   // counts 0..512
 __device__ __forceinline__ double dpp_quad_f64(double v, int j) {
   const uint64_t u = __builtin_bit_cast(uint64_t, v);
@@ -341,246 +329,8 @@ __device__ __forceinline__ double dpp_quad_f64(double v, int j) {
   }
   return __builtin_bit_cast(double, (uint64_t)(uint32_t)hi << 32 | (uint32_t)lo);
 }
-template <int J>
-__device__ __forceinline__ uint32_t dpp_quad_u32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, J | J << 2 | J << 4 | J << 6, 0xf, 0xf, false);
-}
-
-constexpr int SQ_SW = 34;  // staged tile row: columns x0 - 1 .. x0 + 32
-__global__ __launch_bounds__(64 * SQW) void k_vp8l_select_q(SelArgs a, int64_t total) {
-  __shared__ uint32_t hist[SQW][128 * 64];
-  // the tile and its border, staged with estimateEntropy's edge values
-  // already in place (0 left of column 0 and above row 0, the last pixel
-  // repeated right of the last column: TR = T there), so the sample loop
-  // reads five LDS words and has no branches
-  __shared__ uint32_t stile[SQW][33 * SQ_SW];
-  __shared__ double lut[SQ_LUT];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < SQ_LUT; i += 64 * SQW) lut[i] = a.lut[i];
-  uint32_t* const hg = hist[wave];
-#pragma unroll 4
-  for (int i = lane; i < 128 * 64 / 4; i += 64) reinterpret_cast<uint4*>(hg)[i] = make_uint4(0, 0, 0, 0);
-  __syncthreads();  // the LUT; this wave's zeroed histograms
-  const int64_t t_idx = (int64_t)blockIdx.x * SQW + wave;
-  if (t_idx >= total) return;  // (no barrier below)
-  const int tile = (int)(t_idx % a.band_tiles) + a.ty0 * a.tiles_x;
-  const int img = (int)(t_idx / a.band_tiles);
-  const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
-  const uint32_t* argb = a.argb + img * a.pitch;
-  const int ts = 1 << a.bits, w = a.width, h = a.height;
-  const int x0 = tx * ts, y0 = ty * ts;
-  const int x1 = min(x0 + ts, w), y1 = min(y0 + ts, h);
-  const int ystep = (y1 - y0 > 16) ? 2 : 1;
-  const int tw = x1 - x0, rows = (y1 - y0 + ystep - 1) / ystep;
-  // stage rows y0 - 1 .. y1 - 1 (only those with y0 - 1 <= y < y1 are read)
-  uint32_t* const st = stile[wave];
-  {
-    const int srows = y1 - y0 + 1, scols = x1 - x0 + 2;
-    for (int i = lane; i < srows * scols; i += 64) {
-      const int rr = i / scols, cc = i - rr * scols;
-      const int y = y0 - 1 + rr, x = x0 - 1 + cc;
-      uint32_t v = 0;
-      if (y >= 0 && x >= 0) v = argb[(int64_t)y * w + min(x, w - 1)];
-      st[rr * SQ_SW + cc] = v;
-    }
-  }
-  wave_lds_sync();
-  const int m = lane >> 2, s = lane & 3;
-  const uint32_t ctl = m < 14 ? kPredCtl[m] : (uint32_t)C_BLACK;
-  const int shift = 24 - 8 * s;  // as the channel lane: alpha, red, green, blue
-  uint32_t* const myh = hg + lane;
-  auto add = [&](uint32_t r) {
-    const uint32_t b = (r >> shift) & 0xff;
-    __hip_atomic_fetch_add(myh + 64 * (b & 127), b < 128 ? 1u : 0x10000u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-  for (int yy = 0; yy < rows; yy++) {
-    const uint32_t* srow = st + (1 + yy * ystep) * SQ_SW;  // staged row y0 + yy * ystep
-    const uint32_t* sprev = srow - SQ_SW;
-#pragma unroll
-    for (int cx = 0; cx < 32; cx += 4) {
-      if (cx >= tw) continue;  // (wave-uniform)
-      // estimateEntropy's neighbours (encode_predictor.go:226-245): 0 outside
-      // the image, TR = T in the last column (staged that way)
-      const int c = min(cx + s, tw - 1) + 1;  // staged column of x
-      const uint32_t p = srow[c], l = srow[c - 1], t = sprev[c], tl = sprev[c - 1], tr = sprev[c + 1];
-      const uint32_t res = sub_pixels(p, predict_ctl(ctl, l, t, tr, tl));
-      const uint32_t r0 = dpp_quad_u32<0>(res), r1 = dpp_quad_u32<1>(res), r2 = dpp_quad_u32<2>(res),
-                     r3 = dpp_quad_u32<3>(res);
-      const int nv = tw - cx;  // samples of this run inside the tile (wave-uniform)
-      add(r0);
-      if (nv > 1) add(r1);
-      if (nv > 2) add(r2);
-      if (nv > 3) add(r3);
-    }
-  }
-  wave_lds_sync();  // this wave's adds land before its reads
-  const uint32_t count = (uint32_t)(tw * rows);
-  double ce = lut[count];
-#pragma unroll 8
-  for (int k = 0; k < 128; k++) ce -= lut[myh[64 * k] & 0xffff];
-#pragma unroll 8
-  for (int k = 0; k < 128; k++) ce -= lut[myh[64 * k] >> 16];
-  const double e = (((0.0 + dpp_quad_f64(ce, 0)) + dpp_quad_f64(ce, 1)) + dpp_quad_f64(ce, 2)) + dpp_quad_f64(ce, 3);
-  const uint64_t eb = __builtin_bit_cast(uint64_t, e);
-  int best = 0;
-  double best_cost = 1.7976931348623157e308;
-  for (int mm = 0; mm < a.max_mode; mm++) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)eb, 4 * mm);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(eb >> 32), 4 * mm);
-    const double cm = __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
-    if (cm < best_cost) {
-      best_cost = cm;
-      best = mm;
-    }
-  }
-  if (lane == 0) a.modes[(int64_t)img * a.tiles_x * a.tiles_y + tile] = ((uint32_t)best << 8) | ARGB_BLACK;
-}
-
-// The same phase with TWO waves a tile and two tiles' waves a SIMD.
-// k_vp8l_select_q issues at one wave per SIMD (four 37-KB tiles' histograms
-// fill the LDS), i.e. at half the SIMD's VALU rate, with every LDS round
-// trip exposed.  Here a 2-wave workgroup takes one tile:
-//   - the histograms hold only the 56 (mode, channel) columns (stride 56
-//     words, 28 KB): 37.3 KB a workgroup with the staged tile and the LUT, so
-//     four workgroups (8 waves, two a SIMD) fit in the CU's 160 KB;
-//   - wave h takes the sample rows h, h + 2, ... and adds into the shared
-//     histograms (ds_add: the two waves' adds to one word serialise in the
-//     LDS); each row's 40 staged words are read before its first add, so a
-//     row waits on the LDS once;
-//   - after the barrier wave 1 exits and wave 0 runs the 56 float64 sums
-//     (the whole column read first, then the LUT in batches) and the argmin.
-constexpr int SQ2_COLS = 56;
-__global__ __launch_bounds__(128) void k_vp8l_select_q2(SelArgs a, int64_t total) {
-  __shared__ uint32_t hist[128 * SQ2_COLS];
-  __shared__ uint32_t stile[33 * SQ_SW];
-  __shared__ double lut[SQ_LUT];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t t_idx = blockIdx.x;
-  if (t_idx >= total) return;  // (grid = total: never; no barrier skipped)
-  const int tile = (int)(t_idx % a.band_tiles) + a.ty0 * a.tiles_x;
-  const int img = (int)(t_idx / a.band_tiles);
-  const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
-  const uint32_t* argb = a.argb + img * a.pitch;
-  const int ts = 1 << a.bits, w = a.width, h = a.height;
-  const int x0 = tx * ts, y0 = ty * ts;
-  const int x1 = min(x0 + ts, w), y1 = min(y0 + ts, h);
-  const int ystep = (y1 - y0 > 16) ? 2 : 1;
-  const int tw = x1 - x0, rows = (y1 - y0 + ystep - 1) / ystep;
-  {
-    // staged rows y0 - 1 .. y1 - 1 with estimateEntropy's edge values (as
-    // k_vp8l_select_q), every load issued before the first store
-    const int srows = y1 - y0 + 1, scols = x1 - x0 + 2, n = srows * scols;
-    constexpr int SN = (33 * SQ_SW + 127) / 128;
-    uint32_t v[SN];
-#pragma unroll
-    for (int j = 0; j < SN; j++) {
-      const int i = (int)threadIdx.x + 128 * j;
-      v[j] = 0;
-      if (i < n) {
-        const int rr = i / scols, cc = i - rr * scols;
-        const int y = y0 - 1 + rr, x = x0 - 1 + cc;
-        if (y >= 0 && x >= 0) v[j] = argb[(int64_t)y * w + min(x, w - 1)];
-      }
-    }
-    for (int i = threadIdx.x; i < SQ_LUT; i += 128) lut[i] = a.lut[i];
-    for (int i = threadIdx.x; i < 128 * SQ2_COLS / 4; i += 128) reinterpret_cast<uint4*>(hist)[i] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < SN; j++) {
-      const int i = (int)threadIdx.x + 128 * j;
-      if (i < n) stile[(i / scols) * SQ_SW + i % scols] = v[j];
-    }
-  }
-  __syncthreads();
-  const int m = lane >> 2, s = lane & 3;
-  const uint32_t ctl = m < 14 ? kPredCtl[m] : (uint32_t)C_BLACK;
-  const int shift = 24 - 8 * s;  // as the channel lane: alpha, red, green, blue
-  const bool col = lane < SQ2_COLS;
-  uint32_t* const myh = hist + lane;
-  for (int yy = wave; yy < rows; yy += 2) {
-    const uint32_t* srow = stile + (1 + yy * ystep) * SQ_SW;  // staged row y0 + yy * ystep
-    const uint32_t* sprev = srow - SQ_SW;
-    uint32_t P[8], L[8], T[8], TL[8], TR[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      P[j] = L[j] = T[j] = TL[j] = TR[j] = 0;
-      if (4 * j >= tw) continue;  // (wave-uniform)
-      const int c = min(4 * j + s, tw - 1) + 1;  // staged column of x
-      P[j] = srow[c];
-      L[j] = srow[c - 1];
-      T[j] = sprev[c];
-      TL[j] = sprev[c - 1];
-      TR[j] = sprev[c + 1];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      if (4 * j >= tw) continue;
-      const uint32_t res = sub_pixels(P[j], predict_ctl(ctl, L[j], T[j], TR[j], TL[j]));
-      const uint32_t rq[4] = {dpp_quad_u32<0>(res), dpp_quad_u32<1>(res), dpp_quad_u32<2>(res), dpp_quad_u32<3>(res)};
-      const int nv = tw - 4 * j;  // samples of this run inside the tile (wave-uniform)
-      if (col) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          if (q > 0 && nv <= q) break;
-          const uint32_t r = rq[q];
-          const uint32_t b = (r >> shift) & 0xff;
-          __hip_atomic_fetch_add(myh + SQ2_COLS * (b & 127), 1u << ((b >> 7) << 4), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (wave != 0) return;  // (no barrier below)
-  const uint32_t count = (uint32_t)(tw * rows);
-  double ce = 0.0;
-  if (col) {
-    uint32_t hv[128];
-#pragma unroll
-    for (int k = 0; k < 128; k++) hv[k] = myh[SQ2_COLS * k];
-    ce = lut[count];
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-#pragma unroll
-      for (int k0 = 0; k0 < 128; k0 += 32) {
-        double lv[32];
-#pragma unroll
-        for (int k = 0; k < 32; k++) lv[k] = lut[half ? hv[k0 + k] >> 16 : hv[k0 + k] & 0xffff];
-#pragma unroll
-        for (int k = 0; k < 32; k++) ce -= lv[k];
-      }
-    }
-  }
-  const double e = (((0.0 + dpp_quad_f64(ce, 0)) + dpp_quad_f64(ce, 1)) + dpp_quad_f64(ce, 2)) + dpp_quad_f64(ce, 3);
-  const uint64_t eb = __builtin_bit_cast(uint64_t, e);
-  int best = 0;
-  double best_cost = 1.7976931348623157e308;
-  for (int mm = 0; mm < a.max_mode; mm++) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)eb, 4 * mm);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(eb >> 32), 4 * mm);
-    const double cm = __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
-    if (cm < best_cost) {
-      best_cost = cm;
-      best = mm;
-    }
-  }
-  if (lane == 0) a.modes[(int64_t)img * a.tiles_x * a.tiles_y + tile] = ((uint32_t)best << 8) | ARGB_BLACK;
-}
-
-// The same phase with the predictions on SAMPLE lanes (variant 3, the
-// default).  In k_vp8l_select_q2 lane (mode m, sample s) runs the generic
-// branch-free predictor for its one mode: ~57 instructions for one of the
-// 56 (mode, sample) pairs.  Here lane l takes one sample (two sample rows of
-// up to 32 per pass) and forms all 14 predictions at once -- modes 1-4 are
-// its neighbours, the averages share their avg2 terms, only Select and the
-// two clamps cost more -- and its 14 residuals go to an LDS transpose buffer
-// (rows of 68 words: the column lanes' 16-B reads of one sample quad land on
-// 14 disjoint bank quads).  The column lanes (lane 4m + c, as in q2) then
-// read mode m's 64 residuals back and add channel c's bins: a bin's address
-// and increment are two bit-field extracts and two 24-bit multiply-adds.
-// Histogram columns 64 words apart (no bank conflicts between the column
-// lanes' adds); 48.5 KB a workgroup, three workgroups (six waves) a CU.
-// The entropy sums and the argmin are q2's.
+constexpr int SQ_SW = 34;     // staged tile row: columns x0 - 1 .. x0 + 32
+constexpr int SQ2_COLS = 56;  // (mode, channel) column lanes
 constexpr int SQ3_XS = 68;  // transpose buffer row stride (words)
 __global__ __launch_bounds__(128) void k_vp8l_select_q3(SelArgs a, int64_t total) {
   __shared__ uint32_t hist[128 * 64];
@@ -600,8 +350,8 @@ __global__ __launch_bounds__(128) void k_vp8l_select_q3(SelArgs a, int64_t total
   const int ystep = (y1 - y0 > 16) ? 2 : 1;
   const int tw = x1 - x0, rows = (y1 - y0 + ystep - 1) / ystep;
   {
-    // staged rows y0 - 1 .. y1 - 1 with estimateEntropy's edge values (as
-    // k_vp8l_select_q); i / scols by a multiply (exact: i < 2^16 / scols)
+    // staged rows y0 - 1 .. y1 - 1 with estimateEntropy's edge values;
+    // i / scols by a multiply (exact: i < 2^16 / scols)
     const int srows = y1 - y0 + 1, scols = x1 - x0 + 2, n = srows * scols;
     const uint32_t inv = (65535u + (uint32_t)scols) / (uint32_t)scols;  // ceil(2^16 / scols)
     constexpr int SN = (33 * SQ_SW + 127) / 128;
@@ -776,7 +526,7 @@ constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
 // Hand-off between bands: the band's last row writes its pixels as 8-B
 // {pixel, tag} granules, two at a time with one 16-B sc1 (write-through)
 // store (MI355X_MICROARCH.md, R2 granules: untorn, no flag, no drain); the
-// band below loads one granule a step, UPD steps before it needs it, and
+// band below loads one granule a step, UPD = 6 steps before it needs it, and
 // re-polls one whose tag is not set yet.  The band below then trails by the
 // diagonal's 64 steps plus UPD, a step for the pairing and a store's flight.
 //
@@ -786,9 +536,7 @@ constexpr uint64_t SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
 // lane of each pair stores the whole pixels as one 64-B run).
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4a4_t __attribute__((ext_vector_type(4), aligned(4)));  // a row's pixels: 4-B aligned
-#ifndef UPD
-#define UPD 6  // steps between a row-above granule's load and its use
-#endif
+constexpr int UPD = 6;  // steps between a row-above granule's load and its use
 constexpr int INV_ROWS = 32;  // rows per band (a lane pair per row)
 constexpr uint32_t C2_EVEN = 0x0c020c00u, C2_ODD = 0x0c030c01u;  // v_perm selectors: a pixel's c2 halves
 
@@ -798,7 +546,7 @@ __device__ __forceinline__ uint32_t c2_clamp_full(uint32_t a, uint32_t b, uint32
   return as_u(clamp255(as_v2(a) + as_v2(b) - as_v2(c)));
 }
 __device__ __forceinline__ uint32_t c2_clamp_half(uint32_t avg, uint32_t c) { return as_u(half_step(as_v2(avg), as_v2(c))); }
-// predict_ctl on half pixels (c2 form), with the control word's select
+// The kPredCtl predictor on half pixels (c2 form), with the control word's select
 // masks m[b] = (bit b set ? ~0 : 0) read from LDS; `black` is this lane's
 // half of ARGB_BLACK
 __device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t a, uint32_t b) {
@@ -884,12 +632,9 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
     const uint32_t* inrow = in + (int64_t)min(y, a.height - 1) * w;
     uint32_t* orow = out + (int64_t)min(y, a.height - 1) * w;
     uint32_t o1 = 0, first = 0;  // this lane's output (c2) at x - 1; at x = 0
-#ifdef WG_INV_STAMPS
-    // the per-band timeline (tools/inv_timeline.py): s_memrealtime (100 MHz)
-    // at the band's start and end, and the ticks spent re-polling the band above
-    const uint64_t t_band = __builtin_amdgcn_s_memrealtime();
-    uint64_t poll_ticks = 0, polls = 0;
-#endif
+    // (WG_INV_STAMPS builds) the per-band timeline: s_memrealtime (100 MHz) at
+    // the band's start and end, and the ticks spent re-polling the band above
+    WG_IF_INV_STAMPS(const uint64_t t_band = __builtin_amdgcn_s_memrealtime(); uint64_t poll_ticks = 0, polls = 0;)
     const int steps = w + 2 * last_row;
     // the band above's row, one granule a step: column c sits in gr[c & 15],
     // loaded UPD steps before step c - 1 (where it is TR); up_take re-polls it
@@ -908,10 +653,7 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
           __builtin_amdgcn_s_sleep(1);
           g = up_load(c);
           if (__builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) != 0) {
-#ifdef WG_INV_STAMPS
-            poll_ticks += __builtin_amdgcn_s_memrealtime() - t0;
-            polls++;
-#endif
+            WG_IF_INV_STAMPS(poll_ticks += __builtin_amdgcn_s_memrealtime() - t0; polls++;)
             break;
           }
           if ((it & 15) == 15 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
@@ -1058,15 +800,13 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
       for (int u = 0; u < 16; u++) rc[u] = rn[u];
       mc = mn;
     }
-#ifdef WG_INV_STAMPS
-    if (lane == 0) {
+    WG_IF_INV_STAMPS(if (lane == 0) {
       uint64_t* st = a.stamps + 4 * stamp_idx;
       st[0] = t_band;
       st[1] = __builtin_amdgcn_s_memrealtime();
       st[2] = poll_ticks | polls << 32;
       st[3] = blockIdx.x;
-    }
-#endif
+    })
   }
 }
 
@@ -1139,22 +879,9 @@ extern "C" int wg_vp8l_residual_image_rows(const uint32_t* argb, int32_t width, 
   const int64_t tiles = (int64_t)sa.band_tiles * n_images;
   WG_REQUIRE(tiles < (1ll << 31));
   int rc;
-  // A/B switch: 0 = k_vp8l_select (4 waves a tile, a mode a wave), 1 =
-  // k_vp8l_select_q (a wave a tile), default 2 = k_vp8l_select_q2 (two waves
-  // a tile).  (Round 5 also measured q2 in persistent workgroups, three
-  // 10-bit bins a histogram word and the next tile staged by wave 1 while
-  // wave 0 sums: 0.60 -> 0.65 ms at 4096².)
-  const char* sel_env = getenv("WG_VP8L_SELECT");  // (read per call: the tests switch it)
-  const int variant = sel_env ? atoi(sel_env) : 3;
-  if (bits <= 5 && variant == 3) {  // counts <= 512: all modes in one pass over the samples
+  if (bits <= 5) {  // counts <= 512: all modes in one pass over the samples
     hipLaunchKernelGGL(k_vp8l_select_q3, dim3((unsigned)tiles), dim3(128), 0, s, sa, tiles);
     rc = wg::check_launch("k_vp8l_select_q3");
-  } else if (bits <= 5 && variant == 2) {
-    hipLaunchKernelGGL(k_vp8l_select_q2, dim3((unsigned)tiles), dim3(128), 0, s, sa, tiles);
-    rc = wg::check_launch("k_vp8l_select_q2");
-  } else if (bits <= 5 && variant == 1) {
-    hipLaunchKernelGGL(k_vp8l_select_q, dim3((unsigned)((tiles + SQW - 1) / SQW)), dim3(64 * SQW), 0, s, sa, tiles);
-    rc = wg::check_launch("k_vp8l_select_q");
   } else {
     hipLaunchKernelGGL(k_vp8l_select, dim3((unsigned)tiles), dim3(64 * SEL_WAVES), 0, s, sa);
     rc = wg::check_launch("k_vp8l_select");
@@ -1188,11 +915,7 @@ extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32
 extern "C" size_t wg_vp8l_inverse_work_bytes(int32_t width, int32_t height, int32_t n_images) {
   if (width <= 0 || height <= 0 || n_images <= 0) return 0;
   const size_t bands = (size_t)n_images * ((height + INV_ROWS - 1) / INV_ROWS);
-#ifdef WG_INV_STAMPS
-  return 16 + sizeof(uint64_t) * bands * ((width + 1) & ~1) + 32 * bands;  // + the timeline records
-#else
-  return 16 + sizeof(uint64_t) * bands * ((width + 1) & ~1);
-#endif
+  return 16 + sizeof(uint64_t) * bands * ((width + 1) & ~1) WG_IF_INV_STAMPS(+32 * bands);  // (+ the timeline records)
 }
 
 extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, int32_t width, int32_t height,

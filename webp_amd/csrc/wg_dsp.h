@@ -23,8 +23,9 @@ __device__ __forceinline__ int sclip2(int v) { return min(max(v, -16), 15); }
 __device__ __forceinline__ int mul1(int a) { return a + __mulhi(a, 20091 << 16); }
 __device__ __forceinline__ int mul2(int a) { return a + __mulhi(a, (35468 - 65536) * 65536); }
 // The same on the full-rate 24-bit multiplier (v_mul_hi_i32 and v_mul_lo_u32
-// are quarter rate).  For |a| <= 2^16 (an int16 coefficient) a * 35468 fits
-// int32: one v_mul_i32_i24 and a shift.  For |a| < 2^23 (the inverse DCT's
+// are quarter rate).  For |a| <= 2^15 (an int16 coefficient: callers
+// truncate to int16 first, as dequant() does) a * 35468 fits int32 (2^15 *
+// 35468 < 2^31; 2^16 * 35468 does not): one v_mul_i32_i24 and a shift.  For |a| < 2^23 (the inverse DCT's
 // second pass: at most ~2^17.4 from int16 inputs) the 48-bit product is
 // mul_i24 (low 32 bits) + mulhi_i24 (bits 32..47) and bits 16..47 come out
 // of one v_alignbit.  Both equal mul1 / mul2 (Go's 64-bit products) on those
