@@ -94,6 +94,21 @@ def color_pattern(w, h):
 PATTERNS = {"smpte_bars": smpte_bars, "solid_blocks": solid_blocks, "color_gradient": color_pattern}
 
 
+def rich_image(w, h):
+    """richTestImage (encode_test.go:1492-1508): smooth R / G / B gradients."""
+    y, x = np.mgrid[0:h, 0:w]
+    rgb = np.stack([x * 255 // w, y * 255 // h, (x + y) * 255 // (w + h)], -1)
+    return _nrgba((rgb & 0xff).astype(np.uint8))
+
+
+def gradient_image(w, h):
+    """generateGradient (testc/roundtrip/roundtrip_test.go:17-30): R and G
+    gradients, B = 128."""
+    y, x = np.mgrid[0:h, 0:w]
+    rgb = np.stack([x * 255 // w, y * 255 // h, np.full_like(x, 128)], -1)
+    return _nrgba((rgb & 0xff).astype(np.uint8))
+
+
 # --- source planes and PSNR (the tests' own conversion, no gamma) ----------
 
 def rgb_to_y(r, g, b):
@@ -117,6 +132,27 @@ def source_yuv(rgba):
     U = _clip_uv(-9719 * r - 19081 * g + 28800 * b, 1 << 17)
     V = _clip_uv(28800 * r - 24116 * g - 4684 * b, 1 << 17)
     return Y, U, V
+
+
+def go_ycbcr_rgb(Y, U, V, w, h):
+    """What image.YCbCr.At(x, y).RGBA() >> 8 gives for the reference's no-alpha
+    lossy Decode (webp.go:339-372 returns *image.YCbCr, 4:2:0): chroma point
+    sampled at (x / 2, y / 2) and Go's color.YCbCr.RGBA() (image/color,
+    ycbcr.go: 16.16 fixed point with the factors 91881, 22554, 46802,
+    116130, clamped through the 0xff000000 test), as 8-bit (h, w, 3)."""
+    yy = Y[:h, :w].astype(np.int64) * 0x10101
+    cb = np.repeat(np.repeat(U.astype(np.int64), 2, 0), 2, 1)[:h, :w] - 128
+    cr = np.repeat(np.repeat(V.astype(np.int64), 2, 0), 2, 1)[:h, :w] - 128
+
+    def clamp16(v):
+        v = v.astype(np.int64)
+        inside = (v & 0xff000000) == 0       # uint32(v) & 0xff000000 == 0 (v is int32 range)
+        return np.where(inside, v >> 8, np.where(v < 0, 0, 0xffff)) >> 8
+
+    r = clamp16(yy + 91881 * cr)
+    g = clamp16(yy - 22554 * cb - 46802 * cr)
+    b = clamp16(yy + 116130 * cb)
+    return np.stack([r, g, b], -1).astype(np.uint8)
 
 
 def psnr(a, b):
@@ -185,10 +221,27 @@ MB_INFO_DTYPE = np.dtype([
 ])  # wg_mb_info (include/webpgpu.h)
 
 
-def mbdata_from_encoder(enc, info, sharpness=0, simple=False):
+def segment_filter_levels(info, filter_strength):
+    """The segment header's per-segment filter values (buildSegmentHeader,
+    encode_analysis.go:852-866): fDelta = (qstep_s - qstep_0) * FilterStrength
+    / 100 (Go's truncating division), clamped to +-63, with qstep = kAcTable[q]
+    >> 2.  The header marks them absolute (AbsoluteDelta), so the decoder
+    takes fDelta itself as segment s's base level (decode_frame.go:224-231)."""
+    qs = [int(K_AC[min(max(int(info["quant"][s]), 0), 127)]) >> 2 for s in range(4)]
+    out = []
+    for s in range(4):
+        num = (qs[s] - qs[0]) * filter_strength
+        d = abs(num) // 100 * (1 if num >= 0 else -1)
+        out.append(min(max(d, -63), 63))
+    return out
+
+
+def mbdata_from_encoder(enc, info, sharpness=0, simple=False, cfg_filter_strength=None):
     """wg_mb_enc records of one frame + its wg_frame_segs header record ->
     (wg_mb_info array, int16 (n, 384) dequantised coefficients, filter_type),
-    as DecodeFrame would parse them from the encoder's bitstream."""
+    as DecodeFrame would parse them from the encoder's bitstream.  With more
+    than one segment the config's FilterStrength is needed for the segment
+    header's filter values (segment_filter_levels)."""
     n = len(enc)
     segs = int(info["num_segments"])
     base = int(info["base_quant"])
@@ -197,7 +250,11 @@ def mbdata_from_encoder(enc, info, sharpness=0, simple=False):
     # segment header every segment's own (absolute) index
     qidx = [int(info["quant"][s]) if segs > 1 else base for s in range(4)]
     level = int(info["filter_level"])
-    seg_level = [int(info["fstrength"][s]) if segs > 1 else level for s in range(4)]
+    if segs > 1:
+        assert cfg_filter_strength is not None, "the segment header's filter values need FilterStrength"
+        seg_level = segment_filter_levels(info, cfg_filter_strength)
+    else:
+        seg_level = [level] * 4
     ftype = 0 if level == 0 else (1 if simple else 2)
     lv = enc["coeffs"].astype(np.int64)                         # (n, 400)
     seg = (enc["segment"] & 3).astype(np.int64) if segs > 1 else np.zeros(n, np.int64)
@@ -269,6 +326,42 @@ def diag_thresholds(q):
     max_level = 5 if q == 100 else (15 if q <= 50 else 10)
     mn = 50.0 if q == 100 else (42.0 if q >= 75 else 38.0)
     return max_level, mn, mn
+
+
+def rgb_channel_stats(src_rgb, dec_rgb):
+    """TestLossyRoundtrip_PSNR's statistics (encode_test.go:1541-1600):
+    per-channel PSNR (computePSNR: 99 for mse <= 0), the PSNR of the channels'
+    mean MSE, and the per-channel max |delta|."""
+    d = src_rgb.astype(np.int64) - dec_rgb.astype(np.int64)
+    mse = [float((d[..., c] ** 2).sum()) / d[..., c].size for c in range(3)]
+    p = lambda m: 99.0 if m <= 0 else 10.0 * np.log10(255.0 * 255.0 / m)
+    return [p(m) for m in mse], p(sum(mse) / 3.0), [int(np.abs(d[..., c]).max()) for c in range(3)]
+
+
+def rgba_psnr(a, b):
+    """computePSNR of testc/roundtrip/roundtrip_test.go:33-62: all four
+    channels, inf for identical images."""
+    d = a.astype(np.float64).ravel() - b.astype(np.float64).ravel()
+    mse = float(np.dot(d, d)) / d.size
+    return float("inf") if mse == 0 else 10 * np.log10(255.0 * 255.0 / mse)
+
+
+def rgb_psnr(a, b):
+    """TestEncodeCompareRGB's PSNR over packed RGB (encode_compare_test.go:226-235, mse :324-331)."""
+    d = a.astype(np.float64).ravel() - b.astype(np.float64).ravel()
+    return 10 * np.log10(255.0 * 255.0 / (float(np.dot(d, d)) / d.size))
+
+
+# {Quality: 75, Method: 4} with every other EncoderOptions field zero, as
+# TestLossyRoundtrip_PSNR and TestGoEncCDecLossy pass it: encodeLossyWithAlpha
+# (encode.go:478-506) keeps DefaultConfig's 4 segments (Segments 0 is not > 0)
+# and takes SNSStrength 0, FilterStrength 0, FilterType 0 as given
+ZERO_OPTS_Q75 = dict(quality=75, method=4, sns_strength=0, filter_strength=0, filter_sharpness=0, filter_type=0,
+                     segments=4, preprocessing=0)
+# webp.Encode(nil) = DefaultOptions (encode.go:196-214): the bench's configuration
+DEFAULT_OPTS_Q75 = dict(quality=75, method=4, sns_strength=50, filter_strength=60, filter_sharpness=0, filter_type=1,
+                        segments=4, preprocessing=0)
+ROUNDTRIP_SIZES = [(32, 32), (128, 128), (768, 576)]   # roundtrip_test.go:96
 
 
 def compare_thresholds(q):

@@ -203,7 +203,10 @@ def make_encode_compare_fixtures():
     768x576, decoded with `dwebp -yuv`.  Here: libwebp 1.6.0 WebPEncode with
     WebPConfigInit(Q) + segments 1 + method 4 (cwebp's other defaults are the
     config's), WebPDecodeYUV of the result.  Keys cwebp_<w>x<h>_q<Q>_{y,u,v}
-    (decoded planes, h x w and h/2 x w/2) and _webp (the bitstream)."""
+    (decoded planes, h x w and h/2 x w/2) and _webp (the bitstream).
+    TestEncodeCompareRGB's C side (:174-264, `dwebp -ppm`: fancy-upsampled
+    RGB): _rgb, the RGB channels of WebPDecodeRGBA of the same bitstream
+    (h x w x 3; the RGBA decode's colour channels are MODE_RGB's)."""
     import encode_quality as EQ
     out = {}
     for w, h in EQ.COLOR_SIZES:
@@ -214,6 +217,7 @@ def make_encode_compare_fixtures():
             key = "cwebp_%dx%d_q%d" % (w, h, q)
             out[key + "_webp"] = np.frombuffer(data, np.uint8).copy()
             out[key + "_y"], out[key + "_u"], out[key + "_v"] = Y, U[:h // 2, :w // 2], V[:h // 2, :w // 2]
+            out[key + "_rgb"] = np.ascontiguousarray(L.decode_rgba(data)[..., :3])
     path = os.path.join(HERE, "cwebp_compare.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes")
