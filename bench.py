@@ -11,6 +11,10 @@ frames, all inputs resident in HBM before timing starts:
                bitstreams of the same three contents, parsed once on the host by
                wg_vp8_parse (tests/golden/q75_1080p.npz), -> fancy upsample to
                NRGBA (k_upsample)
+Contents: G gradient, N noise, P photo (the reference's
+testdata/test_color.png tiled); frame i of rank r is content i % 3 with seed
+r * batch + i, so every frame of the C4 job is distinct on the encode side
+(the decode side replays the three contents' libwebp streams).
 The encode configuration is webp.Encode's DefaultOptions (quality 75, method
 4, SNS 50, filter strength 60, 4 segments; internal/lossy/encode.go:66-86).
 
@@ -23,7 +27,12 @@ launch).  Then, untimed for `value`:
   - an isolated one-batch pass for each kernel's launch time (the roofline);
   - one-frame encodes (C2), whose RD launch is the macroblock wavefront's
     critical path: the per-MB latency bench reports as the encoder's limiter;
-  - the measured copy-kernel HBM ceiling (tools/libprobe.so).
+  - the measured copy-kernel HBM ceiling (tools/libprobe.so);
+  - `c3`: one real 4096x4096 q75 decode (tests/golden/c3_4096_q75.npz:
+    libwebp's encode of test_color.png tiled), reconstruct + filter +
+    upsample, and `c5`: SubtractGreen + ResidualImage (bits 5, q75), SharpYUV
+    and plane SSIM on a 4096x4096 N + G blend (BASELINE.json configs 2 and 4,
+    one GPU), each with ms, MPix/s and its HBM roofline fraction.
 
 Multi-GPU: one process per GPU, frames sharded across ranks with no data-path
 collective in the timed region ("weak" scaling); value = all pixels / max rank
@@ -65,7 +74,7 @@ BYTES_PER_PX = {
 }
 KERNELS = {"import": "k_import", "analysis": "k_analysis", "segments": "k_segments", "encode": "k_encode_rows",
            "decode": "k_decode_split", "upsample": "k_upsample"}  # decode: set from wg_decode_kernel at report time
-CONTENTS = ("grad", "noise", "blobs")
+CONTENTS = ("grad", "noise", "photo")
 BITSTREAMS = os.path.join(ROOT, "tests", "golden", "q75_1080p.npz")
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 VALU_FILE = os.path.join(ROOT, "profiles", "pmc_valu.json")
@@ -172,6 +181,8 @@ def parse():
                    help="with N > 1, skip the gather of the last batch's outputs to rank 0 (timed apart from value)")
     p.add_argument("--runs", type=int, default=10, help="repeats of the short timed region for the medians")
     p.add_argument("--run-steps", type=int, default=6, help="steps per median run")
+    p.add_argument("--no-c3c5", dest="c3c5", action="store_false",
+                   help="skip the C3 / C5 single-GPU measurements (reported beside value, not in it)")
     p.add_argument("--launcher-check", action="store_true",
                    help="CPU/gloo: start the ranks, join them and time an empty step; no GPU work, no measurement "
                         "(tests/test_bench_launch.py)")
@@ -180,8 +191,13 @@ def parse():
 
 def content_rgba(kind, seed):
     from tools import synth
-    return {"grad": lambda: synth.gradient_rgba(W, H), "noise": lambda: synth.noise_rgba(W, H, seed=seed),
-            "blobs": lambda: synth.blobs_rgba(W, H, seed=seed)}[kind]()
+    return {"grad": lambda: synth.gradient_rgba(W, H, seed=seed), "noise": lambda: synth.noise_rgba(W, H, seed=seed),
+            "photo": lambda: synth.photo_rgba(W, H, seed=seed)}[kind]()
+
+
+def frame_rgba(g):
+    """Global frame g of the job (rank r's frame i: g = r * batch + i): content g % 3, seed g."""
+    return content_rgba(CONTENTS[g % 3], g)
 
 
 def parsed_bitstreams():
@@ -197,14 +213,13 @@ def parsed_bitstreams():
 
 
 def make_inputs(batch, rank, device):
-    """Frame i of rank r is content (i + r) % 3, seeds r*3 + k: every rank
-    owns different frames.  The decode side replicates the parsed bitstreams
-    the same way."""
+    """Frame i of rank r is global frame g = r * batch + i: content g % 3 with
+    seed g (frame_rgba), so every frame of every rank is distinct.  The decode
+    side takes content g % 3's parsed libwebp bitstream."""
     from webp_amd import frames
-    base = [content_rgba(k, rank * 3 + j) for j, k in enumerate(CONTENTS)]
     rgba = torch.empty((batch, H, W, 4), dtype=torch.uint8, device=device)
     for i in range(batch):
-        rgba[i].copy_(torch.from_numpy(base[(i + rank) % 3]))
+        rgba[i].copy_(torch.from_numpy(frame_rgba(rank * batch + i)))
     parsed = parsed_bitstreams()
     per = MBW * MBH
     mb_t = [frames.mb_info_tensor(parsed[k][0], device).view(per, 32) for k in CONTENTS]
@@ -212,8 +227,8 @@ def make_inputs(batch, rank, device):
     mb_all = torch.empty((batch, per, 32), dtype=torch.uint8, device=device)
     co_all = torch.empty((batch, per, 384), dtype=torch.int16, device=device)
     for i in range(batch):
-        mb_all[i].copy_(mb_t[(i + rank) % 3])
-        co_all[i].copy_(co_t[(i + rank) % 3])
+        mb_all[i].copy_(mb_t[(rank * batch + i) % 3])
+        co_all[i].copy_(co_t[(rank * batch + i) % 3])
     return rgba, mb_all.view(-1, 32), co_all.view(-1, 384), parsed
 
 
@@ -374,7 +389,7 @@ def cpu_baseline(seconds, parsed):
     import concurrent.futures as cf
 
     import oracle as O
-    imgs = [content_rgba(k, j) for j, k in enumerate(CONTENTS)]
+    imgs = [frame_rgba(j) for j in range(3)]
     cfg = O.encoder_config(**ENC_CFG)
     proba = O.default_proba()
 
@@ -410,7 +425,7 @@ def cpu_baseline(seconds, parsed):
     return {"value": round(value, 2), "unit": "MPixels/s", "cores": threads, "kind": "port",
             "single_thread_value": round(single, 2),
             "sample": f"{fn} x 1920x1080 frames on {threads} threads (one frame per thread, contents gradient/noise/"
-                      f"blobs in turn; {f1} frames on 1 thread before it) of import+analysis+segments+MB RD+q75 "
+                      f"photo in turn; {f1} frames on 1 thread before it) of import+analysis+segments+MB RD+q75 "
                       "decode+upsample, C restatement of the reference Go CPU path"}
 
 
@@ -490,7 +505,7 @@ def single_frame_encode(device, reps=3):
     steps_cp = MBW + 2 * (MBH - 1)
     res = {}
     for j, kind in enumerate(CONTENTS):
-        rgba = torch.from_numpy(content_rgba(kind, j)[None]).to(device)
+        rgba = torch.from_numpy(frame_rgba(j)[None]).to(device)
         best_path = best_rd = None
         for rep in range(reps + 1):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
@@ -512,6 +527,106 @@ def single_frame_encode(device, reps=3):
                      "mpix_s": round(W * H / best_path / 1e3, 1),
                      "per_mb_us": round(best_rd * 1e3 / steps_cp, 2)}
     return {"frames": res, "critical_path_mb_steps": steps_cp}
+
+
+C3_STREAM = os.path.join(ROOT, "tests", "golden", "c3_4096_q75.npz")
+C5_N = 4096
+# algorithmic HBM bytes per pixel of the C5 stages: ARGB in and
+# out (8), packed RGB in + Y / U / V out (4.5, SharpYUV), two planes in (2, SSIM)
+C5_BYTES_PER_PX = {"subtract_green": 8.0, "residual_image": 8.0, "sharpyuv": 4.5, "plane_ssim": 2.0}
+
+
+def event_ms(fn, reps):
+    """Median over `reps` of fn's device time, HIP events on the current stream
+    (one untimed call first)."""
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def stage_record(ms, px, bytes_per_px, kernel):
+    gbs = bytes_per_px * px / (ms / 1e3) / 1e9
+    return {"kernel": kernel, "ms": round(ms, 4), "MPix/s": round(px / ms / 1e3, 1), "bytes_per_px": bytes_per_px,
+            "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+
+def c3_decode(device, reps=10):
+    """BASELINE.json configs[2]: one 4096x4096 lossy decode -- a libwebp q75
+    stream of test_color.png tiled, parsed on the host by
+    wg_vp8_parse (timed apart), then reconstruct + loop filter and fancy
+    upsample to NRGBA on the GPU; median device times over `reps`."""
+    from webp_amd import _lib, frames
+    data = np.load(C3_STREAM)["webp"].tobytes()
+    t0 = time.perf_counter()
+    dims, mb, co = frames.vp8_parse(data)
+    parse_ms = (time.perf_counter() - t0) * 1e3
+    w, h, mbw, mbh, ft = (dims[k] for k in ("width", "height", "mbw", "mbh", "filter_type"))
+    mbt = frames.mb_info_tensor(mb, device)
+    cot = torch.from_numpy(co).to(device)
+    work = torch.empty(_lib.lib.wg_decode_work_bytes(mbw, mbh, 1), dtype=torch.uint8, device=device)
+    Y, U, V = frames.decode_frames(mbt, cot, ft, mbw, mbh, 1, work=work)
+    out = frames.build_nrgba(Y, U, V, w, h)
+    dec_ms = event_ms(lambda: frames.decode_frames(mbt, cot, ft, mbw, mbh, 1, out=(Y, U, V), work=work), reps)
+    up_ms = event_ms(lambda: frames.build_nrgba(Y, U, V, w, h, out=out), reps)
+    frames.decode_status(work, mbw, 1)
+    dk = {1: "k_decode_split", 2: "k_decode_bands"}.get(_lib.lib.wg_decode_kernel(mbh, 1), "k_decode_split")
+    px = w * h
+    return {"workload": f"one {w}x{h} q75 decode (libwebp stream of testdata/test_color.png tiled, {len(data)} B, "
+                        f"{float(mb['is_i4x4'].mean()):.2f} I4, filter type {ft}), reconstruct + loop filter + fancy "
+                        "upsample to NRGBA",
+            "host_parse_ms": round(parse_ms, 2), "total_ms": round(dec_ms + up_ms, 4),
+            "MPix/s": round(px / (dec_ms + up_ms) / 1e3, 1),
+            "reconstruct_filter": stage_record(dec_ms, px, BYTES_PER_PX["decode"], dk),
+            "upsample": stage_record(up_ms, px, BYTES_PER_PX["upsample"], "k_upsample"),
+            "bound": "the macroblock wavefront of one image (latency), not HBM", "reps": reps}
+
+
+def c5_stages(device, reps=10):
+    """BASELINE.json configs[4] on one GPU: a 4096x4096 RGBA N + G blend
+     through SubtractGreen + ResidualImage (bits 5, q75), SharpYUV
+    (WebP matrix, sRGB) and plane SSIM (Y of the source vs Y + noise);
+    median device times over `reps`."""
+    from tools import synth
+    from webp_amd import frames
+    from webp_amd import lossless as L
+    n = C5_N
+    blend = ((synth.noise_rgba(n, n, seed=55).astype(np.uint16) + 3 * synth.gradient_rgba(n, n).astype(np.uint16))
+             // 4).astype(np.uint8)
+    blend[..., 3] = 255
+    c = blend.astype(np.uint32)
+    argb = (c[..., 3] << 24) | (c[..., 0] << 16) | (c[..., 1] << 8) | c[..., 2]
+    t = L.to_argb_tensor(argb[None], device)
+    px = n * n
+    out = {}
+    g = t.clone()
+    out["subtract_green"] = stage_record(event_ms(lambda: L.SubtractGreen(g), reps), px,
+                                         C5_BYTES_PER_PX["subtract_green"], "k_vp8l_green")
+    L.SubtractGreen(t)
+    modes, res = L.ResidualImage(t, 5, 75)
+    out["residual_image"] = stage_record(event_ms(lambda: L.ResidualImage(t, 5, 75, out=(modes, res)), reps), px,
+                                         C5_BYTES_PER_PX["residual_image"], "k_vp8l_select_q3 + k_vp8l_residual")
+    rgb = torch.from_numpy(np.ascontiguousarray(blend[..., :3])).to(device).unsqueeze(0)
+    Ys, Us, Vs = frames.sharpyuv_convert(rgb)
+    work = torch.empty(frames.lib.wg_sharpyuv_work_bytes(n, n, 1), dtype=torch.uint8, device=device)
+    out["sharpyuv"] = stage_record(event_ms(lambda: frames.sharpyuv_convert(rgb, out=(Ys, Us, Vs), work=work), reps),
+                                   px, C5_BYTES_PER_PX["sharpyuv"], "k_sharp_*")
+    y = torch.from_numpy(np.ascontiguousarray(blend[..., 1])).to(device).unsqueeze(0)
+    y2 = torch.clamp(y.int() + torch.randint(-8, 9, y.shape, device=device, dtype=torch.int32, generator=None),
+                     0, 255).to(torch.uint8)
+    out["plane_ssim"] = stage_record(event_ms(lambda: frames.plane_ssim(y, y2), reps), px,
+                                     C5_BYTES_PER_PX["plane_ssim"], "k_ssim")
+    torch.cuda.synchronize()
+    return {"workload": f"one {n}x{n} RGBA noise + gradient blend (SURVEY 8(d) C5), 1 GPU", "stages": out,
+            "reps": reps}
 
 
 def free_port():
@@ -617,10 +732,13 @@ def main():
         gather = shard.timed_gather_to_root([sl.enc_out, sl.rY, sl.rU, sl.rV, sl.out], world, rank, device)
     del pipe
     c2 = single_frame_encode(device) if rank == 0 else None
-    copy = None
+    copy = c3 = c5 = None
     if rank == 0:
         from tools import fetch_calib
         copy = fetch_calib.copy_peak(device)
+        if args.c3c5:
+            c3 = c3_decode(device)
+            c5 = c5_stages(device)
     torch.cuda.synchronize()
 
     if rank == 0:
@@ -649,7 +767,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic RGBA (gradient/noise/blobs) for the encode side; libwebp q75 encodes of the same three "
+            "data": "synthetic RGBA for the encode side, SURVEY 8(d) G / N / P (gradient, noise, the reference's "
+                    "testdata/test_color.png tiled), a distinct seed per frame; libwebp q75 encodes of the three "
                     "contents, parsed by wg_vp8_parse, for the decode side",
             "config": {"workload": f"{args.batch} x 1920x1080 frames per GPU per step (C2 frame, C4 per-GPU share): "
                                    "import+analysis+segments+MB RD loop (encode DSP) + reconstruct+loopfilter+upsample "
@@ -702,6 +821,10 @@ def main():
             rec["valu"] = valu
         if gather is not None:
             rec["gather"] = gather
+        if c3 is not None:
+            rec["c3"] = c3
+        if c5 is not None:
+            rec["c5"] = c5
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is timed at N = 1 only, after the GPU phase
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds, parsed)
         print(json.dumps(rec), flush=True)

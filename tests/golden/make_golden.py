@@ -134,13 +134,15 @@ def make_c1_fixture(img):
 
 
 def make_bench_bitstreams():
-    """libwebp 1.6.0 q75 (WebPEncodeRGBA defaults) encodes of the bench's three
-    1920x1080 synthetic contents (gradient, noise seed 1, blobs seed 2): the
-    decode side of bench.py parses them with wg_vp8_parse (SURVEY 8(d) C3,
-    "real q75 bitstreams").  Stored as raw bytes in an uncompressed .npz."""
+    """libwebp 1.6.0 q75 (WebPEncodeRGBA defaults) encodes of 1920x1080
+    contents -- gradient, noise seed 1, photo (test_color.png tiled, seed 0;
+    SURVEY 8(d) G / N / P) and blobs seed 2: the decode side of bench.py
+    parses the first three with wg_vp8_parse ("real q75
+    bitstreams").  Stored as raw bytes in an uncompressed .npz."""
     w, h = 1920, 1080
     out = {"grad": L.encode_lossy(synth.gradient_rgba(w, h), 75.0),
            "noise": L.encode_lossy(synth.noise_rgba(w, h, seed=1), 75.0),
+           "photo": L.encode_lossy(synth.photo_rgba(w, h, seed=0), 75.0),
            "blobs": L.encode_lossy(synth.blobs_rgba(w, h, seed=2), 75.0)}
     path = os.path.join(HERE, "q75_1080p.npz")
     np.savez(path, **{k: np.frombuffer(bytes(v), np.uint8) for k, v in out.items()})
@@ -226,5 +228,7 @@ def make_encode_compare_fixtures():
 if __name__ == "__main__":
     if sys.argv[1:] == ["encode_compare"]:
         make_encode_compare_fixtures()
+    elif sys.argv[1:] == ["bench_bitstreams"]:
+        make_bench_bitstreams()
     else:
         main()

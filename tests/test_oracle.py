@@ -50,7 +50,7 @@ def test_decode_bitstreams_vs_libwebp(name):
     assert crop_eq(y, DEC[name + "_y"]) and crop_eq(u, DEC[name + "_u"]) and crop_eq(v, DEC[name + "_v"])
 
 
-@pytest.mark.parametrize("content", ["grad", "noise", "blobs"])
+@pytest.mark.parametrize("content", ["grad", "noise", "photo", "blobs"])
 def test_bench_bitstreams_vs_libwebp(content):
     """The decode side of bench.py: libwebp q75 encodes of the bench's 1080p
     contents (tests/golden/q75_1080p.npz), parsed by wg_vp8_parse and decoded by

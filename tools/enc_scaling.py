@@ -1,7 +1,8 @@
 """Encoder (k_encode_rows) time vs batch size: where the row wavefront's
 critical path (mbw + 2 (mbh - 1) macroblock latencies per image) stops
-bounding the launch and wave slots start to.  Mixed content (gradient /
-noise / blobs in turn), the reference's q75 segment setup, like bench.py.
+bounding the launch and wave slots start to.  The bench's frames
+(bench.frame_rgba: G / N / P in turn, a distinct seed per frame) and the
+reference's q75 segment setup, like bench.py.
 Prints one line per batch size.  Diagnostic only (not the driver bench)."""
 import os
 import sys
@@ -11,17 +12,17 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import oracle as O  # noqa: E402
-from tools import synth  # noqa: E402
+import bench  # noqa: E402
 from webp_amd import frames  # noqa: E402
 
 W, H = 1920, 1080
 MBW, MBH = 120, 68
-gens = [lambda: synth.gradient_rgba(W, H), lambda: synth.noise_rgba(W, H, seed=3), lambda: synth.blobs_rgba(W, H, seed=3)]
-planes = [O.import_rgba(g(), has_alpha=False) for g in gens]
-for B in [int(b) for b in os.environ.get("BATCHES", "1,3,8,16,32,64").split(",")]:
-    Y = torch.from_numpy(np.stack([planes[i % 3][0] for i in range(B)])).cuda()
-    U = torch.from_numpy(np.stack([planes[i % 3][1] for i in range(B)])).cuda()
-    V = torch.from_numpy(np.stack([planes[i % 3][2] for i in range(B)])).cuda()
+BATCHES = [int(b) for b in os.environ.get("BATCHES", "1,3,8,16,32,64").split(",")]
+planes = [O.import_rgba(bench.frame_rgba(g), has_alpha=False) for g in range(max(BATCHES))]
+for B in BATCHES:
+    Y = torch.from_numpy(np.stack([planes[i][0] for i in range(B)])).cuda()
+    U = torch.from_numpy(np.stack([planes[i][1] for i in range(B)])).cuda()
+    V = torch.from_numpy(np.stack([planes[i][2] for i in range(B)])).cuda()
     alphas, uv_sum = frames.analysis_alphas(Y, U, V, W, H)
     seg_ids, segs, _ = frames.segment_analysis(frames.encoder_config(), alphas, uv_sum, MBW, MBH)
     proba = O.default_proba()

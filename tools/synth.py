@@ -1,7 +1,11 @@
 """Seeded synthetic inputs shared by tests/ and bench.py.
 
-Images:  gradient  R=x%256, G=y%256, B=(x+y)%256 (bench_test.go:97-111)
+Images:  gradient  R=x%256, G=y%256, B=(x+y)%256 (bench_test.go:97-111);
+                   with a seed, the same pattern from origin (13 seed, 7 seed)
          noise     uniform bytes (seeded)
+         photo     testdata/test_color.png (1536x1024, the reference's own test
+                   image, committed as tests/golden/test_color_png.npz) tiled,
+                   from a seed-dependent origin
          blobs     smooth low-frequency pattern (lets the loop filters fire)
 Macroblocks: parsed VP8 macroblock data in the wire format of
 include/webpgpu.h (wg_mb_info + int16[384] coefficients): a seeded mix of
@@ -21,8 +25,9 @@ MB_INFO_DTYPE = np.dtype([
 ])
 
 
-def gradient_rgba(w, h):
+def gradient_rgba(w, h, seed=0):
     y, x = np.mgrid[0:h, 0:w]
+    x, y = x + 13 * seed, y + 7 * seed
     img = np.empty((h, w, 4), np.uint8)
     img[..., 0] = x % 256
     img[..., 1] = y % 256
@@ -37,6 +42,36 @@ def noise_rgba(w, h, seed=42, alpha=False):
     if not alpha:
         img[..., 3] = 255
     return img
+
+
+_PHOTO = None
+
+
+def test_color_rgba():
+    """testdata/test_color.png as RGBA (1024 x 1536 x 4), decoded once from the
+    committed PNG bytes."""
+    global _PHOTO
+    if _PHOTO is None:
+        import io
+        import os
+
+        from PIL import Image
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                            "test_color_png.npz")
+        png = np.load(path)["png"].tobytes()
+        _PHOTO = np.ascontiguousarray(np.array(Image.open(io.BytesIO(png)).convert("RGBA")))
+    return _PHOTO
+
+
+def photo_rgba(w, h, seed=0):
+    """SURVEY 8(d) "P": test_color.png tiled to w x h (seed 0: from its
+    top-left corner, as tests/golden/make_golden.py's C3 image), other seeds
+    from the origin (97 seed mod 1536, 61 seed mod 1024) of the tiling."""
+    img = test_color_rgba()
+    ih, iw = img.shape[:2]
+    x0, y0 = (97 * seed) % iw, (61 * seed) % ih
+    reps = (-(-(h + y0) // ih), -(-(w + x0) // iw), 1)
+    return np.ascontiguousarray(np.tile(img, reps)[y0:y0 + h, x0:x0 + w])
 
 
 def blobs_rgba(w, h, seed=7, alpha=False):
