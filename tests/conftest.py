@@ -25,16 +25,52 @@ def cuda():
     return torch.device("cuda:0")
 
 
+_HIP = None
+
+
+def _hip():
+    """The HIP runtime torch already loaded (raw calls for the drain probe)."""
+    global _HIP
+    if _HIP is None:
+        import ctypes
+        _HIP = ctypes.CDLL("libamdhip64.so")
+        _HIP.hipGetErrorName.restype = ctypes.c_char_p
+    return _HIP
+
+
 @pytest.fixture(autouse=True)
 def _gpu_drain(request):
     """After every GPU test, wait for ALL the device's work (every stream)
-    and surface any asynchronous kernel fault there: a fault is then reported
-    as the teardown error of the test that launched the kernel, not by the
-    next test's first HIP call (a fault reported in
-    test_gpu_rescale_large whose kernel was never identified)."""
+    and surface any asynchronous device fault there, so that it is reported
+    as the teardown error of the test that launched the faulting work, not by
+    a later test's first HIP call (an illegal-address error
+    first reported in test_gpu_rescale_large, twice, whose kernel was never
+    identified).  The probe is hipDeviceSynchronize plus a fresh hipMalloc /
+    hipFree -- a new device allocation is the call that reported the sticky
+    error both times, where the stream synchronisations of the tests before it
+    had returned success.  WG_DRAIN_SLEEP_MS (diagnostic runs) waits that long
+    before the probe, for a fault whose notification lags the kernel's end."""
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
+    import ctypes
+    import os
+    import time
+
     import torch
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
+    if not torch.cuda.is_available():
+        return
+    torch.cuda.synchronize()
+    ms = float(os.environ.get("WG_DRAIN_SLEEP_MS", "0"))
+    if ms > 0:
+        time.sleep(ms / 1e3)
+    hip = _hip()
+    rc_sync = hip.hipDeviceSynchronize()
+    p = ctypes.c_void_p()
+    rc_malloc = hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(1 << 21))
+    if rc_malloc == 0:
+        hip.hipFree(p)
+    if rc_sync or rc_malloc:
+        names = [hip.hipGetErrorName(rc).decode() for rc in (rc_sync, rc_malloc)]
+        pytest.fail(f"device error after {request.node.nodeid}: hipDeviceSynchronize -> {names[0]}, "
+                    f"hipMalloc -> {names[1]}")

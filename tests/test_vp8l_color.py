@@ -32,6 +32,12 @@ def images():
     r = (g * 3 // 2 + rng.integers(-3, 4, g.shape)) & 0xff
     b = (255 - g + rng.integers(-2, 3, g.shape)) & 0xff
     yield "correlated", ((0xff << 24) | (r << 16) | (g << 8) | b).astype(np.uint32)
+    # ties: green 0 makes every multiplier cost the same (the scan's first
+    # candidate wins); two-level content ties many candidates
+    yield "green0", ((0xff << 24) | (rng.integers(0, 256, (33, 35)).astype(np.int64) << 16) |
+                     rng.integers(0, 256, (33, 35)).astype(np.int64)).astype(np.uint32)
+    lv = rng.integers(0, 2, (40, 36)).astype(np.int64) * 128
+    yield "levels", ((0xff << 24) | (lv << 16) | ((255 - lv) << 8) | (lv // 2)).astype(np.uint32)
 
 
 @pytest.mark.parametrize("bits", [2, 3, 5])
@@ -99,8 +105,9 @@ def test_color_index_inverse(xbits):
 
 # ---------------------------------------------------------------- GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("bits", [2, 4, 5, 6, 7])
+@pytest.mark.parametrize("bits", [2, 3, 4, 5, 6, 7])
 def test_gpu_color_space_transform(cuda, bits):
+    """bits <= 5: k_cc_select_q (packed-byte search); 6, 7: k_cc_select."""
     from webp_amd import lossless as L
     for name, a in list(images()) + [("big", argb_of(synth.noise_rgba(300, 170, seed=4, alpha=True)))]:
         data, t = O.vp8l_color_space_transform(a, bits)

@@ -1,6 +1,7 @@
 """Diagnostic: the row timeline of one k_encode_rows launch over the bench's
-batch (64 mixed 1080p frames: gradient / noise / blobs in turn, the q75
-segment setup and the row schedule, as bench.py).  Answers what bounds the
+batch (64 1080p frames: bench.py's frame_rgba contents -- gradient / noise /
+photo in turn, a distinct seed each -- the q75 segment setup and the row
+schedule, as bench.py).  Answers what bounds the
 launch: when each content's frames finish, how many rows are in flight over
 time (the tail), and how long a row takes by content.
 
@@ -18,13 +19,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+import bench  # noqa: E402
 import oracle as O  # noqa: E402
-from tools import synth  # noqa: E402
 from webp_amd import _lib, frames  # noqa: E402
 
 B, W, H = int(os.environ.get("BATCH", "64")), 1920, 1080
 MBW, MBH = 120, 68
-KINDS = ["gradient", "noise", "blobs"]
+KINDS = ["grad", "noise", "photo"]
 if os.environ.get("PAIR") is not None:
     os.environ["WG_ENCODE_PAIR"] = os.environ["PAIR"]
 lib = _lib.lib
@@ -32,11 +33,8 @@ if not hasattr(lib, "wg_debug_enc_rows"):
     sys.exit("needs WEBPGPU_LIB=webp_amd/libwebpgpu_rowtimes.so")
 lib.wg_debug_enc_rows.argtypes = [ctypes.c_void_p, ctypes.c_int]
 
-gens = [lambda: synth.gradient_rgba(W, H), lambda: synth.noise_rgba(W, H, seed=3), lambda: synth.blobs_rgba(W, H, seed=3)]
-planes = [O.import_rgba(g(), has_alpha=False) for g in gens]
-Y = torch.from_numpy(np.stack([planes[i % 3][0] for i in range(B)])).cuda()
-U = torch.from_numpy(np.stack([planes[i % 3][1] for i in range(B)])).cuda()
-V = torch.from_numpy(np.stack([planes[i % 3][2] for i in range(B)])).cuda()
+rgba = torch.from_numpy(np.stack([bench.frame_rgba(g) for g in range(B)])).cuda()
+Y, U, V = frames.import_rgba(rgba, has_alpha=False)
 alphas, uv_sum = frames.analysis_alphas(Y, U, V, W, H)
 seg_ids, segs, _ = frames.segment_analysis(frames.encoder_config(), alphas, uv_sum, MBW, MBH)
 proba = O.default_proba()
@@ -79,7 +77,14 @@ print("  rows in flight at 0,1,2.. ms:", inflight)
 last = np.argsort(t1)[-10:]
 print("  last rows (img, y, kind, start ms, end ms):",
       [(int(img[i]), int(y[i]), KINDS[kind[i]], round(t0[i] / 1e3, 2), round(t1[i] / 1e3, 2)) for i in last])
-summ.update({"launch_ms": round(ms, 3), "span_ms": round(span / 1e3, 3), "inflight_per_ms": inflight})
+# slot occupancy: wave-time inside rows (waits for the row above included)
+# over the resident wave slots x the span, and the waits before a row's
+# first macroblock are not separable here (start = dequeue)
+slots = int(os.environ.get("SLOTS", "2048"))
+busy = float((t1 - t0).sum()) / (slots * span)
+print(f"  row-time / (slots {slots} x span): {busy:.3f}")
+summ.update({"launch_ms": round(ms, 3), "span_ms": round(span / 1e3, 3), "inflight_per_ms": inflight,
+             "row_time_fill": round(busy, 3)})
 if os.environ.get("RAW"):  # the raw timeline: dequeue index -> (ro, start us, end us, block << 8 | wave)
     np.savez_compressed(os.environ["RAW"], ro=ro, t0=t0, t1=t1, who=buf[:, 3].astype(np.int64), launch_ms=ms)
 if os.environ.get("JSON"):

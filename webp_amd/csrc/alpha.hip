@@ -28,6 +28,7 @@
 //                       any-transparent / all-opaque results
 // Bit-exact with oracle/alpha.c.
 #include "wg_common.h"
+#include "wg_instr.h"
 
 namespace {
 
@@ -407,11 +408,13 @@ __device__ __forceinline__ int byte_at(uint32_t v, int i) { return (int)((v >> (
 // 64 columns of a lane's ring back to its row, as 16-B pieces (w % 16 == 0:
 // a piece is either inside the row or past its end); no loop with a
 // run-time count, so the compiler keeps its load-wait bookkeeping exact
-__device__ __forceinline__ void gd_store_block(const uint8_t* ring_row, uint8_t* row, int c0, int w) {
+// (data / data_n: the batch's planes and their extent, for WG_BOUNDS builds)
+__device__ __forceinline__ void gd_store_block(const uint8_t* ring_row, uint8_t* row, int c0, int w, const uint8_t* data,
+                                               int64_t data_n) {
   const uint32_t* l = reinterpret_cast<const uint32_t*>(ring_row + (c0 & 127));
 #pragma unroll
   for (int q = 0; q < 4; q++)
-    if (c0 + 16 * q < w)
+    if (c0 + 16 * q < w && WG_CHK(row + c0 + 16 * q, 16, data, data_n, "k_alpha_gdiag row store"))
       *reinterpret_cast<uint4*>(row + c0 + 16 * q) = make_uint4(l[4 * q], l[4 * q + 1], l[4 * q + 2], l[4 * q + 3]);
 }
 
@@ -422,8 +425,13 @@ __global__ __launch_bounds__(256) void k_alpha_row0_granules(GdArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)gw * a.n_img) return;
   const int img = (int)(i / gw), g = (int)(i % gw);
-  const uint32_t px = *reinterpret_cast<const uint32_t*>(a.data + img * a.pitch + 4 * g);
-  a.hand[(int64_t)img * (a.bands + 1) * gw + g] = 1ull << 32 | px;
+  const uint8_t* src = a.data + img * a.pitch + 4 * g;
+  uint64_t* const dst = a.hand + (int64_t)img * (a.bands + 1) * gw + g;
+  if (!WG_CHK(src, 4, a.data, a.n_img * a.pitch, "k_alpha_row0_granules data") ||
+      !WG_CHK(dst, 8, a.hand, 8ll * a.n_img * (a.bands + 1) * gw, "k_alpha_row0_granules hand"))
+    return;
+  const uint32_t px = *reinterpret_cast<const uint32_t*>(src);
+  *dst = 1ull << 32 | px;
 }
 
 __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
@@ -433,6 +441,8 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
   const int w = a.w, gw = w >> 2;
   const int total = a.bands * a.n_img;
   uint8_t* my_ring = ring + lane * GB_STRIDE;
+  // (WG_BOUNDS) the buffers' extents from the entry point's shapes
+  [[maybe_unused]] const int64_t data_n = a.n_img * a.pitch, hand_n = 8ll * a.n_img * (a.bands + 1) * gw;
   // the lane's window within a 16-B aligned 32-B load: chunk starts are
   // multiples of 16, so (s0 - k) & 15 = (-k) & 15
   const int o = (-lane) & 15, q = o >> 2, rsh = o & 3;
@@ -463,8 +473,11 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
     // end is clamped, and only x >= w can read the clamped bytes)
     auto ld_res = [&](int s0, uint4& lo, uint4& hi) {
       const int a16 = s0 - lane - o;
-      lo = *reinterpret_cast<const uint4*>(my_row + min(a16, w - 16));
-      hi = *reinterpret_cast<const uint4*>(my_row + min(a16 + 16, w - 16));
+      const uint8_t *p0 = my_row + min(a16, w - 16), *p1 = my_row + min(a16 + 16, w - 16);
+      lo = WG_CHK(p0, 16, a.data, data_n, "k_alpha_gdiag residuals") ? *reinterpret_cast<const uint4*>(p0)
+                                                                       : make_uint4(0, 0, 0, 0);
+      hi = WG_CHK(p1, 16, a.data, data_n, "k_alpha_gdiag residuals") ? *reinterpret_cast<const uint4*>(p1)
+                                                                       : make_uint4(0, 0, 0, 0);
     };
     // (x < 0 residuals read as 0: every output left of column 0 is then 0,
     // which makes x == 0's left = top_left = top rule hold with no select)
@@ -491,9 +504,12 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
     // before the launch, k_alpha_row0_granules)
     auto ld_up = [&](int s0, uint64_t U[5]) {
 #pragma unroll
-      for (int t = 0; t < 5; t++)
-        U[t] = __hip_atomic_load(hand_above + min(max((s0 >> 2) - 1 + t, 0), gw - 1), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+      for (int t = 0; t < 5; t++) {
+        const uint64_t* g = hand_above + min(max((s0 >> 2) - 1 + t, 0), gw - 1);
+        U[t] = WG_CHK(g, 8, a.hand, hand_n, "k_alpha_gdiag hand load")
+                   ? __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : 0ull;
+      }
     };
     // Prefetch three chunks ahead in three register sets that the unrolled
     // chunk loop rotates by role, never by copying (a copy of a register a
@@ -518,7 +534,7 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
     // m + 1) into R and refills raw with chunk m + 4 and Uc with chunk m + 3
     auto chunk = [&](int m, uint64_t (&Uc)[5], uint4 (&raw)[2]) {
       const int s0 = m * GD_CH;
-      if ((s0 & 63) == 0 && s0 >= 128 && live) gd_store_block(my_ring, my_row, s0 - 128, w);  // every lane is past it
+      if ((s0 & 63) == 0 && s0 >= 128 && live) gd_store_block(my_ring, my_row, s0 - 128, w, a.data, data_n);  // every lane is past it
       {  // the row above: re-poll the granules whose tag is still clear
         bool ready = true;
 #pragma unroll
@@ -588,7 +604,7 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
 #pragma unroll
         for (int j = 0; j < GD_CH / 4; j++) {
           const int g = pub + j;
-          if (g < done && lane == last_lane) {
+          if (g < done && lane == last_lane && WG_CHK(hand_mine + g, 8, a.hand, hand_n, "k_alpha_gdiag hand store")) {
             const uint32_t px = *reinterpret_cast<const uint32_t*>(my_ring + ((4 * g) & 127));
             __hip_atomic_store(hand_mine + g, 1ull << 32 | px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
@@ -612,8 +628,8 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
     // the last two 64-column blocks (or one) have not been stored yet
     const int chunks = (w + 63) >> 6;
     if (live) {
-      if (chunks >= 2) gd_store_block(my_ring, my_row, (chunks - 2) * 64, w);
-      gd_store_block(my_ring, my_row, (chunks - 1) * 64, w);
+      if (chunks >= 2) gd_store_block(my_ring, my_row, (chunks - 2) * 64, w, a.data, data_n);
+      gd_store_block(my_ring, my_row, (chunks - 1) * 64, w, a.data, data_n);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // the ring is reused by the next band this wave dequeues

@@ -798,6 +798,10 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
   const int ys = 16 * mbw, uvs = 8 * mbw;
   const bool luma_only = a.filter_type == 1;
   int* const progress_f = a.progress + (int64_t)a.n_img * mbh;
+  // (WG_BOUNDS) the buffers' extents from wg_decode_frames' shapes
+  [[maybe_unused]] const int64_t n_mb = (int64_t)a.n_img * mbh * mbw, top_size = n_mb / mbh * TOP_BYTES,
+                                 bot_size = n_mb / mbh * BOT_BYTES, prog_size = 8ll * a.n_img * mbh,
+                                 y_size = n_mb * 256, uv_size = n_mb * 64;
   STAMP_DECL;
 
   for (;;) {
@@ -831,8 +835,13 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
       int seen_t = 0;  // lane 0 only: tprog of the row above (in the band)
       const int64_t row_mb0 = ((int64_t)img * mbh + mby) * mbw;
       int4 pf = make_int4(0, 0, 0, 0);
-      if (lane < 48) pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384) + lane);
-      else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + row_mb0)[lane - 48];
+      if (lane < 48) {
+        if (WG_IN(reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384) + lane, 16, a.coeffs, n_mb * 768, &a.ctl[1]))
+          pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + row_mb0 * 384) + lane);
+      } else if (lane < 50) {
+        if (WG_IN(reinterpret_cast<const int4*>(a.mb + row_mb0) + lane - 48, 16, a.mb, n_mb * 32, &a.ctl[1]))
+          pf = reinterpret_cast<const int4*>(a.mb + row_mb0)[lane - 48];
+      }
       for (int mbx = 0; mbx < mbw; mbx++) {
         const int64_t mbi = row_mb0 + mbx;
         const int slot = mbx & (RING - 1), mslot = mbx & (RING_M - 1);
@@ -924,15 +933,15 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         if (!from_lds && mby > 0) {
           const uint8_t* tc = top + mbx * TOP_BYTES;
           if (lane >= 48 && lane < 52) {
-            const uint64_t w = ld_sc1_64(tc + 8 * (lane - 48));
+            const uint64_t w = WG_IN(tc + 8 * (lane - 48), 8, a.top, top_size, &a.ctl[1]) ? ld_sc1_64(tc + 8 * (lane - 48)) : 0;
             const int k = lane - 48;
             uint8_t* dst = k < 2 ? wb + LY - WG_BPS + 8 * k : (k == 2 ? wb + LU - WG_BPS : wb + LV - WG_BPS);
             *reinterpret_cast<uint64_t*>(dst) = w;
           }
           if (lane == 0) {
             uint32_t tr;
-            if (mbx < mbw - 1) tr = (uint32_t)ld_sc1_64(tc + TOP_BYTES);
-            else tr = 0x01010101u * (uint32_t)(ld_sc1_64(tc + 8) >> 56);
+            if (mbx < mbw - 1) tr = WG_IN(tc + TOP_BYTES, 8, a.top, top_size, &a.ctl[1]) ? (uint32_t)ld_sc1_64(tc + TOP_BYTES) : 0u;
+            else tr = 0x01010101u * (uint32_t)((WG_IN(tc + 8, 8, a.top, top_size, &a.ctl[1]) ? ld_sc1_64(tc + 8) : 0ull) >> 56);
             *reinterpret_cast<uint32_t*>(wb + LY - WG_BPS + 16) = tr;
           }
         } else if (mby == 0) {
@@ -942,8 +951,13 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         }
         lds_sync();
         if (mbx + 1 < mbw) {  // prefetch the next MB
-          if (lane < 48) pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384) + lane);
-          else if (lane < 50) pf = reinterpret_cast<const int4*>(a.mb + mbi + 1)[lane - 48];
+          if (lane < 48) {
+            if (WG_IN(reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384) + lane, 16, a.coeffs, n_mb * 768, &a.ctl[1]))
+              pf = ld_stream(reinterpret_cast<const int4*>(a.coeffs + (mbi + 1) * 384) + lane);
+          } else if (lane < 50) {
+            if (WG_IN(reinterpret_cast<const int4*>(a.mb + mbi + 1) + lane - 48, 16, a.mb, n_mb * 32, &a.ctl[1]))
+              pf = reinterpret_cast<const int4*>(a.mb + mbi + 1)[lane - 48];
+          }
         }
         const int is_i4 = w6 & 0xff, uv_mode = (w6 >> 8) & 0xff;
         // replicate the top-right down to rows 3, 7, 11 (:155-160) where it is
@@ -998,7 +1012,8 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                     v = seen;  // (unused in the band)
                   } else {
                     v = seen < mbx + 2 ? wait_progress<true>(prog_above, mbx + 2, &a.ctl[1], mbw, a.diag) : seen;
-                    tr = (uint32_t)ld_sc1_64(top + (mbx + 1) * TOP_BYTES);
+                    tr = WG_IN(top + (mbx + 1) * TOP_BYTES, 8, a.top, top_size, &a.ctl[1])
+                             ? (uint32_t)ld_sc1_64(top + (mbx + 1) * TOP_BYTES) : 0u;
                   }
 #pragma unroll
                   for (int k = 0; k < 4; k++) *reinterpret_cast<uint32_t*>(wb + LY + (4 * k - 1) * WG_BPS + 16) = tr;
@@ -1059,7 +1074,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
               const uint64_t u = lds64(wb + LU + 7 * WG_BPS), v = lds64(wb + LV + 7 * WG_BPS);
               w = make_uint4((uint32_t)u, (uint32_t)(u >> 32), (uint32_t)v, (uint32_t)(v >> 32));
             }
-            st_sc1_128(top + mbx * TOP_BYTES + 16 * k, w);
+            if (WG_IN(top + mbx * TOP_BYTES + 16 * k, 16, a.top, top_size, &a.ctl[1])) st_sc1_128(top + mbx * TOP_BYTES + 16 * k, w);
           }
         }
         lds_sync();
@@ -1067,7 +1082,8 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         // ---- publish: LDS for F(y) and R(y+1) in the band; global for the next band ----
         if (!to_lds && mby < mbh - 1) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the top record is out before the flag
-          if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0 && WG_IN(prog_mine, 4, a.progress, prog_size, &a.ctl[1]))
+            __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (lane == 0) __hip_atomic_store(&prog_r[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         STAMP(6);
@@ -1138,7 +1154,10 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         uint64_t cv = 0, bv = 0;
         if (y_lane) yv = *reinterpret_cast<const uint4*>(ms + LY + lane * WG_BPS);
         if (c_lane) cv = lds64(ms + (c_pl ? LV : LU) + c_j * WG_BPS);
-        if (b_lane) bv = from_lds ? lds64(bot_ring[r - 1][slot] + b_src) : ld_sc1_64(bot_img + mbx * BOT_BYTES + b_src);
+        if (b_lane)
+          bv = from_lds ? lds64(bot_ring[r - 1][slot] + b_src)
+                        : (WG_IN(bot_img + mbx * BOT_BYTES + b_src, 8, a.bot, bot_size, &a.ctl[1])
+                               ? ld_sc1_64(bot_img + mbx * BOT_BYTES + b_src) : 0ull);
         const uint32_t w7v = reinterpret_cast<const uint32_t*>(info_ring[r][mslot])[7];
         asm volatile("" ::: "memory");  // (reads above, writes below)
         if (rot) {
@@ -1207,10 +1226,11 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
               const uint64_t a0 = lds64(src), a1 = lds64(src + FC_STRIDE);
               w = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
             }
-            st_sc1_128(bot_img + x * BOT_BYTES + 16 * k, w);
+            if (WG_IN(bot_img + x * BOT_BYTES + 16 * k, 16, a.bot, bot_size, &a.ctl[1])) st_sc1_128(bot_img + x * BOT_BYTES + 16 * k, w);
           }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record is out before the flag
-          if (lane == 0) __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0 && WG_IN(prog_mine, 4, a.progress, prog_size, &a.ctl[1]))
+            __hip_atomic_store(prog_mine, mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         {
           const bool last = mbx == mbw - 1;
@@ -1274,11 +1294,19 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           if (sb)
             bb = lds64(lane < 8 ? fy + (16 + (lane >> 1)) * FY_STRIDE + FY_X0 + 8 * (lane & 1)
                                 : (bpl ? fv : fu) + (8 + brr) * FC_STRIDE + FC_X0);
-          if (sy) *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby + yj) * ys + 16 * yx) = ym;
-          if (sc0) *reinterpret_cast<uint64_t*>(((ci0 >> 3) & 1 ? Vp : Up) + (int64_t)(8 * mby + (ci0 & 7)) * uvs + 8 * cx0) = cm0;
-          if (sc1) *reinterpret_cast<uint64_t*>(((ci1 >> 3) & 1 ? Vp : Up) + (int64_t)(8 * mby + (ci1 & 7)) * uvs + 8 * cx1) = cm1;
-          if (syt) *reinterpret_cast<uint4*>(Yp + (int64_t)(16 * mby - 4 + tr_) * ys + 16 * tx) = yt;
-          if (sct) *reinterpret_cast<uint64_t*>((cpl ? Vp : Up) + (int64_t)(8 * mby - 4 + crr) * uvs + 8 * cx) = ct;
+#define DEC_ST(cond, T, p, v, base, size) \
+  if (cond) {                               \
+    uint8_t* const q_ = (p);                \
+    if (WG_IN(q_, (int)sizeof(T), (base), (size), &a.ctl[1])) *reinterpret_cast<T*>(q_) = (v); \
+  }
+          DEC_ST(sy, uint4, Yp + (int64_t)(16 * mby + yj) * ys + 16 * yx, ym, a.Y, y_size)
+          DEC_ST(sc0, uint64_t, ((ci0 >> 3) & 1 ? Vp : Up) + (int64_t)(8 * mby + (ci0 & 7)) * uvs + 8 * cx0, cm0,
+                 (ci0 >> 3) & 1 ? a.V : a.U, uv_size)
+          DEC_ST(sc1, uint64_t, ((ci1 >> 3) & 1 ? Vp : Up) + (int64_t)(8 * mby + (ci1 & 7)) * uvs + 8 * cx1, cm1,
+                 (ci1 >> 3) & 1 ? a.V : a.U, uv_size)
+          DEC_ST(syt, uint4, Yp + (int64_t)(16 * mby - 4 + tr_) * ys + 16 * tx, yt, a.Y, y_size)
+          DEC_ST(sct, uint64_t, (cpl ? Vp : Up) + (int64_t)(8 * mby - 4 + crr) * uvs + 8 * cx, ct, cpl ? a.V : a.U, uv_size)
+#undef DEC_ST
           if (sb)
             *reinterpret_cast<uint64_t*>(bot_ring[r][slot] + (lane < 8 ? 16 * (lane >> 1) + 8 * (lane & 1) : 64 + 32 * bpl + 8 * brr)) = bb;
         }

@@ -1239,7 +1239,9 @@ WG_IF_ROWTIMES(__device__ unsigned long long g_row_times[16384][4];)
 // An image's four segment tables (4 x 224 B = 56 x 16 B) into LDS
 __device__ __forceinline__ void load_segments(const EncArgs& a, int img, Segment* dst, int lane) {
   const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.segs) + img * a.segs_pitch);
-  if (lane < 56) reinterpret_cast<uint4*>(dst)[lane] = src[lane];
+  if (lane < 56 && WG_CHK(src + lane, 16, a.segs, a.segs_pitch ? a.n_img * a.segs_pitch : 4 * (int64_t)sizeof(Segment),
+                          "k_encode_rows segs"))
+    reinterpret_cast<uint4*>(dst)[lane] = src[lane];
 }
 
 // The barrier of one group of WAVES waves inside a larger workgroup: each
@@ -1439,6 +1441,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
     uint8_t* RU = a.ru + img * a.uv_pitch;
     uint8_t* RV = a.rv + img * a.uv_pitch;
     uint8_t* top = a.top + (int64_t)img * mbw * REC;
+    // (WG_BOUNDS) the buffers' extents from wg_encode_mbs' shapes
+    [[maybe_unused]] const int64_t y_n = a.n_img * a.y_pitch, uv_n = a.n_img * a.uv_pitch,
+                                   top_n = (int64_t)a.n_img * mbw * REC, mb_n = (int64_t)a.n_img * mbw * mbh;
     if (PAIR && isA) load_segments(a, img, s_seg[0], lane);  // (B reads them after the MB's first join barrier)
     // left context (encodeRow :257-282)
     if (lane < 16) s.yout[YOFF - 1 + lane * BPS] = 129;
@@ -1476,7 +1481,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
           const uint32_t want = (uint32_t)mby;  // row mby - 1's tag
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           for (uint32_t it = 0;; it++) {
-            const uint64_t g = lane < n ? ld_granule(rec + 8 * lane) : 0;
+            const uint64_t g =
+                lane < n && WG_CHK(rec + 8 * lane, 8, a.top, top_n, "k_encode_rows record load") ? ld_granule(rec + 8 * lane) : 0;
             w = (uint32_t)g;
             if (__ballot(lane < n && (uint32_t)(g >> 32) != want) == 0) break;
             if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
@@ -1495,7 +1501,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
       uint32_t above = 0;
       if (isA) above = poll_rec(top + mbx * REC, REC_WORDS);
       ESTAMP(1);
-      const int segid = a.segments ? (a.segments[mbi] & 3) : 0;
+      const int segid =
+          a.segments && WG_CHK(a.segments + mbi, 1, a.segments, mb_n, "k_encode_rows segment ids") ? (a.segments[mbi] & 3) : 0;
       const Segment& sg = s_seg[PAIR ? 0 : (LOOSE ? (q & 1) : grp)][segid];
       uint32_t top_nz = 0, top_modes = 0;
       int top_nz_dc = 0;
@@ -1513,7 +1520,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
           const int r = min(lane, hh - 1);
           const uint8_t* src = Y + (int64_t)(y + r) * ys + x;
           if (16 * ((mbx & ~1) + 2) <= a.width) {  // the pair is whole
-            if ((mbx & 1) == 0) {
+            if ((mbx & 1) == 0 && WG_CHK(src, 32, a.y, y_n, "k_encode_rows Y")) {
               stg0 = *reinterpret_cast<const uint4*>(src);
               stg1 = *reinterpret_cast<const uint4*>(src + 16);
             }
@@ -1521,7 +1528,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
             *reinterpret_cast<uint2*>(s.yin + YOFF + lane * BPS) = make_uint2(v.x, v.y);
             *reinterpret_cast<uint2*>(s.yin + YOFF + lane * BPS + 8) = make_uint2(v.z, v.w);
           } else {
-            for (int c = 0; c < 16; c++) s.yin[YOFF + lane * BPS + c] = src[min(c, ww - 1)];
+            for (int c = 0; c < 16; c++)
+              s.yin[YOFF + lane * BPS + c] = WG_CHK(src + min(c, ww - 1), 1, a.y, y_n, "k_encode_rows Y") ? src[min(c, ww - 1)] : 0;
           }
         } else if (lane < 32) {
           const int k = lane - 16, pl = k >> 3, j = k & 7;
@@ -1529,7 +1537,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
           const int r = min(j, uvh - 1);
           const uint8_t* P = (pl ? V : U) + (int64_t)(8 * mby + r) * uvs + 8 * mbx;
           if (16 * ((mbx & ~3) + 4) <= a.width) {  // the quad is whole (rows 8-B aligned: 8-B loads)
-            if ((mbx & 3) == 0) {
+            if ((mbx & 3) == 0 && WG_CHK(P, 32, pl ? a.v : a.u, uv_n, "k_encode_rows UV")) {
               const uint2 p0 = reinterpret_cast<const uint2*>(P)[0], p1 = reinterpret_cast<const uint2*>(P)[1];
               const uint2 p2 = reinterpret_cast<const uint2*>(P)[2], p3 = reinterpret_cast<const uint2*>(P)[3];
               stg0 = make_uint4(p0.x, p0.y, p1.x, p1.y);
@@ -1539,7 +1547,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
             *reinterpret_cast<uint2*>(s.yin + (pl ? VOFF : UOFF) + j * BPS) =
                 (mbx & 1) ? make_uint2(h.z, h.w) : make_uint2(h.x, h.y);
           } else {
-            for (int c = 0; c < 8; c++) s.yin[(pl ? VOFF : UOFF) + j * BPS + c] = P[min(c, uvw - 1)];
+            for (int c = 0; c < 8; c++)
+              s.yin[(pl ? VOFF : UOFF) + j * BPS + c] =
+                  WG_CHK(P + min(c, uvw - 1), 1, pl ? a.v : a.u, uv_n, "k_encode_rows UV") ? P[min(c, uvw - 1)] : 0;
           }
         }
       }
@@ -2447,7 +2457,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
       left_nz = out_l;
       // hand-off record for the row below: lane i publishes word i with the
       // row's tag in one 64-bit store (no drain, no flag)
-      if (mby < mbh - 1 && lane < REC_WORDS) {
+      if (mby < mbh - 1 && lane < REC_WORDS &&
+          WG_CHK(top + mbx * REC + 8 * lane, 8, a.top, top_n, "k_encode_rows record store")) {
         uint32_t v;
         if (lane < 8) {
           const int so = lane < 4 ? YOFF + 15 * BPS + 4 * lane
@@ -2483,7 +2494,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
         // the whole 864-B record: 54 lanes x 16 B, one store instruction
         uint4* dst = reinterpret_cast<uint4*>(o);
         const uint4* srcv = reinterpret_cast<const uint4*>(s.coeffs);
-        if (lane < 54) dst[lane] = srcv[lane];
+        if (lane < 54 && WG_CHK(dst + lane, 16, a.out, mb_n * (int64_t)sizeof(MbEnc), "k_encode_rows MBEncInfo"))
+          dst[lane] = srcv[lane];
       }
       {
         const int x = 16 * mbx, y = 16 * mby;
@@ -2493,7 +2505,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
         // go out back to back with the last one's, so L2 never writes a
         // partial sector back (a 16-B / 8-B piece per MB was written back
         // before the next MB's piece arrived).
-        if (lane < hy) {
+        if (lane < hy && WG_CHK(RY + (int64_t)(y + lane) * ys + x - (wy == 16 && 16 * ((mbx & ~1) + 2) <= a.width ? 16 * (mbx & 1) : 0),
+                                wy == 16 && 16 * ((mbx & ~1) + 2) <= a.width && (mbx & 1) ? 32 : 16, a.ry, y_n,
+                                "k_encode_rows recon Y")) {
           const uint8_t* srow = s.yout + YOFF + lane * BPS;  // 8-B aligned in LDS
           uint8_t* drow = RY + (int64_t)(y + lane) * ys + x;
           if (wy == 16) {  // one 16-B store per row
@@ -2513,7 +2527,11 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
             for (int c = 0; c < wy; c++) drow[c] = srow[c];
           }
         }
-        if (lane >= 16 && lane < 32) {  // U / V rows: 8 B each
+        if (lane >= 16 && lane < 32 &&
+            WG_CHK(((lane - 16) >> 3 ? RV : RU) + (int64_t)(8 * mby + ((lane - 16) & 7)) * uvs + 8 * (mbx & ~3), 8,
+                   (lane - 16) >> 3 ? a.rv : a.ru, uv_n, "k_encode_rows recon UV") &&
+            WG_CHK(((lane - 16) >> 3 ? RV : RU) + (int64_t)(8 * mby + ((lane - 16) & 7)) * uvs + 8 * mbx, 8,
+                   (lane - 16) >> 3 ? a.rv : a.ru, uv_n, "k_encode_rows recon UV")) {  // U / V rows: 8 B each
           const int k = lane - 16, pl = k >> 3, j = k & 7;
           uint2* drow = reinterpret_cast<uint2*>((pl ? RV : RU) + (int64_t)(8 * mby + j) * uvs + 8 * mbx);
           const uint2 v = *reinterpret_cast<const uint2*>(s.yout + (pl ? VOFF : UOFF) + j * BPS);

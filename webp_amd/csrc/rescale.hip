@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "wg_common.h"
+#include "wg_instr.h"
 
 namespace {
 
@@ -59,7 +60,7 @@ __host__ __device__ inline uint32_t mult_fix(uint32_t x, uint32_t y) {
 }
 inline uint32_t frac_of(int64_t x, int64_t y) { return y == 0 ? 0u : (uint32_t)(((uint64_t)x << kRFix) / (uint64_t)y); }
 
-size_t plan_bytes(int dw, int dh) { return sizeof(Header) + sizeof(XEntry) * (size_t)dw + sizeof(YEntry) * (size_t)dh; }
+__host__ __device__ inline size_t plan_bytes(int dw, int dh) { return sizeof(Header) + sizeof(XEntry) * (size_t)dw + sizeof(YEntry) * (size_t)dh; }
 
 // Walks RescalerInit / ImportRow / ExportRow (rescale.go:63-257) over sizes only.
 void build_plan(int sw, int sh, int dw, int dh, std::vector<uint8_t>& out) {
@@ -140,18 +141,22 @@ void build_plan(int sw, int sh, int dw, int dh, std::vector<uint8_t>& out) {
 }
 
 // FRow[x] of one source row (ImportRow's horizontal half)
+// (sb / sn: the source buffer and its extent, for WG_BOUNDS builds)
 __device__ __forceinline__ uint32_t frow_at(const uint8_t* __restrict__ row, const XEntry& e, int x_expand,
-                                            int32_t x_add, int32_t x_sub, uint32_t fx_scale) {
+                                            int32_t x_add, int32_t x_sub, uint32_t fx_scale, const uint8_t* sb,
+                                            int64_t sn) {
   if (x_expand) {
-    const uint32_t left = row[e.a], right = row[e.b];
+    const uint32_t left = WG_CHK(row + e.a, 1, sb, sn, "k_rescale src") ? row[e.a] : 0;
+    const uint32_t right = WG_CHK(row + e.b, 1, sb, sn, "k_rescale src") ? row[e.b] : 0;
     return right * (uint32_t)x_add + (left - right) * (uint32_t)e.c;
   }
   uint32_t sum = 0;
-  if (e.prev_idx >= 0 && e.prev_negacc != 0) sum = mult_fix((uint32_t)row[e.prev_idx] * e.prev_negacc, fx_scale);
+  if (e.prev_idx >= 0 && e.prev_negacc != 0 && WG_CHK(row + e.prev_idx, 1, sb, sn, "k_rescale src"))
+    sum = mult_fix((uint32_t)row[e.prev_idx] * e.prev_negacc, fx_scale);
   uint32_t base = 0;
   const uint8_t* p = row + e.a;
   for (int i = 0; i < e.b; i++) {
-    base = p[i];
+    base = WG_CHK(p + i, 1, sb, sn, "k_rescale src") ? p[i] : 0;
     sum += base;
   }
   sum += base * (uint32_t)e.c;
@@ -165,16 +170,22 @@ __global__ void __launch_bounds__(256) k_rescale(const uint8_t* __restrict__ pla
   const int x = blockIdx.x * 256 + threadIdx.x;
   const int y = blockIdx.y;
   if (x >= hd.dw || y >= hd.rows) return;
+  // (WG_BOUNDS) the extents the entry point's shapes give every buffer
+  [[maybe_unused]] const int64_t plan_n = (int64_t)plan_bytes(hd.dw, hd.dh), src_n = (int64_t)gridDim.z * src_pitch,
+                                 dst_n = (int64_t)gridDim.z * dst_pitch;
+  (void)WG_CHK(plan + sizeof(Header) + sizeof(XEntry) * (size_t)x, sizeof(XEntry), plan, plan_n, "k_rescale xtab");
+  (void)WG_CHK(plan + sizeof(Header) + sizeof(XEntry) * (size_t)hd.dw + sizeof(YEntry) * (size_t)y, sizeof(YEntry),
+               plan, plan_n, "k_rescale ytab");
   const XEntry e = reinterpret_cast<const XEntry*>(plan + sizeof(Header))[x];
   const YEntry ye = reinterpret_cast<const YEntry*>(plan + sizeof(Header) + sizeof(XEntry) * (size_t)hd.dw)[y];
   const uint8_t* img = src + (int64_t)blockIdx.z * src_pitch;
   uint32_t v;
   if (hd.y_expand) {  // rescalerExportRowExpand (:203-231)
-    const uint32_t f = frow_at(img + ye.s0 * src_stride, e, hd.x_expand, hd.x_add, hd.x_sub, hd.fx_scale);
+    const uint32_t f = frow_at(img + ye.s0 * src_stride, e, hd.x_expand, hd.x_add, hd.x_sub, hd.fx_scale, src, src_n);
     uint32_t j = f;
     if (ye.b != 0) {
       const uint32_t ir = ye.s1 < 0 ? 0u : frow_at(img + ye.s1 * src_stride, e, hd.x_expand, hd.x_add, hd.x_sub,
-                                                  hd.fx_scale);
+                                                  hd.fx_scale, src, src_n);
       const uint32_t a = (uint32_t)((((uint64_t)1) << kRFix) - ye.b);
       const uint64_t i = (uint64_t)a * f + (uint64_t)ye.b * ir;
       j = (uint32_t)((i + ((uint64_t)1 << (kRFix - 1))) >> kRFix);
@@ -183,10 +194,11 @@ __global__ void __launch_bounds__(256) k_rescale(const uint8_t* __restrict__ pla
   } else {  // IRow = sum of FRow since the previous export; rescalerExportRowShrink (:235-257)
     uint32_t acc = 0;
     for (int s = ye.s0; s <= ye.s1; s++)
-      acc += frow_at(img + s * src_stride, e, hd.x_expand, hd.x_add, hd.x_sub, hd.fx_scale);
+      acc += frow_at(img + s * src_stride, e, hd.x_expand, hd.x_add, hd.x_sub, hd.fx_scale, src, src_n);
     v = mult_fix(acc, hd.fxy_scale);
   }
-  dst[(int64_t)blockIdx.z * dst_pitch + y * dst_stride + x] = (uint8_t)(v > 255u ? 255u : v);
+  uint8_t* const d = dst + (int64_t)blockIdx.z * dst_pitch + y * dst_stride + x;
+  if (WG_CHK(d, 1, dst, dst_n, "k_rescale dst")) *d = (uint8_t)(v > 255u ? 255u : v);
 }
 
 }  // namespace

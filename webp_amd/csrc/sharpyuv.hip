@@ -33,6 +33,7 @@
 #include <algorithm>
 
 #include "wg_common.h"
+#include "wg_instr.h"
 
 namespace {
 
@@ -84,6 +85,8 @@ struct SharpArgs {
   int* prog;       // [n_img][4] row pairs finished per iteration
   int* iters;      // [n_img] iterations the reference runs (-1: a dependency wait timed out)
   int n_img;
+  const uint8_t* work0;  // (WG_BOUNDS) the whole work buffer and its size
+  int64_t work_n;
 };
 
 __device__ __forceinline__ void load_tabs(SharpTabs& dst, const SharpTabs* src) {
@@ -112,9 +115,10 @@ __global__ __launch_bounds__(256) void k_sharp_init(SharpArgs a, int n_img) {
     for (int k = 0; k < 2; k++) {
       const int x = min(2 * i + k, a.width - 1);  // odd width: replicate the last pixel
       const uint8_t* px = rgb + (int64_t)row * a.rgb_stride + 3 * x;
-      c[r][k][0] = px[0] << SFIX;
-      c[r][k][1] = px[1] << SFIX;
-      c[r][k][2] = px[2] << SFIX;
+      const bool in = WG_CHK(px, 3, a.rgb, (int64_t)n_img * a.rgb_pitch, "k_sharp_init rgb");
+      c[r][k][0] = in ? px[0] << SFIX : 0;
+      c[r][k][1] = in ? px[1] << SFIX : 0;
+      c[r][k][2] = in ? px[2] << SFIX : 0;
     }
   }
   uint16_t* by = a.best_y + img * a.img_y;
@@ -123,6 +127,9 @@ __global__ __launch_bounds__(256) void k_sharp_init(SharpArgs a, int n_img) {
   for (int r = 0; r < 2; r++)
     for (int k = 0; k < 2; k++) {
       const int64_t o = (int64_t)(j + r) * a.w + 2 * i + k;
+      if (!WG_CHK(by + o, 2, a.work0, a.work_n, "k_sharp_init best_y") ||
+          !WG_CHK(ty + o, 2, a.work0, a.work_n, "k_sharp_init target_y"))
+        continue;
       by[o] = (uint16_t)gray(c[r][k][0], c[r][k][1], c[r][k][2]);  // storeGray
       for (int ch = 0; ch < 3; ch++) lin[r][k][ch] = to_linear(t.g2l, c[r][k][ch]);
       ty[o] = (uint16_t)from_lin<LUT>(t.l2g, a.lut, a.lut_n, (uint32_t)gray(lin[r][k][0], lin[r][k][1], lin[r][k][2]));  // updateW
@@ -135,8 +142,8 @@ __global__ __launch_bounds__(256) void k_sharp_init(SharpArgs a, int n_img) {
   int16_t* buv = a.best_uv + img * a.img_uv + (int64_t)ju * a.uv_rs;
   for (int ch = 0; ch < 3; ch++) {
     const int16_t d = (int16_t)(rgbv[ch] - gv);
-    tuv[ch * a.uvw + i] = d;
-    buv[ch * a.uvw + i] = d;
+    if (WG_CHK(tuv + ch * a.uvw + i, 2, a.work0, a.work_n, "k_sharp_init target_uv")) tuv[ch * a.uvw + i] = d;
+    if (WG_CHK(buv + ch * a.uvw + i, 2, a.work0, a.work_n, "k_sharp_init best_uv")) buv[ch * a.uvw + i] = d;
   }
 }
 
@@ -267,9 +274,17 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
 
   // wait (the whole wave, on one wave-uniform address) until band bb of
   // iteration ii has finished `need` row pairs; the progress seen (uvh for a band that does not exist)
+  // (WG_BOUNDS) every work-buffer access of the walk checked against the buffer
+  auto ld_w = [&](const uint32_t* p, const char* site) -> uint32_t {
+    return WG_CHK(p, 4, a.work0, a.work_n, site) ? ld_sc1(p) : 0u;
+  };
+  auto ld_t = [&](const uint32_t* p, const char* site) -> uint32_t {
+    return WG_CHK(p, 4, a.work0, a.work_n, site) ? *p : 0u;
+  };
   auto wait_for = [&](int ii, int bb, int need) -> int {
     if (bb < 0 || bb >= nb || timed_out) return uvh;
     const int* p = prog_img + ii * nb + bb;
+    if (!WG_CHK(p, 4, a.work0, a.work_n, "k_sharp_wave prog load")) return uvh;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t k = 0;; k++) {
       const int v = __builtin_amdgcn_readfirstlane((int)ld_sc1(p));
@@ -330,7 +345,7 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     Row r;
     const uint32_t ub = (uint32_t)min(row, uvh - 1) * uv_row_bytes;  // clamped: the last row pair's next is its cur
 #pragma unroll
-    for (int ch = 0; ch < 3; ch++) r.v[ch] = ld_sc1(at(in_uv, ub, lo_uv[ch]));
+    for (int ch = 0; ch < 3; ch++) r.v[ch] = ld_w(at(in_uv, ub, lo_uv[ch]), "k_sharp_wave in_uv");
     return r;
   };
   // this role's luma row of a row pair: the input state's and the target's
@@ -342,12 +357,12 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     In r;
     const int jc = min(jp, uvh - 1);
     const uint32_t yb = (uint32_t)(2 * jc + ROLE) * y_row_bytes;
-    r.y = ld_sc1(at(in_y, yb, lo_y));
-    r.ty = *at(ty, yb, lo_y);
+    r.y = ld_w(at(in_y, yb, lo_y), "k_sharp_wave in_y");
+    r.ty = ld_t(at(ty, yb, lo_y), "k_sharp_wave target_y");
     if constexpr (ROLE == 0) {
       const uint32_t ub = (uint32_t)jc * uv_row_bytes;
 #pragma unroll
-      for (int ch = 0; ch < 3; ch++) r.tuv[ch] = *at(tuv, ub, lo_uv[ch]);
+      for (int ch = 0; ch < 3; ch++) r.tuv[ch] = ld_t(at(tuv, ub, lo_uv[ch]), "k_sharp_wave target_uv");
     }
     return r;
   };
@@ -378,7 +393,7 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
         if (act && !own) {
           const uint32_t ub = (uint32_t)(ju - 1) * uv_row_bytes;
 #pragma unroll
-          for (int ch = 0; ch < 3; ch++) P.v[ch] = ld_sc1(at(out_uv, ub, lo_uv[ch]));
+          for (int ch = 0; ch < 3; ch++) P.v[ch] = ld_w(at(out_uv, ub, lo_uv[ch]), "k_sharp_wave halo");
         }
       }
     } else {
@@ -444,7 +459,7 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
       // hand A this row pair's linear sums, then store the luma row
       x.sum[ju % XD][lane] = make_uint4(lin[0][0] + lin[1][0], lin[0][1] + lin[1][1], lin[0][2] + lin[1][2], 0u);
       if (lane == 0) lds_release(&x.prog_b, ju + 1);
-      if (own) st_sc1(oy + lo_y, ynew);
+      if (own && WG_CHK(oy + lo_y, 4, a.work0, a.work_n, "k_sharp_wave out_y")) st_sc1(oy + lo_y, ynew);
       if ((ju + 1) % WB_PUB == 0 || ju + 1 == uvh) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) lds_release(&x.drained_b, ju + 1);
@@ -474,8 +489,9 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
       if (own) {
         uint8_t* ob = reinterpret_cast<uint8_t*>(out_uv) + (uint32_t)ju * uv_row_bytes;
 #pragma unroll
-        for (int ch = 0; ch < 3; ch++) st_sc1_16(ob + st_uv[ch], (uint16_t)upd[ch]);
-        st_sc1(oy + lo_y, ynew);
+        for (int ch = 0; ch < 3; ch++)
+          if (WG_CHK(ob + st_uv[ch], 2, a.work0, a.work_n, "k_sharp_wave out_uv")) st_sc1_16(ob + st_uv[ch], (uint16_t)upd[ch]);
+        if (WG_CHK(oy + lo_y, 4, a.work0, a.work_n, "k_sharp_wave out_y")) st_sc1(oy + lo_y, ynew);
       }
 #pragma unroll
       for (int ch = 0; ch < 3; ch++) P.v[ch] = (uint32_t)(uint16_t)upd[ch] << hs[ch];  // prev <- the updated cur (in its half)
@@ -485,7 +501,7 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
         // WB_PUB steps)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wait_lds(&x.drained_b, ju + 1);
-        if (lane == 0) st_sc1(prog_out, (uint32_t)(ju + 1));
+        if (lane == 0 && WG_CHK(prog_out, 4, a.work0, a.work_n, "k_sharp_wave prog store")) st_sc1(prog_out, (uint32_t)(ju + 1));
       }
     }
   };
@@ -500,7 +516,8 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
   // (:254-263); k_sharp_final applies the exit rule
   unsigned long long sm = own ? my_sum : 0u;
   for (int off = 32; off > 0; off >>= 1) sm += __shfl_down(sm, off, 64);
-  if (lane == 0) {
+  if (lane == 0 && WG_CHK(a.sums + img * 4 + it, 8, a.work0, a.work_n, "k_sharp_wave sums") &&
+      WG_CHK(a.iters + img, 4, a.work0, a.work_n, "k_sharp_wave iters")) {
     atomicAdd(reinterpret_cast<unsigned long long*>(a.sums + img * 4 + it), sm);
     if (timed_out) a.iters[img] = -1;
   }
@@ -546,6 +563,8 @@ struct FinalArgs {
   int64_t img_y, state_y, img_uv, state_uv, out_y_pitch, out_uv_pitch;
   int y_stride, uv_stride, width, height, w, uvw, uvh, uv_rs;
   int m[12];
+  const uint8_t* work0;  // (WG_BOUNDS) the work buffer and its size
+  int64_t work_n;
 };
 
 // convertWRGBToYUV (:390-432) of the state the reference stops at: thread
@@ -564,6 +583,14 @@ __global__ __launch_bounds__(256) void k_sharp_final(FinalArgs a, int n_img) {
   constexpr int SHIFT = 16 + SFIX;
   const int64_t rounder = (int64_t)1 << (SHIFT - 1);
   const int uvi = (j / 2) * a.uv_rs + (i >> 1);
+  if (!WG_CHK(by + (int64_t)j * a.w + i, 2, a.work0, a.work_n, "k_sharp_final best_y") ||
+      !WG_CHK(buv + uvi, 2, a.work0, a.work_n, "k_sharp_final best_uv") ||
+      !WG_CHK(buv + uvi + 2 * a.uvw, 2, a.work0, a.work_n, "k_sharp_final best_uv") ||
+      !WG_CHK(a.y + img * a.out_y_pitch + (int64_t)j * a.y_stride + i, 1, a.y, (int64_t)n_img * a.out_y_pitch,
+              "k_sharp_final y") ||
+      !WG_CHK(a.u + img * a.out_uv_pitch + (int64_t)(j >> 1) * a.uv_stride + (i >> 1), 1, a.u,
+              (int64_t)n_img * a.out_uv_pitch, "k_sharp_final uv"))
+    return;
   const int64_t wv = by[(int64_t)j * a.w + i];
   const int64_t r = buv[uvi] + wv, g = buv[uvi + a.uvw] + wv, b = buv[uvi + 2 * a.uvw] + wv;
   const int64_t yv = (int64_t)a.m[0] * r + (int64_t)a.m[1] * g + (int64_t)a.m[2] * b + ((int64_t)a.m[3] << SFIX) + rounder;
@@ -731,6 +758,8 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
   a.iters = reinterpret_cast<int*>(tail + (size_t)n_images * 32);
   a.prog = a.iters + n_images;
   a.n_img = n_images;
+  a.work0 = base;
+  a.work_n = (int64_t)wg_sharpyuv_work_bytes(width, height, n_images);
   if (hipMemsetAsync(tail, 0, (size_t)n_images * (32 + 4 + 16 * nb), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(sharpyuv)");
   const int64_t cells = (int64_t)uvw * uvh * n_images;
@@ -790,6 +819,8 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
   f.uvh = uvh;
   f.uv_rs = L.uv_rs;
   for (int k = 0; k < 12; k++) f.m[k] = matrix_host[k];
+  f.work0 = a.work0;
+  f.work_n = a.work_n;
   const int64_t px = (int64_t)width * height * n_images;
   hipLaunchKernelGGL(k_sharp_final, dim3(wg::blocks_for(px, 256)), dim3(256), 0, s, f, n_images);
   return wg::check_launch("k_sharp_final");

@@ -21,6 +21,7 @@
 // (N = 256) use 32-bit products where they fit.  Partial sums per (16-row
 // tile row, strip) are reduced by a second, fixed-order pass.
 #include "wg_common.h"
+#include "wg_instr.h"
 #include "wg_dsp.h"
 
 #include <cstdlib>
@@ -108,10 +109,15 @@ __global__ __launch_bounds__(64) void k_plane_ssim(const SsimArgs p) {
   // y1 + 2: clamped to the rows the band owns with its halo, which a band
   // buffer of wg_plane_ssim_devices holds; their outputs are not kept)
   const int r_lo = max(y0 - 3, 0), r_hi = min(y1 + 2, p.h - 1);
+  // (WG_BOUNDS) the rows the launch's band owns with its halo
+  [[maybe_unused]] const int band_lo = max(p.ty0 * TILE - 3, 0), band_hi = min((p.ty0 + p.tiles_y) * TILE + 3, p.h);
   auto load = [&](int r, uint32_t& va, uint32_t& vb) {
     const int rc = min(max(r, r_lo), r_hi);
-    va = A[(uint32_t)(rc * p.a_stride) + xo];
-    vb = B[(uint32_t)(rc * p.b_stride) + xo];
+    const uint8_t *qa = A + (uint32_t)(rc * p.a_stride) + xo, *qb = B + (uint32_t)(rc * p.b_stride) + xo;
+    va = WG_CHK(qa, 1, A + (int64_t)band_lo * p.a_stride, (int64_t)(band_hi - band_lo) * p.a_stride, "k_plane_ssim a")
+             ? *qa : 0u;
+    vb = WG_CHK(qb, 1, B + (int64_t)band_lo * p.b_stride, (int64_t)(band_hi - band_lo) * p.b_stride, "k_plane_ssim b")
+             ? *qb : 0u;
   };
   // running sums: Bv = box4 of the rows' stats, Tv = box4 of Bv = the vertical
   // hat.  Stat 0 packs x | y << 16: every partial sum of x or y stays below
@@ -170,7 +176,9 @@ __global__ __launch_bounds__(64) void k_plane_ssim(const SsimArgs p) {
       if (((y + 1) % TILE) == 0 || y + 1 == y1) {  // the tile row is complete
         const double tot = wave_sum(out_lane ? acc : 0.0);
         acc = 0.0;
-        if (lane == 0) p.partial[((int64_t)img * p.tiles_y + (y / TILE - p.ty0)) * p.strips + s] = tot;
+        double* const q = p.partial + ((int64_t)img * p.tiles_y + (y / TILE - p.ty0)) * p.strips + s;
+        if (lane == 0 && WG_CHK(q, 8, p.partial, 8ll * (blockIdx.x / per + 1) * p.tiles_y * p.strips, "k_plane_ssim partial"))
+          *q = tot;
       }
     }
   };

@@ -224,6 +224,11 @@ __global__ __launch_bounds__(64 * SEL_WAVES) void k_vp8l_select(SelArgs a) {
   const int tw = x1 - x0, rows = (y1 - y0 + ystep - 1) / ystep;
   const uint32_t count = (uint32_t)(tw * rows);
   uint32_t* hg = hist[wave];
+  // (WG_BOUNDS) the rows this launch may read: its band's and the one above
+  [[maybe_unused]] const int r_lo = max(a.ty0 * ts - 1, 0), r_hi = min((a.ty0 + a.band_tiles / a.tiles_x) * ts, h);
+  [[maybe_unused]] const uint32_t* band_px = argb + (int64_t)r_lo * w;
+  [[maybe_unused]] const int64_t band_n = (int64_t)(r_hi - r_lo) * w * 4;
+  auto px = [&](const uint32_t* p) { return WG_CHK(p, 4, band_px, band_n, "k_vp8l_select argb") ? *p : 0u; };
 
   for (int mode = wave; mode < a.max_mode; mode += SEL_WAVES) {
     for (int i = lane; i < 4 * 256; i += 64) hg[i] = 0;
@@ -232,14 +237,14 @@ __global__ __launch_bounds__(64 * SEL_WAVES) void k_vp8l_select(SelArgs a) {
       const int x = x0 + i % tw, y = y0 + (i / tw) * ystep;
       const uint32_t* row = argb + (int64_t)y * w;
       uint32_t l = 0, t = 0, tr = 0, tl = 0;
-      if (x > 0) l = row[x - 1];
+      if (x > 0) l = px(row + x - 1);
       if (y > 0) {
         const uint32_t* prev = row - w;
-        t = prev[x];
-        if (x > 0) tl = prev[x - 1];
-        tr = (x < w - 1) ? prev[x + 1] : t;
+        t = px(prev + x);
+        if (x > 0) tl = px(prev + x - 1);
+        tr = (x < w - 1) ? px(prev + x + 1) : t;
       }
-      const uint32_t res = sub_pixels(row[x], predict(mode, l, t, tr, tl));
+      const uint32_t res = sub_pixels(px(row + x), predict(mode, l, t, tr, tl));
       atomicAdd(&hg[0 * 256 + ((res >> 24) & 0xff)], 1u);
       atomicAdd(&hg[1 * 256 + ((res >> 16) & 0xff)], 1u);
       atomicAdd(&hg[2 * 256 + ((res >> 8) & 0xff)], 1u);
@@ -349,6 +354,10 @@ __global__ __launch_bounds__(128) void k_vp8l_select_q3(SelArgs a, int64_t total
   const int x1 = min(x0 + ts, w), y1 = min(y0 + ts, h);
   const int ystep = (y1 - y0 > 16) ? 2 : 1;
   const int tw = x1 - x0, rows = (y1 - y0 + ystep - 1) / ystep;
+  // (WG_BOUNDS) the rows this launch may read: its band's and the one above
+  [[maybe_unused]] const int r_lo = max(a.ty0 * ts - 1, 0), r_hi = min((a.ty0 + a.band_tiles / a.tiles_x) * ts, h);
+  [[maybe_unused]] const uint32_t* band_px = argb + (int64_t)r_lo * w;
+  [[maybe_unused]] const int64_t band_n = (int64_t)(r_hi - r_lo) * w * 4;
   {
     // staged rows y0 - 1 .. y1 - 1 with estimateEntropy's edge values;
     // i / scols by a multiply (exact: i < 2^16 / scols)
@@ -365,7 +374,8 @@ __global__ __launch_bounds__(128) void k_vp8l_select_q3(SelArgs a, int64_t total
       at[j] = rr * SQ_SW + cc;
       if (i < n) {
         const int y = y0 - 1 + rr, x = x0 - 1 + cc;
-        if (y >= 0 && x >= 0) v[j] = argb[(int64_t)y * w + min(x, w - 1)];
+        const uint32_t* p = argb + (int64_t)y * w + min(x, w - 1);
+        if (y >= 0 && x >= 0 && WG_CHK(p, 4, band_px, band_n, "k_vp8l_select_q3 argb")) v[j] = *p;
       }
     }
     for (int i = threadIdx.x; i < SQ_LUT; i += 128) lut[i] = a.lut[i];
@@ -454,7 +464,10 @@ __global__ __launch_bounds__(128) void k_vp8l_select_q3(SelArgs a, int64_t total
       best = mm;
     }
   }
-  if (lane == 0) a.modes[(int64_t)img * a.tiles_x * a.tiles_y + tile] = ((uint32_t)best << 8) | ARGB_BLACK;
+  uint32_t* const mp = a.modes + (int64_t)img * a.tiles_x * a.tiles_y + tile;
+  if (lane == 0 && WG_CHK(mp, 4, a.modes + (int64_t)img * a.tiles_x * a.tiles_y + a.ty0 * a.tiles_x, 4ll * a.band_tiles,
+                          "k_vp8l_select_q3 modes"))
+    *mp = ((uint32_t)best << 8) | ARGB_BLACK;
 }
 
 struct ResArgs {
@@ -477,19 +490,29 @@ __global__ __launch_bounds__(256) void k_vp8l_residual(ResArgs a) {
   const int y = a.y0 + (int)blockIdx.y, img = (int)blockIdx.z;
   const int64_t p = (int64_t)y * a.width + x;
   const uint32_t* cur = a.argb + img * a.pitch + (int64_t)y * a.width;
+  // (WG_BOUNDS) reads: the launch's rows and the one above; writes: its rows;
+  // modes: its tile rows
+  [[maybe_unused]] const int r_lo = max(a.y0 - 1, 0);
+  [[maybe_unused]] const uint32_t* rows_px = a.argb + img * a.pitch + (int64_t)r_lo * a.width;
+  [[maybe_unused]] const int64_t rows_n = (int64_t)(a.y0 + a.rows - r_lo) * a.width * 4;
+  auto px = [&](const uint32_t* q) { return WG_CHK(q, 4, rows_px, rows_n, "k_vp8l_residual argb") ? *q : 0u; };
   uint32_t pred;
   if (y == 0) {
-    pred = x == 0 ? ARGB_BLACK : cur[x - 1];
+    pred = x == 0 ? ARGB_BLACK : px(cur + x - 1);
   } else if (x == 0) {
-    pred = cur[-a.width];
+    pred = px(cur - a.width);
   } else {
     const uint32_t* up = cur - a.width;
-    const int mode =
-        (int)((a.modes[(int64_t)img * a.tiles_x * a.tiles_y + (y >> a.bits) * a.tiles_x + (x >> a.bits)] >> 8) & 0xff);
-    const uint32_t tr = (x < a.width - 1) ? up[x + 1] : cur[0];
-    pred = predict(mode, cur[x - 1], up[x], tr, up[x - 1]);
+    const uint32_t* mp = a.modes + (int64_t)img * a.tiles_x * a.tiles_y + (y >> a.bits) * a.tiles_x + (x >> a.bits);
+    [[maybe_unused]] const uint32_t* mrows = a.modes + (int64_t)img * a.tiles_x * a.tiles_y + (a.y0 >> a.bits) * a.tiles_x;
+    const int mode = WG_CHK(mp, 4, mrows, 4ll * a.tiles_x * (((a.y0 + a.rows - 1) >> a.bits) - (a.y0 >> a.bits) + 1),
+                            "k_vp8l_residual modes") ? (int)((*mp >> 8) & 0xff) : 0;
+    const uint32_t tr = (x < a.width - 1) ? px(up + x + 1) : px(cur);
+    pred = predict(mode, px(cur + x - 1), px(up + x), tr, px(up + x - 1));
   }
-  a.out[img * a.pitch + p] = sub_pixels(cur[x], pred);
+  uint32_t* const o = a.out + img * a.pitch + p;
+  if (WG_CHK(o, 4, a.out + img * a.pitch + (int64_t)a.y0 * a.width, (int64_t)a.rows * a.width * 4, "k_vp8l_residual out"))
+    *o = sub_pixels(px(cur + x), pred);
 }
 
 struct InvArgs {
@@ -632,6 +655,9 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
     const uint32_t* inrow = in + (int64_t)min(y, a.height - 1) * w;
     uint32_t* orow = out + (int64_t)min(y, a.height - 1) * w;
     uint32_t o1 = 0, first = 0;  // this lane's output (c2) at x - 1; at x = 0
+    // (WG_BOUNDS) the buffers' extents from the entry point's shapes
+    [[maybe_unused]] const int64_t px_n = 4ll * a.n_img * a.pitch, modes_n = 4ll * a.n_img * a.tiles_x * a.tiles_y,
+                                   hand_n = 8ll * a.n_img * a.bands * ((w + 1) & ~1);
     // (WG_INV_STAMPS builds) the per-band timeline: s_memrealtime (100 MHz) at
     // the band's start and end, and the ticks spent re-polling the band above
     WG_IF_INV_STAMPS(const uint64_t t_band = __builtin_amdgcn_s_memrealtime(); uint64_t poll_ticks = 0, polls = 0;)
@@ -643,7 +669,10 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
     // the compiler drain every load before its use)
     // (band 0: up_row is any valid row, values unused)
     auto up_load = [&](int c) -> uint64_t {
-      return __hip_atomic_load(up_row + min(c, w - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t* g = up_row + min(c, w - 1);
+      return WG_CHK(g, 8, a.hand, hand_n, "k_vp8l_inverse hand load")
+                 ? __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                 : 0ull;
     };
     auto up_take = [&](int c, uint64_t g) -> uint32_t {
       const uint2 gw = __builtin_bit_cast(uint2, g);
@@ -675,7 +704,7 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
     // tiles of >= 16 pixels (TILE16) a chunk touches at most two tiles, t0
     // for u < ub and the next one past it.
     auto ld_res = [&](int x0, uint32_t* r) {
-      if (x0 >= 0 && x0 + 15 < w) {
+      if (x0 >= 0 && x0 + 15 < w && WG_CHK(inrow + x0, 64, a.in, px_n, "k_vp8l_inverse in")) {
         const u32x4a4_t* p = reinterpret_cast<const u32x4a4_t*>(inrow + x0);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -687,7 +716,10 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
         }
       } else {
 #pragma unroll
-        for (int u = 0; u < 16; u++) r[u] = inrow[min(max(x0 + u, 0), w - 1)];
+        for (int u = 0; u < 16; u++) {
+          const uint32_t* q = inrow + min(max(x0 + u, 0), w - 1);
+          r[u] = WG_CHK(q, 4, a.in, px_n, "k_vp8l_inverse in") ? *q : 0u;
+        }
       }
     };
     struct Modes {
@@ -697,12 +729,16 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
     auto ld_modes = [&](int x0, Modes& m) {
       if constexpr (TILE16) {
         const int t0 = min(max(x0, 0), w - 1) >> a.bits;
-        m.m[0] = mrow[t0];
-        m.m[1] = mrow[min(t0 + 1, a.tiles_x - 1)];
+        const uint32_t *q0 = mrow + t0, *q1 = mrow + min(t0 + 1, a.tiles_x - 1);
+        m.m[0] = WG_CHK(q0, 4, a.modes, modes_n, "k_vp8l_inverse modes") ? *q0 : 0u;
+        m.m[1] = WG_CHK(q1, 4, a.modes, modes_n, "k_vp8l_inverse modes") ? *q1 : 0u;
         m.ub = ((t0 + 1) << a.bits) - x0;
       } else {
 #pragma unroll
-        for (int u = 0; u < 16; u++) m.m[u] = mrow[min(max(x0 + u, 0), w - 1) >> a.bits];
+        for (int u = 0; u < 16; u++) {
+          const uint32_t* q = mrow + (min(max(x0 + u, 0), w - 1) >> a.bits);
+          m.m[u] = WG_CHK(q, 4, a.modes, modes_n, "k_vp8l_inverse modes") ? *q : 0u;
+        }
         m.ub = 0;
       }
     };
@@ -768,11 +804,12 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
         // store the pair (x - 1, x); an odd width's last pixel goes alone
         // (the hand-off lane's row is live)
         if (u & 1) {
-          if (hands_off && (uint32_t)x < (uint32_t)w) {
+          if (hands_off && (uint32_t)x < (uint32_t)w &&
+              WG_CHK(hand_mine + x - 1, 16, a.hand, hand_n, "k_vp8l_inverse hand store")) {
             const u32x4_t g2 = {ov[u - 1], 1u, full, 1u};
             asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(hand_mine + x - 1), "v"(g2) : "memory");
           }
-        } else if (hands_off && x == w - 1) {
+        } else if (hands_off && x == w - 1 && WG_CHK(hand_mine + x, 8, a.hand, hand_n, "k_vp8l_inverse hand store")) {
           __hip_atomic_store(hand_mine + x, 1ull << 32 | full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (starts) first = x == 0 ? v : first;
@@ -784,7 +821,7 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
       }
       // this chunk's outputs: pixels x0 .. x0 + 15 of the row, from the even lane
       if ((lane & 1) == 0 && live) {
-        if (x0 >= 0 && x0 + 15 < w) {
+        if (x0 >= 0 && x0 + 15 < w && WG_CHK(orow + x0, 64, a.out, px_n, "k_vp8l_inverse out")) {
           uint64_t* d = reinterpret_cast<uint64_t*>(orow + x0);
 #pragma unroll
           for (int j = 0; j < 8; j++) d[j] = (uint64_t)ov[2 * j + 1] << 32 | ov[2 * j];
@@ -792,7 +829,7 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
 #pragma unroll
           for (int u = 0; u < 16; u++) {
             const int x = x0 + u;
-            if (x >= 0 && x < w) orow[x] = ov[u];
+            if (x >= 0 && x < w && WG_CHK(orow + x, 4, a.out, px_n, "k_vp8l_inverse out")) orow[x] = ov[u];
           }
         }
       }

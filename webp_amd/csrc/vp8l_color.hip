@@ -199,6 +199,194 @@ __global__ __launch_bounds__(CC_THREADS) void k_cc_select(CcArgs a) {
   }
 }
 
+// ---- k_cc_select_q: the same search for tiles of at most 32 x 32 (bits <= 5)
+// on packed byte arithmetic, one 256-lane workgroup a tile.
+//
+// A candidate's cost is sum_i |int8(t_i - delta(m, s_i))|.  With t' = t + 128
+// (mod 256) that is sum_i |u_i - 128| for the byte u_i = t'_i - delta (mod
+// 256), so four pixels' terms are one v_sad_u8 against 0x80808080 once their
+// four u bytes sit in one word.  The tile is staged once as 4-pixel groups:
+// the sources as two packed int16 pairs (sign-extended bytes: delta of two
+// pixels is one v_pk_mul_lo_u16 and one v_pk_ashrrev_i16 -- m * int8(s) fits
+// int16 and its low byte is all that counts), and each target as T1 = t' |
+// 0x80 and T2 = (t' & 0x80) ^ 0x80 per byte, so the byte-wise subtraction
+// mod 256 is (T1 - (d & 0x7f..)) ^ T2 ^ (d & 0x80..) with no borrow crossing a
+// byte.  Lane = candidate: every lane of a wave reads the same group (an LDS
+// broadcast) and adds 4 terms per ~10 VALU instructions.  Groups past the
+// tile's pixels are padding (source 0, t' = 128: term 0).
+//   A  coarse green->red (lanes 0-31) and green->blue (32-63), m = -128 + 8j;
+//      wave w sums groups 64w .. 64w + 63
+//   B  their fine searches (m = best - 7 + j, j < 15), a pixel half per
+//      half-wave
+//   C  red->blue coarse on the adjusted channels (restaged), a half a half-wave
+//   D  its fine search, a pixel quarter per 16 lanes
+// Each search's winner is the reference's: the first strict minimum in scan
+// order (the minimum of cost << 5 | j), and a fine candidate replaces the
+// coarse best only with a strictly lower cost.  Sums are integers, so the
+// order they are added in does not matter.
+constexpr int CQ_GROUPS = 256;  // 4-pixel groups of a 32 x 32 tile
+typedef short cq_s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cq_sext_pair(uint32_t a, uint32_t b) {  // int8 bytes a, b -> int16 pair
+  return ((uint32_t)(int32_t)(int8_t)a & 0xffffu) | (uint32_t)(int32_t)(int8_t)b << 16;
+}
+// T1 / T2 of four target bytes (t' = t + 128)
+__device__ __forceinline__ uint2 cq_target(uint32_t t4) {
+  const uint32_t tp = t4 ^ 0x80808080u;
+  return make_uint2(tp | 0x80808080u, (tp & 0x80808080u) ^ 0x80808080u);
+}
+// four terms of candidate mm (m in both int16 halves) on one group
+__device__ __forceinline__ uint32_t cq_terms(uint32_t mm, uint2 src, uint2 tgt, uint32_t acc) {
+  const cq_s16x2 m2 = __builtin_bit_cast(cq_s16x2, mm);
+  const cq_s16x2 p0 = (m2 * __builtin_bit_cast(cq_s16x2, src.x)) >> (cq_s16x2){5, 5};
+  const cq_s16x2 p1 = (m2 * __builtin_bit_cast(cq_s16x2, src.y)) >> (cq_s16x2){5, 5};
+  const uint32_t d = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p1), __builtin_bit_cast(uint32_t, p0), 0x06040200u);
+  const uint32_t z = tgt.x - (d & 0x7f7f7f7fu);
+  const uint32_t u = z ^ tgt.y ^ (d & 0x80808080u);
+  return __builtin_amdgcn_sad_u8(u, 0x80808080u, acc);
+}
+__device__ __forceinline__ int cq_min(int v, int width) {  // min over aligned groups of `width` lanes
+  for (int o = width >> 1; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_cc_select_q(CcArgs a) {
+  __shared__ uint2 gsrc[CQ_GROUPS];     // source int16 pairs (pixels 0, 1 | 2, 3)
+  __shared__ uint2 gtgt[CQ_GROUPS][2];  // target T1 / T2: [0] red (then adjusted blue), [1] blue
+  __shared__ int part[4][64];
+  __shared__ int best[3], cbest[3];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles = a.tiles_x * a.tiles_y;
+  const int img = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int tx = tile % a.tiles_x, ty = tile / a.tiles_x, ts = 1 << a.bits;
+  const int x0 = tx * ts, y0 = ty * ts;
+  const int tw = min(ts, a.width - x0), th = min(ts, a.height - y0), n = tw * th;
+  uint32_t* base = a.argb + img * a.pitch + (int64_t)y0 * a.width + x0;
+  // this thread's group: pixels 4 tid .. 4 tid + 3 of the tile (row-major), kept for the transform
+  uint32_t px[4];
+  bool in[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int i = 4 * tid + k;
+    in[k] = i < n;
+    px[k] = in[k] ? base[(int64_t)(i / tw) * a.width + i % tw] : 0u;
+  }
+  auto bytes4 = [&](int sh) {  // channel byte at shift sh of the 4 pixels (padding: 0)
+    return ((px[0] >> sh) & 0xffu) | ((px[1] >> sh) & 0xffu) << 8 | ((px[2] >> sh) & 0xffu) << 16 |
+           ((px[3] >> sh) & 0xffu) << 24;
+  };
+  {
+    const uint32_t g4 = bytes4(8);
+    gsrc[tid] = make_uint2(cq_sext_pair(g4, g4 >> 8), cq_sext_pair(g4 >> 16, g4 >> 24));
+    gtgt[tid][0] = cq_target(bytes4(16));
+    gtgt[tid][1] = cq_target(bytes4(0));
+  }
+  __syncthreads();
+  auto pack_m = [](int m) { return ((uint32_t)m & 0xffffu) | (uint32_t)m << 16; };
+  // ---- A: coarse green->red / green->blue ----
+  {
+    const int ch = lane >> 5, j = lane & 31;
+    const uint32_t mm = pack_m(-128 + 8 * j);
+    uint32_t acc = 0;
+    for (int g = 64 * wave; g < 64 * wave + 64; g++) acc = cq_terms(mm, gsrc[g], gtgt[g][ch], acc);
+    part[wave][lane] = (int)acc;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const int cost = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    const int key = cq_min(cost * 32 + (lane & 31), 32);
+    if ((lane & 31) == 0) {
+      best[lane >> 5] = -128 + 8 * (key & 31);
+      cbest[lane >> 5] = key >> 5;
+    }
+  }
+  __syncthreads();
+  // ---- B: fine green->red (lanes 0-15 of a half) / green->blue (16-31) ----
+  {
+    const int h = lane >> 5, ch = (lane >> 4) & 1, j = lane & 15;
+    const uint32_t mm = pack_m(best[ch] - 7 + j);
+    uint32_t acc = 0;
+    for (int g = 64 * wave + 32 * h; g < 64 * wave + 32 * h + 32; g++) acc = cq_terms(mm, gsrc[g], gtgt[g][ch], acc);
+    acc += __shfl_xor(acc, 32, 64);
+    if (lane < 32) part[wave][lane] = (int)acc;
+  }
+  __syncthreads();
+  if (wave == 0 && lane < 32) {
+    const int ch = lane >> 4, j = lane & 15, m = best[ch] - 7 + j;
+    const int cost = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    const bool valid = j < 15 && m >= -128 && m <= 127;
+    const int key = cq_min(valid ? cost * 16 + j : 0x7fffffff, 16);
+    if (j == 0 && (key >> 4) < cbest[ch]) best[ch] = best[ch] - 7 + (key & 15);
+  }
+  __syncthreads();
+  // ---- C: restage: adjusted red -> sources, adjusted blue -> targets; coarse red->blue ----
+  const int g2r = best[0], g2b = best[1];
+  {
+    uint32_t ar = 0, ab = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int gr = (px[k] >> 8) & 0xff, rd = (px[k] >> 16) & 0xff, bl = px[k] & 0xff;
+      const uint32_t r2 = in[k] ? (uint32_t)((rd - cc_delta(g2r, gr)) & 0xff) : 0u;
+      const uint32_t b2 = in[k] ? (uint32_t)((bl - cc_delta(g2b, gr)) & 0xff) : 0u;
+      ar |= r2 << (8 * k);
+      ab |= b2 << (8 * k);
+    }
+    gsrc[tid] = make_uint2(cq_sext_pair(ar, ar >> 8), cq_sext_pair(ar >> 16, ar >> 24));
+    gtgt[tid][0] = cq_target(ab);
+  }
+  __syncthreads();
+  {
+    const int h = lane >> 5, j = lane & 31;
+    const uint32_t mm = pack_m(-128 + 8 * j);
+    uint32_t acc = 0;
+    for (int g = 64 * wave + 32 * h; g < 64 * wave + 32 * h + 32; g++) acc = cq_terms(mm, gsrc[g], gtgt[g][0], acc);
+    acc += __shfl_xor(acc, 32, 64);
+    if (lane < 32) part[wave][lane] = (int)acc;
+  }
+  __syncthreads();
+  if (wave == 0 && lane < 32) {
+    const int cost = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    const int key = cq_min(cost * 32 + lane, 32);
+    if (lane == 0) {
+      best[2] = -128 + 8 * (key & 31);
+      cbest[2] = key >> 5;
+    }
+  }
+  __syncthreads();
+  // ---- D: fine red->blue, a pixel quarter per 16 lanes ----
+  {
+    const int q = lane >> 4, j = lane & 15;
+    const uint32_t mm = pack_m(best[2] - 7 + j);
+    uint32_t acc = 0;
+    for (int g = 64 * wave + 16 * q; g < 64 * wave + 16 * q + 16; g++) acc = cq_terms(mm, gsrc[g], gtgt[g][0], acc);
+    acc += __shfl_xor(acc, 16, 64);
+    acc += __shfl_xor(acc, 32, 64);
+    if (lane < 16) part[wave][lane] = (int)acc;
+  }
+  __syncthreads();
+  if (wave == 0 && lane < 16) {
+    const int j = lane, m = best[2] - 7 + j;
+    const int cost = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    const bool valid = j < 15 && m >= -128 && m <= 127;
+    const int key = cq_min(valid ? cost * 16 + j : 0x7fffffff, 16);
+    if (j == 0 && (key >> 4) < cbest[2]) best[2] = best[2] - 7 + (key & 15);
+  }
+  __syncthreads();
+  const int r2b = best[2];
+  if (tid == 0)
+    a.data[(int64_t)img * tiles + tile] = (uint32_t)(uint8_t)g2r | (uint32_t)(uint8_t)g2b << 8 | (uint32_t)(uint8_t)r2b << 16;
+  // applyColorTransformPixel (:497-507) over the thread's group, in place
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (!in[k]) continue;
+    const int i = 4 * tid + k;
+    const uint32_t p = px[k];
+    const int gr = (p >> 8) & 0xff, rd = (p >> 16) & 0xff, bl = p & 0xff;
+    const int nr = (rd - cc_delta(g2r, gr)) & 0xff;
+    const int nb = (bl - cc_delta(g2b, gr) - cc_delta(r2b, rd)) & 0xff;
+    base[(int64_t)(i / tw) * a.width + i % tw] = (p & 0xff00ff00u) | ((uint32_t)nr << 16) | (uint32_t)nb;
+  }
+}
+
 struct CiArgs {
   const uint32_t* data;
   const uint32_t* src;
@@ -268,6 +456,10 @@ extern "C" int wg_vp8l_color_space_transform(uint32_t* argb, int32_t width, int3
   a.tiles_y = (height + (1 << bits) - 1) >> bits;
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * n_images;
   WG_REQUIRE(blocks < (1ll << 31));
+  if (bits <= 5) {  // tiles of at most 1024 pixels: the packed-byte search
+    hipLaunchKernelGGL(k_cc_select_q, dim3((unsigned)blocks), dim3(256), 0, wg::as_stream(stream), a);
+    return wg::check_launch("k_cc_select_q");
+  }
   hipLaunchKernelGGL(k_cc_select, dim3((unsigned)blocks), dim3(CC_THREADS), 0, wg::as_stream(stream), a);
   return wg::check_launch("k_cc_select");
 }

@@ -29,15 +29,29 @@
 #include <stdint.h>
 
 // ---- WG_BOUNDS ----
+// WG_CHK(p, bytes, base, size, "site"): the access of `bytes` at p must lie in
+// [base, base + size) -- the buffer's extent implied by the entry point's
+// shape arguments; one outside it is skipped and printed (device printf, one
+// line per lane: tools/gpu_bounds_suite.sh greps the log for "WG_BOUNDS").
+// WG_IN also ORs 4 into the launch's status word (*flag).
 #ifdef WG_BOUNDS
-__device__ __forceinline__ bool wg_in_buf(const void* p, int bytes, const void* base, int64_t size, int* flag) {
+__device__ __forceinline__ bool wg_chk(const void* p, int bytes, const void* base, int64_t size, const char* site) {
   const int64_t o = static_cast<const char*>(p) - static_cast<const char*>(base);
   const bool ok = o >= 0 && o + bytes <= size;
+  if (!ok)
+    printf("WG_BOUNDS %s: bytes [%lld, %lld) of a %lld-byte buffer, block %d thread %d\n", site, (long long)o,
+           (long long)(o + bytes), (long long)size, (int)blockIdx.x, (int)threadIdx.x);
+  return ok;
+}
+__device__ __forceinline__ bool wg_in_buf(const void* p, int bytes, const void* base, int64_t size, int* flag) {
+  const bool ok = wg_chk(p, bytes, base, size, "k_decode_bands");
   if (!ok) __hip_atomic_fetch_or(flag, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return ok;
 }
+#define WG_CHK(p, bytes, base, size, site) wg_chk((p), (bytes), (base), (size), (site))
 #define WG_IN(p, bytes, base, size, flag) wg_in_buf((p), (bytes), (base), (size), (flag))
 #else
+#define WG_CHK(p, bytes, base, size, site) true
 #define WG_IN(p, bytes, base, size, flag) true
 #endif
 
