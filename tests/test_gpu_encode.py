@@ -181,8 +181,9 @@ def test_row_schedule_keeps_outputs(cuda, monkeypatch, schedule):
 
 def test_row_schedule_table(cuda):
     """k_row_slack / k_row_order build exactly the order the key (y - slack_i, y, i)
-    sorts to, slack_i = (mbh / 4) * (255 - mean alpha_i) / 255 (integer), and
-    every frame's rows appear in row order (the kernel's waits stay on running waves)."""
+    sorts to, slack_i = (2 mbh / 5) (1 - (m_i / 242)^4), m_i = min(mean alpha_i,
+    242) (integers), and every frame's rows appear in row order (the kernel's
+    waits stay on running waves)."""
     w, h = 320, 240
     rgba = np.stack([[synth.gradient_rgba, synth.noise_rgba, synth.blobs_rgba][i % 3](w, h, **({} if i % 3 == 0 else
                      {"seed": i})) for i in range(7)])
@@ -197,7 +198,9 @@ def test_row_schedule_table(cuda):
     order, slack = words[base + 4:base + 4 + rows], words[base + 4 + rows:base + 4 + rows + n]
     a = np.clip(alphas.cpu().numpy().astype(np.int64), 0, 255)
     mean = a.sum(axis=1) // a.shape[1]
-    assert (slack == (mbh // 4) * (255 - mean) // 255).all()
+    m4 = np.minimum(mean, 242) ** 4
+    f4 = 242 ** 4
+    assert (slack == (2 * mbh // 5) * (f4 - m4) // f4).all()
     keys = sorted(((y - slack[i], y, i) for y in range(mbh) for i in range(n)))
     assert order.tolist() == [y * n + i for (_, y, i) in keys]
     assert slack[1] > slack[0] and slack[1] > slack[2]  # the noise frame goes ahead

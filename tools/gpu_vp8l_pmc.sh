@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU box: counter passes over the C5 stages (tools/bench_c5.py) for the
-# VP8L kernels (k_vp8l_select_q3 -- the default tile selection --, k_vp8l_residual, k_vp8l_inverse, ...): two SQ passes and
+# VP8L kernels (k_vp8l_select_q3 -- the default tile selection --, k_vp8l_residual, k_vp8l_inverse, the
+# cross-colour k_cc_select_q / k_cc_inverse, k_ci_inverse): two SQ passes and
 # two HBM passes, each its own rocprofv3 run, summarised per kernel into
 # gpurun_out/vp8l_pmc/*.json (tools/pmc_summary.py).
 OUT=gpurun_out/vp8l_pmc; mkdir -p $OUT && export TMPDIR=/tmp
@@ -19,7 +20,7 @@ import json
 out = {}
 for n in ("sq1", "sq2", "hbm"):
     for k, v in json.load(open(f"gpurun_out/vp8l_pmc/{n}.json")).items():
-        if "vp8l" in k:
+        if "vp8l" in k or "k_cc_" in k or "k_ci_" in k:
             out.setdefault(k, {}).update(v)
 json.dump(out, open("gpurun_out/vp8l_pmc/summary.json", "w"), indent=1)
 for k, v in out.items():

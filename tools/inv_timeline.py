@@ -1,7 +1,7 @@
 """Per-band timeline of k_vp8l_inverse on C5's 4096x4096 (bits 5) image.
 
-  make -C webp_amd variant NAME=invstamps DEFS=-DWG_INV_STAMPS
-  WEBPGPU_LIB=webp_amd/libwebpgpu_invstamps.so python tools/inv_timeline.py [out.json]
+  make -C webp_amd variant NAME=timelines DEFS=-DWG_TIMELINES
+  WEBPGPU_LIB=webp_amd/libwebpgpu_timelines.so python tools/inv_timeline.py [out.json]
 
 The stamps build records per band (32 rows) the s_memrealtime (100 MHz) at
 its start and end and the ticks it spent re-polling the band above's
@@ -66,7 +66,7 @@ def main():
     bands = (N + 31) // 32
     wb = lib.wg_vp8l_inverse_work_bytes(N, N, 1)
     hand = 16 + 8 * bands * ((N + 1) & ~1)
-    assert wb == hand + 32 * bands, "not a WG_INV_STAMPS build (work bytes %d)" % wb
+    assert wb == hand + 32 * bands, "not a WG_TIMELINES build (work bytes %d)" % wb
     work = torch.empty(wb, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     for _ in range(3):  # warm-up, then the recorded launch

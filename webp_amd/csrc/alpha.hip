@@ -447,11 +447,9 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
   // multiples of 16, so (s0 - k) & 15 = (-k) & 15
   const int o = (-lane) & 15, q = o >> 2, rsh = o & 3;
   const uint32_t mq1 = (q & 1) ? ~0u : 0u, mq2 = (q & 2) ? ~0u : 0u;
-  auto bfi = [](uint32_t m, uint32_t a1, uint32_t a0) {  // m ? a1 : a0, bitwise
-    uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a1), "v"(a0));
-    return r;
-  };
+  // m ? a1 : a0, bitwise (one v_bitop3_b32 / v_bfi_b32; as inline asm the
+  // compiler put an s_nop on each side of it)
+  auto bfi = [](uint32_t m, uint32_t a1, uint32_t a0) { return (m & a1) | (~m & a0); };
   for (;;) {
     if (lane == 0) sh_band = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();

@@ -1861,6 +1861,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
             src_row = *reinterpret_cast<const uint32_t*>(s.yin + off + qr * BPS);
           }
           SSTAMP(1);
+          CSTAMP(-1);
           // candidates: prediction + transform (lane hl = candidate hl)
       WG_REP_BEGIN(CAND)
           if constexpr (FUSE) {  // the lane of mode cm[c] stores candidate c's coefficients
@@ -1870,7 +1871,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
               for (int i = 0; i < 4; i++) st_co4(&s.co_buf[half * 3 + c][4 * i], pco + 4 * i);
             }
           } else if (cand) {
-            CSTAMP(-1);
             int pred[16], co[16];
             pred4_lut(t.pcode[mode], s.pv[half], pred);
             fdct(src, pred, co);
@@ -1883,10 +1883,10 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
 #pragma unroll
               for (int i = 0; i < 16; i++) s.cand_q[slot][i] = q[i];
             }
-            CSTAMP(0);
           }
       WG_REP_END
           lds_sync();
+          CSTAMP(0);
           // (TRELLIS + TAIL) the candidate's nz count and rate, straight from
           // the DP into the reconstruction quad's registers (the same lanes)
           int dp_nz = 0, dp_rate = 0;
@@ -1911,6 +1911,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
       WG_REP_END
           const uint64_t pnz_mask = __ballot(pnz);
           lds_sync();
+          CSTAMP(1);
           DSTAMP(-1);
           // the trellis DP: one lane quad per candidate (lane 4c + k owns end context k)
           if (bvalid && hl < 4 * K) {
@@ -1961,7 +1962,6 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
             part = token_cost_pos<3>(t, s.cand_q[sl], n0, nzc, nz_ctx, 0) + token_cost_pos<3>(t, s.cand_q[sl], n0 + 1, nzc, nz_ctx, 0);
           }
           {
-            CSTAMP(1);
             int res[4], pr[4], sr[4], rr[4];
             qnz = TRELLIS ? dp_nz : s.cand_nz[qsl];
             if constexpr (TAIL) {
@@ -2108,8 +2108,8 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
             rate = (qmode > 0 && cnt <= 3) ? 140 : 0;
             rate += tok_rate + hdr;
             score = rd_score(disto, rate, sg.lambda_i4);
-            CSTAMP(3);
           }
+          CSTAMP(3);
           SSTAMP(2);
           // first minimum over this half's candidates (strict '<' in candidate
           // order): candidate c's score sits in lane 32 * half + 4c, i.e. lane
@@ -2657,12 +2657,19 @@ namespace {
 // A launch over many frames ends on the critical path of its slowest frame:
 // mbw + ~2 (mbh - 1) macroblock times of the frame whose macroblocks take
 // longest (textured content, where the I4 RD dominates).  Its rows are
-// therefore dequeued up to mbh / 4 rows ahead of the others: frame i's row y
-// takes the key (y - slack_i, y, i), slack_i = (mbh / 4) * (255 - mean alpha_i)
-// / 255 (computeAlphas' alpha is low for textured macroblocks).  Keys grow
-// with y within a frame, so a row is always dequeued after the row above
-// (the kernel's waits stay on running waves); the outputs do not depend on
-// the order.  64 mixed 1080p frames: 25.4 -> 23.3 ms.
+// therefore dequeued up to 2 mbh / 5 rows ahead of the others: frame i's row
+// y takes the key (y - slack_i, y, i), slack_i = (2 mbh / 5) (1 - (m_i /
+// 242)^4), m_i = min(mean alpha_i, 242) (computeAlphas' alpha is low for
+// textured macroblocks), in integers.  The slack is proportional to the
+// frame's expected macroblock time above the smoothest content's: per MB,
+// 44 / 62 / 69 us for the bench's gradient / photo / noise frames (mean
+// alpha 240 / 187 / 1.4; tools/enc_timeline.py), which (m / 242)^4 fits; the
+// round-5 linear form (mbh / 4) (255 - mean) / 255 gave the photo frames 4
+// rows and they finished last.  Keys grow with y within a frame, so a row is
+// always dequeued after the row above (the kernel's waits stay on running
+// waves); the outputs do not depend on the order.  64 mixed 1080p frames:
+// 25.4 -> 23.3 ms (round 3); the bench's G / N / P batch 20.30 -> 19.96 ms
+// (round 6, profiles/r06_enc_timeline*.json).
 __global__ __launch_bounds__(256) void k_row_slack(const int32_t* alphas, int n_mb, int mbh, int* tag, int* slack) {
   __shared__ long long part[256];
   long long sum = 0;
@@ -2676,7 +2683,8 @@ __global__ __launch_bounds__(256) void k_row_slack(const int32_t* alphas, int n_
   }
   if (threadIdx.x == 0) {
     const int mean = (int)(part[0] / n_mb);
-    slack[blockIdx.x] = (mbh / 4) * (255 - mean) / 255;
+    const long long m = min(mean, 242), m4 = m * m * m * m, f4 = 242ll * 242 * 242 * 242;
+    slack[blockIdx.x] = (int)((long long)(2 * mbh / 5) * (f4 - m4) / f4);
     if (blockIdx.x == 0) {  // the encoder reads it after k_row_order (same stream)
       tag[0] = ORDER_TAG ^ (int)gridDim.x;
       tag[1] = ~(ORDER_TAG ^ mbh);

@@ -87,6 +87,8 @@ struct SharpArgs {
   int n_img;
   const uint8_t* work0;  // (WG_BOUNDS) the whole work buffer and its size
   int64_t work_n;
+  uint64_t* stamps;  // (WG_TIMELINES builds) per k_sharp_wave block and role [4]: start, end,
+                     // global-wait ticks | waits << 32, LDS-wait ticks | waits << 32
 };
 
 __device__ __forceinline__ void load_tabs(SharpTabs& dst, const SharpTabs* src) {
@@ -268,6 +270,9 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
   int* prog_img = a.prog + (int64_t)img * 4 * nb;  // [iteration][band]: row pairs finished
   int* prog_out = prog_img + it * nb + band;
   bool timed_out = false;  // wave-uniform
+  // (WG_TIMELINES builds) s_memrealtime (100 MHz) at the walk's start and
+  // end, and the ticks spent in the two kinds of dependency wait
+  WG_IF_TIMELINES(const uint64_t t_walk = __builtin_amdgcn_s_memrealtime(); uint64_t gw_ticks = 0, gw_n = 0, lw_ticks = 0, lw_n = 0;)
   // byte offsets inside one state plane fit 32 bits (a 16383^2 image's Y
   // state is 537 MB): 32-bit scalar row offsets, not 64-bit products
   const uint32_t uv_row_bytes = 2u * (uint32_t)rs, y_row_bytes = 2u * (uint32_t)w;
@@ -288,7 +293,10 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t k = 0;; k++) {
       const int v = __builtin_amdgcn_readfirstlane((int)ld_sc1(p));
-      if (v >= need) return v;
+      if (v >= need) {
+        WG_IF_TIMELINES(if (k > 0) { gw_ticks += __builtin_amdgcn_s_memrealtime() - t0; gw_n++; })
+        return v;
+      }
       if ((k & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
         timed_out = true;
         return uvh;
@@ -302,7 +310,10 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t k = 0;; k++) {
       __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_readfirstlane(lds_acquire(p)) >= need) return;
+      if (__builtin_amdgcn_readfirstlane(lds_acquire(p)) >= need) {
+        WG_IF_TIMELINES(lw_ticks += __builtin_amdgcn_s_memrealtime() - t0; lw_n++;)
+        return;
+      }
       if ((k & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
         timed_out = true;
         return;
@@ -521,6 +532,13 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     atomicAdd(reinterpret_cast<unsigned long long*>(a.sums + img * 4 + it), sm);
     if (timed_out) a.iters[img] = -1;
   }
+  WG_IF_TIMELINES(if (lane == 0) {
+    uint64_t* st = a.stamps + 4 * (2 * (((int64_t)img * 4 + it) * nb + band) + ROLE);
+    st[0] = t_walk;
+    st[1] = __builtin_amdgcn_s_memrealtime();
+    st[2] = gw_ticks | gw_n << 32;
+    st[3] = lw_ticks | lw_n << 32;
+  })
 }
 
 template <bool LUT>
@@ -682,7 +700,8 @@ extern "C" size_t wg_sharpyuv_work_bytes(int32_t width, int32_t height, int32_t 
   if (width <= 0 || height <= 0 || n_images <= 0) return 0;
   const SharpLayout L = sharp_layout(width, height);
   const int nb = sharp_bands(width);
-  return n_images * L.bytes_img + (size_t)n_images * (4 * 8 + 4 + 4 * 4 * nb) + 16;
+  // (+ the timeline records: 32 B a wave, two waves a block, 4 * nb blocks an image)
+  return n_images * L.bytes_img + (size_t)n_images * (4 * 8 + 4 + 4 * 4 * nb) + 16 WG_IF_TIMELINES(+(size_t)n_images * 4 * nb * 64);
 }
 
 extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t height, int32_t rgb_stride,
@@ -760,6 +779,8 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
   a.n_img = n_images;
   a.work0 = base;
   a.work_n = (int64_t)wg_sharpyuv_work_bytes(width, height, n_images);
+  // (WG_TIMELINES builds: the records follow the counters, 8-B aligned)
+  a.stamps = reinterpret_cast<uint64_t*>(tail + (((size_t)n_images * (32 + 4 + 16 * nb) + 7) & ~(size_t)7));
   if (hipMemsetAsync(tail, 0, (size_t)n_images * (32 + 4 + 16 * nb), s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(sharpyuv)");
   const int64_t cells = (int64_t)uvw * uvh * n_images;

@@ -522,7 +522,7 @@ struct InvArgs {
   int* ctl;        // [0] band dequeue counter, [1] error flag (wait timeout)
   int* diag;       // wg::diag_words + DIAG_VP8L_INVERSE
   uint64_t* hand;  // [n_img][bands][width] {pixel, tag} granules of each band's last row
-  uint64_t* stamps;  // (WG_INV_STAMPS builds) [band idx][4]: start, end, poll ticks | polls << 32, block
+  uint64_t* stamps;  // (WG_TIMELINES builds) [band idx][4]: start, end, poll ticks | polls << 32, block
   int64_t pitch;
   int width, height, bits, tiles_x, tiles_y, bands, n_img;
 };
@@ -571,11 +571,11 @@ __device__ __forceinline__ uint32_t c2_clamp_full(uint32_t a, uint32_t b, uint32
 __device__ __forceinline__ uint32_t c2_clamp_half(uint32_t avg, uint32_t c) { return as_u(half_step(as_v2(avg), as_v2(c))); }
 // The kPredCtl predictor on half pixels (c2 form), with the control word's select
 // masks m[b] = (bit b set ? ~0 : 0) read from LDS; `black` is this lane's
-// half of ARGB_BLACK
+// half of ARGB_BLACK.  msel is m ? a : b bitwise: one v_bitop3_b32 (gfx950's
+// three-input logic op); as an inline-asm v_bfi_b32 the compiler put an
+// s_nop on each side of every select (round 6: C5 inverse 3.53 -> 3.47 ms)
 __device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
-  return r;
+  return (m & a) | (~m & b);
 }
 struct SelMasks {
   uint32_t m[13];
@@ -658,9 +658,9 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
     // (WG_BOUNDS) the buffers' extents from the entry point's shapes
     [[maybe_unused]] const int64_t px_n = 4ll * a.n_img * a.pitch, modes_n = 4ll * a.n_img * a.tiles_x * a.tiles_y,
                                    hand_n = 8ll * a.n_img * a.bands * ((w + 1) & ~1);
-    // (WG_INV_STAMPS builds) the per-band timeline: s_memrealtime (100 MHz) at
+    // (WG_TIMELINES builds) the per-band timeline: s_memrealtime (100 MHz) at
     // the band's start and end, and the ticks spent re-polling the band above
-    WG_IF_INV_STAMPS(const uint64_t t_band = __builtin_amdgcn_s_memrealtime(); uint64_t poll_ticks = 0, polls = 0;)
+    WG_IF_TIMELINES(const uint64_t t_band = __builtin_amdgcn_s_memrealtime(); uint64_t poll_ticks = 0, polls = 0;)
     const int steps = w + 2 * last_row;
     // the band above's row, one granule a step: column c sits in gr[c & 15],
     // loaded UPD steps before step c - 1 (where it is TR); up_take re-polls it
@@ -674,27 +674,33 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
                  ? __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                  : 0ull;
     };
-    auto up_take = [&](int c, uint64_t g) -> uint32_t {
-      const uint2 gw = __builtin_bit_cast(uint2, g);
-      if (band > 0 && c < w && __builtin_amdgcn_readfirstlane((int)gw.y) == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (uint32_t it = 0;; it++) {
-          __builtin_amdgcn_s_sleep(1);
-          g = up_load(c);
-          if (__builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) != 0) {
-            WG_IF_INV_STAMPS(poll_ticks += __builtin_amdgcn_s_memrealtime() - t0; polls++;)
-            break;
+    // re-poll column c's granule until its tag is set (band > 0, c < w)
+    auto up_poll = [&](int c) -> uint64_t {
+      uint64_t g = 0;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (uint32_t it = 0;; it++) {
+        __builtin_amdgcn_s_sleep(1);
+        g = up_load(c);
+        if (__builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) != 0) {
+          WG_IF_TIMELINES(poll_ticks += __builtin_amdgcn_s_memrealtime() - t0; polls++;)
+          break;
+        }
+        if ((it & 15) == 15 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+                                __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          if (lane == 0) {
+            __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            wg::note_timeout(a.diag, c, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0, 0);
           }
-          if ((it & 15) == 15 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
-                                  __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-            if (lane == 0) {
-              __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              wg::note_timeout(a.diag, c, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0, 0);
-            }
-            break;
-          }
+          break;
         }
       }
+      return g;
+    };
+    // (round 6: the tag tested by a VALU compare and an exec-mask branch
+    // instead of v_readfirstlane + a scalar branch, and the check made every
+    // other step for two columns, both measured slower at C5: 3.53 -> 3.57 ms)
+    auto up_take = [&](int c, uint64_t g) -> uint32_t {
+      if (band > 0 && c < w && __builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) == 0) g = up_poll(c);
       return band > 0 ? (uint32_t)g : 0u;
     };
     // A chunk's inputs: the residuals of pixels x0 .. x0 + 15 of the lane's
@@ -837,7 +843,7 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
       for (int u = 0; u < 16; u++) rc[u] = rn[u];
       mc = mn;
     }
-    WG_IF_INV_STAMPS(if (lane == 0) {
+    WG_IF_TIMELINES(if (lane == 0) {
       uint64_t* st = a.stamps + 4 * stamp_idx;
       st[0] = t_band;
       st[1] = __builtin_amdgcn_s_memrealtime();
@@ -952,7 +958,7 @@ extern "C" int wg_vp8l_residual_image(const uint32_t* argb, int32_t width, int32
 extern "C" size_t wg_vp8l_inverse_work_bytes(int32_t width, int32_t height, int32_t n_images) {
   if (width <= 0 || height <= 0 || n_images <= 0) return 0;
   const size_t bands = (size_t)n_images * ((height + INV_ROWS - 1) / INV_ROWS);
-  return 16 + sizeof(uint64_t) * bands * ((width + 1) & ~1) WG_IF_INV_STAMPS(+32 * bands);  // (+ the timeline records)
+  return 16 + sizeof(uint64_t) * bands * ((width + 1) & ~1) WG_IF_TIMELINES(+32 * bands);  // (+ the timeline records)
 }
 
 extern "C" int wg_vp8l_inverse_predictor(const uint32_t* modes, int32_t bits, int32_t width, int32_t height,

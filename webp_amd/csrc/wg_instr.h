@@ -23,7 +23,9 @@
 //   -DWG_DEC_SKIPW=mask  bit k drops k_decode_bands' store site k (WRITE_SIZE
 //                        per site, tools/gpu_dec_write_sites.sh; the output is
 //                        then wrong, the control flow unchanged)
-//   -DWG_INV_STAMPS      the VP8L inverse's per-band timeline (tools/inv_timeline.py)
+//   -DWG_TIMELINES       per-wave timelines of the dependency walks: the VP8L
+//                        inverse's bands (tools/inv_timeline.py) and SharpYUV's
+//                        (image, iteration, band) waves (tools/sharp_timeline.py)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -61,7 +63,7 @@ __device__ __forceinline__ bool wg_in_buf(const void* p, int bytes, const void* 
 #endif
 #define DEC_SITE(bit) ((WG_DEC_SKIPW & (bit)) == 0)
 
-// ---- WG_STAMPS / WG_ROWTIMES / WG_INV_STAMPS: code present only in those builds ----
+// ---- WG_STAMPS / WG_ROWTIMES / WG_TIMELINES: code present only in those builds ----
 #ifdef WG_STAMPS
 #define WG_IF_STAMPS(...) __VA_ARGS__
 #else
@@ -72,10 +74,10 @@ __device__ __forceinline__ bool wg_in_buf(const void* p, int bytes, const void* 
 #else
 #define WG_IF_ROWTIMES(...)
 #endif
-#ifdef WG_INV_STAMPS
-#define WG_IF_INV_STAMPS(...) __VA_ARGS__
+#ifdef WG_TIMELINES
+#define WG_IF_TIMELINES(...) __VA_ARGS__
 #else
-#define WG_IF_INV_STAMPS(...)
+#define WG_IF_TIMELINES(...)
 #endif
 
 #define WG_STAMP_NOW(ts_)                                                        \
