@@ -1823,15 +1823,55 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
           constexpr bool FUSE = TRELLIS;
           int pco[FUSE ? 16 : 1];
       WG_REP_BEGIN(PRE)
-          // (the lane's mode code read first: in flight while the table is built)
-          const uint4 pcw = *reinterpret_cast<const uint4*>(t.pcode[min(hl, 9)]);
+          // two lanes a mode (round 6): lane m (the half's first DPP row)
+          // takes rows 0-1 of mode m's residual, lane m + 16 rows 3-2; each
+          // makes the SSE of its rows and the row pass of its pair, the pairs
+          // trade halves with one v_permlane16_swap (rows of 16 lanes), and
+          // each lane finishes two columns of the FTransform (columns 2 part,
+          // 2 part + 1).  Half the LDS reads and transform work on the step's
+          // chain: 156.5k -> 151.2k cycles a macroblock (stamped build), the
+          // isolated 64 x 1080p launch 20.1-20.3 -> 19.7-19.8 ms
+          const int pm_mode = hl & 15, part = hl >> 4;
+          const uint2 pcw2 = *reinterpret_cast<const uint2*>(&t.pcode[min(pm_mode, 9)][8 * part]);
           pred4_values(s.yout2, off, hl, s.pv[half]);
           lds_sync();
-          if (bvalid && hl < 10) {
-            int pred[16];
-            pred4_lut(pcw, s.pv[half], pred);
-            sse_lane = sse16(src, pred);
-            if constexpr (FUSE) fdct(src, pred, pco);
+          if (bvalid && pm_mode < 10) {
+            // this lane's two rows: part 0 rows 0, 1; part 1 rows 3, 2 (the
+            // packed FTransform's (3, 2) pair order)
+            const uint32_t ca = part ? pcw2.y : pcw2.x, cb = part ? pcw2.x : pcw2.y;
+            const int ra = part ? 3 : 0, rb = part ? 2 : 1;
+            wg::s16x2_t d[4];
+            int sse = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              const int pa = s.pv[half][(ca >> (8 * k)) & 0xff], pb = s.pv[half][(cb >> (8 * k)) & 0xff];
+              const int da = src[4 * ra + k] - pa, db = src[4 * rb + k] - pb;
+              sse += da * da + db * db;
+              d[k] = (wg::s16x2_t){(short)da, (short)db};
+            }
+            wg::s16x2_t T[4];
+            wg::fdct4x4_rowpair(d, T);  // part 0: P = rows (0, 1); part 1: Q = rows (3, 2)
+            // the partner's SSE and the two row-pass pairs of this lane's columns
+            auto other = [&](uint32_t v) {
+              const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+              return part ? r[0] : r[1];
+            };
+            sse_lane = sse + (int)other((uint32_t)sse);
+            const uint32_t x0 = __builtin_bit_cast(uint32_t, part ? T[0] : T[2]);
+            const uint32_t x1 = __builtin_bit_cast(uint32_t, part ? T[1] : T[3]);
+            const wg::s16x2_t R0 = __builtin_bit_cast(wg::s16x2_t, other(x0));
+            const wg::s16x2_t R1 = __builtin_bit_cast(wg::s16x2_t, other(x1));
+            const wg::s16x2_t one = {1, 1}, pmv = {1, -1}, k4 = {5352, 2217}, k12 = {2217, -5352};
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+              const wg::s16x2_t Pc = part ? (j ? R1 : R0) : T[j];
+              const wg::s16x2_t Qc = part ? T[2 + j] : (j ? R1 : R0);
+              const wg::s16x2_t S = Pc + Qc, D = Pc - Qc;  // (a0, a1), (a3, a2)
+              pco[j] = (int16_t)(wg::sdot2_acc(S, one, 7) >> 4);                                // row 0
+              pco[4 + j] = (int16_t)((wg::sdot2_acc(D, k4, 12000) >> 16) + (D.x != 0));          // row 1
+              pco[8 + j] = (int16_t)(wg::sdot2_acc(S, pmv, 7) >> 4);                             // row 2
+              pco[12 + j] = (int16_t)(wg::sdot2_acc(D, k12, 51000) >> 16);                        // row 3
+            }
           }
       WG_REP_END
           SSTAMP(0);
@@ -1841,7 +1881,9 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
           if (!has_left) eligible &= ~0x31au;  // TM HE RD HD HU need the left column
           const int K = bvalid ? min(max_modes, __builtin_popcount(eligible)) : 0;
           int cm[3];
-          select_i4_modes(sse_lane, hl, eligible, K, cm);
+          // (both DPP rows of the half hold every mode's total SSE, at lane
+          // mode and mode + 16: each row's minimum search gives the same cm[])
+          select_i4_modes(sse_lane, hl & 15, eligible, K, cm);
           const bool cand = bvalid && hl < K;
           const int mode = pick3(hl, cm[0], cm[1], cm[2]);
           const int slot = half * 3 + min(hl, 2);  // candidate slot in the trellis / level buffers
@@ -1865,10 +1907,13 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
           // candidates: prediction + transform (lane hl = candidate hl)
       WG_REP_BEGIN(CAND)
           if constexpr (FUSE) {  // the lane of mode cm[c] stores candidate c's coefficients
-            const int c = (K > 0 && cm[0] == hl) ? 0 : ((K > 1 && cm[1] == hl) ? 1 : ((K > 2 && cm[2] == hl) ? 2 : 3));
-            if (bvalid && hl < 10 && c < 3) {
+            // (both lanes of the mode: columns 2 part, 2 part + 1 of each row)
+            const int pm = hl & 15, pp = hl >> 4;
+            const int c = (K > 0 && cm[0] == pm) ? 0 : ((K > 1 && cm[1] == pm) ? 1 : ((K > 2 && cm[2] == pm) ? 2 : 3));
+            if (bvalid && pm < 10 && c < 3) {
 #pragma unroll
-              for (int i = 0; i < 4; i++) st_co4(&s.co_buf[half * 3 + c][4 * i], pco + 4 * i);
+              for (int i = 0; i < 4; i++)
+                *reinterpret_cast<uint32_t*>(&s.co_buf[half * 3 + c][4 * i + 2 * pp]) = pack16(pco[4 * i], pco[4 * i + 1]);
             }
           } else if (cand) {
             int pred[16], co[16];
