@@ -751,7 +751,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
 // wherever the MB above-right is not needed.  Cross-band hand-off: R by
 // progress_r + the top records, F by progress_f + the frame rows (sc1 stores,
 // drained before the flag), as in k_decode_bands.
-constexpr int SW = 4;         // rows per band (one R and one F wave each)
+constexpr int SW = 4;  // rows per band (one R and one F wave each; round 6, C3 real: 2 / 4 / 8 -> 3.96 / 3.72-3.75 / 4.67-4.68 ms)
 constexpr int RING_M = 4; // R -> F ring depth (R's work buffers of unfiltered MBs)
 
 // The first I4 wavefront step (i4_schedule) that reads the MB above-right,
@@ -1105,26 +1105,18 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         const int slot = mbx & (RING - 1), mslot = mbx & (RING_M - 1);
         STAMP(0);
         lane = opaque_lane() & 63;
-        // ---- this row's MB from R, the row above's filtered rows, ring space below ----
+        // ---- this row's MB from R, ring space below (the row above: before the column pass) ----
         if (lane == 0) {
           if (have < mbx + 1) have = wait_progress<false>(&prog_r[r], mbx + 1, &a.ctl[1], mbw, a.diag);
-          if (mby > 0) {
-            // in the band: MB x's bottom rows above (bot_f); across bands the
-            // frame rows, final once the row above has finished MB x + 1
-            const int need = from_lds ? mbx + 1 : min(mbx + 2, mbw);
-            if (seen < need)
-              seen = from_lds ? wait_progress<false>(&bot_f[r - 1], need, &a.ctl[1], mbw, a.diag)
-                              : wait_progress<true>(prog_above, need, &a.ctl[1], mbw, a.diag);
-          }
           if (to_lds && mbx >= RING - 1) wait_progress<false>(&prog_f[r + 1], mbx - RING + 2, &a.ctl[1], mbw, a.diag);
         }
         lds_sync();
         STAMP(7);
         // rotate the filter tiles (the MBs to the left move one MB further
-        // left), then the MB into the tiles (rows 4..) and the filter rows
-        // above (rows 0..3): every read of both first, then the writes (one
-        // LDS round trip; the rotation reads the columns the copy-in and the
-        // rotation itself overwrite, so all reads precede all writes)
+        // left), then the MB into the tiles (rows 4..): every read of both
+        // first, then the writes (one LDS round trip; the rotation reads the
+        // columns the copy-in and the rotation itself overwrite, so all reads
+        // precede all writes)
         const bool rot = mbx > 0;
         uint4 y0 = make_uint4(0, 0, 0, 0);
         uint64_t c[2] = {0, 0};
@@ -1141,23 +1133,11 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         }
         const uint8_t* ms = wb_all[r][mslot];
         const bool y_lane = lane < 16, c_lane = lane >= 16 && lane < 32;
-        // the rows above from bot_ring / the cross-band record (same layout):
-        // lanes 52-59 Y rows 0..3 in 8-B halves, 60-63 U, 44-47 V
-        const bool b_lane = mby > 0 && (lane >= 52 || (lane >= 44 && lane < 48));
-        const int bk = lane - 52;
-        const int b_src = lane >= 60 ? 64 + 8 * (lane - 60) : (lane >= 52 ? 16 * (bk >> 1) + 8 * (bk & 1) : 96 + 8 * (lane - 44));
-        uint8_t* const b_dst = lane >= 60 ? fu + (lane - 60) * FC_STRIDE + FC_X0
-                                          : (lane >= 52 ? fy + (bk >> 1) * FY_STRIDE + FY_X0 + 8 * (bk & 1)
-                                                        : fv + (lane - 44) * FC_STRIDE + FC_X0);
         const int c_pl = lane >= 24, c_j = (lane - 16) & 7;
         uint4 yv = make_uint4(0, 0, 0, 0);
-        uint64_t cv = 0, bv = 0;
+        uint64_t cv = 0;
         if (y_lane) yv = *reinterpret_cast<const uint4*>(ms + LY + lane * WG_BPS);
         if (c_lane) cv = lds64(ms + (c_pl ? LV : LU) + c_j * WG_BPS);
-        if (b_lane)
-          bv = from_lds ? lds64(bot_ring[r - 1][slot] + b_src)
-                        : (WG_IN(bot_img + mbx * BOT_BYTES + b_src, 8, a.bot, bot_size, &a.ctl[1])
-                               ? ld_sc1_64(bot_img + mbx * BOT_BYTES + b_src) : 0ull);
         const uint32_t w7v = reinterpret_cast<const uint32_t*>(info_ring[r][mslot])[7];
         asm volatile("" ::: "memory");  // (reads above, writes below)
         if (rot) {
@@ -1173,7 +1153,6 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
         }
         if (y_lane) *reinterpret_cast<uint4*>(fy + (lane + 4) * FY_STRIDE + FY_X0) = yv;
         if (c_lane) *reinterpret_cast<uint64_t*>((c_pl ? fv : fu) + (c_j + 4) * FC_STRIDE + FC_X0) = cv;
-        if (b_lane) *reinterpret_cast<uint64_t*>(b_dst) = bv;
         const uint32_t w7 = __builtin_amdgcn_readfirstlane(w7v);
         lds_sync();
         if (lane == 0) __hip_atomic_store(&cons_f[r], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1201,6 +1180,38 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           }
           lds_sync();
           if (lane == 0) __hip_atomic_store(&bot_f[r], mbx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        // ---- the row above: only now (round 6) ----
+        // The rotation, the copy-in and the row pass touch this row's tile
+        // rows 4.. and the MBs to the left; the column pass (the top edge)
+        // and the stores of the rows above need the row above's MB x final:
+        // in the band its bottom rows (bot_f, published once MB x + 1 above
+        // has run its row pass); across bands the frame rows, final once the
+        // row above has finished MB x + 1.  Waiting here instead of before
+        // the tiles takes the copy-in and the row pass off the rows' chain
+        // (C3 real 3.66-3.67 -> 3.42 ms).  They go into the tile rows 0..3
+        // from bot_ring / the cross-band record (same layout): lanes 52-59 Y
+        // rows 0..3 in 8-B halves, 60-63 U, 44-47 V.
+        if (mby > 0) {
+          if (lane == 0) {
+            const int need = from_lds ? mbx + 1 : min(mbx + 2, mbw);
+            if (seen < need)
+              seen = from_lds ? wait_progress<false>(&bot_f[r - 1], need, &a.ctl[1], mbw, a.diag)
+                              : wait_progress<true>(prog_above, need, &a.ctl[1], mbw, a.diag);
+          }
+          lds_sync();
+          const int bk = lane - 52;
+          const int b_src = lane >= 60 ? 64 + 8 * (lane - 60) : (lane >= 52 ? 16 * (bk >> 1) + 8 * (bk & 1) : 96 + 8 * (lane - 44));
+          uint8_t* const b_dst = lane >= 60 ? fu + (lane - 60) * FC_STRIDE + FC_X0
+                                            : (lane >= 52 ? fy + (bk >> 1) * FY_STRIDE + FY_X0 + 8 * (bk & 1)
+                                                          : fv + (lane - 44) * FC_STRIDE + FC_X0);
+          if (lane >= 52 || (lane >= 44 && lane < 48)) {
+            const uint64_t bv = from_lds ? lds64(bot_ring[r - 1][slot] + b_src)
+                                         : (WG_IN(bot_img + mbx * BOT_BYTES + b_src, 8, a.bot, bot_size, &a.ctl[1])
+                                                ? ld_sc1_64(bot_img + mbx * BOT_BYTES + b_src) : 0ull);
+            *reinterpret_cast<uint64_t*>(b_dst) = bv;
+          }
+          lds_sync();
         }
         if (do_filter) {
           if (a.filter_type == 2) filter_mb_cols<true>(fy, fu, fv, lane, true, mby > 0, inner, f_limit, ilevel, hev_t);
