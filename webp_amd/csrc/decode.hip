@@ -752,7 +752,7 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
 // progress_r + the top records, F by progress_f + the frame rows (sc1 stores,
 // drained before the flag), as in k_decode_bands.
 constexpr int SW = 4;  // rows per band (one R and one F wave each; round 6, C3 real: 2 / 4 / 8 -> 3.96 / 3.72-3.75 / 4.67-4.68 ms)
-constexpr int RING_M = 4; // R -> F ring depth (R's work buffers of unfiltered MBs)
+constexpr int RING_M = 4; // R -> F ring depth (R's work buffers of unfiltered MBs; round 6, C3 real: 8 -> 3.43-3.46 ms against 3.42-3.43)
 
 // The first I4 wavefront step (i4_schedule) that reads the MB above-right,
 // or 99: blocks 3, 7, 11, 15 read it in VE4 / LD4 / VL4 (wg_dsp.h pred4_row).

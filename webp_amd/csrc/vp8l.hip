@@ -696,11 +696,18 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
       }
       return g;
     };
-    // (round 6: the tag tested by a VALU compare and an exec-mask branch
-    // instead of v_readfirstlane + a scalar branch, and the check made every
-    // other step for two columns, both measured slower at C5: 3.53 -> 3.57 ms)
+    // (round 6, also measured: the tag tested by a VALU compare and an
+    // exec-mask branch, and the check made every other step for two columns:
+    // both slower, 3.53 -> 3.57 ms)
+    // The tag word alone goes through one v_readfirstlane and a scalar
+    // compare: made opaque first, so the compiler does not fold the test into
+    // a 64-bit compare of the whole granule (two v_readfirstlane, a 64-bit
+    // v_cmp and the VCC branch hazard on every step of a band that follows
+    // another: C5 inverse 3.51 -> 3.39 ms, round 6)
     auto up_take = [&](int c, uint64_t g) -> uint32_t {
-      if (band > 0 && c < w && __builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) == 0) g = up_poll(c);
+      uint32_t tag = __builtin_bit_cast(uint2, g).y;
+      asm volatile("" : "+v"(tag));
+      if (band > 0 && c < w && __builtin_amdgcn_readfirstlane((int)tag) == 0) g = up_poll(c);
       return band > 0 ? (uint32_t)g : 0u;
     };
     // A chunk's inputs: the residuals of pixels x0 .. x0 + 15 of the lane's
