@@ -38,7 +38,7 @@ def layout(width, height, n=1):
     bytes_img = 2 * (6 * y_elems + 6 * uv_elems)
     nb = (w // 2 + WB_OWN - 1) // WB_OWN
     tail = n * bytes_img
-    return tail + ((n * (32 + 4 + 16 * nb) + 7) & ~7), nb
+    return tail + ((n * (32 + 4 + 16 * nb) + 7) & ~7) + n * 4 * nb * 2 * WB_OWN * 8, nb  # (after the edge granules)
 
 
 def main():

@@ -84,6 +84,7 @@ struct SharpArgs {
   uint64_t* sums;  // [n_img][4]
   int* prog;       // [n_img][4] row pairs finished per iteration
   int* iters;      // [n_img] iterations the reference runs (-1: a dependency wait timed out)
+  uint64_t* hand;  // [n_img][4][bands][2][WB_OWN] edge granules {3 x int16 updated chroma, row tag} (halo reloads)
   int n_img;
   const uint8_t* work0;  // (WG_BOUNDS) the whole work buffer and its size
   int64_t work_n;
@@ -162,6 +163,9 @@ __device__ __forceinline__ uint32_t ld_sc1(const void* p) {
 __device__ __forceinline__ void st_sc1(void* p, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ uint64_t ld_sc1_64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void st_sc1_16(void* p, uint16_t v) {
   __hip_atomic_store(reinterpret_cast<uint16_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -184,9 +188,18 @@ __device__ __forceinline__ void st_sc1_16(void* p, uint16_t v) {
 // lanes read garbage neighbours, which eats one halo column per step (through
 // prev, the only row this iteration produces itself; cur / next / luma come
 // from the previous state in memory every step), so every WB_HALO row pairs
-// the halo lanes reload prev from the neighbour bands' published output.
-constexpr int WB_OWN = 32, WB_HALO = (64 - WB_OWN) / 2, WB_PUB = WB_HALO;
-static_assert(WB_OWN + 2 * WB_HALO == 64 && WB_HALO % WB_PUB == 0, "wave band layout");
+// the halo lanes reload prev from the neighbour bands' updated row above:
+// since round 6 from 8-B {values, row tag} granules of the neighbours' own
+// columns, written as each WB_HALO-th row is made and polled by tag (before:
+// the neighbours' progress words after their store drains, then the row --
+// a drain and two dependent round trips a reload; iteration 0's walk 1,614
+// -> 1,528 µs at 4096^2).
+// WB_PUB: row pairs between progress publications (each a store drain),
+// for the next iteration's input waits only since round 6 (the halo reloads
+// take the neighbours' edge granules): 16 / 32 / 64 -> C5 SharpYUV
+// 1.92-1.94 / 1.89-1.92 / 1.95 ms
+constexpr int WB_OWN = 32, WB_HALO = (64 - WB_OWN) / 2, WB_PUB = 32;
+static_assert(WB_OWN + 2 * WB_HALO == 64, "wave band layout");
 
 // (bound_ctrl: the wave's end lanes, always halo lanes, read 0 -- no register to initialise)
 __device__ __forceinline__ int dpp_from_left(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); }   // wave_shr:1: lane i <- i - 1
@@ -269,6 +282,7 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
   const int16_t* tuv = a.target_uv + img * a.img_uv;
   int* prog_img = a.prog + (int64_t)img * 4 * nb;  // [iteration][band]: row pairs finished
   int* prog_out = prog_img + it * nb + band;
+  uint64_t* hand_it = a.hand + ((int64_t)img * 4 + it) * nb * 2 * WB_OWN;  // this iteration's bands' edge granules
   bool timed_out = false;  // wave-uniform
   // (WG_TIMELINES builds) s_memrealtime (100 MHz) at the walk's start and
   // end, and the ticks spent in the two kinds of dependency wait
@@ -398,13 +412,31 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
   auto step = [&](int ju, const Row& C, const Row& N, Row& pf_row, const In& in_cur, In& pf_in) {
     wait_input(min(ju + 4, uvh));  // UV row ju + 3 and luma pair ju + 3 of the input state
     if constexpr (ROLE == 0) {
-      if (ju > 0 && ju % WB_HALO == 0) {  // the halo lanes' prev: the neighbours' row ju - 1 of this iteration
-        wait_for(it, band - 1, ju);
-        wait_for(it, band + 1, ju);
-        if (act && !own) {
-          const uint32_t ub = (uint32_t)(ju - 1) * uv_row_bytes;
+      if (ju > 0 && ju % WB_HALO == 0) {
+        // the halo lanes' prev: the neighbours' updated row ju - 1, polled
+        // straight from their edge granules (tag ju: no progress word, no
+        // store drain between the bands)
+        const bool need = act && !own;
+        const uint64_t* g = hand_it + (int64_t)((lane < WB_HALO ? band - 1 : band + 1) * 2 + ((ju / WB_HALO) & 1)) * WB_OWN +
+                            (lane < WB_HALO ? lane + WB_HALO : lane - WB_HALO - WB_OWN);
+        uint64_t v = 0;
+        if (need && WG_CHK(g, 8, a.work0, a.work_n, "k_sharp_wave halo")) v = ld_sc1_64(g);
+        if (__builtin_amdgcn_ballot_w64(need && (int)(v >> 48) != ju)) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          for (uint32_t k = 0;; k++) {
+            __builtin_amdgcn_s_sleep(1);
+            if (need && (int)(v >> 48) != ju && WG_CHK(g, 8, a.work0, a.work_n, "k_sharp_wave halo")) v = ld_sc1_64(g);
+            if (!__builtin_amdgcn_ballot_w64(need && (int)(v >> 48) != ju)) break;
+            if ((k & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+              timed_out = true;
+              break;
+            }
+          }
+          WG_IF_TIMELINES(gw_ticks += __builtin_amdgcn_s_memrealtime() - t0; gw_n++;)
+        }
+        if (need) {
 #pragma unroll
-          for (int ch = 0; ch < 3; ch++) P.v[ch] = ld_w(at(out_uv, ub, lo_uv[ch]), "k_sharp_wave halo");
+          for (int ch = 0; ch < 3; ch++) P.v[ch] = (uint32_t)(uint16_t)(v >> (16 * ch)) << hs[ch];
         }
       }
     } else {
@@ -506,6 +538,17 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
       }
 #pragma unroll
       for (int ch = 0; ch < 3; ch++) P.v[ch] = (uint32_t)(uint16_t)upd[ch] << hs[ch];  // prev <- the updated cur (in its half)
+      if ((ju + 1) % WB_HALO == 0 && ju + 1 < uvh && own) {
+        // the neighbours' next halo reload: this row's own columns as 8-B
+        // granules, one write-through store each (untorn: the tag ju + 1
+        // comes with the values); two slots, so a slot is rewritten only
+        // after both neighbours have passed the reload that read it
+        uint64_t* gm = hand_it + (int64_t)(band * 2 + (((ju + 1) / WB_HALO) & 1)) * WB_OWN + (lane - WB_HALO);
+        const uint64_t gv = (uint64_t)(uint16_t)upd[0] | (uint64_t)(uint16_t)upd[1] << 16 | (uint64_t)(uint16_t)upd[2] << 32 |
+                            (uint64_t)(ju + 1) << 48;
+        if (WG_CHK(gm, 8, a.work0, a.work_n, "k_sharp_wave hand store"))
+          __hip_atomic_store(gm, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if ((ju + 1) % WB_PUB == 0 || ju + 1 == uvh) {
         // publish row pairs <= ju once this wave's stores of them are done,
         // and B's (a drain also waits for the loads in flight, so only every
@@ -689,6 +732,9 @@ SharpLayout sharp_layout(int width, int height) {
   L.bytes_img = 2 * (L.img_y + L.img_uv);
   return L;
 }
+// the tail after the images: sums [n][4] u64 | iters [n] | prog [n][4][bands]
+// | (8-B aligned) hand [n][4][bands][2][WB_OWN] | (WG_TIMELINES) stamps
+size_t sharp_hand_offset(int n, int nb) { return ((size_t)n * (32 + 4 + 16 * nb) + 7) & ~(size_t)7; }
 // one-wave column bands of one refinement iteration (k_sharp_wave)
 int sharp_bands(int width) {
   const int uvw = ((width + 1) & ~1) / 2;
@@ -701,7 +747,9 @@ extern "C" size_t wg_sharpyuv_work_bytes(int32_t width, int32_t height, int32_t 
   const SharpLayout L = sharp_layout(width, height);
   const int nb = sharp_bands(width);
   // (+ the timeline records: 32 B a wave, two waves a block, 4 * nb blocks an image)
-  return n_images * L.bytes_img + (size_t)n_images * (4 * 8 + 4 + 4 * 4 * nb) + 16 WG_IF_TIMELINES(+(size_t)n_images * 4 * nb * 64);
+  // (+ the edge granules: 2 slots of WB_OWN 8-B granules per band and iteration)
+  return n_images * L.bytes_img + sharp_hand_offset(n_images, nb) + (size_t)n_images * 4 * nb * 2 * WB_OWN * 8 + 16
+         WG_IF_TIMELINES(+(size_t)n_images * 4 * nb * 64);
 }
 
 extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t height, int32_t rgb_stride,
@@ -771,17 +819,19 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
   a.tabs = static_cast<const SharpTabs*>(tabs);
   a.lut = reinterpret_cast<const uint16_t*>(static_cast<const uint8_t*>(tabs) + sizeof(SharpTabs));
   a.lut_n = lut_n;
-  // tail: sums [n][4] u64 | iters [n] | prog [n][4][bands]
+  // tail: sums [n][4] u64 | iters [n] | prog [n][4][bands] | hand (sharp_hand_offset)
   uint8_t* tail = base + n_images * L.bytes_img;
   a.sums = reinterpret_cast<uint64_t*>(tail);
   a.iters = reinterpret_cast<int*>(tail + (size_t)n_images * 32);
   a.prog = a.iters + n_images;
+  a.hand = reinterpret_cast<uint64_t*>(tail + sharp_hand_offset(n_images, nb));
   a.n_img = n_images;
   a.work0 = base;
   a.work_n = (int64_t)wg_sharpyuv_work_bytes(width, height, n_images);
   // (WG_TIMELINES builds: the records follow the counters, 8-B aligned)
-  a.stamps = reinterpret_cast<uint64_t*>(tail + (((size_t)n_images * (32 + 4 + 16 * nb) + 7) & ~(size_t)7));
-  if (hipMemsetAsync(tail, 0, (size_t)n_images * (32 + 4 + 16 * nb), s) != hipSuccess)
+  const size_t tail_n = sharp_hand_offset(n_images, nb) + (size_t)n_images * 4 * nb * 2 * WB_OWN * 8;
+  a.stamps = reinterpret_cast<uint64_t*>(tail + tail_n);
+  if (hipMemsetAsync(tail, 0, tail_n, s) != hipSuccess)
     return wg::check_launch("hipMemsetAsync(sharpyuv)");
   const int64_t cells = (int64_t)uvw * uvh * n_images;
   if (lut)
@@ -808,6 +858,7 @@ extern "C" int wg_sharpyuv_convert_ex(const uint8_t* rgb, int32_t width, int32_t
     c.target_uv += i0 * a.img_uv;
     c.sums += 4 * i0;
     c.prog += 4 * nb * i0;
+    c.hand += (int64_t)4 * nb * 2 * WB_OWN * i0;
     c.iters += i0;
     const unsigned grid = (unsigned)(c.n_img * 4 * nb);
     if (lut)
