@@ -73,11 +73,16 @@ __device__ __forceinline__ void st_sc1_64(uint8_t* p, uint64_t v) {
 __device__ __forceinline__ void st_sc1_32(uint8_t* p, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// one 16-B write-through store (a bottom-row record leaves as 8 x 16 B, one 128-B line)
+// one 16-B write-through store (a bottom-row record leaves as 8 x 16 B, one 128-B line).
+// The s_nop: a store of more than 8 bytes reads its data VGPRs after issue,
+// and a VALU write to them in the next cycle corrupts the stored bytes; the
+// compiler's hazard recognizer does not look inside the asm (round 6: a
+// variant of k_decode_split got its next address computation into the data
+// registers right after the store, and stored address bits)
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_sc1_128(uint8_t* p, uint4 w) {
   const u32x4_t v = {w.x, w.y, w.z, w.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 // Coefficients are read exactly once: non-temporal loads, so the stream
 // (2 B / coefficient, the kernel's largest input) does not push the frame's

@@ -822,7 +822,8 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
           if (hands_off && (uint32_t)x < (uint32_t)w &&
               WG_CHK(hand_mine + x - 1, 16, a.hand, hand_n, "k_vp8l_inverse hand store")) {
             const u32x4_t g2 = {ov[u - 1], 1u, full, 1u};
-            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(hand_mine + x - 1), "v"(g2) : "memory");
+            // (s_nop: the data VGPRs are read after issue -- see st_sc1_128 in decode.hip)
+            asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(hand_mine + x - 1), "v"(g2) : "memory");
           }
         } else if (hands_off && x == w - 1 && WG_CHK(hand_mine + x, 8, a.hand, hand_n, "k_vp8l_inverse hand store")) {
           __hip_atomic_store(hand_mine + x, 1ull << 32 | full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
