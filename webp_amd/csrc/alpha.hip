@@ -295,14 +295,14 @@ __global__ __launch_bounds__(64) void k_alpha_gbands(GArgs a) {
         if (band > 0) {
           const int need = min(s + 64, w);
           if (lane == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            const uint64_t t0 = wg::wait_clock();
             for (uint32_t it = 0;; it++) {
               const int seen = __hip_atomic_load(prog_above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               if (seen >= need) break;
-              if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+              if ((it & 63) == 63 && (wg::wait_clock() - t0 > SPIN_TICKS ||
                                       __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                 __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                wg::note_timeout(a.diag, need, seen, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0);
+                wg::note_timeout(a.diag, need, seen, (int)(wg::wait_clock() - t0), (int)blockIdx.x, 0, 0);
                 break;
               }
               __builtin_amdgcn_s_sleep(2);
@@ -539,7 +539,7 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
         for (int t = 0; t < 5; t++) ready &= __builtin_amdgcn_readfirstlane((int)(Uc[t] >> 32)) != 0;
         if (!ready) {  // (re-polled into other registers: a load into Uc here would make every
                        // chunk's first use of its Uc wait for all loads in flight)
-          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          const uint64_t t0 = wg::wait_clock();
           uint64_t T[5];
           for (uint32_t it = 0;; it++) {
             __builtin_amdgcn_s_sleep(1);
@@ -550,10 +550,10 @@ __global__ __launch_bounds__(64) void k_alpha_gdiag(GdArgs a) {
             if (ready) break;
             // (the timeout alone ends the wait: a vector load of the error flag
             // here made the compiler treat the chunk buffers as just loaded)
-            if ((it & 15) == 15 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+            if ((it & 15) == 15 && wg::wait_clock() - t0 > SPIN_TICKS) {
               if (lane == 0) {
                 __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                wg::note_timeout(a.diag, s0, band, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0);
+                wg::note_timeout(a.diag, s0, band, (int)(wg::wait_clock() - t0), (int)blockIdx.x, 0, 0);
               }
               break;
             }

@@ -218,7 +218,7 @@ constexpr int BOT_BYTES = 128;  // final rows 12..15 of an MB: Y 4 x 16, U 4 x 8
 // bounded spin on a progress word (LDS or agent-scope global) by lane 0
 template <bool GLOBAL>
 __device__ __forceinline__ int wait_progress(const int* p, int need, int* err_flag, int give_up, int* diag) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t t0 = wg::wait_clock();
   for (uint32_t it = 0;; it++) {
     int v;
     if (GLOBAL) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -226,10 +226,10 @@ __device__ __forceinline__ int wait_progress(const int* p, int need, int* err_fl
     if (v >= need) return v;
     // never hang the GPU: after SPIN_TICKS (or once any wait has timed out)
     // flag the error and carry on with whatever is in memory
-    if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+    if ((it & 63) == 63 && (wg::wait_clock() - t0 > SPIN_TICKS ||
                             __hip_atomic_load(err_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
       __hip_atomic_fetch_or(err_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      wg::note_timeout(diag, need, v, GLOBAL ? 1 : 0, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x,
+      wg::note_timeout(diag, need, v, GLOBAL ? 1 : 0, (int)(wg::wait_clock() - t0), (int)blockIdx.x,
                        (int)(threadIdx.x >> 6));
       return give_up;
     }

@@ -1343,14 +1343,14 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
   int q = 0;  // LOOSE: this wave's band sequence number in the workgroup
   // LOOSE: bounded LDS spin of the whole wave until *p >= need (acquire)
   auto wait_lds = [&](const int* p, int need) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t0 = wg::wait_clock();
     for (uint32_t it = 0;; it++) {
       if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >= need)
         return;
-      if ((it & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+      if ((it & 63) == 63 && wg::wait_clock() - t0 > SPIN_TICKS) {
         if (lane == 0) {
           __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          wg::note_timeout(a.diag, -1, q, need, 0, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x);
+          wg::note_timeout(a.diag, -1, q, need, 0, (int)(wg::wait_clock() - t0), (int)blockIdx.x);
         }
         return;
       }
@@ -1433,7 +1433,7 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
       row = WAVES * band + gw;
     }
     const bool live = mby < mbh;  // (the last band of an image may have fewer rows)
-    WG_IF_ROWTIMES(const unsigned long long row_t0 = __builtin_amdgcn_s_memrealtime();)
+    WG_IF_ROWTIMES(const unsigned long long row_t0 = wg::wait_clock();)
     const uint8_t* Y = a.y + img * a.y_pitch;
     const uint8_t* U = a.u + img * a.uv_pitch;
     const uint8_t* V = a.v + img * a.uv_pitch;
@@ -1479,17 +1479,17 @@ __global__ __launch_bounds__(64 * (PAIR ? 2 : WAVES * GROUPS), PAIR ? 2 : 2) voi
         uint32_t w = 0;
         if (mby > 0) {
           const uint32_t want = (uint32_t)mby;  // row mby - 1's tag
-          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          const uint64_t t0 = wg::wait_clock();
           for (uint32_t it = 0;; it++) {
             const uint64_t g =
                 lane < n && WG_CHK(rec + 8 * lane, 8, a.top, top_n, "k_encode_rows record load") ? ld_granule(rec + 8 * lane) : 0;
             w = (uint32_t)g;
             if (__ballot(lane < n && (uint32_t)(g >> 32) != want) == 0) break;
-            if ((it & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+            if ((it & 63) == 63 && (wg::wait_clock() - t0 > SPIN_TICKS ||
                                     __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
               if (lane == 0) {
                 __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                wg::note_timeout(a.diag, mby, img, mbx, n, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x);
+                wg::note_timeout(a.diag, mby, img, mbx, n, (int)(wg::wait_clock() - t0), (int)blockIdx.x);
               }
               break;
             }

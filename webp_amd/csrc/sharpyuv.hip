@@ -304,14 +304,14 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
     if (bb < 0 || bb >= nb || timed_out) return uvh;
     const int* p = prog_img + ii * nb + bb;
     if (!WG_CHK(p, 4, a.work0, a.work_n, "k_sharp_wave prog load")) return uvh;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t0 = wg::wait_clock();
     for (uint32_t k = 0;; k++) {
       const int v = __builtin_amdgcn_readfirstlane((int)ld_sc1(p));
       if (v >= need) {
-        WG_IF_TIMELINES(if (k > 0) { gw_ticks += __builtin_amdgcn_s_memrealtime() - t0; gw_n++; })
+        WG_IF_TIMELINES(if (k > 0) { gw_ticks += wg::wait_clock() - t0; gw_n++; })
         return v;
       }
-      if ((k & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+      if ((k & 63) == 63 && wg::wait_clock() - t0 > SPIN_TICKS) {
         timed_out = true;
         return uvh;
       }
@@ -321,14 +321,14 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
   // the same for the other wave's LDS progress word
   auto wait_lds = [&](const int* p, int need) {
     if (timed_out || __builtin_amdgcn_readfirstlane(lds_acquire(p)) >= need) return;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t0 = wg::wait_clock();
     for (uint32_t k = 0;; k++) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_readfirstlane(lds_acquire(p)) >= need) {
-        WG_IF_TIMELINES(lw_ticks += __builtin_amdgcn_s_memrealtime() - t0; lw_n++;)
+        WG_IF_TIMELINES(lw_ticks += wg::wait_clock() - t0; lw_n++;)
         return;
       }
-      if ((k & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+      if ((k & 63) == 63 && wg::wait_clock() - t0 > SPIN_TICKS) {
         timed_out = true;
         return;
       }
@@ -422,17 +422,17 @@ __device__ __forceinline__ void sharp_wave_band(const SharpArgs& a, const SharpT
         uint64_t v = 0;
         if (need && WG_CHK(g, 8, a.work0, a.work_n, "k_sharp_wave halo")) v = ld_sc1_64(g);
         if (__builtin_amdgcn_ballot_w64(need && (int)(v >> 48) != ju)) {
-          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          const uint64_t t0 = wg::wait_clock();
           for (uint32_t k = 0;; k++) {
             __builtin_amdgcn_s_sleep(1);
             if (need && (int)(v >> 48) != ju && WG_CHK(g, 8, a.work0, a.work_n, "k_sharp_wave halo")) v = ld_sc1_64(g);
             if (!__builtin_amdgcn_ballot_w64(need && (int)(v >> 48) != ju)) break;
-            if ((k & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+            if ((k & 63) == 63 && wg::wait_clock() - t0 > SPIN_TICKS) {
               timed_out = true;
               break;
             }
           }
-          WG_IF_TIMELINES(gw_ticks += __builtin_amdgcn_s_memrealtime() - t0; gw_n++;)
+          WG_IF_TIMELINES(gw_ticks += wg::wait_clock() - t0; gw_n++;)
         }
         if (need) {
 #pragma unroll

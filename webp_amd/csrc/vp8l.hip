@@ -679,19 +679,19 @@ __device__ __forceinline__ void inv_band(const InvArgs& a, const uint32_t (*mtab
     // re-poll column c's granule until its tag is set (band > 0, c < w)
     auto up_poll = [&](int c) -> uint64_t {
       uint64_t g = 0;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      const uint64_t t0 = wg::wait_clock();
       for (uint32_t it = 0;; it++) {
         __builtin_amdgcn_s_sleep(1);
         g = up_load(c);
         if (__builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(uint2, g).y) != 0) {
-          WG_IF_TIMELINES(poll_ticks += __builtin_amdgcn_s_memrealtime() - t0; polls++;)
+          WG_IF_TIMELINES(poll_ticks += wg::wait_clock() - t0; polls++;)
           break;
         }
-        if ((it & 15) == 15 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+        if ((it & 15) == 15 && (wg::wait_clock() - t0 > SPIN_TICKS ||
                                 __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
           if (lane == 0) {
             __hip_atomic_fetch_or(&a.ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            wg::note_timeout(a.diag, c, (int)(__builtin_amdgcn_s_memrealtime() - t0), (int)blockIdx.x, 0, 0, 0);
+            wg::note_timeout(a.diag, c, (int)(wg::wait_clock() - t0), (int)blockIdx.x, 0, 0, 0);
           }
           break;
         }

@@ -45,6 +45,19 @@ int* diag_words(hipStream_t s);
 int take_new_timeouts(hipStream_t s, int family, int total);
 
 // lane-0 call on a timed-out wait: counts it and records the first one
+// s_memrealtime for the start of a bounded wait, waited for at once.  The
+// wait's slow path reads it; left outstanding, it reaches the join with the
+// fast path, where the compiler then puts an lgkmcnt(0) -- which waits for
+// every LDS read in flight too -- before the first reuse of its SGPRs, on
+// every pass of the fast path (round 6: one a step in k_vp8l_inverse's walk).
+// 0xC07F = lgkmcnt(0), vmcnt / expcnt unconstrained; the builtin, unlike
+// inline asm, is seen by the compiler's wait bookkeeping.
+__device__ __forceinline__ uint64_t wait_clock() {
+  const uint64_t t = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  return t;
+}
+
 __device__ inline void note_timeout(int* diag, int c2, int c3, int c4, int c5, int c6, int c7) {
   __hip_atomic_fetch_add(&diag[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int z = 0;
