@@ -736,6 +736,76 @@ __global__ __launch_bounds__(64 * DW) void k_decode_bands(DecArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Table-driven 4x4 intra prediction of one row (k_decode_split, round 6).
+// Every pixel of the ten modes (pred4_row, predict_lossy.go:185-424) is one
+// value of a small per-row pool: with E = L3 L2 L1 L0 X T0..T7 (E[-1] = L3,
+// E[13..] = T7), A3[i] = avg3(E[i-1], E[i], E[i+1]) for i < 16 and
+// A2[i] = avg2(E[i], E[i+1]) for i < 12 -- DC, TM and the left column raw
+// aside.  The block's four lanes (a DPP quad: lane = 4 block + row) load its
+// context as seven dwords between them, build E packed with v_perm /
+// v_alignbyte, take A3 four at a time as two v_lerp_u8 (avg3(a, b, c) =
+// (((a + c) >> 1) + b + 1) >> 1: a floor then a rounding byte average) and A2
+// as one, write the pool (40 B) to the lane's LDS slot and read the row's
+// four bytes back by the mode's code word: no branch on the mode, where
+// pred4_row's switch runs every mode present in the step one after another.
+// Pool: bytes 0-15 A3, 16-27 A2, 28-31 E[0..3], 32-35 DC, 36-39 TM's row.
+// kI4Code[mode][row]: the pool byte of pixel x in byte x (checked against
+// pred4_row on random and saturated contexts, all modes and rows).
+constexpr uint32_t i4c(int a, int b, int c, int d) { return (uint32_t)a | (uint32_t)b << 8 | (uint32_t)c << 16 | (uint32_t)d << 24; }
+__constant__ uint32_t kI4Code[40] = {
+    i4c(32, 33, 34, 35), i4c(32, 33, 34, 35), i4c(32, 33, 34, 35), i4c(32, 33, 34, 35),  // DC
+    i4c(36, 37, 38, 39), i4c(36, 37, 38, 39), i4c(36, 37, 38, 39), i4c(36, 37, 38, 39),  // TM
+    i4c(5, 6, 7, 8), i4c(5, 6, 7, 8), i4c(5, 6, 7, 8), i4c(5, 6, 7, 8),                  // VE
+    i4c(3, 3, 3, 3), i4c(2, 2, 2, 2), i4c(1, 1, 1, 1), i4c(0, 0, 0, 0),                  // HE
+    i4c(4, 5, 6, 7), i4c(3, 4, 5, 6), i4c(2, 3, 4, 5), i4c(1, 2, 3, 4),                  // RD
+    i4c(20, 21, 22, 23), i4c(4, 5, 6, 7), i4c(3, 20, 21, 22), i4c(2, 4, 5, 6),          // VR
+    i4c(6, 7, 8, 9), i4c(7, 8, 9, 10), i4c(8, 9, 10, 11), i4c(9, 10, 11, 12),            // LD
+    i4c(21, 22, 23, 24), i4c(6, 7, 8, 9), i4c(22, 23, 24, 10), i4c(7, 8, 9, 11),         // VL
+    i4c(19, 4, 5, 6), i4c(18, 3, 19, 4), i4c(17, 2, 18, 3), i4c(16, 1, 17, 2),           // HD
+    i4c(18, 2, 17, 1), i4c(17, 1, 16, 0), i4c(16, 0, 28, 28), i4c(28, 28, 28, 28)};     // HU
+template <int K>
+__device__ __forceinline__ uint32_t quad_b(uint32_t v) {  // lane K of the quad to all four (quad_perm [K,K,K,K])
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xf, 0xf, false);
+}
+// (code: the lane's kI4Code word from LDS; pool: its 48-B LDS slot)
+__device__ __forceinline__ uint32_t pred4_row_tab(const uint8_t* wb, int off, int rr, uint32_t cw, uint32_t* pool) {
+  const uint8_t* d = wb + off;
+  // lane rr: its row's left dword (L[rr] in byte 3); lanes 0 / 1 / 2 the top
+  // row's two dwords and the dword ending in X
+  const uint32_t ld = lds32(d - 4 + rr * WG_BPS);
+  const uint32_t q = lds32(d + (rr == 1 ? 4 - WG_BPS : (rr == 2 ? -4 - WG_BPS : -WG_BPS)));
+  const uint32_t l0 = quad_b<0>(ld), l1 = quad_b<1>(ld), l2 = quad_b<2>(ld), l3 = quad_b<3>(ld);
+  const uint32_t tlo = quad_b<0>(q), thi = quad_b<1>(q), xd = quad_b<2>(q);
+  const uint32_t e0 = __builtin_amdgcn_perm(l2, l3, 0x0c0c0703u) | __builtin_amdgcn_perm(l0, l1, 0x07030c0cu);  // L3 L2 L1 L0
+  const uint32_t e1 = __builtin_amdgcn_alignbyte(tlo, xd, 3);                                                    // X T0 T1 T2
+  const uint32_t e2 = __builtin_amdgcn_alignbyte(thi, tlo, 3);                                                   // T3 .. T6
+  const uint32_t e3 = __builtin_amdgcn_perm(thi, thi, 0x07070707u);                                              // T7 x 4
+  const uint32_t lf0 = __builtin_amdgcn_perm(e0, e0, 0x02010000u), lf1 = __builtin_amdgcn_alignbyte(e1, e0, 3);
+  const uint32_t lf2 = __builtin_amdgcn_alignbyte(e2, e1, 3), lf3 = __builtin_amdgcn_alignbyte(e3, e2, 3);
+  const uint32_t rt0 = __builtin_amdgcn_alignbyte(e1, e0, 1), rt1 = __builtin_amdgcn_alignbyte(e2, e1, 1);
+  const uint32_t rt2 = __builtin_amdgcn_alignbyte(e3, e2, 1);
+  constexpr uint32_t UP = 0x01010101u;
+  auto a3 = [](uint32_t l, uint32_t c, uint32_t r) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(l, r, 0u), c, UP); };
+  const uint32_t dc = (__builtin_amdgcn_sad_u8(tlo, 0u, __builtin_amdgcn_sad_u8(e0, 0u, 4u)) >> 3) * UP;
+  // TM: clip(L[rr] - X + T[x]) on 16-bit pairs
+  const int base = (int)(ld >> 24) - (int)(xd >> 24);
+  const wg::s16x2_t b2 = {(short)base, (short)base};
+  wg::s16x2_t tl = __builtin_bit_cast(wg::s16x2_t, __builtin_amdgcn_perm(0u, tlo, 0x0c010c00u)) + b2;
+  wg::s16x2_t th = __builtin_bit_cast(wg::s16x2_t, __builtin_amdgcn_perm(0u, tlo, 0x0c030c02u)) + b2;
+  const wg::s16x2_t z = {0, 0}, m = {255, 255};
+  tl = __builtin_elementwise_min(__builtin_elementwise_max(tl, z), m);
+  th = __builtin_elementwise_min(__builtin_elementwise_max(th, z), m);
+  const uint32_t tm = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, th), __builtin_bit_cast(uint32_t, tl), 0x06040200u);
+  uint4* pv = reinterpret_cast<uint4*>(pool);
+  pv[0] = make_uint4(a3(lf0, e0, rt0), a3(lf1, e1, rt1), a3(lf2, e2, rt2), a3(lf3, e3, e3));
+  pv[1] = make_uint4(__builtin_amdgcn_lerp(e0, rt0, UP), __builtin_amdgcn_lerp(e1, rt1, UP), __builtin_amdgcn_lerp(e2, rt2, UP), e0);
+  pv[2] = make_uint4(dc, tm, 0u, 0u);
+  const uint8_t* pb = reinterpret_cast<const uint8_t*>(pool);
+  return (uint32_t)pb[cw & 0xff] | (uint32_t)pb[(cw >> 8) & 0xff] << 8 | (uint32_t)pb[(cw >> 16) & 0xff] << 16 |
+         (uint32_t)pb[cw >> 24] << 24;
+}
+
+// ---------------------------------------------------------------------------
 // k_decode_split: the same work as k_decode_bands with reconstruction and loop
 // filtering on two waves per macroblock row.  Intra prediction reads
 // UNFILTERED pixels (the top context is saved before filtering,
@@ -792,6 +862,8 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
   // block for the top row as well measured slower: C3 4.19 -> 4.34 ms.)
   __shared__ int tprog[SW];
   __shared__ int sh_word;
+  __shared__ __attribute__((aligned(16))) uint32_t i4pool[SW][64][12];  // pred4_row_tab's per-lane pools
+  __shared__ uint32_t i4code[40];
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool is_f = wave >= SW;
@@ -808,6 +880,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                                  bot_size = n_mb / mbh * BOT_BYTES, prog_size = 8ll * a.n_img * mbh,
                                  y_size = n_mb * 256, uv_size = n_mb * 64;
   STAMP_DECL;
+  for (int i = threadIdx.x; i < 40; i += blockDim.x) i4code[i] = kI4Code[i];  // (ordered by the loop's barrier)
 
   for (;;) {
     if (threadIdx.x == 0) sh_word = __hip_atomic_fetch_add(&a.ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1001,7 +1074,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
           } else {
             const int my_step = (int)(sched >> (4 * blk)) & 15;
             const int n_steps = (int)(sched >> 60) + 1;  // block 15 is last
-            const int mode = imodes[blk];
+            const uint32_t cw = i4code[4 * imodes[blk] + rr];  // (pred4_row_tab's code word)
             for (int st = 0; st < n_steps; st++) {
               if (st == tr_step) {
                 // the first block that reads the top-right: only now wait for
@@ -1027,9 +1100,7 @@ __global__ __launch_bounds__(128 * SW) void k_decode_split(DecArgs a) {
                 lds_sync();
               }
               if (st == my_step) {
-                int X, T[8], L[4];
-                pred4_ctx(wb, LY + 4 * by * WG_BPS + 4 * bx, X, T, L);
-                const uint32_t pred = pred4_row(mode, rr, X, T, L);
+                const uint32_t pred = pred4_row_tab(wb, LY + 4 * by * WG_BPS + 4 * bx, rr, cw, i4pool[r][lane]);
                 const uint32_t row = pack4(clip8(byte_of(pred, 0) + res[0]), clip8(byte_of(pred, 1) + res[1]),
                                            clip8(byte_of(pred, 2) + res[2]), clip8(byte_of(pred, 3) + res[3]));
                 *reinterpret_cast<uint32_t*>(wb + off) = row;
