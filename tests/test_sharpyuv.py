@@ -90,6 +90,23 @@ def test_gpu_wide(cuda, w, h):
     assert (Y[0].cpu().numpy() == ey).all() and (U[0].cpu().numpy() == eu).all() and (V[0].cpu().numpy() == ev).all()
 
 
+@pytest.mark.gpu
+def test_gpu_batch_over_several_launches(cuda):
+    """A batch larger than one launch holds (k_sharp_wave runs at most as many
+    images as the device keeps resident: 4 iterations x 32 bands an image at
+    this width, ~14 images a launch), so the images' progress words and
+    halo edge granules (per image, iteration and band) are offset per
+    launch; every image bit-exact."""
+    import torch
+    from webp_amd import frames
+    imgs = np.stack([synth.noise_rgba(2000, 20, seed=s)[..., :3] for s in range(40)])
+    Y, U, V = frames.sharpyuv_convert(torch.from_numpy(imgs).cuda())
+    torch.cuda.synchronize()
+    for i in range(imgs.shape[0]):
+        ey, eu, ev, _ = O.sharpyuv_convert(imgs[i])
+        assert (Y[i].cpu().numpy() == ey).all() and (U[i].cpu().numpy() == eu).all() and (V[i].cpu().numpy() == ev).all(), i
+
+
 # ---- the other transfer functions and convertStandard (sharpyuv.go:68-115, gamma.go:125-446) ----
 
 NON_SRGB = [tf for tf in O.TRANSFER_FUNCS if tf != 13]
